@@ -1,0 +1,225 @@
+"""Benchmark: full PALFA-beam dedispersion (BASELINE.json metric) on MI355X.
+
+A step = one whole beam through the reference's Mock DDplan: 57 passes x (stage 1
+subbanding + stage 2 DM sweep), 4188 DM trials of N/ds samples each, inputs (raw beam,
+mask) resident in HBM, outputs left resident (no .dat writes: the end-to-end file path is
+measured separately).  At N GPUs every rank dedisperses its own beam (the
+7-beam ALFA pointing of configs[4]; per-GPU work fixed -> "weak" scaling); value = total
+output samples of all ranks / max-over-ranks wall time.
+
+  python bench.py --gpus N --steps K --warmup W
+  torchrun --nproc-per-node N ... bench.py --gpus N ...     (one rank per GPU)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "pipeline2.0_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+METRIC = "dedispersed samples/sec (DM-trials x samples/s, node) + % HBM peak, PALFA beam"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+VALU_ADD_PEAK = 78.6e12        # fp32 vector adds/s (157.3 TFLOPS / 2), SURVEY §8d
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--nspec", type=int, default=1 << 22, help="spectra per beam (2^22 = config 2)")
+    ap.add_argument("--nbits", type=int, default=8)
+    ap.add_argument("--variant", type=int, default=0, help="stage-2 kernel: 0 auto, 1 direct, 2 LDS")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU-baseline leg")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU work for the baseline sample")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", init_method="env://")
+        return world, rank, local, dist, torch
+    return 1, 0, 0, None, None
+
+
+def barrier(dist, torch):
+    if dist is not None:
+        dist.barrier()
+
+
+def max_over_ranks(x, dist, torch):
+    if dist is None:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def build_plans(eng, obs, ddplans, variant):
+    from hipdedisp import PassParams, plan as P
+    plans = []
+    for d in ddplans:
+        for i in range(d.numpasses):
+            pp = PassParams(subdm=float(d.subdmlist[i]), lodm=float(d.lodm_arg(i)),
+                            dmstep=float(d.dmstep_arg()), numdms=d.dmsperpass, nsub=d.numsub,
+                            ds=d.sub_downsamp, numout=P.choose_N(obs.N / d.downsamp))
+            p = eng.plan(pp)
+            if variant:
+                p.set_variant(variant)
+            plans.append(p)
+    return plans
+
+
+def run_step(eng, plans):
+    for p in plans:
+        p.run_subband()
+        p.run_dedisp(to_host=False)
+    eng.sync()
+
+
+def cpu_baseline(obs, synth, ddplans, target_s):
+    """Oracle (restatement of prepsubband's two stages) on the host cores, on a bounded
+    sample: the first W output samples of one pass per DDplan stage, extrapolated to the
+    whole plan by passes x (N/ds)/W.  W is sized so the sample costs ~target_s seconds."""
+    import numpy as np
+    import oracle as OR
+    from hipdedisp import Opts
+    from hipdedisp.synth import host_spectra
+    opts = Opts()
+    threads = OR.num_threads(True)
+
+    def one(d, W):
+        subdm = float(d.subdmlist[0])
+        off = OR.dm_offsets(obs, opts, d.numsub, d.sub_downsamp, float(d.lodm_arg(0)), d.dmstep, d.dmsperpass)
+        idd = OR.chan_delays(obs, d.numsub, subdm)
+        ws = W + int(off.max())
+        nraw = min(obs.N, ws * d.sub_downsamp + int(idd.max()) + d.sub_downsamp)
+        raw = host_spectra(obs, synth, 0, nraw)
+        t0 = time.perf_counter()
+        sub = OR.stage1(obs, opts, raw, d.numsub, d.sub_downsamp, subdm, t0=0, count=ws, omp=True)
+        OR.stage2(sub, off, 0, W, omp=True)
+        return time.perf_counter() - t0
+
+    # per stage: probe a small window, then size the measured window to ~target_s/6 seconds
+    budget = target_s / len(ddplans)
+    est_full, done_out, done_t = 0.0, 0, 0.0
+    for d in ddplans:
+        nds = obs.N // d.sub_downsamp
+        probe_w = 16384
+        tp = one(d, probe_w)
+        W = int(min(nds - 8192, max(probe_w, probe_w * budget / max(tp, 1e-3))))
+        t = one(d, W)
+        est_full += d.numpasses * t * nds / W
+        done_out += d.dmsperpass * W
+        done_t += t
+    total_out = sum(d.numpasses * d.dmsperpass * (obs.N // d.sub_downsamp) for d in ddplans)
+    return {"value": total_out / est_full, "unit": "samples/s", "cores": threads, "kind": "port",
+            "sample": "oracle/prepsubband_oracle.c (OpenMP, %d threads): first W output samples of pass 0 of "
+                      "each of the 6 DDplan stages (%d DM-samples, %.1f s), extrapolated by passes x (N/ds)/W "
+                      "to the full 57-pass beam (est. %.0f s)" % (threads, done_out, done_t, est_full),
+            "est_full_beam_s": est_full}
+
+
+def main():
+    args = parse()
+    world, rank, local, dist, torch = dist_setup(args)
+    from hipdedisp import Engine, Opts, plan as P
+    from hipdedisp.synth import palfa_obs, palfa_synth, rfifind_ptsperint, synth_mask
+
+    obs = palfa_obs(N=args.nspec, nbits=args.nbits)
+    synth = palfa_synth(beam=rank, nbits=args.nbits)
+    ddplans = P.ddplans_for("pdev")
+    eng = Engine(local)
+    eng.set_obs(obs, Opts())
+    eng.synth_device(synth)
+    pts = rfifind_ptsperint(obs.dt)
+    mask, pad = synth_mask(obs, synth, pts)
+    eng.set_mask(mask, pts, pad)
+    plans = build_plans(eng, obs, ddplans, args.variant)
+    out_per_step = sum(p.pp.numdms * p.nds for p in plans)
+
+    for _ in range(args.warmup):
+        run_step(eng, plans)
+    barrier(dist, torch)
+    eng.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run_step(eng, plans)
+    eng.sync()
+    barrier(dist, torch)
+    dt = time.perf_counter() - t0
+    dt_max = max_over_ranks(dt, dist, torch)
+
+    # per-kernel device time of the last step (hipEvents on the engine's stream)
+    ms1 = ms2 = 0.0
+    for p in plans:
+        a, b = p.last_ms()
+        ms1 += a
+        ms2 += b
+    raw_bytes = obs.N * obs.rowbytes
+    sub_bytes = sum(p.pp.nsub * p.nds * 2 for p in plans)
+    adds2 = sum(p.pp.numdms * p.nds * p.pp.nsub for p in plans)
+    # algorithmic bytes per output sample (SURVEY §8d compulsory model): raw once + 4 B out
+    b_unit = (raw_bytes + 4.0 * out_per_step) / out_per_step
+    if ms2 >= ms1:
+        dom = "k_stage2 (DM sweep)"
+        achieved = out_per_step * b_unit / (ms2 * 1e-3) / 1e9
+        launch_ms = ms2 / len(plans)
+    else:
+        dom = "k_stage1 (subband formation)"
+        achieved = (len(plans) * raw_bytes + sub_bytes) / (ms1 * 1e-3) / 1e9
+        launch_ms = ms1 / len(plans)
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_r01.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch", {}).get(dom.split()[0])
+        except Exception:
+            traffic = None
+    step_s = dt_max / args.steps
+    line = {
+        "metric": METRIC,
+        "value": world * out_per_step * args.steps / dt_max,
+        "unit": "samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": step_s * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8->f32 subbanding, i16 subbands, i16x2/i32 exact sums, f32 out",
+        "data": "synthetic",
+        "config": {"workload": "C2: full PALFA Mock beam per GPU (960 ch x 2^22 x %d-bit, 65.476 us), "
+                               "57-pass DDplan = 4188 DM trials, rfifind-style mask" % args.nbits,
+                   "nchan": obs.nchan, "nspec": obs.N, "nbits": obs.nbits, "dm_trials": 4188, "passes": len(plans),
+                   "out_samples_per_beam": out_per_step, "parallelism": "beam-per-GPU x%d" % world},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "avg_launch_ms": launch_ms, "bytes_per_unit": b_unit},
+        "kernel_ms_per_step": {"stage1": ms1, "stage2": ms2},
+        "step_compulsory_hbm_frac": (raw_bytes + 4.0 * out_per_step) / step_s / (HBM_PEAK_GBS * 1e9),
+        "stage2_valu_frac": adds2 / (ms2 * 1e-3) / VALU_ADD_PEAK if ms2 > 0 else None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline(obs, synth, ddplans, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    for p in plans:
+        p.destroy()
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

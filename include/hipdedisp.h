@@ -1,0 +1,196 @@
+/*
+ * hipdedisp.h — C ABI of libhipdedisp.so, the MI355X dedispersion engine that
+ * replaces the two `prepsubband` invocations of the PALFA search loop.
+ *
+ * Reference interface being replaced (pipeline2.0, read as text):
+ *   lib/python/PALFA2_presto_search.py:506-511  stage 1: prepsubband -sub -subdm S -downsamp ds
+ *                                                 -nsub 96 -mask M -o tmp/subbands/<base> <raw>
+ *   lib/python/PALFA2_presto_search.py:514-520  stage 2: prepsubband -lodm L -dmstep D -numdms n
+ *                                                 -downsamp 1 -nsub 96 -numout choose_N(N/ds)
+ *                                                 -o tmp/<base> tmp/subbands/<base>_DM<S>.sub[0-9]*
+ *   lib/python/PALFA2_presto_search.py:522-529  use_subbands=False variant (raw -> .dat directly)
+ *   lib/python/PALFA2_presto_search.py:95-139   timed_execute: non-zero status -> PrestoError
+ *
+ * The reference crosses this boundary as a shell command + files; the ABI below is the
+ * in-process equivalent.  Conventions:
+ *   - every call returns int: HD_OK (0) or a negative HD_E_* code; no exceptions cross;
+ *   - hd_last_error(ctx) returns the message of the last failure on that context
+ *     (ctx == NULL: last failure of a call that had no context, e.g. hd_open);
+ *   - plain C types only; all host buffers are caller-owned and are not retained past
+ *     the call that receives them (hd_push_raw copies synchronously into device memory);
+ *   - a context is bound to one HIP device and one stream and is NOT thread-safe; use one
+ *     context per host thread (contexts on different devices run concurrently);
+ *   - channel index c is ascending-frequency order (after the PSRFITS band flip) everywhere
+ *     except raw bytes, which stay in file order.
+ */
+#ifndef HIPDEDISP_H
+#define HIPDEDISP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Only the hd_* entry points are exported (the library builds with -fvisibility=hidden). */
+#define HD_API __attribute__((visibility("default")))
+
+#define HD_OK        0
+#define HD_E_INVAL  -1   /* bad argument / inconsistent shapes          */
+#define HD_E_NODEV  -2   /* no HIP device / device index out of range   */
+#define HD_E_HIP    -3   /* HIP runtime error (message has the detail)  */
+#define HD_E_NOMEM  -4   /* device or host allocation failed            */
+#define HD_E_STATE  -5   /* call out of order (e.g. no raw data yet)    */
+#define HD_E_IO     -6   /* file I/O failed                             */
+
+/* Subband sample storage (PRESTO writes .subNN as 16-bit ints; f32 keeps them exact). */
+#define HD_SUB_I16   0
+#define HD_SUB_F32   1
+/* Downsampling of subbands: sum of ds samples, or their mean. */
+#define HD_DS_SUM    0
+#define HD_DS_MEAN   1
+/* Padding of a DM series from its length N/ds up to numout. */
+#define HD_PAD_MEAN  0   /* mean of the series' data samples (double sum, cast to f32) */
+#define HD_PAD_ZERO  1
+
+typedef struct hd_ctx  hd_ctx;
+typedef struct hd_plan hd_plan;
+
+/* Observation, as read from the PSRFITS headers
+ * (reference: lib/python/formats/psrfits.py:116-134, 210-220, 272-314). */
+typedef struct {
+    int32_t   nchan;     /* NCHAN                                                   */
+    int32_t   nbits;     /* NBITS: 4, 8 or 16                                       */
+    int32_t   npol;      /* NPOL (only 1 supported: summed polarisations)          */
+    int32_t   flip;      /* 1: raw channels are in descending frequency (need_flipband) */
+    double    dt;        /* TBIN, seconds                                           */
+    double    lofreq;    /* MHz, centre of the lowest-frequency channel             */
+    double    df;        /* MHz, channel width, > 0                                 */
+    int64_t   N;         /* spectra in the observation                              */
+    int32_t   nsblk;     /* NSBLK, spectra per PSRFITS row                          */
+    int32_t   _pad0;
+    double    voverc;    /* average barycentric v/c; 0 == prepsubband -nobary      */
+} hd_obs;
+
+/* PRESTO-semantics switches.  Defaults: hd_opts_default(). */
+typedef struct {
+    int32_t   sub_dtype;       /* HD_SUB_I16 (default) | HD_SUB_F32                      */
+    int32_t   ds_mode;         /* HD_DS_SUM (default)  | HD_DS_MEAN                      */
+    int32_t   pad_mode;        /* HD_PAD_MEAN (default) | HD_PAD_ZERO                    */
+    int32_t   nibble_hi_first; /* 4-bit: first sample in the high nibble (default 1)     */
+    int32_t   be16;            /* 16-bit samples big-endian as stored in FITS (default 1)*/
+    int32_t   inf_roundtrip;   /* subband-level freq/dt pass through "%.12g"/"%.15g" text,
+                                  as they do through the .sub.inf file (default 1)        */
+    float     clip_sigma;      /* time-domain clip threshold; 0 disables  */
+    int32_t   _pad0;
+} hd_opts;
+
+/* One prepsubband pass: stage-1 subbanding at subdm + stage-2 sweep over numdms DMs. */
+typedef struct {
+    double    subdm;     /* -subdm                                      */
+    double    lodm;      /* stage-2 -lodm (value of the "%.2f" argument) */
+    double    dmstep;    /* stage-2 -dmstep                             */
+    int32_t   numdms;    /* stage-2 -numdms                             */
+    int32_t   nsub;      /* -nsub (nchan % nsub == 0)                   */
+    int32_t   ds;        /* stage-1 -downsamp (stage 2 runs at -downsamp 1) */
+    int32_t   flags;     /* HD_PASS_* below                             */
+    int64_t   numout;    /* stage-2 -numout; 0 == N/ds (no padding)     */
+} hd_pass;
+
+/* hd_pass.flags: the observation IS the subband file set (stage-2-only prepsubband run on
+ * .subNN input): nsub == nchan, ds == 1, and lofreq/df/dt are taken as read from the
+ * .sub.inf, without re-deriving them.  Only hd_set_subbands + hd_run_dedisp apply.      */
+#define HD_PASS_SUB_INPUT 1
+
+/* Synthetic PALFA-like beam description for hd_synth_* (SURVEY.md §8d). */
+#define HD_SYNTH_MAX_PSR 8
+typedef struct {
+    uint64_t  seed;
+    float     base_level;      /* mean level of a channel (digitiser units)      */
+    float     bandpass_slope;  /* fractional level change across the band        */
+    float     noise_sigma;     /* per-channel noise sigma (digitiser units)      */
+    int32_t   npsr;            /* periodic sources in psr_* below                */
+    int32_t   nspulse;         /* single pulses in sp_* below                    */
+    double    psr_period[HD_SYNTH_MAX_PSR];  /* s   */
+    double    psr_dm[HD_SYNTH_MAX_PSR];
+    double    psr_width[HD_SYNTH_MAX_PSR];   /* s   */
+    float     psr_amp[HD_SYNTH_MAX_PSR];     /* digitiser units per channel */
+    double    sp_time[HD_SYNTH_MAX_PSR];     /* s, arrival time at the top of the band */
+    double    sp_dm[HD_SYNTH_MAX_PSR];
+    double    sp_width[HD_SYNTH_MAX_PSR];
+    float     sp_amp[HD_SYNTH_MAX_PSR];
+    int32_t   rfi_nchan;       /* persistent narrowband RFI channels (ascending index list) */
+    int32_t   rfi_chan[8];
+    float     rfi_amp;
+    float     burst_frac;      /* fraction of (interval, channel) cells with bursty RFI */
+    int32_t   burst_len;       /* samples per bursty interval                   */
+    float     burst_amp;
+    float     spike_frac;      /* fraction of spectra carrying a zero-DM broadband spike */
+    float     spike_amp;
+} hd_synth;
+
+/* ---- library / context -------------------------------------------------------- */
+HD_API const char* hd_version(void);
+HD_API void        hd_opts_default(hd_opts* opts);
+HD_API void        hd_synth_default(hd_synth* s);
+HD_API int         hd_device_count(int* n);
+HD_API int         hd_open(int device, hd_ctx** out);
+HD_API int         hd_close(hd_ctx* ctx);
+HD_API const char* hd_last_error(const hd_ctx* ctx);
+HD_API int         hd_sync(hd_ctx* ctx);
+
+/* Observation + switches.  The device raw block (N * nchan * nbits/8 bytes) is allocated
+ * on the first hd_push_raw / hd_synth_device. */
+HD_API int hd_set_obs(hd_ctx* ctx, const hd_obs* obs, const hd_opts* opts);
+/* Per-raw-channel DAT_SCL / DAT_OFFS / DAT_WTS (file channel order); NULL = identity.
+ * Value = ((raw * scl) + offs) * wts, as PSRFITS defines.                         */
+HD_API int hd_set_chan_calib(hd_ctx* ctx, const float* scl, const float* offs, const float* wts);
+/* rfifind mask as a dense bitmap mask[numint][nchan] (1 = zapped), ascending-frequency
+ * channels; masked samples become padvals[c].  padvals also fill reads past the end
+ * of the data.  mask == NULL clears the mask (padvals may still be given).          */
+HD_API int hd_set_mask(hd_ctx* ctx, const uint8_t* mask, int32_t numint, int32_t ptsperint,
+                const float* padvals);
+/* Copy nspectra raw spectra (file layout, rows of nchan*nbits/8 bytes) to device
+ * spectra [start, start + nspectra).  Host memory may be pageable or pinned.       */
+HD_API int hd_push_raw(hd_ctx* ctx, const void* spectra, int64_t start, int64_t nspectra);
+/* Fill the device raw block with the synthetic beam (bit-identical to hd_synth_host). */
+HD_API int hd_synth_device(hd_ctx* ctx, const hd_synth* s);
+/* Host generator: spectra [start, start+count) of the same beam into out (file layout).
+ * Needs only the observation geometry; usable without a GPU.                        */
+HD_API int hd_synth_host(const hd_obs* obs, const hd_synth* s, int64_t start, int64_t count,
+                  void* out);
+
+/* Copy device spectra [start, start+count) back to host (file layout). */
+HD_API int hd_get_raw(hd_ctx* ctx, void* out, int64_t start, int64_t count);
+
+/* ---- passes --------------------------------------------------------------------- */
+/* Host-only: the integer tables and subband-level parameters a plan would use, without
+ * a device (chan_delays[nchan], dm_offsets[numdms*nsub]; any output may be NULL).     */
+HD_API int hd_plan_tables(const hd_obs* obs, const hd_opts* opts, const hd_pass* pass,
+                   int32_t* chan_delays, int32_t* dm_offsets,
+                   double* sub_lofreq, double* sub_chanwid, double* sub_dt);
+HD_API int hd_plan_create(hd_ctx* ctx, const hd_pass* pass, hd_plan** out);
+HD_API int hd_plan_destroy(hd_plan* plan);
+/* Integer delay tables: chan_delays[nchan] (stage-1 idispdt, samples at dt) and
+ * dm_offsets[numdms*nsub] (stage-2 offsets, samples at dt*ds).  Either may be NULL. */
+HD_API int hd_plan_get_delays(const hd_plan* plan, int32_t* chan_delays, int32_t* dm_offsets);
+/* Subband-level parameters as written to (and read back from) the .sub.inf file.   */
+HD_API int hd_plan_sub_params(const hd_plan* plan, double* sub_lofreq, double* sub_chanwid,
+                       double* sub_dt, int64_t* nds);
+/* Stage 1: raw (+calib, mask) -> nsub subbands of N/ds samples, kept on device.     */
+HD_API int hd_run_subband(hd_plan* plan);
+/* Subbands device <-> host, layout [nsub][N/ds] of int16 or f32 (opts.sub_dtype).   */
+HD_API int hd_get_subbands(hd_plan* plan, void* host);
+HD_API int hd_set_subbands(hd_plan* plan, const void* host);
+/* Stage 2: subbands -> numdms series of numout f32 samples.  host_out [numdms][numout]
+ * receives them when non-NULL; otherwise they stay resident on the device.          */
+HD_API int hd_run_dedisp(hd_plan* plan, float* host_out);
+/* Device-time of the last hd_run_subband / hd_run_dedisp of this plan, ms.           */
+HD_API int hd_plan_last_ms(const hd_plan* plan, float* ms_subband, float* ms_dedisp);
+/* Kernel variant for stage 2 (0 = auto, 1 = direct/global, 2 = LDS-tiled).          */
+HD_API int hd_plan_set_variant(hd_plan* plan, int32_t variant);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HIPDEDISP_H */

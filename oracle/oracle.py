@@ -1,0 +1,159 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes wrapper of the C oracle (oracle/liboracle*.so).
+
+Imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, as the
+checker.  Parity status: see oracle/oracle.h (PRESTO absent -> pinned by the reference's
+plan code, analytic KATs and an independent numpy restatement, oracle/oracle_np.py).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+class or_obs(ctypes.Structure):
+    _fields_ = [("nchan", ctypes.c_int32), ("nbits", ctypes.c_int32), ("npol", ctypes.c_int32),
+                ("flip", ctypes.c_int32), ("dt", ctypes.c_double), ("lofreq", ctypes.c_double),
+                ("df", ctypes.c_double), ("N", ctypes.c_int64), ("nsblk", ctypes.c_int32),
+                ("_pad0", ctypes.c_int32), ("voverc", ctypes.c_double)]
+
+
+class or_opts(ctypes.Structure):
+    _fields_ = [("sub_dtype", ctypes.c_int32), ("ds_mode", ctypes.c_int32), ("pad_mode", ctypes.c_int32),
+                ("nibble_hi_first", ctypes.c_int32), ("be16", ctypes.c_int32),
+                ("inf_roundtrip", ctypes.c_int32), ("clip_sigma", ctypes.c_float), ("_pad0", ctypes.c_int32)]
+
+
+_libs = {}
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib(omp=False):
+    key = bool(omp)
+    if key not in _libs:
+        path = os.path.join(HERE, "liboracle_omp.so" if omp else "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = ctypes.CDLL(path)
+        vp, i32, i64, d = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
+        P = ctypes.POINTER
+        L.or_chan_delays.argtypes = [P(or_obs), ctypes.c_int, d, P(ctypes.c_int32)]
+        L.or_sub_params.argtypes = [P(or_obs), P(or_opts), ctypes.c_int, ctypes.c_int, P(d), P(d), P(d)]
+        L.or_dm_offsets.argtypes = [P(or_obs), P(or_opts), ctypes.c_int, ctypes.c_int, d, d, ctypes.c_int,
+                                    P(ctypes.c_int32)]
+        L.or_dm_offsets_sub.argtypes = [ctypes.c_int, d, d, d, d, d, d, ctypes.c_int, P(ctypes.c_int32)]
+        L.or_stage1.argtypes = [P(or_obs), P(or_opts), vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, vp,
+                                ctypes.c_int, ctypes.c_int, vp, i64, i64, vp, i64]
+        L.or_stage2.argtypes = [vp, ctypes.c_int, i64, i64, ctypes.c_int, vp, ctypes.c_int, i64, i64, vp, i64]
+        L.or_pad.argtypes = [vp, ctypes.c_int, i64, i64, ctypes.c_int]
+        L.or_pad.restype = None
+        L.or_num_threads.restype = ctypes.c_int
+        L.or_nearest_long.restype = i64
+        L.or_nearest_long.argtypes = [d]
+        L.or_delay_from_dm.restype = d
+        L.or_delay_from_dm.argtypes = [d, d]
+        _libs[key] = L
+    return _libs[key]
+
+
+def _obs(o):
+    return or_obs(nchan=o.nchan, nbits=o.nbits, npol=o.npol, flip=int(bool(o.flip)), dt=o.dt,
+                  lofreq=o.lofreq, df=o.df, N=int(o.N), nsblk=o.nsblk, voverc=o.voverc)
+
+
+def _opts(p):
+    return or_opts(sub_dtype=p.sub_dtype, ds_mode=p.ds_mode, pad_mode=p.pad_mode,
+                   nibble_hi_first=int(p.nibble_hi_first), be16=int(p.be16),
+                   inf_roundtrip=int(p.inf_roundtrip), clip_sigma=p.clip_sigma)
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def chan_delays(obs, nsub, subdm):
+    out = np.zeros(obs.nchan, np.int32)
+    o = _obs(obs)
+    lib().or_chan_delays(ctypes.byref(o), nsub, subdm, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+    return out
+
+
+def sub_params(obs, opts, nsub, ds):
+    a, b, c = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+    o, p = _obs(obs), _opts(opts)
+    lib().or_sub_params(ctypes.byref(o), ctypes.byref(p), nsub, ds, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+    return a.value, b.value, c.value
+
+
+def dm_offsets(obs, opts, nsub, ds, lodm, dmstep, numdms):
+    out = np.zeros((numdms, nsub), np.int32)
+    o, p = _obs(obs), _opts(opts)
+    lib().or_dm_offsets(ctypes.byref(o), ctypes.byref(p), nsub, ds, lodm, dmstep, numdms,
+                        out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+    return out
+
+
+def dm_offsets_sub(nsub, lof, bw, dsdt, lodm, dmstep, numdms, voverc=0.0):
+    out = np.zeros((numdms, nsub), np.int32)
+    lib().or_dm_offsets_sub(nsub, lof, bw, dsdt, voverc, lodm, dmstep, numdms,
+                            out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+    return out
+
+
+def stage1(obs, opts, raw, nsub, ds, subdm, t0=0, count=None, calib=(None, None, None),
+           mask=None, ptsperint=0, padvals=None, omp=False):
+    """Subbands [nsub][count] for output samples [t0, t0+count)."""
+    nds = obs.N // ds
+    if count is None:
+        count = nds - t0
+    idd = chan_delays(obs, nsub, subdm)
+    dt = np.int16 if opts.sub_dtype == 0 else np.float32
+    out = np.zeros((nsub, count), dt)
+    raw = np.ascontiguousarray(raw, np.uint8)
+    cal = [None if c is None else np.ascontiguousarray(c, np.float32) for c in calib]
+    m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+    pv = None if padvals is None else np.ascontiguousarray(padvals, np.float32)
+    o, p = _obs(obs), _opts(opts)
+    rc = lib(omp).or_stage1(ctypes.byref(o), ctypes.byref(p), _ptr(raw), _ptr(cal[0]), _ptr(cal[1]), _ptr(cal[2]),
+                            _ptr(m), 0 if m is None else m.shape[0], int(ptsperint), _ptr(pv), nsub, ds,
+                            _ptr(idd), int(t0), int(count), _ptr(out), int(count))
+    if rc:
+        raise ValueError("or_stage1 rejected its arguments")
+    return out
+
+
+def stage2(sub, off, t0=0, count=None, omp=False):
+    """DM series [numdms][count] for samples [t0, t0+count) (no padding)."""
+    sub = np.ascontiguousarray(sub)
+    nsub, nds = sub.shape
+    numdms = off.shape[0]
+    if count is None:
+        count = nds - t0
+    out = np.zeros((numdms, count), np.float32)
+    sd = 0 if sub.dtype == np.int16 else 1
+    off = np.ascontiguousarray(off, np.int32)
+    lib(omp).or_stage2(_ptr(sub), sd, nds, nds, nsub, _ptr(off), numdms, int(t0), int(count), _ptr(out), int(count))
+    return out
+
+
+def run_pass(obs, opts, raw, pp, calib=(None, None, None), mask=None, ptsperint=0, padvals=None, omp=False):
+    """Full pass -> (subbands [nsub][nds], series [numdms][numout]) exactly as the engine defines it."""
+    nds = obs.N // pp.ds
+    numout = pp.numout if pp.numout > 0 else nds
+    sub = stage1(obs, opts, raw, pp.nsub, pp.ds, pp.subdm, calib=calib, mask=mask, ptsperint=ptsperint,
+                 padvals=padvals, omp=omp)
+    off = dm_offsets(obs, opts, pp.nsub, pp.ds, pp.lodm, pp.dmstep, pp.numdms)
+    out = np.zeros((pp.numdms, numout), np.float32)
+    n = min(numout, nds)
+    out[:, :n] = stage2(sub, off, 0, n, omp=omp)
+    lib(omp).or_pad(_ptr(out), pp.numdms, nds, numout, opts.pad_mode)
+    return sub, out
+
+
+def num_threads(omp=True):
+    return lib(omp).or_num_threads()

@@ -1,0 +1,879 @@
+// hd_api.hip — C ABI of libhipdedisp.so (declared in include/hipdedisp.h).
+//
+// Host side of the engine: observation/mask/calibration state, integer delay tables
+// (double precision, PRESTO NEAREST_LONG), device buffers, launch sequencing and
+// hipEvent timing.  One context = one device + one stream; plans are per DDplan pass.
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "hd_internal.h"
+#include "../../include/hipdedisp.h"
+
+#define HD_VERSION_STR "hipdedisp 0.1.0 (gfx950)"
+
+struct hd_ctx {
+    int device = -1;
+    hipStream_t stream = nullptr;
+    std::string err;
+    bool have_obs = false;
+    hd_obs obs{};
+    hd_opts opts{};
+    int32_t rowbytes = 0;
+    uint8_t* d_raw = nullptr;
+    bool raw_ready = false;
+    float *d_scl = nullptr, *d_offs = nullptr, *d_wts = nullptr;
+    uint8_t* d_mask = nullptr;
+    int32_t numint = 0, ptsperint = 0;
+    float* d_padvals = nullptr;
+    void* d_sub = nullptr;          // shared subband scratch
+    size_t sub_bytes = 0;
+    const hd_plan* sub_owner = nullptr;
+    double* d_partial = nullptr;    // shared per-tile partial sums
+    size_t partial_bytes = 0;
+};
+
+struct hd_plan {
+    hd_ctx* ctx = nullptr;
+    hd_pass pass{};
+    int64_t nds = 0, numout = 0, nvalid = 0;
+    int64_t sub_stride = 0, out_stride = 0;
+    double sub_lofreq = 0, sub_chanwid = 0, sub_dt = 0;
+    std::vector<int32_t> idispdt, off;
+    int32_t maxdelay = 0;
+    int32_t* d_idispdt = nullptr;
+    int32_t* d_off = nullptr;
+    int32_t* d_maxabs = nullptr;
+    // LDS-variant tables
+    int32_t q = 0, dpb = 0, nyblk = 0, wstride = 0;
+    bool lds_ok = false;
+    int32_t* d_omin = nullptr;
+    int32_t* d_boff = nullptr;
+    int32_t variant = 0;
+    float* d_out = nullptr;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    bool ran_sub = false, ran_dd = false;
+};
+
+static thread_local std::string g_err;
+
+static int fail(hd_ctx* ctx, int code, const char* fmt, ...)
+{
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (ctx) ctx->err = buf;
+    g_err = buf;
+    return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                          \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess)                                                                      \
+            return fail((ctx), HD_E_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_),    \
+                        __FILE__, __LINE__);                                                       \
+    } while (0)
+
+static void dfree(void* p)
+{
+    if (p) (void)hipFree(p);
+}
+
+// ---------------------------------------------------------------------------------------
+// delay tables (PRESTO src/dispersion.c semantics; the oracle restates the same rules)
+// ---------------------------------------------------------------------------------------
+static double delay_from_dm(double dm, double f) { return dm / (0.000241 * f * f); }
+static double doppler(double f, double v) { return f * (1.0 + v); }
+static int64_t nearest_long(double x) { return (int64_t)(x < 0 ? ceil(x - 0.5) : floor(x + 0.5)); }
+
+static void dedisp_delays(int n, double dm, double lof, double cw, double v, double* out)
+{
+    for (int i = 0; i < n; i++) out[i] = delay_from_dm(dm, doppler(lof + i * cw, v));
+}
+static void subband_delays(int nchan, int nsub, double dm, double lof, double cw, double v, double* out)
+{
+    const int cps = nchan / nsub;
+    const double sbw = cw * cps;
+    const double losubhi = lof + sbw - cw;
+    dedisp_delays(nsub, dm, losubhi, sbw, v, out);
+}
+
+static double text_roundtrip(double v, const char* fmt)
+{
+    char buf[64];
+    snprintf(buf, sizeof buf, fmt, v);
+    return strtod(buf, nullptr);
+}
+
+static size_t round_up(size_t x, size_t m) { return (x + m - 1) / m * m; }
+
+// ---------------------------------------------------------------------------------------
+// library / context
+// ---------------------------------------------------------------------------------------
+extern "C" const char* hd_version(void) { return HD_VERSION_STR; }
+
+extern "C" void hd_opts_default(hd_opts* o)
+{
+    if (!o) return;
+    memset(o, 0, sizeof *o);
+    o->sub_dtype = HD_SUB_I16;
+    o->ds_mode = HD_DS_SUM;
+    o->pad_mode = HD_PAD_MEAN;
+    o->nibble_hi_first = 1;
+    o->be16 = 1;
+    o->inf_roundtrip = 1;
+    o->clip_sigma = 0.0f;
+}
+
+extern "C" int hd_device_count(int* n)
+{
+    if (!n) return fail(nullptr, HD_E_INVAL, "hd_device_count: n is NULL");
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    *n = (e == hipSuccess) ? c : 0;
+    return HD_OK;
+}
+
+extern "C" int hd_open(int device, hd_ctx** out)
+{
+    if (!out) return fail(nullptr, HD_E_INVAL, "hd_open: out is NULL");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        return fail(nullptr, HD_E_NODEV, "hd_open: no HIP device available");
+    if (device < 0 || device >= n)
+        return fail(nullptr, HD_E_NODEV, "hd_open: device %d out of range (have %d)", device, n);
+    hd_ctx* c = new hd_ctx();
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return fail(nullptr, HD_E_HIP, "hd_open: cannot initialise device %d", device);
+    }
+    *out = c;
+    return HD_OK;
+}
+
+static void free_obs_buffers(hd_ctx* c)
+{
+    dfree(c->d_raw); c->d_raw = nullptr;
+    dfree(c->d_scl); c->d_scl = nullptr;
+    dfree(c->d_offs); c->d_offs = nullptr;
+    dfree(c->d_wts); c->d_wts = nullptr;
+    dfree(c->d_mask); c->d_mask = nullptr;
+    dfree(c->d_padvals); c->d_padvals = nullptr;
+    c->raw_ready = false;
+    c->numint = c->ptsperint = 0;
+}
+
+extern "C" int hd_close(hd_ctx* c)
+{
+    if (!c) return HD_OK;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    free_obs_buffers(c);
+    dfree(c->d_sub);
+    dfree(c->d_partial);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return HD_OK;
+}
+
+extern "C" const char* hd_last_error(const hd_ctx* c) { return c ? c->err.c_str() : g_err.c_str(); }
+
+extern "C" int hd_sync(hd_ctx* c)
+{
+    if (!c) return fail(nullptr, HD_E_INVAL, "hd_sync: NULL context");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return HD_OK;
+}
+
+static int check_obs(hd_ctx* c, const hd_obs* o)
+{
+    if (!o) return fail(c, HD_E_INVAL, "obs is NULL");
+    if (o->nchan <= 0) return fail(c, HD_E_INVAL, "nchan must be > 0 (got %d)", o->nchan);
+    if (o->nbits != 4 && o->nbits != 8 && o->nbits != 16)
+        return fail(c, HD_E_INVAL, "nbits must be 4, 8 or 16 (got %d)", o->nbits);
+    if (o->npol != 1) return fail(c, HD_E_INVAL, "only npol == 1 (summed polarisations) is supported (got %d)", o->npol);
+    if (((int64_t)o->nchan * o->nbits) % 8) return fail(c, HD_E_INVAL, "nchan*nbits must be a whole number of bytes");
+    if (o->N <= 0) return fail(c, HD_E_INVAL, "N must be > 0");
+    if (!(o->dt > 0) || !(o->df > 0) || !(o->lofreq > 0))
+        return fail(c, HD_E_INVAL, "dt, df and lofreq must be > 0");
+    return HD_OK;
+}
+
+extern "C" int hd_set_obs(hd_ctx* c, const hd_obs* o, const hd_opts* opts)
+{
+    if (!c) return fail(nullptr, HD_E_INVAL, "hd_set_obs: NULL context");
+    int rc = check_obs(c, o);
+    if (rc) return rc;
+    hd_opts op;
+    if (opts) op = *opts; else hd_opts_default(&op);
+    if (op.sub_dtype != HD_SUB_I16 && op.sub_dtype != HD_SUB_F32) return fail(c, HD_E_INVAL, "bad sub_dtype");
+    if (op.ds_mode != HD_DS_SUM && op.ds_mode != HD_DS_MEAN) return fail(c, HD_E_INVAL, "bad ds_mode");
+    if (op.pad_mode != HD_PAD_MEAN && op.pad_mode != HD_PAD_ZERO) return fail(c, HD_E_INVAL, "bad pad_mode");
+    if (op.clip_sigma != 0.0f)
+        return fail(c, HD_E_INVAL, "clip_sigma != 0 is not implemented yet (see DESIGN.md, clipping row)");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    free_obs_buffers(c);
+    c->obs = *o;
+    c->opts = op;
+    c->rowbytes = (int32_t)((int64_t)o->nchan * o->nbits / 8);
+    c->have_obs = true;
+    c->sub_owner = nullptr;
+    return HD_OK;
+}
+
+static int ensure_raw(hd_ctx* c)
+{
+    if (c->d_raw) return HD_OK;
+    const size_t bytes = (size_t)c->obs.N * c->rowbytes;
+    if (hipMalloc(&c->d_raw, bytes) != hipSuccess) {
+        c->d_raw = nullptr;
+        return fail(c, HD_E_NOMEM, "cannot allocate %zu bytes of raw data", bytes);
+    }
+    return HD_OK;
+}
+
+static int upload(hd_ctx* c, float** dst, const float* src, size_t n)
+{
+    dfree(*dst);
+    *dst = nullptr;
+    if (!src) return HD_OK;
+    HIPCHK(c, hipMalloc(dst, n * sizeof(float)));
+    HIPCHK(c, hipMemcpy(*dst, src, n * sizeof(float), hipMemcpyHostToDevice));
+    return HD_OK;
+}
+
+extern "C" int hd_set_chan_calib(hd_ctx* c, const float* scl, const float* offs, const float* wts)
+{
+    if (!c) return fail(nullptr, HD_E_INVAL, "hd_set_chan_calib: NULL context");
+    if (!c->have_obs) return fail(c, HD_E_STATE, "hd_set_chan_calib before hd_set_obs");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    int rc;
+    if ((rc = upload(c, &c->d_scl, scl, c->obs.nchan))) return rc;
+    if ((rc = upload(c, &c->d_offs, offs, c->obs.nchan))) return rc;
+    if ((rc = upload(c, &c->d_wts, wts, c->obs.nchan))) return rc;
+    c->sub_owner = nullptr;
+    return HD_OK;
+}
+
+extern "C" int hd_set_mask(hd_ctx* c, const uint8_t* mask, int32_t numint, int32_t ptsperint, const float* padvals)
+{
+    if (!c) return fail(nullptr, HD_E_INVAL, "hd_set_mask: NULL context");
+    if (!c->have_obs) return fail(c, HD_E_STATE, "hd_set_mask before hd_set_obs");
+    if (mask && (numint <= 0 || ptsperint <= 0))
+        return fail(c, HD_E_INVAL, "hd_set_mask: numint and ptsperint must be > 0");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    dfree(c->d_mask);
+    c->d_mask = nullptr;
+    c->numint = c->ptsperint = 0;
+    if (mask) {
+        const size_t n = (size_t)numint * c->obs.nchan;
+        HIPCHK(c, hipMalloc(&c->d_mask, n));
+        HIPCHK(c, hipMemcpy(c->d_mask, mask, n, hipMemcpyHostToDevice));
+        c->numint = numint;
+        c->ptsperint = ptsperint;
+    }
+    int rc = upload(c, &c->d_padvals, padvals, c->obs.nchan);
+    c->sub_owner = nullptr;
+    return rc;
+}
+
+extern "C" int hd_push_raw(hd_ctx* c, const void* spectra, int64_t start, int64_t n)
+{
+    if (!c) return fail(nullptr, HD_E_INVAL, "hd_push_raw: NULL context");
+    if (!c->have_obs) return fail(c, HD_E_STATE, "hd_push_raw before hd_set_obs");
+    if (!spectra || start < 0 || n < 0 || start + n > c->obs.N)
+        return fail(c, HD_E_INVAL, "hd_push_raw: range [%lld, %lld) outside [0, %lld)", (long long)start,
+                    (long long)(start + n), (long long)c->obs.N);
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc = ensure_raw(c);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->d_raw + (size_t)start * c->rowbytes, spectra, (size_t)n * c->rowbytes,
+                             hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->raw_ready = true;
+    c->sub_owner = nullptr;
+    return HD_OK;
+}
+
+extern "C" int hd_get_raw(hd_ctx* c, void* out, int64_t start, int64_t n)
+{
+    if (!c) return fail(nullptr, HD_E_INVAL, "hd_get_raw: NULL context");
+    if (!c->raw_ready || !c->d_raw) return fail(c, HD_E_STATE, "hd_get_raw: no raw data");
+    if (!out || start < 0 || n < 0 || start + n > c->obs.N) return fail(c, HD_E_INVAL, "hd_get_raw: bad range");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpyAsync(out, c->d_raw + (size_t)start * c->rowbytes, (size_t)n * c->rowbytes,
+                             hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return HD_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// synthetic beam
+// ---------------------------------------------------------------------------------------
+extern "C" void hd_synth_default(hd_synth* s)
+{
+    if (!s) return;
+    memset(s, 0, sizeof *s);
+    s->seed = 20261015ull;
+    s->base_level = 96.0f;
+    s->bandpass_slope = 0.25f;
+    s->noise_sigma = 12.0f;
+    s->npsr = 3;
+    s->psr_period[0] = 0.0046;  s->psr_dm[0] = 71.0;  s->psr_width[0] = 0.0004; s->psr_amp[0] = 4.0f;
+    s->psr_period[1] = 0.253;   s->psr_dm[1] = 217.3; s->psr_width[1] = 0.008;  s->psr_amp[1] = 3.0f;
+    s->psr_period[2] = 1.2;     s->psr_dm[2] = 612.0; s->psr_width[2] = 0.03;   s->psr_amp[2] = 3.0f;
+    s->nspulse = 1;
+    s->sp_time[0] = 1.5; s->sp_dm[0] = 350.0; s->sp_width[0] = 0.002; s->sp_amp[0] = 20.0f;
+    s->rfi_nchan = 3;
+    s->rfi_chan[0] = 101; s->rfi_chan[1] = 460; s->rfi_chan[2] = 777;
+    s->rfi_amp = 30.0f;
+    s->burst_frac = 0.01f;
+    s->burst_len = 4096;
+    s->burst_amp = 25.0f;
+    s->spike_frac = 0.0005f;
+    s->spike_amp = 15.0f;
+}
+
+static int64_t fp16(double x) { return (int64_t)llround(x * 65536.0); }
+static uint32_t thresh32(double p)
+{
+    if (!(p > 0)) return 0;
+    if (p >= 1) return 0xFFFFFFFFu;
+    return (uint32_t)(p * 4294967296.0);
+}
+
+static int build_synth_table(const hd_obs* o, const hd_synth* s, std::vector<uint8_t>& buf, std::string& err)
+{
+    if (s->npsr < 0 || s->npsr > HD_SYNTH_MAX_PSR || s->nspulse < 0 || s->nspulse > HD_SYNTH_MAX_PSR ||
+        s->rfi_nchan < 0 || s->rfi_nchan > 8) {
+        err = "synth: bad source counts";
+        return HD_E_INVAL;
+    }
+    const int nchan = o->nchan;
+    buf.assign(hd_synth_tab_bytes(nchan, s->npsr, s->nspulse), 0);
+    hd_synth_tab* tb = (hd_synth_tab*)buf.data();
+    tb->nchan = nchan;
+    tb->nbits = o->nbits;
+    tb->flip = o->flip;
+    tb->npsr = s->npsr;
+    tb->nsp = s->nspulse;
+    tb->burst_len = s->burst_len;
+    tb->N = o->N;
+    tb->seed = s->seed;
+    if (o->nbits == 16) { tb->maxv = 32767; tb->minv = -32768; }
+    else { tb->maxv = (1 << o->nbits) - 1; tb->minv = 0; }
+    tb->burst_thresh = thresh32(s->burst_frac);
+    tb->spike_thresh = thresh32(s->spike_frac);
+    tb->burst_q4 = (int32_t)lround(16.0 * s->burst_amp);
+    tb->spike_q4 = (int32_t)lround(16.0 * s->spike_amp);
+    tb->rfi_q4 = (int32_t)lround(16.0 * s->rfi_amp);
+    const double ftop = o->lofreq + (nchan - 1) * o->df;
+    for (int p = 0; p < s->npsr; p++) {
+        tb->psr_amp_q4[p] = (int32_t)lround(16.0 * s->psr_amp[p]);
+        tb->psr_period_fp[p] = std::max<int64_t>(1, fp16(s->psr_period[p] / o->dt));
+        tb->psr_width_fp[p] = fp16(s->psr_width[p] / o->dt);
+    }
+    for (int p = 0; p < s->nspulse; p++) {
+        tb->sp_amp_q4[p] = (int32_t)lround(16.0 * s->sp_amp[p]);
+        tb->sp_t0_fp[p] = fp16(s->sp_time[p] / o->dt);
+        tb->sp_width_fp[p] = fp16(s->sp_width[p] / o->dt);
+    }
+    const int32_t *cb, *cn, *cr;
+    const int64_t *pd, *sd;
+    hd_synth_arrays(tb, &cb, &cn, &cr, &pd, &sd);
+    int32_t* base_q4 = (int32_t*)cb;
+    int32_t* noise_mul = (int32_t*)cn;
+    int32_t* rfi = (int32_t*)cr;
+    int64_t* psr_delay = (int64_t*)pd;
+    int64_t* sp_delay = (int64_t*)sd;
+    for (int c = 0; c < nchan; c++) {
+        const double x = nchan > 1 ? (double)c / (nchan - 1) - 0.5 : 0.0;
+        base_q4[c] = (int32_t)lround(16.0 * s->base_level * (1.0 + s->bandpass_slope * x));
+        noise_mul[c] = (int32_t)lround(s->noise_sigma / 147.8 * 4096.0);
+        rfi[c] = 0;
+        const double f = o->lofreq + c * o->df;
+        for (int p = 0; p < s->npsr; p++)
+            psr_delay[(size_t)p * nchan + c] =
+                fp16((delay_from_dm(s->psr_dm[p], f) - delay_from_dm(s->psr_dm[p], ftop)) / o->dt);
+        for (int p = 0; p < s->nspulse; p++)
+            sp_delay[(size_t)p * nchan + c] =
+                fp16((delay_from_dm(s->sp_dm[p], f) - delay_from_dm(s->sp_dm[p], ftop)) / o->dt);
+    }
+    for (int i = 0; i < s->rfi_nchan; i++)
+        if (s->rfi_chan[i] >= 0 && s->rfi_chan[i] < nchan) rfi[s->rfi_chan[i]] = 1;
+    return HD_OK;
+}
+
+extern "C" int hd_synth_host(const hd_obs* o, const hd_synth* s, int64_t start, int64_t count, void* out)
+{
+    int rc = check_obs(nullptr, o);
+    if (rc) return rc;
+    if (!s || !out || start < 0 || count < 0 || start + count > o->N)
+        return fail(nullptr, HD_E_INVAL, "hd_synth_host: bad arguments");
+    std::vector<uint8_t> buf;
+    std::string err;
+    if ((rc = build_synth_table(o, s, buf, err))) return fail(nullptr, rc, "%s", err.c_str());
+    const hd_synth_tab* tb = (const hd_synth_tab*)buf.data();
+    const int32_t *cb, *cn, *cr;
+    const int64_t *pd, *sd;
+    hd_synth_arrays(tb, &cb, &cn, &cr, &pd, &sd);
+    const int32_t rowbytes = (int32_t)((int64_t)o->nchan * o->nbits / 8);
+    uint8_t* dst = (uint8_t*)out;
+    unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (count < 4096) nth = 1;
+    std::vector<std::thread> th;
+    for (unsigned k = 0; k < nth; k++) {
+        th.emplace_back([=]() {
+            const int64_t a = count * k / nth, b = count * (k + 1) / nth;
+            for (int64_t t = a; t < b; t++)
+                for (int32_t by = 0; by < rowbytes; by++)
+                    dst[t * rowbytes + by] = hd_synth_byte(tb, cb, cn, cr, pd, sd, start + t, by);
+        });
+    }
+    for (auto& x : th) x.join();
+    return HD_OK;
+}
+
+extern "C" int hd_synth_device(hd_ctx* c, const hd_synth* s)
+{
+    if (!c) return fail(nullptr, HD_E_INVAL, "hd_synth_device: NULL context");
+    if (!c->have_obs) return fail(c, HD_E_STATE, "hd_synth_device before hd_set_obs");
+    if (!s) return fail(c, HD_E_INVAL, "hd_synth_device: synth is NULL");
+    std::vector<uint8_t> buf;
+    std::string err;
+    int rc = build_synth_table(&c->obs, s, buf, err);
+    if (rc) return fail(c, rc, "%s", err.c_str());
+    HIPCHK(c, hipSetDevice(c->device));
+    if ((rc = ensure_raw(c))) return rc;
+    void* d_tab = nullptr;
+    HIPCHK(c, hipMalloc(&d_tab, buf.size()));
+    HIPCHK(c, hipMemcpy(d_tab, buf.data(), buf.size(), hipMemcpyHostToDevice));
+    hipError_t e = hd::launch_synth(c->d_raw, c->obs.N, c->rowbytes, (const hd_synth_tab*)d_tab, c->stream);
+    hipError_t e2 = hipStreamSynchronize(c->stream);
+    (void)hipFree(d_tab);
+    if (e != hipSuccess || e2 != hipSuccess)
+        return fail(c, HD_E_HIP, "synth kernel failed: %s", hipGetErrorString(e != hipSuccess ? e : e2));
+    c->raw_ready = true;
+    c->sub_owner = nullptr;
+    return HD_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// plans
+// ---------------------------------------------------------------------------------------
+static const int kTT = 256, kSC = 8;
+
+static void plan_free(hd_plan* p)
+{
+    dfree(p->d_idispdt);
+    dfree(p->d_off);
+    dfree(p->d_maxabs);
+    dfree(p->d_omin);
+    dfree(p->d_boff);
+    dfree(p->d_out);
+    for (auto& e : p->ev)
+        if (e) (void)hipEventDestroy(e);
+}
+
+struct Tables {
+    std::vector<int32_t> idispdt, off;
+    int32_t maxdelay = 0;
+    double lof = 0, sbw = 0, sdt = 0;
+};
+
+// Validation + integer tables for one pass (shared by hd_plan_create and hd_plan_tables).
+static int compute_tables(hd_ctx* c, const hd_obs& o, const hd_opts& opts, const hd_pass* ps, Tables& T)
+{
+    if (ps->nsub <= 0 || o.nchan % ps->nsub)
+        return fail(c, HD_E_INVAL, "nsub (%d) must divide nchan (%d)", ps->nsub, o.nchan);
+    if (ps->ds < 1) return fail(c, HD_E_INVAL, "ds must be >= 1");
+    if (ps->numdms < 1) return fail(c, HD_E_INVAL, "numdms must be >= 1");
+    if (ps->subdm < 0 || ps->lodm < 0 || ps->lodm + (ps->numdms - 1) * ps->dmstep < 0)
+        return fail(c, HD_E_INVAL, "negative DMs are not supported");
+    if (ps->numout < 0) return fail(c, HD_E_INVAL, "numout must be >= 0");
+    const bool sub_input = (ps->flags & HD_PASS_SUB_INPUT) != 0;
+    if (sub_input && (ps->nsub != o.nchan || ps->ds != 1))
+        return fail(c, HD_E_INVAL, "HD_PASS_SUB_INPUT needs nsub == nchan (%d) and ds == 1", o.nchan);
+    const int nchan = o.nchan, nsub = ps->nsub, cps = nchan / nsub;
+
+    // stage-1 channel delays at subdm (subband_search_delays / dt)
+    std::vector<double> d(nchan), sd(nsub);
+    dedisp_delays(nchan, ps->subdm, o.lofreq, o.df, o.voverc, d.data());
+    subband_delays(nchan, nsub, ps->subdm, o.lofreq, o.df, o.voverc, sd.data());
+    T.idispdt.assign(nchan, 0);
+    T.maxdelay = 0;
+    if (!sub_input)
+        for (int s = 0, ch = 0; s < nsub; s++)
+            for (int k = 0; k < cps; k++, ch++) {
+                T.idispdt[ch] = (int32_t)nearest_long((d[ch] - sd[s]) / o.dt);
+                T.maxdelay = std::max(T.maxdelay, T.idispdt[ch]);
+            }
+
+    // subband-level parameters as carried by the .sub.inf
+    double lof = o.lofreq + o.df * cps - o.df, sbw = o.df * cps, sdt = o.dt * ps->ds;
+    if (sub_input) {   // the .sub.inf values, as read
+        lof = o.lofreq;
+        sbw = o.df;
+        sdt = o.dt;
+    } else if (opts.inf_roundtrip) {
+        lof = text_roundtrip(lof, "%.12g");
+        sbw = text_roundtrip(sbw, "%.12g");
+        sdt = text_roundtrip(sdt, "%.15g");
+    }
+    T.lof = lof;
+    T.sbw = sbw;
+    T.sdt = sdt;
+
+    // stage-2 offsets
+    T.off.resize((size_t)ps->numdms * nsub);
+    for (int i = 0; i < ps->numdms; i++) {
+        const double dm = ps->lodm + i * ps->dmstep;
+        subband_delays(nsub, nsub, dm, lof, sbw, o.voverc, sd.data());
+        const double top = sd[nsub - 1];
+        for (int s = 0; s < nsub; s++) T.off[(size_t)i * nsub + s] = (int32_t)nearest_long((sd[s] - top) / sdt);
+    }
+    return HD_OK;
+}
+
+extern "C" int hd_plan_tables(const hd_obs* o, const hd_opts* opts, const hd_pass* ps, int32_t* chan_delays,
+                              int32_t* dm_offsets, double* sub_lofreq, double* sub_chanwid, double* sub_dt)
+{
+    int rc = check_obs(nullptr, o);
+    if (rc) return rc;
+    if (!ps) return fail(nullptr, HD_E_INVAL, "hd_plan_tables: pass is NULL");
+    hd_opts op;
+    if (opts) op = *opts; else hd_opts_default(&op);
+    Tables T;
+    if ((rc = compute_tables(nullptr, *o, op, ps, T))) return rc;
+    if (chan_delays) memcpy(chan_delays, T.idispdt.data(), sizeof(int32_t) * T.idispdt.size());
+    if (dm_offsets) memcpy(dm_offsets, T.off.data(), sizeof(int32_t) * T.off.size());
+    if (sub_lofreq) *sub_lofreq = T.lof;
+    if (sub_chanwid) *sub_chanwid = T.sbw;
+    if (sub_dt) *sub_dt = T.sdt;
+    return HD_OK;
+}
+
+extern "C" int hd_plan_create(hd_ctx* c, const hd_pass* ps, hd_plan** out)
+{
+    if (!c) return fail(nullptr, HD_E_INVAL, "hd_plan_create: NULL context");
+    if (!ps || !out) return fail(c, HD_E_INVAL, "hd_plan_create: NULL argument");
+    *out = nullptr;
+    if (!c->have_obs) return fail(c, HD_E_STATE, "hd_plan_create before hd_set_obs");
+    const hd_obs& o = c->obs;
+    Tables T;
+    int rc0 = compute_tables(c, o, c->opts, ps, T);
+    if (rc0) return rc0;
+
+    hd_plan* p = new hd_plan();
+    p->ctx = c;
+    p->pass = *ps;
+    p->nds = o.N / ps->ds;
+    p->numout = ps->numout > 0 ? ps->numout : p->nds;
+    p->nvalid = std::min(p->nds, p->numout);
+    p->sub_stride = (int64_t)round_up((size_t)std::max<int64_t>(p->nds, 1), 64);
+    p->out_stride = (int64_t)round_up((size_t)p->numout, 64);
+    const int nchan = o.nchan, nsub = ps->nsub;
+    p->idispdt = std::move(T.idispdt);
+    p->off = std::move(T.off);
+    p->maxdelay = T.maxdelay;
+    p->sub_lofreq = T.lof;
+    p->sub_chanwid = T.sbw;
+    p->sub_dt = T.sdt;
+
+    // LDS-variant tables
+    const int need = (ps->numdms + 3) / 4;
+    p->q = need <= 8 ? 8 : need <= 16 ? 16 : need <= 19 ? 19 : 24;
+    p->dpb = 4 * p->q;
+    p->nyblk = (ps->numdms + p->dpb - 1) / p->dpb;
+    std::vector<int32_t> omin((size_t)p->nyblk * nsub), boff((size_t)p->nyblk * nsub * p->dpb);
+    int32_t maxspan = 0;
+    for (int yb = 0; yb < p->nyblk; yb++)
+        for (int s = 0; s < nsub; s++) {
+            int32_t lo = INT32_MAX, hi = INT32_MIN;
+            for (int k = 0; k < p->dpb; k++) {
+                const int dm = std::min(yb * p->dpb + k, ps->numdms - 1);
+                const int32_t v = p->off[(size_t)dm * nsub + s];
+                lo = std::min(lo, v);
+                hi = std::max(hi, v);
+            }
+            omin[(size_t)yb * nsub + s] = lo;
+            maxspan = std::max(maxspan, hi - lo);
+        }
+    p->wstride = (int32_t)round_up((size_t)(kTT + maxspan + 4), 4);
+    const size_t lds_bytes = (size_t)kSC * 4 * p->wstride * sizeof(int16_t);
+    p->lds_ok = (c->opts.sub_dtype == HD_SUB_I16) && lds_bytes <= 64 * 1024;
+    for (int yb = 0; yb < p->nyblk; yb++)
+        for (int s = 0; s < nsub; s++)
+            for (int k = 0; k < p->dpb; k++) {
+                const int dm = std::min(yb * p->dpb + k, ps->numdms - 1);
+                const int32_t o2 = p->off[(size_t)dm * nsub + s] - omin[(size_t)yb * nsub + s];
+                const int32_t sl = s % kSC;
+                boff[((size_t)yb * nsub + s) * p->dpb + k] = ((sl * 4 + (o2 & 3)) * p->wstride + (o2 & ~3)) * 2;
+            }
+
+    int rc = HD_OK;
+    hipError_t e = hipSetDevice(c->device);
+    if (e == hipSuccess) e = hipMalloc(&p->d_idispdt, sizeof(int32_t) * nchan);
+    if (e == hipSuccess) e = hipMemcpy(p->d_idispdt, p->idispdt.data(), sizeof(int32_t) * nchan, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&p->d_off, sizeof(int32_t) * p->off.size());
+    if (e == hipSuccess) e = hipMemcpy(p->d_off, p->off.data(), sizeof(int32_t) * p->off.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&p->d_maxabs, sizeof(int32_t));
+    if (e == hipSuccess) e = hipMemset(p->d_maxabs, 0, sizeof(int32_t));
+    if (e == hipSuccess) e = hipMalloc(&p->d_omin, sizeof(int32_t) * omin.size());
+    if (e == hipSuccess) e = hipMemcpy(p->d_omin, omin.data(), sizeof(int32_t) * omin.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&p->d_boff, sizeof(int32_t) * boff.size());
+    if (e == hipSuccess) e = hipMemcpy(p->d_boff, boff.data(), sizeof(int32_t) * boff.size(), hipMemcpyHostToDevice);
+    for (int i = 0; i < 4 && e == hipSuccess; i++) e = hipEventCreate(&p->ev[i]);
+    if (e != hipSuccess) {
+        rc = fail(c, HD_E_HIP, "hd_plan_create: %s", hipGetErrorString(e));
+        plan_free(p);
+        delete p;
+        return rc;
+    }
+    *out = p;
+    return HD_OK;
+}
+
+extern "C" int hd_plan_destroy(hd_plan* p)
+{
+    if (!p) return HD_OK;
+    hd_ctx* c = p->ctx;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    if (c->sub_owner == p) c->sub_owner = nullptr;
+    plan_free(p);
+    delete p;
+    return HD_OK;
+}
+
+extern "C" int hd_plan_get_delays(const hd_plan* p, int32_t* chan_delays, int32_t* dm_offsets)
+{
+    if (!p) return fail(nullptr, HD_E_INVAL, "hd_plan_get_delays: NULL plan");
+    if (chan_delays) memcpy(chan_delays, p->idispdt.data(), sizeof(int32_t) * p->idispdt.size());
+    if (dm_offsets) memcpy(dm_offsets, p->off.data(), sizeof(int32_t) * p->off.size());
+    return HD_OK;
+}
+
+extern "C" int hd_plan_sub_params(const hd_plan* p, double* lof, double* cw, double* dt, int64_t* nds)
+{
+    if (!p) return fail(nullptr, HD_E_INVAL, "hd_plan_sub_params: NULL plan");
+    if (lof) *lof = p->sub_lofreq;
+    if (cw) *cw = p->sub_chanwid;
+    if (dt) *dt = p->sub_dt;
+    if (nds) *nds = p->nds;
+    return HD_OK;
+}
+
+extern "C" int hd_plan_set_variant(hd_plan* p, int32_t v)
+{
+    if (!p) return fail(nullptr, HD_E_INVAL, "hd_plan_set_variant: NULL plan");
+    if (v < 0 || v > 2) return fail(p->ctx, HD_E_INVAL, "variant must be 0, 1 or 2");
+    if (v == 2 && !p->lds_ok) return fail(p->ctx, HD_E_INVAL, "LDS variant unavailable for this plan (needs int16 subbands and a window that fits 64 KiB)");
+    p->variant = v;
+    return HD_OK;
+}
+
+static size_t sub_elem(const hd_ctx* c) { return c->opts.sub_dtype == HD_SUB_I16 ? 2 : 4; }
+
+static int ensure_sub(hd_ctx* c, const hd_plan* p)
+{
+    const size_t need = sub_elem(c) * (size_t)p->pass.nsub * (size_t)p->sub_stride;
+    if (c->sub_bytes >= need) return HD_OK;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    dfree(c->d_sub);
+    c->d_sub = nullptr;
+    c->sub_bytes = 0;
+    c->sub_owner = nullptr;
+    if (hipMalloc(&c->d_sub, need) != hipSuccess) {
+        c->d_sub = nullptr;
+        return fail(c, HD_E_NOMEM, "cannot allocate %zu bytes of subbands", need);
+    }
+    c->sub_bytes = need;
+    return HD_OK;
+}
+
+extern "C" int hd_run_subband(hd_plan* p)
+{
+    if (!p) return fail(nullptr, HD_E_INVAL, "hd_run_subband: NULL plan");
+    hd_ctx* c = p->ctx;
+    if (p->pass.flags & HD_PASS_SUB_INPUT)
+        return fail(c, HD_E_STATE, "hd_run_subband: a HD_PASS_SUB_INPUT plan takes hd_set_subbands");
+    if (!c->raw_ready) return fail(c, HD_E_STATE, "hd_run_subband: no raw data (hd_push_raw / hd_synth_device)");
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc = ensure_sub(c, p);
+    if (rc) return rc;
+    hd::Stage1Args a{};
+    a.rd.raw = c->d_raw;
+    a.rd.N = c->obs.N;
+    a.rd.rowbytes = c->rowbytes;
+    a.rd.nchan = c->obs.nchan;
+    a.rd.nbits = c->obs.nbits;
+    a.rd.flip = c->obs.flip;
+    a.rd.nibble_hi_first = c->opts.nibble_hi_first;
+    a.rd.be16 = c->opts.be16;
+    a.rd.scl = c->d_scl;
+    a.rd.offs = c->d_offs;
+    a.rd.wts = c->d_wts;
+    a.rd.mask = c->d_mask;
+    a.rd.numint = c->numint;
+    a.rd.ptsperint = c->ptsperint;
+    a.rd.padvals = c->d_padvals;
+    a.idispdt = p->d_idispdt;
+    a.nsub = p->pass.nsub;
+    a.cps = c->obs.nchan / p->pass.nsub;
+    a.ds = p->pass.ds;
+    a.ds_mode = c->opts.ds_mode;
+    a.sub_dtype = c->opts.sub_dtype;
+    a.maxdelay = p->maxdelay;
+    a.nds = p->nds;
+    a.out_stride = p->sub_stride;
+    a.out = c->d_sub;
+    a.maxabs = p->d_maxabs;
+    HIPCHK(c, hipMemsetAsync(p->d_maxabs, 0, sizeof(int32_t), c->stream));
+    HIPCHK(c, hipEventRecord(p->ev[0], c->stream));
+    HIPCHK(c, hd::launch_stage1_direct(a, c->stream));
+    HIPCHK(c, hipEventRecord(p->ev[1], c->stream));
+    c->sub_owner = p;
+    p->ran_sub = true;
+    return HD_OK;
+}
+
+extern "C" int hd_get_subbands(hd_plan* p, void* host)
+{
+    if (!p || !host) return fail(p ? p->ctx : nullptr, HD_E_INVAL, "hd_get_subbands: NULL argument");
+    hd_ctx* c = p->ctx;
+    if (c->sub_owner != p) return fail(c, HD_E_STATE, "hd_get_subbands: subbands of this plan are not resident");
+    const size_t es = sub_elem(c);
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpy2DAsync(host, es * p->nds, c->d_sub, es * p->sub_stride, es * p->nds, p->pass.nsub,
+                               hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return HD_OK;
+}
+
+extern "C" int hd_set_subbands(hd_plan* p, const void* host)
+{
+    if (!p || !host) return fail(p ? p->ctx : nullptr, HD_E_INVAL, "hd_set_subbands: NULL argument");
+    hd_ctx* c = p->ctx;
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc = ensure_sub(c, p);
+    if (rc) return rc;
+    const size_t es = sub_elem(c);
+    HIPCHK(c, hipMemcpy2DAsync(c->d_sub, es * p->sub_stride, host, es * p->nds, es * p->nds, p->pass.nsub,
+                               hipMemcpyHostToDevice, c->stream));
+    if (c->opts.sub_dtype == HD_SUB_I16) {
+        int32_t m = 0;
+        const int16_t* h = (const int16_t*)host;
+        const size_t n = (size_t)p->pass.nsub * p->nds;
+        for (size_t i = 0; i < n; i++) m = std::max(m, h[i] < 0 ? -(int32_t)h[i] : (int32_t)h[i]);
+        HIPCHK(c, hipMemcpyAsync(p->d_maxabs, &m, sizeof m, hipMemcpyHostToDevice, c->stream));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->sub_owner = p;
+    return HD_OK;
+}
+
+extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
+{
+    if (!p) return fail(nullptr, HD_E_INVAL, "hd_run_dedisp: NULL plan");
+    hd_ctx* c = p->ctx;
+    if (c->sub_owner != p) return fail(c, HD_E_STATE, "hd_run_dedisp: run hd_run_subband (or hd_set_subbands) for this plan first");
+    HIPCHK(c, hipSetDevice(c->device));
+    if (!p->d_out) {
+        const size_t bytes = sizeof(float) * (size_t)p->pass.numdms * p->out_stride;
+        if (hipMalloc(&p->d_out, bytes) != hipSuccess) {
+            p->d_out = nullptr;
+            return fail(c, HD_E_NOMEM, "cannot allocate %zu bytes of DM series", bytes);
+        }
+    }
+    const bool pad = p->numout > p->nds;
+    const int ntiles = (int)((p->nvalid + kTT - 1) / kTT);
+    double* partial = nullptr;
+    if (pad && c->opts.pad_mode == HD_PAD_MEAN) {
+        const size_t need = sizeof(double) * (size_t)p->pass.numdms * std::max(ntiles, 1);
+        if (c->partial_bytes < need) {
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            dfree(c->d_partial);
+            c->d_partial = nullptr;
+            c->partial_bytes = 0;
+            HIPCHK(c, hipMalloc(&c->d_partial, need));
+            c->partial_bytes = need;
+        }
+        partial = c->d_partial;
+    }
+    hd::Stage2Args a{};
+    a.sub = c->d_sub;
+    a.sub_dtype = c->opts.sub_dtype;
+    a.nsub = p->pass.nsub;
+    a.numdms = p->pass.numdms;
+    a.nds = p->nds;
+    a.sub_stride = p->sub_stride;
+    a.nvalid = p->nvalid;
+    a.out = p->d_out;
+    a.out_stride = p->out_stride;
+    a.partial = partial;
+    a.ntiles = ntiles;
+    a.tile = kTT;
+    a.maxabs = p->d_maxabs;
+    a.omin = p->d_omin;
+    a.wstride = p->wstride;
+    a.dms_per_blk = p->dpb;
+    const bool use_lds = p->variant == 2 || (p->variant == 0 && p->lds_ok);
+    HIPCHK(c, hipEventRecord(p->ev[2], c->stream));
+    if (use_lds) {
+        a.off = p->d_boff;
+        HIPCHK(c, hd::launch_stage2_lds(a, p->q, c->stream));
+    } else {
+        a.off = p->d_off;
+        HIPCHK(c, hd::launch_stage2_direct(a, c->stream));
+    }
+    if (pad)
+        HIPCHK(c, hd::launch_pad(p->d_out, p->out_stride, p->pass.numdms, p->nds, p->numout, partial, ntiles,
+                                 c->opts.pad_mode, c->stream));
+    HIPCHK(c, hipEventRecord(p->ev[3], c->stream));
+    p->ran_dd = true;
+    if (host_out) {
+        HIPCHK(c, hipMemcpy2DAsync(host_out, sizeof(float) * p->numout, p->d_out, sizeof(float) * p->out_stride,
+                                   sizeof(float) * p->numout, p->pass.numdms, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    return HD_OK;
+}
+
+extern "C" int hd_plan_last_ms(const hd_plan* p, float* ms_sub, float* ms_dd)
+{
+    if (!p) return fail(nullptr, HD_E_INVAL, "hd_plan_last_ms: NULL plan");
+    hd_ctx* c = p->ctx;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (ms_sub) {
+        *ms_sub = 0.0f;
+        if (p->ran_sub) {
+            HIPCHK(c, hipEventSynchronize(p->ev[1]));
+            HIPCHK(c, hipEventElapsedTime(ms_sub, p->ev[0], p->ev[1]));
+        }
+    }
+    if (ms_dd) {
+        *ms_dd = 0.0f;
+        if (p->ran_dd) {
+            HIPCHK(c, hipEventSynchronize(p->ev[3]));
+            HIPCHK(c, hipEventElapsedTime(ms_dd, p->ev[2], p->ev[3]));
+        }
+    }
+    return HD_OK;
+}

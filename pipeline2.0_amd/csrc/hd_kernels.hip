@@ -1,0 +1,391 @@
+// hd_kernels.hip — CDNA4 (gfx950) kernels of the dedispersion engine.
+//
+//   k_stage1_direct  raw PSRFITS block -> nsub subbands at subdm, downsampled, int16/f32
+//                    (prepsubband -sub; reference PALFA2_presto_search.py:506-511)
+//   k_stage2_direct  subbands -> numdms DM series, one output per thread, global reads
+//   k_stage2_lds     same result; LDS-tiled: 4 shifted copies of each subband window so
+//                    every lane reads 4 consecutive samples with one aligned ds_read_b64,
+//                    packed int16 accumulation (v_pk_add_u16) widened to int32 every G
+//                    subbands (G from the pass's max |subband|, so no wrap is possible)
+//                    (prepsubband -lodm/-dmstep/-numdms; PALFA2_presto_search.py:514-520)
+//   k_pad            per-DM mean (fixed-order reduction of per-tile partials) fill of
+//                    samples [N/ds, numout)
+//   k_synth          synthetic beam, bit-identical to the host generator
+//
+// Arithmetic contract with the oracle (oracle/prepsubband_oracle.c): float sums in the
+// same order from 0.0f, no FP contraction (built with -ffp-contract=off), correctly
+// rounded division; int16 subbands make every stage-2 sum an exact integer, so any
+// summation order (including the packed int16 one) is bit-identical.
+#include "hd_internal.h"
+
+namespace hd {
+
+// ------------------------------------------------------------------------------------
+// stage 1
+// ------------------------------------------------------------------------------------
+
+__device__ __forceinline__ float raw_value(const RawDesc& rd, int64_t t, int c)
+{
+    const int rc = rd.flip ? rd.nchan - 1 - c : c;
+    const uint8_t* row = rd.raw + t * rd.rowbytes;
+    float x;
+    if (rd.nbits == 8) {
+        x = (float)row[rc];
+    } else if (rd.nbits == 4) {
+        const uint8_t b = row[rc >> 1];
+        const bool first = (rc & 1) == 0;
+        const bool hi = rd.nibble_hi_first ? first : !first;
+        x = (float)(hi ? (b >> 4) : (b & 15));
+    } else {
+        const uint8_t* p = row + 2 * rc;
+        const uint16_t u = rd.be16 ? (uint16_t)((p[0] << 8) | p[1]) : (uint16_t)((p[1] << 8) | p[0]);
+        x = (float)(int16_t)u;
+    }
+    if (rd.scl) x = x * rd.scl[rc];
+    if (rd.offs) x = x + rd.offs[rc];
+    if (rd.wts) x = x * rd.wts[rc];
+    return x;
+}
+
+__device__ __forceinline__ float chan_value(const RawDesc& rd, int64_t t, int c)
+{
+    if (t >= rd.N) return rd.padvals ? rd.padvals[c] : 0.0f;
+    if (rd.mask && rd.ptsperint > 0) {
+        const int64_t iv = t / rd.ptsperint;
+        if (iv < rd.numint && rd.mask[iv * rd.nchan + c]) return rd.padvals ? rd.padvals[c] : 0.0f;
+    }
+    return raw_value(rd, t, c);
+}
+
+// PRESTO NEAREST_LONG, saturated to int16.
+__device__ __forceinline__ int16_t quant_i16(float x)
+{
+    const double d = (double)x;
+    double r = d < 0 ? ceil(d - 0.5) : floor(d + 0.5);
+    r = r > 32767.0 ? 32767.0 : r;
+    r = r < -32768.0 ? -32768.0 : r;
+    return (int16_t)r;
+}
+
+__device__ __forceinline__ int wave_max_i32(int v)
+{
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v = max(v, __shfl_xor(v, m, 64));
+    return v;
+}
+
+__global__ __launch_bounds__(256) void k_stage1_direct(Stage1Args a)
+{
+    const int s = blockIdx.y;
+    const int64_t tp = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool valid = tp < a.nds;
+    int amax = 0;
+    if (valid) {
+        float acc = 0.0f;
+        for (int k = 0; k < a.ds; k++) {
+            float sk = 0.0f;
+            const int64_t tb = tp * a.ds + k;
+            for (int cc = 0; cc < a.cps; cc++) {
+                const int c = s * a.cps + cc;
+                sk += chan_value(a.rd, tb + a.idispdt[c], c);
+            }
+            acc += sk;
+        }
+        if (a.ds_mode == 1) acc = acc / (float)a.ds;
+        if (a.sub_dtype == 0) {
+            const int16_t q = quant_i16(acc);
+            ((int16_t*)a.out)[(int64_t)s * a.out_stride + tp] = q;
+            amax = q < 0 ? -(int)q : (int)q;
+        } else {
+            ((float*)a.out)[(int64_t)s * a.out_stride + tp] = acc;
+        }
+    }
+    if (a.sub_dtype == 0 && a.maxabs) {
+        amax = wave_max_i32(amax);
+        if ((threadIdx.x & 63) == 0 && amax > 0) atomicMax(a.maxabs, amax);
+    }
+}
+
+hipError_t launch_stage1_direct(const Stage1Args& a, hipStream_t st)
+{
+    if (a.nds <= 0) return hipSuccess;
+    dim3 grid((unsigned)((a.nds + 255) / 256), (unsigned)a.nsub);
+    hipLaunchKernelGGL(k_stage1_direct, grid, dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------
+// stage 2, direct
+// ------------------------------------------------------------------------------------
+
+__device__ __forceinline__ double block_sum_f64(double v, double* red /* [4] */)
+{
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    double r = 0.0;
+    if (threadIdx.x == 0) r = ((red[0] + red[1]) + red[2]) + red[3];
+    return r;
+}
+
+__global__ __launch_bounds__(256) void k_stage2_direct(Stage2Args a)
+{
+    __shared__ double red[4];
+    const int d = blockIdx.y;
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int32_t* off = a.off + (int64_t)d * a.nsub;
+    float acc = 0.0f;
+    if (t < a.nvalid) {
+        if (a.sub_dtype == 0) {
+            const int16_t* sub = (const int16_t*)a.sub;
+            for (int s = 0; s < a.nsub; s++) {
+                const int64_t idx = t + off[s];
+                const float v = idx < a.nds ? (float)sub[(int64_t)s * a.sub_stride + idx] : 0.0f;
+                acc += v;
+            }
+        } else {
+            const float* sub = (const float*)a.sub;
+            for (int s = 0; s < a.nsub; s++) {
+                const int64_t idx = t + off[s];
+                const float v = idx < a.nds ? sub[(int64_t)s * a.sub_stride + idx] : 0.0f;
+                acc += v;
+            }
+        }
+        a.out[(int64_t)d * a.out_stride + t] = acc;
+    }
+    if (a.partial) {
+        const double tot = block_sum_f64(t < a.nvalid ? (double)acc : 0.0, red);
+        if (threadIdx.x == 0) a.partial[(int64_t)d * a.ntiles + blockIdx.x] = tot;
+    }
+}
+
+hipError_t launch_stage2_direct(const Stage2Args& a, hipStream_t st)
+{
+    if (a.nvalid <= 0) return hipSuccess;
+    dim3 grid((unsigned)((a.nvalid + 255) / 256), (unsigned)a.numdms);
+    hipLaunchKernelGGL(k_stage2_direct, grid, dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------
+// stage 2, LDS-tiled (int16 subbands)
+// ------------------------------------------------------------------------------------
+//
+// Workgroup = 4 waves = one tile of 256 output samples x (4*Q) DMs.  Lane l owns the 4
+// consecutive samples t0+4l .. t0+4l+3; wave w owns DMs d0+wQ .. d0+wQ+Q-1.
+// Subbands are staged SC at a time.  For subband s the workgroup needs samples
+// [t0+omin_s, t0+256+omax_s+3]; LDS keeps 4 copies of that window, copy j shifted by j
+// samples, so the 4 samples at any offset o start 8-byte aligned in copy (o-omin)&3.
+// boff[yblk][s][q'] (host table) is that byte offset, and lane l adds 8*l.
+
+constexpr int kTT = 256;   // output samples per workgroup
+constexpr int kSC = 8;     // subbands per LDS stage
+
+typedef short short2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ int xcd_remap(int b, int nb)
+{
+    const int xcd = b & 7, q = nb >> 3, r = nb & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
+template <int Q>
+__global__ __launch_bounds__(256) void k_stage2_lds(Stage2Args a, const int32_t* __restrict__ boff)
+{
+    extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+    int16_t* lds = (int16_t*)lds_raw;
+
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t t0 = (int64_t)tile * kTT;
+    const int yb = blockIdx.y;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int dpb = a.dms_per_blk;
+    const int dblk0 = yb * dpb;
+    const int ws = a.wstride;
+    const int16_t* sub = (const int16_t*)a.sub;
+    const int32_t* omin = a.omin + (int64_t)yb * a.nsub;
+    const int32_t* bo = boff + (int64_t)yb * a.nsub * dpb + wave * Q;
+
+    int maxabs = *a.maxabs;
+    maxabs = maxabs < 1 ? 1 : maxabs;
+    int G = 32767 / maxabs;
+    G = G < 1 ? 1 : (G > 64 ? 64 : G);
+    G = __builtin_amdgcn_readfirstlane(G);
+
+    int acc32[Q][4];
+    short2v acc16[Q][2];
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) acc32[q][j] = 0;
+        acc16[q][0] = short2v{0, 0};
+        acc16[q][1] = short2v{0, 0};
+    }
+    int gcount = 0;
+    const uint32_t lane_byte = (uint32_t)lane * 8u;
+
+    for (int sc0 = 0; sc0 < a.nsub; sc0 += kSC) {
+        const int nsc = (a.nsub - sc0) < kSC ? (a.nsub - sc0) : kSC;
+        __syncthreads();
+        // ---- fill: element m of subband window -> copies j with i = m - j
+        const int welems = ws + 3;
+        for (int e = threadIdx.x; e < nsc * welems; e += 256) {
+            const int sl = e / welems;
+            const int m = e - sl * welems;
+            const int s = sc0 + sl;
+            const int64_t gi = t0 + omin[s] + m;
+            const int16_t v = gi < a.nds ? sub[(int64_t)s * a.sub_stride + gi] : (int16_t)0;
+            int16_t* base = lds + (sl * 4) * ws;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int i = m - j;
+                if (i >= 0 && i < ws) base[j * ws + i] = v;
+            }
+        }
+        __syncthreads();
+        // ---- accumulate
+        for (int sl = 0; sl < nsc; sl++) {
+            const int32_t* bs = bo + (int64_t)(sc0 + sl) * dpb;
+#pragma unroll
+            for (int q = 0; q < Q; q++) {
+                const uint32_t addr = (uint32_t)bs[q] + lane_byte;
+                const uint2 v = *(const uint2*)(lds_raw + addr);
+                acc16[q][0] += __builtin_bit_cast(short2v, v.x);
+                acc16[q][1] += __builtin_bit_cast(short2v, v.y);
+            }
+            if (++gcount == G) {
+                gcount = 0;
+#pragma unroll
+                for (int q = 0; q < Q; q++) {
+                    acc32[q][0] += acc16[q][0].x;
+                    acc32[q][1] += acc16[q][0].y;
+                    acc32[q][2] += acc16[q][1].x;
+                    acc32[q][3] += acc16[q][1].y;
+                    acc16[q][0] = short2v{0, 0};
+                    acc16[q][1] = short2v{0, 0};
+                }
+            }
+        }
+    }
+    // ---- finish, store, per-tile partial sums
+    const int64_t tl = t0 + 4 * lane;
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+        acc32[q][0] += acc16[q][0].x;
+        acc32[q][1] += acc16[q][0].y;
+        acc32[q][2] += acc16[q][1].x;
+        acc32[q][3] += acc16[q][1].y;
+        const int d = dblk0 + wave * Q + q;
+        if (d < a.numdms && d < dblk0 + dpb) {
+            float* o = a.out + (int64_t)d * a.out_stride + tl;
+            int64_t part = 0;
+            if (tl + 3 < a.nvalid) {
+                *(float4*)o = make_float4((float)acc32[q][0], (float)acc32[q][1], (float)acc32[q][2],
+                                          (float)acc32[q][3]);
+                part = (int64_t)acc32[q][0] + acc32[q][1] + acc32[q][2] + acc32[q][3];
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (tl + j < a.nvalid) {
+                        o[j] = (float)acc32[q][j];
+                        part += acc32[q][j];
+                    }
+            }
+            if (a.partial) {
+#pragma unroll
+                for (int m = 32; m >= 1; m >>= 1) part += __shfl_xor(part, m, 64);
+                if (lane == 0) a.partial[(int64_t)d * a.ntiles + tile] = (double)part;
+            }
+        }
+    }
+}
+
+template <int Q>
+static hipError_t launch_lds_q(const Stage2Args& a, const int32_t* boff, int nyblk, hipStream_t st)
+{
+    const unsigned ntiles = (unsigned)((a.nvalid + kTT - 1) / kTT);
+    const size_t lds = (size_t)kSC * 4 * a.wstride * sizeof(int16_t);
+    hipLaunchKernelGGL(k_stage2_lds<Q>, dim3(ntiles, (unsigned)nyblk), dim3(256), lds, st, a, boff);
+    return hipGetLastError();
+}
+
+// boff is passed through Stage2Args.off for this variant (host-built [nyblk][nsub][4Q]).
+hipError_t launch_stage2_lds(const Stage2Args& a, int q, hipStream_t st)
+{
+    if (a.nvalid <= 0) return hipSuccess;
+    const int nyblk = (a.numdms + a.dms_per_blk - 1) / a.dms_per_blk;
+    switch (q) {
+    case 8: return launch_lds_q<8>(a, a.off, nyblk, st);
+    case 16: return launch_lds_q<16>(a, a.off, nyblk, st);
+    case 19: return launch_lds_q<19>(a, a.off, nyblk, st);
+    case 24: return launch_lds_q<24>(a, a.off, nyblk, st);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// padding
+// ------------------------------------------------------------------------------------
+
+__global__ __launch_bounds__(256) void k_pad(float* out, int64_t out_stride, int64_t nds, int64_t numout,
+                                            const double* partial, int ntiles, int pad_mode)
+{
+    __shared__ double red[256];
+    __shared__ float padv;
+    const int d = blockIdx.x;
+    double s = 0.0;
+    if (pad_mode == 0 && partial)
+        for (int i = threadIdx.x; i < ntiles; i += 256) s += partial[(int64_t)d * ntiles + i];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w >= 1; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) padv = (pad_mode == 0 && nds > 0) ? (float)(red[0] / (double)nds) : 0.0f;
+    __syncthreads();
+    const float v = padv;
+    for (int64_t t = nds + threadIdx.x; t < numout; t += 256) out[(int64_t)d * out_stride + t] = v;
+}
+
+hipError_t launch_pad(float* out, int64_t out_stride, int numdms, int64_t nds, int64_t numout,
+                      const double* partial, int ntiles, int pad_mode, hipStream_t st)
+{
+    if (numout <= nds || numdms <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_pad, dim3((unsigned)numdms), dim3(256), 0, st, out, out_stride, nds, numout,
+                       partial, ntiles, pad_mode);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------
+// synthetic beam
+// ------------------------------------------------------------------------------------
+
+__global__ __launch_bounds__(256) void k_synth(uint8_t* raw, int64_t N, int32_t rowbytes,
+                                              const hd_synth_tab* __restrict__ tb)
+{
+    const int32_t *base_q4, *noise_mul, *rfi_flag;
+    const int64_t *psr_delay, *sp_delay;
+    hd_synth_arrays(tb, &base_q4, &noise_mul, &rfi_flag, &psr_delay, &sp_delay);
+    const int64_t total = N * rowbytes;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+        const int64_t t = i / rowbytes;
+        const int32_t b = (int32_t)(i - t * rowbytes);
+        raw[i] = hd_synth_byte(tb, base_q4, noise_mul, rfi_flag, psr_delay, sp_delay, t, b);
+    }
+}
+
+hipError_t launch_synth(uint8_t* raw, int64_t N, int32_t rowbytes, const hd_synth_tab* tab_dev, hipStream_t st)
+{
+    const int64_t total = N * rowbytes;
+    int64_t nb = (total + 255) / 256;
+    if (nb > 256 * 64) nb = 256 * 64;
+    if (nb < 1) nb = 1;
+    hipLaunchKernelGGL(k_synth, dim3((unsigned)nb), dim3(256), 0, st, raw, N, rowbytes, tab_dev);
+    return hipGetLastError();
+}
+
+}  // namespace hd

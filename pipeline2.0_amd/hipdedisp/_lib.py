@@ -1,0 +1,141 @@
+"""ctypes binding of libhipdedisp.so (the C ABI in include/hipdedisp.h).
+
+The shared library is built in-tree (pipeline2.0_amd/libhipdedisp.so) by
+``__graft_entry__.build()`` / ``make -C pipeline2.0_amd/csrc``.  There is no
+Python or CPU fallback: if the library is missing, importing the engine fails
+loudly (HipDedispUnavailable) instead of silently computing elsewhere.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "libhipdedisp.so")
+
+HD_OK = 0
+HD_E_INVAL = -1
+HD_E_NODEV = -2
+HD_E_HIP = -3
+HD_E_NOMEM = -4
+HD_E_STATE = -5
+HD_E_IO = -6
+
+HD_SUB_I16, HD_SUB_F32 = 0, 1
+HD_DS_SUM, HD_DS_MEAN = 0, 1
+HD_PAD_MEAN, HD_PAD_ZERO = 0, 1
+HD_PASS_SUB_INPUT = 1
+
+ERROR_NAMES = {HD_E_INVAL: "HD_E_INVAL", HD_E_NODEV: "HD_E_NODEV", HD_E_HIP: "HD_E_HIP",
+               HD_E_NOMEM: "HD_E_NOMEM", HD_E_STATE: "HD_E_STATE", HD_E_IO: "HD_E_IO"}
+
+# Every symbol include/hipdedisp.h declares (checked by tests/test_abi.py).
+EXPORTED = [
+    "hd_version", "hd_opts_default", "hd_synth_default", "hd_device_count", "hd_open",
+    "hd_close", "hd_last_error", "hd_sync", "hd_set_obs", "hd_set_chan_calib", "hd_set_mask",
+    "hd_push_raw", "hd_synth_device", "hd_synth_host", "hd_plan_create", "hd_plan_destroy",
+    "hd_plan_get_delays", "hd_plan_sub_params", "hd_run_subband", "hd_get_subbands",
+    "hd_set_subbands", "hd_run_dedisp", "hd_plan_last_ms", "hd_plan_set_variant",
+    "hd_get_raw", "hd_plan_tables",
+]
+
+
+class HipDedispUnavailable(RuntimeError):
+    """libhipdedisp.so could not be loaded (not built, or no ROCm runtime)."""
+
+
+class hd_obs(ctypes.Structure):
+    _fields_ = [("nchan", ctypes.c_int32), ("nbits", ctypes.c_int32), ("npol", ctypes.c_int32),
+                ("flip", ctypes.c_int32), ("dt", ctypes.c_double), ("lofreq", ctypes.c_double),
+                ("df", ctypes.c_double), ("N", ctypes.c_int64), ("nsblk", ctypes.c_int32),
+                ("_pad0", ctypes.c_int32), ("voverc", ctypes.c_double)]
+
+
+class hd_opts(ctypes.Structure):
+    _fields_ = [("sub_dtype", ctypes.c_int32), ("ds_mode", ctypes.c_int32),
+                ("pad_mode", ctypes.c_int32), ("nibble_hi_first", ctypes.c_int32),
+                ("be16", ctypes.c_int32), ("inf_roundtrip", ctypes.c_int32),
+                ("clip_sigma", ctypes.c_float), ("_pad0", ctypes.c_int32)]
+
+
+class hd_pass(ctypes.Structure):
+    _fields_ = [("subdm", ctypes.c_double), ("lodm", ctypes.c_double), ("dmstep", ctypes.c_double),
+                ("numdms", ctypes.c_int32), ("nsub", ctypes.c_int32), ("ds", ctypes.c_int32),
+                ("flags", ctypes.c_int32), ("numout", ctypes.c_int64)]
+
+
+_NPSR = 8
+
+
+class hd_synth(ctypes.Structure):
+    _fields_ = [("seed", ctypes.c_uint64), ("base_level", ctypes.c_float),
+                ("bandpass_slope", ctypes.c_float), ("noise_sigma", ctypes.c_float),
+                ("npsr", ctypes.c_int32), ("nspulse", ctypes.c_int32),
+                ("psr_period", ctypes.c_double * _NPSR), ("psr_dm", ctypes.c_double * _NPSR),
+                ("psr_width", ctypes.c_double * _NPSR), ("psr_amp", ctypes.c_float * _NPSR),
+                ("sp_time", ctypes.c_double * _NPSR), ("sp_dm", ctypes.c_double * _NPSR),
+                ("sp_width", ctypes.c_double * _NPSR), ("sp_amp", ctypes.c_float * _NPSR),
+                ("rfi_nchan", ctypes.c_int32), ("rfi_chan", ctypes.c_int32 * 8),
+                ("rfi_amp", ctypes.c_float), ("burst_frac", ctypes.c_float),
+                ("burst_len", ctypes.c_int32), ("burst_amp", ctypes.c_float),
+                ("spike_frac", ctypes.c_float), ("spike_amp", ctypes.c_float)]
+
+
+_lib = None
+
+
+def load():
+    """Load (once) and return the ctypes handle; raise HipDedispUnavailable if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise HipDedispUnavailable(
+            "%s is not built; run `python -c 'import __graft_entry__ as g; g.build()'` "
+            "or `make -C pipeline2.0_amd/csrc`" % LIB_PATH)
+    try:
+        lib = ctypes.CDLL(LIB_PATH)
+    except OSError as e:
+        raise HipDedispUnavailable("cannot load %s: %s" % (LIB_PATH, e))
+    P = ctypes.POINTER
+    vp, i32, i64, f32p = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, P(ctypes.c_float)
+    sig = {
+        "hd_version": (ctypes.c_char_p, []),
+        "hd_opts_default": (None, [P(hd_opts)]),
+        "hd_synth_default": (None, [P(hd_synth)]),
+        "hd_device_count": (ctypes.c_int, [P(ctypes.c_int)]),
+        "hd_open": (ctypes.c_int, [ctypes.c_int, P(vp)]),
+        "hd_close": (ctypes.c_int, [vp]),
+        "hd_last_error": (ctypes.c_char_p, [vp]),
+        "hd_sync": (ctypes.c_int, [vp]),
+        "hd_set_obs": (ctypes.c_int, [vp, P(hd_obs), P(hd_opts)]),
+        "hd_set_chan_calib": (ctypes.c_int, [vp, f32p, f32p, f32p]),
+        "hd_set_mask": (ctypes.c_int, [vp, P(ctypes.c_uint8), i32, i32, f32p]),
+        "hd_push_raw": (ctypes.c_int, [vp, vp, i64, i64]),
+        "hd_synth_device": (ctypes.c_int, [vp, P(hd_synth)]),
+        "hd_synth_host": (ctypes.c_int, [P(hd_obs), P(hd_synth), i64, i64, vp]),
+        "hd_plan_create": (ctypes.c_int, [vp, P(hd_pass), P(vp)]),
+        "hd_plan_destroy": (ctypes.c_int, [vp]),
+        "hd_plan_get_delays": (ctypes.c_int, [vp, P(ctypes.c_int32), P(ctypes.c_int32)]),
+        "hd_plan_sub_params": (ctypes.c_int, [vp, P(ctypes.c_double), P(ctypes.c_double),
+                                              P(ctypes.c_double), P(ctypes.c_int64)]),
+        "hd_run_subband": (ctypes.c_int, [vp]),
+        "hd_get_subbands": (ctypes.c_int, [vp, vp]),
+        "hd_set_subbands": (ctypes.c_int, [vp, vp]),
+        "hd_run_dedisp": (ctypes.c_int, [vp, f32p]),
+        "hd_plan_last_ms": (ctypes.c_int, [vp, f32p, f32p]),
+        "hd_plan_set_variant": (ctypes.c_int, [vp, i32]),
+        "hd_get_raw": (ctypes.c_int, [vp, vp, i64, i64]),
+        "hd_plan_tables": (ctypes.c_int, [P(hd_obs), P(hd_opts), P(hd_pass), P(ctypes.c_int32),
+                                          P(ctypes.c_int32), P(ctypes.c_double), P(ctypes.c_double),
+                                          P(ctypes.c_double)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def last_error(ctx=None):
+    msg = load().hd_last_error(ctx)
+    return msg.decode() if msg else ""

@@ -1,0 +1,256 @@
+"""Python view of the engine: contexts (one GPU each) and per-pass plans.
+
+Errors are raised as PrestoError, the exception the reference's search driver
+raises when a PRESTO program fails (lib/python/PALFA2_presto_search.py:740-744,
+raised at :123-128), so callers' retry/cleanup semantics are unchanged.
+"""
+import ctypes
+from dataclasses import dataclass, field
+from typing import Optional
+
+import numpy as np
+
+from . import _lib
+from ._lib import hd_obs, hd_opts, hd_pass, hd_synth
+
+
+class PrestoError(Exception):
+    """Error raised when a dedispersion step fails (reference: PALFA2_presto_search.py:740)."""
+
+
+def _check(rc, what, ctx=None):
+    if rc != _lib.HD_OK:
+        raise PrestoError("Execution of command (%s) failed with status (%s)! %s"
+                          % (what, _lib.ERROR_NAMES.get(rc, rc), _lib.last_error(ctx)))
+
+
+@dataclass
+class ObsParams:
+    """Observation parameters (reference: lib/python/formats/psrfits.py:116-134, 210-314)."""
+    nchan: int
+    nbits: int
+    dt: float
+    lofreq: float          # MHz, lowest-frequency channel centre (after flip)
+    df: float              # MHz, > 0
+    N: int
+    nsblk: int = 2048
+    flip: bool = False     # raw channel order descending in frequency
+    npol: int = 1
+    voverc: float = 0.0
+
+    @property
+    def rowbytes(self):
+        return self.nchan * self.nbits // 8
+
+    def to_c(self):
+        return hd_obs(nchan=self.nchan, nbits=self.nbits, npol=self.npol, flip=int(bool(self.flip)),
+                      dt=self.dt, lofreq=self.lofreq, df=self.df, N=int(self.N),
+                      nsblk=self.nsblk, voverc=self.voverc)
+
+
+@dataclass
+class Opts:
+    """PRESTO-semantics switches; defaults mirror the reference's use."""
+    sub_dtype: int = _lib.HD_SUB_I16
+    ds_mode: int = _lib.HD_DS_SUM
+    pad_mode: int = _lib.HD_PAD_MEAN
+    nibble_hi_first: bool = True
+    be16: bool = True
+    inf_roundtrip: bool = True
+    clip_sigma: float = 0.0
+
+    def to_c(self):
+        return hd_opts(sub_dtype=self.sub_dtype, ds_mode=self.ds_mode, pad_mode=self.pad_mode,
+                       nibble_hi_first=int(self.nibble_hi_first), be16=int(self.be16),
+                       inf_roundtrip=int(self.inf_roundtrip), clip_sigma=self.clip_sigma)
+
+
+@dataclass
+class PassParams:
+    """One prepsubband pass (the two calls at PALFA2_presto_search.py:506-520)."""
+    subdm: float
+    lodm: float
+    dmstep: float
+    numdms: int
+    nsub: int
+    ds: int
+    numout: int = 0
+    sub_input: bool = False   # stage-2-only run on .subNN files (obs describes the .sub.inf)
+
+    def to_c(self):
+        return hd_pass(subdm=self.subdm, lodm=self.lodm, dmstep=self.dmstep, numdms=self.numdms,
+                       nsub=self.nsub, ds=self.ds, numout=int(self.numout),
+                       flags=_lib.HD_PASS_SUB_INPUT if self.sub_input else 0)
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    _check(_lib.load().hd_device_count(ctypes.byref(n)), "hd_device_count")
+    return n.value
+
+
+def plan_tables(obs: "ObsParams", opts: "Opts", pp: "PassParams"):
+    """Host-only integer tables of a pass (no device needed):
+    (idispdt [nchan], offsets [numdms][nsub], (sub_lofreq, sub_chanwid, sub_dt))."""
+    L = _lib.load()
+    idd = np.zeros(obs.nchan, np.int32)
+    off = np.zeros((pp.numdms, pp.nsub), np.int32)
+    a, b, c = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+    o, p, q = obs.to_c(), (opts or Opts()).to_c(), pp.to_c()
+    I32 = ctypes.POINTER(ctypes.c_int32)
+    _check(L.hd_plan_tables(ctypes.byref(o), ctypes.byref(p), ctypes.byref(q), idd.ctypes.data_as(I32),
+                            off.ctypes.data_as(I32), ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)),
+           "hd_plan_tables")
+    return idd, off, (a.value, b.value, c.value)
+
+
+def _f32p(a):
+    if a is None:
+        return None
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+class Engine:
+    """One device context (hd_ctx)."""
+
+    def __init__(self, device=0):
+        self._L = _lib.load()
+        self._ctx = ctypes.c_void_p()
+        _check(self._L.hd_open(device, ctypes.byref(self._ctx)), "hd_open(%d)" % device)
+        self.device = device
+        self.obs: Optional[ObsParams] = None
+        self.opts: Optional[Opts] = None
+        self._keep = []
+
+    # -- lifecycle --
+    def close(self):
+        if self._ctx:
+            self._L.hd_close(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _chk(self, rc, what):
+        _check(rc, what, self._ctx)
+
+    def sync(self):
+        self._chk(self._L.hd_sync(self._ctx), "hd_sync")
+
+    # -- observation state --
+    def set_obs(self, obs: ObsParams, opts: Optional[Opts] = None):
+        opts = opts or Opts()
+        o, p = obs.to_c(), opts.to_c()
+        self._chk(self._L.hd_set_obs(self._ctx, ctypes.byref(o), ctypes.byref(p)), "hd_set_obs")
+        self.obs, self.opts = obs, opts
+
+    def set_calib(self, scl=None, offs=None, wts=None):
+        arrs = [None if a is None else np.ascontiguousarray(a, dtype=np.float32) for a in (scl, offs, wts)]
+        self._chk(self._L.hd_set_chan_calib(self._ctx, *[_f32p(a) for a in arrs]), "hd_set_chan_calib")
+
+    def set_mask(self, mask=None, ptsperint=0, padvals=None):
+        m = None
+        numint = 0
+        if mask is not None:
+            mask = np.ascontiguousarray(mask, dtype=np.uint8)
+            numint = mask.shape[0]
+            m = mask.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+        pv = None if padvals is None else np.ascontiguousarray(padvals, dtype=np.float32)
+        self._chk(self._L.hd_set_mask(self._ctx, m, numint, int(ptsperint), _f32p(pv)), "hd_set_mask")
+
+    def push_raw(self, spectra, start=0):
+        a = np.ascontiguousarray(spectra, dtype=np.uint8)
+        n = a.size // self.obs.rowbytes
+        self._chk(self._L.hd_push_raw(self._ctx, a.ctypes.data_as(ctypes.c_void_p), int(start), int(n)),
+                  "hd_push_raw")
+
+    def get_raw(self, start=0, count=None):
+        count = self.obs.N - start if count is None else count
+        out = np.empty((count, self.obs.rowbytes), np.uint8)
+        self._chk(self._L.hd_get_raw(self._ctx, out.ctypes.data_as(ctypes.c_void_p), int(start), int(count)),
+                  "hd_get_raw")
+        return out
+
+    def synth_device(self, synth: hd_synth):
+        self._chk(self._L.hd_synth_device(self._ctx, ctypes.byref(synth)), "hd_synth_device")
+
+    def plan(self, pp: PassParams):
+        return Plan(self, pp)
+
+
+class Plan:
+    """One DDplan pass on a context (hd_plan)."""
+
+    def __init__(self, eng: Engine, pp: PassParams):
+        self.eng, self.pp = eng, pp
+        self._p = ctypes.c_void_p()
+        c = pp.to_c()
+        eng._chk(eng._L.hd_plan_create(eng._ctx, ctypes.byref(c), ctypes.byref(self._p)),
+                 "hd_plan_create(subdm=%.2f)" % pp.subdm)
+        lof, cw, dt, nds = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
+        eng._chk(eng._L.hd_plan_sub_params(self._p, ctypes.byref(lof), ctypes.byref(cw), ctypes.byref(dt),
+                                           ctypes.byref(nds)), "hd_plan_sub_params")
+        self.sub_lofreq, self.sub_chanwid, self.sub_dt, self.nds = lof.value, cw.value, dt.value, nds.value
+        self.numout = pp.numout if pp.numout > 0 else self.nds
+
+    def destroy(self):
+        if self._p:
+            self.eng._L.hd_plan_destroy(self._p)
+            self._p = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            if self._p and self.eng._ctx:
+                self.destroy()
+        except Exception:
+            pass
+
+    def delays(self):
+        nchan = self.eng.obs.nchan
+        idd = np.zeros(nchan, dtype=np.int32)
+        off = np.zeros((self.pp.numdms, self.pp.nsub), dtype=np.int32)
+        self.eng._chk(self.eng._L.hd_plan_get_delays(
+            self._p, idd.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+            off.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))), "hd_plan_get_delays")
+        return idd, off
+
+    def set_variant(self, v):
+        self.eng._chk(self.eng._L.hd_plan_set_variant(self._p, int(v)), "hd_plan_set_variant")
+
+    def run_subband(self):
+        self.eng._chk(self.eng._L.hd_run_subband(self._p), "prepsubband -sub -subdm %.2f" % self.pp.subdm)
+
+    def _sub_dtype(self):
+        return np.int16 if self.eng.opts.sub_dtype == _lib.HD_SUB_I16 else np.float32
+
+    def get_subbands(self):
+        out = np.empty((self.pp.nsub, self.nds), dtype=self._sub_dtype())
+        self.eng._chk(self.eng._L.hd_get_subbands(self._p, out.ctypes.data_as(ctypes.c_void_p)),
+                      "hd_get_subbands")
+        return out
+
+    def set_subbands(self, sub):
+        a = np.ascontiguousarray(sub, dtype=self._sub_dtype())
+        if a.shape != (self.pp.nsub, self.nds):
+            raise PrestoError("subbands must have shape %s, got %s" % ((self.pp.nsub, self.nds), a.shape))
+        self.eng._chk(self.eng._L.hd_set_subbands(self._p, a.ctypes.data_as(ctypes.c_void_p)),
+                      "hd_set_subbands")
+
+    def run_dedisp(self, to_host=True):
+        out = None
+        ptr = None
+        if to_host:
+            out = np.empty((self.pp.numdms, self.numout), dtype=np.float32)
+            ptr = _f32p(out)
+        self.eng._chk(self.eng._L.hd_run_dedisp(self._p, ptr),
+                      "prepsubband -lodm %.2f -dmstep %.2f -numdms %d"
+                      % (self.pp.lodm, self.pp.dmstep, self.pp.numdms))
+        return out
+
+    def last_ms(self):
+        a, b = ctypes.c_float(), ctypes.c_float()
+        self.eng._chk(self.eng._L.hd_plan_last_ms(self._p, ctypes.byref(a), ctypes.byref(b)), "hd_plan_last_ms")
+        return a.value, b.value

@@ -1,0 +1,191 @@
+"""GPU parity: the HIP engine (through the C ABI) against the CPU oracle on the same inputs.
+
+Bar: bit-exact.  Integer delay tables, int16 subbands and every stage-2 sum of int16
+subbands are exact integers; the float stage-1 paths (calibration, fractional mask pad
+values, mean downsampling, f32 subbands) follow the oracle's operation order with FP
+contraction off, so they are bit-exact too.  The only float tolerance in this file is the
+north-star's 1e-5 relative bound, applied to the f32-subband padding mean (a double sum in
+a different association order), see test_stage2_f32_subbands.
+"""
+import numpy as np
+import pytest
+
+import oracle as OR
+from hipdedisp import Opts, PassParams, PrestoError, plan
+from hipdedisp.synth import host_spectra, palfa_obs, palfa_synth, rfifind_ptsperint, synth_mask
+
+pytestmark = pytest.mark.gpu
+
+REL_TOL = 1e-5   # north_star: max relative error per sample for float32 outputs
+
+
+def load_beam(eng, obs, opts=None, synth=None, device_synth=True):
+    eng.set_obs(obs, opts or Opts())
+    s = synth or palfa_synth(nbits=obs.nbits)
+    if device_synth:
+        eng.synth_device(s)
+        raw = host_spectra(obs, s)
+    else:
+        raw = host_spectra(obs, s)
+        eng.push_raw(raw)
+    return raw
+
+
+def test_device_synth_bytes_equal_host(engine):
+    for nbits in (4, 8, 16):
+        obs = palfa_obs(N=6144, nbits=nbits)
+        raw = load_beam(engine, obs)
+        assert np.array_equal(engine.get_raw(), raw), nbits
+
+
+@pytest.mark.parametrize("nbits,flip,ds", [(8, True, 1), (8, False, 2), (4, True, 3), (16, True, 5),
+                                          (8, True, 10), (4, False, 6)])
+def test_stage1_bitexact(engine, nbits, flip, ds):
+    obs = palfa_obs(N=12288, nbits=nbits, flip=flip)
+    raw = load_beam(engine, obs)
+    pp = PassParams(subdm=612.0, lodm=600.0, dmstep=0.5, numdms=8, nsub=96, ds=ds)
+    p = engine.plan(pp)
+    p.run_subband()
+    got = p.get_subbands()
+    want = OR.stage1(obs, Opts(), raw, 96, ds, 612.0)
+    assert np.array_equal(got, want)
+    idd, off = p.delays()
+    assert np.array_equal(idd, OR.chan_delays(obs, 96, 612.0))
+    assert np.array_equal(off, OR.dm_offsets(obs, Opts(), 96, ds, 600.0, 0.5, 8))
+
+
+@pytest.mark.parametrize("sub_dtype,ds_mode", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_stage1_calib_mask_bitexact(engine, sub_dtype, ds_mode):
+    rng = np.random.default_rng(17 + sub_dtype + 2 * ds_mode)
+    obs = palfa_obs(N=16384, nbits=8)
+    opts = Opts(sub_dtype=sub_dtype, ds_mode=ds_mode)
+    raw = load_beam(engine, obs, opts, device_synth=False)
+    scl = rng.uniform(0.5, 2.0, obs.nchan).astype(np.float32)
+    offs = rng.uniform(-20, 20, obs.nchan).astype(np.float32)
+    wts = (rng.random(obs.nchan) > 0.05).astype(np.float32)
+    engine.set_calib(scl, offs, wts)
+    pts = 2048
+    mask, pad = synth_mask(obs, palfa_synth(), pts, frac=0.05)
+    engine.set_mask(mask, pts, pad)
+    p = engine.plan(PassParams(subdm=350.0, lodm=340.0, dmstep=0.3, numdms=4, nsub=96, ds=3))
+    p.run_subband()
+    want = OR.stage1(obs, opts, raw, 96, 3, 350.0, calib=(scl, offs, wts), mask=mask, ptsperint=pts, padvals=pad)
+    assert np.array_equal(p.get_subbands(), want)
+    engine.set_calib()
+    engine.set_mask()
+
+
+@pytest.mark.parametrize("numdms,ds,numout_mode", [(76, 1, "none"), (64, 2, "none"), (76, 3, "pad"),
+                                                   (5, 1, "trunc"), (100, 5, "pad"), (76, 10, "pad")])
+@pytest.mark.parametrize("variant", [1, 2])
+def test_stage2_bitexact(engine, numdms, ds, numout_mode, variant):
+    obs = palfa_obs(N=3 * 8192, nbits=8)
+    raw = load_beam(engine, obs)
+    nds = obs.N // ds
+    numout = {"none": 0, "pad": plan.choose_N(obs.N / ds) if obs.N / ds >= 10000 else nds + 777,
+              "trunc": nds - 1000}[numout_mode]
+    lodm = 534.4 if ds > 1 else 12.3
+    pp = PassParams(subdm=lodm + 19.0, lodm=lodm, dmstep=0.5, numdms=numdms, nsub=96, ds=ds, numout=numout)
+    p = engine.plan(pp)
+    p.set_variant(variant)
+    p.run_subband()
+    got = p.run_dedisp()
+    sub, want = OR.run_pass(obs, Opts(), raw, pp)
+    assert got.shape == want.shape
+    assert np.array_equal(got, want)
+
+
+def test_stage2_f32_subbands(engine):
+    obs = palfa_obs(N=16384, nbits=8)
+    opts = Opts(sub_dtype=1, ds_mode=1)
+    raw = load_beam(engine, obs, opts)
+    pp = PassParams(subdm=230.0, lodm=222.4, dmstep=0.3, numdms=20, nsub=96, ds=2, numout=8192 + 300)
+    p = engine.plan(pp)
+    p.run_subband()
+    got = p.run_dedisp()
+    _, want = OR.run_pass(obs, opts, raw, pp)
+    nds = obs.N // 2
+    assert np.array_equal(got[:, :nds], want[:, :nds])
+    # padding mean: double sums in a different association order -> within REL_TOL
+    np.testing.assert_allclose(got[:, nds:], want[:, nds:], rtol=REL_TOL, atol=0)
+
+
+def test_sub_input_mode_matches_one_shot(engine):
+    """Stage 2 fed from .subNN data (HD_PASS_SUB_INPUT, .sub.inf values) == one-shot pass."""
+    obs = palfa_obs(N=20000, nbits=8)
+    raw = load_beam(engine, obs)
+    pp = PassParams(subdm=454.6, lodm=443.2, dmstep=0.3, numdms=76, nsub=96, ds=3, numout=7000)
+    p = engine.plan(pp)
+    p.run_subband()
+    sub = p.get_subbands()
+    ref = p.run_dedisp()
+    sobs = palfa_obs(N=sub.shape[1], nchan=96, flip=False)
+    sobs.lofreq, sobs.df, sobs.dt = p.sub_lofreq, p.sub_chanwid, p.sub_dt
+    engine.set_obs(sobs, Opts())
+    q = engine.plan(PassParams(subdm=454.6, lodm=443.2, dmstep=0.3, numdms=76, nsub=96, ds=1, numout=7000,
+                               sub_input=True))
+    q.set_subbands(sub)
+    assert np.array_equal(q.run_dedisp(), ref)
+
+
+def test_state_errors(engine):
+    obs = palfa_obs(N=4096, nbits=8)
+    engine.set_obs(obs, Opts())
+    p = engine.plan(PassParams(subdm=10.0, lodm=0.0, dmstep=1.0, numdms=4, nsub=96, ds=1))
+    with pytest.raises(PrestoError, match="no raw data"):
+        p.run_subband()
+    with pytest.raises(PrestoError, match="hd_run_subband"):
+        p.run_dedisp()
+    with pytest.raises(PrestoError, match="nsub"):
+        engine.plan(PassParams(subdm=10.0, lodm=0.0, dmstep=1.0, numdms=4, nsub=97, ds=1))
+    with pytest.raises(PrestoError, match="negative"):
+        engine.plan(PassParams(subdm=10.0, lodm=-5.0, dmstep=1.0, numdms=4, nsub=96, ds=1))
+
+
+def test_c1_config_three_passes_with_mask(engine):
+    """Config 1 (BASELINE.json configs[0]): 960 ch x 2^20 samples, one pass each from DDplan
+    stages 0, 1 and 3 (216 DMs), rfifind-style mask: full-length bit-exact vs the oracle."""
+    N = 1 << 20
+    obs = palfa_obs(N=N, nbits=8)
+    s = palfa_synth()
+    raw = load_beam(engine, obs, synth=s)
+    pts = rfifind_ptsperint(obs.dt)
+    mask, pad = synth_mask(obs, s, pts)
+    engine.set_mask(mask, pts, pad)
+    ps = plan.ddplans_for("pdev")
+    for st, i in ((0, 0), (1, 0), (3, 0)):
+        d = ps[st]
+        pp = PassParams(subdm=float(d.subdmlist[i]), lodm=float(d.lodm_arg(i)), dmstep=float(d.dmstep_arg()),
+                        numdms=d.dmsperpass, nsub=d.numsub, ds=d.sub_downsamp, numout=plan.choose_N(N / d.downsamp))
+        p = engine.plan(pp)
+        p.run_subband()
+        got_sub = p.get_subbands()
+        got = p.run_dedisp()
+        want_sub, want = OR.run_pass(obs, Opts(), raw, pp, mask=mask, ptsperint=pts, padvals=pad, omp=True)
+        assert np.array_equal(got_sub, want_sub), st
+        assert np.array_equal(got, want), st
+        p.destroy()
+    engine.set_mask()
+
+
+def test_injected_single_pulse_recovered(engine):
+    """The DM-350 single pulse of the synthetic beam peaks in the trial nearest DM 350 at the
+    injected arrival sample (top of band), on the full-resolution pass that covers it."""
+    N = 1 << 18
+    obs = palfa_obs(N=N, nbits=8)
+    s = palfa_synth()
+    s.npsr = 0
+    s.sp_time[0], s.sp_dm[0], s.sp_amp[0], s.sp_width[0] = 4.0, 350.0, 20.0, 0.002
+    s.burst_frac, s.spike_frac = 0.0, 0.0
+    load_beam(engine, obs, synth=s)
+    pp = PassParams(subdm=350.0, lodm=340.0, dmstep=0.5, numdms=40, nsub=96, ds=1)
+    p = engine.plan(pp)
+    p.run_subband()
+    out = p.run_dedisp().astype(np.float64)
+    z = (out - np.median(out, axis=1, keepdims=True)) / out.std(axis=1, keepdims=True)
+    d, t = np.unravel_index(np.argmax(z), z.shape)
+    assert abs((pp.lodm + d * pp.dmstep) - 350.0) <= 1.0
+    t0 = int(round(4.0 / obs.dt))
+    w = int(round(0.002 / obs.dt))
+    assert t0 - 2 <= t <= t0 + w + 2
+    assert z[d, t] > 8.0
