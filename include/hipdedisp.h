@@ -179,6 +179,10 @@ HD_API int hd_plan_sub_params(const hd_plan* plan, double* sub_lofreq, double* s
                        double* sub_dt, int64_t* nds);
 /* Stage 1: raw (+calib, mask) -> nsub subbands of N/ds samples, kept on device.     */
 HD_API int hd_run_subband(hd_plan* plan);
+/* Stage 1 for several passes of one DDplan stage (same nsub and ds, same context) with a
+ * single read of the raw block per 32 passes.  Device time of each launch is attributed to
+ * the first plan of its group of 32 (hd_plan_last_ms of the others reports 0).        */
+HD_API int hd_run_subband_multi(hd_plan** plans, int32_t n);
 /* Subbands device <-> host, layout [nsub][N/ds] of int16 or f32 (opts.sub_dtype).   */
 HD_API int hd_get_subbands(hd_plan* plan, void* host);
 HD_API int hd_set_subbands(hd_plan* plan, const void* host);
@@ -187,7 +191,8 @@ HD_API int hd_set_subbands(hd_plan* plan, const void* host);
 HD_API int hd_run_dedisp(hd_plan* plan, float* host_out);
 /* Device-time of the last hd_run_subband / hd_run_dedisp of this plan, ms.           */
 HD_API int hd_plan_last_ms(const hd_plan* plan, float* ms_subband, float* ms_dedisp);
-/* Kernel variant for stage 2 (0 = auto, 1 = direct/global, 2 = LDS-tiled).          */
+/* Kernel variants: (s1 << 8) | s2.  s2: 0 auto, 1 direct, 2 LDS-tiled; s1: 0 auto (tiled,
+ * multi-pass), 1 direct (one thread per subband sample, for cross-checks).           */
 HD_API int hd_plan_set_variant(hd_plan* plan, int32_t variant);
 
 #ifdef __cplusplus

@@ -33,9 +33,7 @@ struct hd_ctx {
     uint8_t* d_mask = nullptr;
     int32_t numint = 0, ptsperint = 0;
     float* d_padvals = nullptr;
-    void* d_sub = nullptr;          // shared subband scratch
-    size_t sub_bytes = 0;
-    const hd_plan* sub_owner = nullptr;
+    size_t lds_attr_set = 64 * 1024;   // dynamic-LDS limit already granted to the tiled kernels
     double* d_partial = nullptr;    // shared per-tile partial sums
     size_t partial_bytes = 0;
 };
@@ -58,6 +56,10 @@ struct hd_plan {
     int32_t* d_boff = nullptr;
     int32_t variant = 0;
     float* d_out = nullptr;
+    void* d_sub = nullptr;          // this pass's subbands [nsub][sub_stride]
+    size_t sub_bytes = 0;
+    bool sub_valid = false;
+    int32_t s1_variant = 0;         // stage 1: 0 auto (tiled), 1 direct
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     bool ran_sub = false, ran_dd = false;
 };
@@ -181,7 +183,6 @@ extern "C" int hd_close(hd_ctx* c)
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     free_obs_buffers(c);
-    dfree(c->d_sub);
     dfree(c->d_partial);
     (void)hipStreamDestroy(c->stream);
     delete c;
@@ -231,7 +232,6 @@ extern "C" int hd_set_obs(hd_ctx* c, const hd_obs* o, const hd_opts* opts)
     c->opts = op;
     c->rowbytes = (int32_t)((int64_t)o->nchan * o->nbits / 8);
     c->have_obs = true;
-    c->sub_owner = nullptr;
     return HD_OK;
 }
 
@@ -266,7 +266,6 @@ extern "C" int hd_set_chan_calib(hd_ctx* c, const float* scl, const float* offs,
     if ((rc = upload(c, &c->d_scl, scl, c->obs.nchan))) return rc;
     if ((rc = upload(c, &c->d_offs, offs, c->obs.nchan))) return rc;
     if ((rc = upload(c, &c->d_wts, wts, c->obs.nchan))) return rc;
-    c->sub_owner = nullptr;
     return HD_OK;
 }
 
@@ -289,7 +288,6 @@ extern "C" int hd_set_mask(hd_ctx* c, const uint8_t* mask, int32_t numint, int32
         c->ptsperint = ptsperint;
     }
     int rc = upload(c, &c->d_padvals, padvals, c->obs.nchan);
-    c->sub_owner = nullptr;
     return rc;
 }
 
@@ -307,7 +305,6 @@ extern "C" int hd_push_raw(hd_ctx* c, const void* spectra, int64_t start, int64_
                              hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->raw_ready = true;
-    c->sub_owner = nullptr;
     return HD_OK;
 }
 
@@ -470,7 +467,6 @@ extern "C" int hd_synth_device(hd_ctx* c, const hd_synth* s)
     if (e != hipSuccess || e2 != hipSuccess)
         return fail(c, HD_E_HIP, "synth kernel failed: %s", hipGetErrorString(e != hipSuccess ? e : e2));
     c->raw_ready = true;
-    c->sub_owner = nullptr;
     return HD_OK;
 }
 
@@ -487,6 +483,7 @@ static void plan_free(hd_plan* p)
     dfree(p->d_omin);
     dfree(p->d_boff);
     dfree(p->d_out);
+    dfree(p->d_sub);
     for (auto& e : p->ev)
         if (e) (void)hipEventDestroy(e);
 }
@@ -656,7 +653,6 @@ extern "C" int hd_plan_destroy(hd_plan* p)
     hd_ctx* c = p->ctx;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    if (c->sub_owner == p) c->sub_owner = nullptr;
     plan_free(p);
     delete p;
     return HD_OK;
@@ -683,7 +679,11 @@ extern "C" int hd_plan_sub_params(const hd_plan* p, double* lof, double* cw, dou
 extern "C" int hd_plan_set_variant(hd_plan* p, int32_t v)
 {
     if (!p) return fail(nullptr, HD_E_INVAL, "hd_plan_set_variant: NULL plan");
-    if (v < 0 || v > 2) return fail(p->ctx, HD_E_INVAL, "variant must be 0, 1 or 2");
+    // bits 0-7: stage-2 variant (0 auto, 1 direct, 2 LDS); bits 8-15: stage-1 (0 auto/tiled, 1 direct)
+    const int32_t v1 = (v >> 8) & 0xFF;
+    v &= 0xFF;
+    if (v < 0 || v > 2 || v1 > 1) return fail(p->ctx, HD_E_INVAL, "variant must be (s1<<8)|s2 with s1 in 0..1, s2 in 0..2");
+    p->s1_variant = v1;
     if (v == 2 && !p->lds_ok) return fail(p->ctx, HD_E_INVAL, "LDS variant unavailable for this plan (needs int16 subbands and a window that fits 64 KiB)");
     p->variant = v;
     return HD_OK;
@@ -691,77 +691,178 @@ extern "C" int hd_plan_set_variant(hd_plan* p, int32_t v)
 
 static size_t sub_elem(const hd_ctx* c) { return c->opts.sub_dtype == HD_SUB_I16 ? 2 : 4; }
 
-static int ensure_sub(hd_ctx* c, const hd_plan* p)
+// Each plan owns its subband block (so one launch can form the subbands of many passes).
+static int ensure_sub(hd_ctx* c, hd_plan* p)
 {
     const size_t need = sub_elem(c) * (size_t)p->pass.nsub * (size_t)p->sub_stride;
-    if (c->sub_bytes >= need) return HD_OK;
+    if (p->d_sub && p->sub_bytes >= need) return HD_OK;
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    dfree(c->d_sub);
-    c->d_sub = nullptr;
-    c->sub_bytes = 0;
-    c->sub_owner = nullptr;
-    if (hipMalloc(&c->d_sub, need) != hipSuccess) {
-        c->d_sub = nullptr;
+    dfree(p->d_sub);
+    p->d_sub = nullptr;
+    p->sub_bytes = 0;
+    if (hipMalloc(&p->d_sub, need) != hipSuccess) {
+        p->d_sub = nullptr;
         return fail(c, HD_E_NOMEM, "cannot allocate %zu bytes of subbands", need);
     }
-    c->sub_bytes = need;
+    p->sub_bytes = need;
+    return HD_OK;
+}
+
+static hd::RawDesc raw_desc(const hd_ctx* c)
+{
+    hd::RawDesc rd{};
+    rd.raw = c->d_raw;
+    rd.N = c->obs.N;
+    rd.rowbytes = c->rowbytes;
+    rd.nchan = c->obs.nchan;
+    rd.nbits = c->obs.nbits;
+    rd.flip = c->obs.flip;
+    rd.nibble_hi_first = c->opts.nibble_hi_first;
+    rd.be16 = c->opts.be16;
+    rd.scl = c->d_scl;
+    rd.offs = c->d_offs;
+    rd.wts = c->d_wts;
+    rd.mask = c->d_mask;
+    rd.numint = c->numint;
+    rd.ptsperint = c->ptsperint;
+    rd.padvals = c->d_padvals;
+    return rd;
+}
+
+// Tiling of the multi-pass stage-1 kernel: sg subbands per workgroup (64*sg threads),
+// `to` outputs per tile, within an LDS budget (64 KiB when that still gives long tiles,
+// up to 160 KiB for strongly downsampled / high-DM passes).
+static bool stage1_tiling(const hd_ctx* c, int nsub, int ds, int dmax, hd::Stage1Multi& a, int& vw)
+{
+    const int nbits = c->obs.nbits, nchan = c->obs.nchan, cps = nchan / nsub;
+    if (c->rowbytes % 4 || !hd::stage1_tiled_supports_cps(cps)) return false;
+    int sg = 0;
+    for (int cand : {8, 4, 2, 1})
+        if (nsub % cand == 0 && ((int64_t)cand * cps * nbits) % 32 == 0) { sg = cand; break; }
+    if (!sg) return false;
+    const int G = sg * cps;
+    const int gbytes = G * nbits / 8;
+    vw = 4;
+    for (int cand : {16, 8}) {
+        // every group's byte offset (g*G or nchan-(g+1)*G channels) and the row pitch must align
+        if (gbytes % cand == 0 && c->rowbytes % cand == 0 && ((int64_t)nchan * nbits / 8) % cand == 0) { vw = cand; break; }
+    }
+    int rs = (gbytes + 3) & ~3;
+    if (((rs / 4) & 1) == 0) rs += 4;
+    int to = 0;
+    for (size_t budget : {(size_t)64 * 1024, (size_t)96 * 1024, (size_t)156 * 1024}) {
+        const int64_t rows_max = (int64_t)((budget - 64) / (size_t)(rs + 4));
+        to = (int)std::min<int64_t>(2048, (rows_max - dmax) / ds);
+        if (to >= 256) break;
+    }
+    if (to < 32) return false;
+    a.sg = sg;
+    a.to = to;
+    a.rs = rs;
+    a.dmax = dmax;
+    a.ngroups = nsub / sg;
+    return true;
+}
+
+static int run_subband_chunk(hd_ctx* c, hd_plan** plans, int n)
+{
+    hd_plan* p0 = plans[0];
+    int dmax = 0;
+    for (int i = 0; i < n; i++) dmax = std::max(dmax, plans[i]->maxdelay);
+    hd::Stage1Multi m{};
+    int vw = 4;
+    const bool tiled = p0->s1_variant != 1 && stage1_tiling(c, p0->pass.nsub, p0->pass.ds, dmax, m, vw);
+    for (int i = 0; i < n; i++) HIPCHK(c, hipMemsetAsync(plans[i]->d_maxabs, 0, sizeof(int32_t), c->stream));
+    HIPCHK(c, hipEventRecord(p0->ev[0], c->stream));
+    if (tiled) {
+        m.rd = raw_desc(c);
+        m.npass = n;
+        m.nsub = p0->pass.nsub;
+        m.cps = c->obs.nchan / p0->pass.nsub;
+        m.ds = p0->pass.ds;
+        m.ds_mode = c->opts.ds_mode;
+        m.sub_dtype = c->opts.sub_dtype;
+        m.nds = p0->nds;
+        m.out_stride = p0->sub_stride;
+        m.ntiles = (int)((p0->nds + m.to - 1) / m.to);
+        for (int i = 0; i < n; i++) {
+            m.dly[i] = plans[i]->d_idispdt;
+            m.out[i] = plans[i]->d_sub;
+            m.maxabs[i] = plans[i]->d_maxabs;
+        }
+        const size_t lds = hd::stage1_tiled_lds_bytes(m);
+        if (lds > c->lds_attr_set) {
+            HIPCHK(c, hd::stage1_tiled_set_lds_limit(lds));
+            c->lds_attr_set = lds;
+        }
+        HIPCHK(c, hd::launch_stage1_tiled(m, vw, c->stream));
+    } else {
+        for (int i = 0; i < n; i++) {
+            hd_plan* p = plans[i];
+            hd::Stage1Args a{};
+            a.rd = raw_desc(c);
+            a.idispdt = p->d_idispdt;
+            a.nsub = p->pass.nsub;
+            a.cps = c->obs.nchan / p->pass.nsub;
+            a.ds = p->pass.ds;
+            a.ds_mode = c->opts.ds_mode;
+            a.sub_dtype = c->opts.sub_dtype;
+            a.maxdelay = p->maxdelay;
+            a.nds = p->nds;
+            a.out_stride = p->sub_stride;
+            a.out = p->d_sub;
+            a.maxabs = p->d_maxabs;
+            HIPCHK(c, hd::launch_stage1_direct(a, c->stream));
+        }
+    }
+    HIPCHK(c, hipEventRecord(p0->ev[1], c->stream));
+    for (int i = 0; i < n; i++) {
+        plans[i]->sub_valid = true;
+        plans[i]->ran_sub = (i == 0);   // the launch's time is attributed to its first plan
+    }
+    return HD_OK;
+}
+
+extern "C" int hd_run_subband_multi(hd_plan** plans, int32_t n)
+{
+    if (!plans || n < 1 || !plans[0]) return fail(nullptr, HD_E_INVAL, "hd_run_subband_multi: no plans");
+    hd_ctx* c = plans[0]->ctx;
+    for (int i = 0; i < n; i++) {
+        hd_plan* p = plans[i];
+        if (!p) return fail(c, HD_E_INVAL, "hd_run_subband_multi: plan %d is NULL", i);
+        if (p->ctx != c) return fail(c, HD_E_INVAL, "hd_run_subband_multi: plans from different contexts");
+        if (p->pass.nsub != plans[0]->pass.nsub || p->pass.ds != plans[0]->pass.ds)
+            return fail(c, HD_E_INVAL, "hd_run_subband_multi: plans must share nsub and ds");
+        if (p->pass.flags & HD_PASS_SUB_INPUT)
+            return fail(c, HD_E_STATE, "hd_run_subband: a HD_PASS_SUB_INPUT plan takes hd_set_subbands");
+    }
+    if (!c->raw_ready) return fail(c, HD_E_STATE, "hd_run_subband: no raw data (hd_push_raw / hd_synth_device)");
+    HIPCHK(c, hipSetDevice(c->device));
+    for (int i = 0; i < n; i++) {
+        int rc = ensure_sub(c, plans[i]);
+        if (rc) return rc;
+    }
+    for (int i0 = 0; i0 < n; i0 += hd::kMaxPass) {
+        int rc = run_subband_chunk(c, plans + i0, std::min(hd::kMaxPass, n - i0));
+        if (rc) return rc;
+    }
     return HD_OK;
 }
 
 extern "C" int hd_run_subband(hd_plan* p)
 {
     if (!p) return fail(nullptr, HD_E_INVAL, "hd_run_subband: NULL plan");
-    hd_ctx* c = p->ctx;
-    if (p->pass.flags & HD_PASS_SUB_INPUT)
-        return fail(c, HD_E_STATE, "hd_run_subband: a HD_PASS_SUB_INPUT plan takes hd_set_subbands");
-    if (!c->raw_ready) return fail(c, HD_E_STATE, "hd_run_subband: no raw data (hd_push_raw / hd_synth_device)");
-    HIPCHK(c, hipSetDevice(c->device));
-    int rc = ensure_sub(c, p);
-    if (rc) return rc;
-    hd::Stage1Args a{};
-    a.rd.raw = c->d_raw;
-    a.rd.N = c->obs.N;
-    a.rd.rowbytes = c->rowbytes;
-    a.rd.nchan = c->obs.nchan;
-    a.rd.nbits = c->obs.nbits;
-    a.rd.flip = c->obs.flip;
-    a.rd.nibble_hi_first = c->opts.nibble_hi_first;
-    a.rd.be16 = c->opts.be16;
-    a.rd.scl = c->d_scl;
-    a.rd.offs = c->d_offs;
-    a.rd.wts = c->d_wts;
-    a.rd.mask = c->d_mask;
-    a.rd.numint = c->numint;
-    a.rd.ptsperint = c->ptsperint;
-    a.rd.padvals = c->d_padvals;
-    a.idispdt = p->d_idispdt;
-    a.nsub = p->pass.nsub;
-    a.cps = c->obs.nchan / p->pass.nsub;
-    a.ds = p->pass.ds;
-    a.ds_mode = c->opts.ds_mode;
-    a.sub_dtype = c->opts.sub_dtype;
-    a.maxdelay = p->maxdelay;
-    a.nds = p->nds;
-    a.out_stride = p->sub_stride;
-    a.out = c->d_sub;
-    a.maxabs = p->d_maxabs;
-    HIPCHK(c, hipMemsetAsync(p->d_maxabs, 0, sizeof(int32_t), c->stream));
-    HIPCHK(c, hipEventRecord(p->ev[0], c->stream));
-    HIPCHK(c, hd::launch_stage1_direct(a, c->stream));
-    HIPCHK(c, hipEventRecord(p->ev[1], c->stream));
-    c->sub_owner = p;
-    p->ran_sub = true;
-    return HD_OK;
+    return hd_run_subband_multi(&p, 1);
 }
 
 extern "C" int hd_get_subbands(hd_plan* p, void* host)
 {
     if (!p || !host) return fail(p ? p->ctx : nullptr, HD_E_INVAL, "hd_get_subbands: NULL argument");
     hd_ctx* c = p->ctx;
-    if (c->sub_owner != p) return fail(c, HD_E_STATE, "hd_get_subbands: subbands of this plan are not resident");
+    if (!p->sub_valid) return fail(c, HD_E_STATE, "hd_get_subbands: no subbands formed for this plan yet");
     const size_t es = sub_elem(c);
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipMemcpy2DAsync(host, es * p->nds, c->d_sub, es * p->sub_stride, es * p->nds, p->pass.nsub,
+    HIPCHK(c, hipMemcpy2DAsync(host, es * p->nds, p->d_sub, es * p->sub_stride, es * p->nds, p->pass.nsub,
                                hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return HD_OK;
@@ -775,7 +876,7 @@ extern "C" int hd_set_subbands(hd_plan* p, const void* host)
     int rc = ensure_sub(c, p);
     if (rc) return rc;
     const size_t es = sub_elem(c);
-    HIPCHK(c, hipMemcpy2DAsync(c->d_sub, es * p->sub_stride, host, es * p->nds, es * p->nds, p->pass.nsub,
+    HIPCHK(c, hipMemcpy2DAsync(p->d_sub, es * p->sub_stride, host, es * p->nds, es * p->nds, p->pass.nsub,
                                hipMemcpyHostToDevice, c->stream));
     if (c->opts.sub_dtype == HD_SUB_I16) {
         int32_t m = 0;
@@ -785,7 +886,7 @@ extern "C" int hd_set_subbands(hd_plan* p, const void* host)
         HIPCHK(c, hipMemcpyAsync(p->d_maxabs, &m, sizeof m, hipMemcpyHostToDevice, c->stream));
     }
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    c->sub_owner = p;
+    p->sub_valid = true;
     return HD_OK;
 }
 
@@ -793,7 +894,7 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
 {
     if (!p) return fail(nullptr, HD_E_INVAL, "hd_run_dedisp: NULL plan");
     hd_ctx* c = p->ctx;
-    if (c->sub_owner != p) return fail(c, HD_E_STATE, "hd_run_dedisp: run hd_run_subband (or hd_set_subbands) for this plan first");
+    if (!p->sub_valid) return fail(c, HD_E_STATE, "hd_run_dedisp: run hd_run_subband (or hd_set_subbands) for this plan first");
     HIPCHK(c, hipSetDevice(c->device));
     if (!p->d_out) {
         const size_t bytes = sizeof(float) * (size_t)p->pass.numdms * p->out_stride;
@@ -818,7 +919,7 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         partial = c->d_partial;
     }
     hd::Stage2Args a{};
-    a.sub = c->d_sub;
+    a.sub = p->d_sub;
     a.sub_dtype = c->opts.sub_dtype;
     a.nsub = p->pass.nsub;
     a.numdms = p->pass.numdms;

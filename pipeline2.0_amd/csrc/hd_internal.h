@@ -31,6 +31,25 @@ struct Stage1Args {
     int32_t* maxabs;          // device int: max |subband value| (i16 path), atomicMax
 };
 
+// Tiled stage 1 over up to kMaxPass passes that share nsub and ds (one DDplan stage):
+// every workgroup copies a raw tile (sg subbands x (to*ds + dmax) spectra) into LDS once
+// and forms the subbands of all its passes from it.
+constexpr int kMaxPass = 32;
+struct Stage1Multi {
+    RawDesc rd;
+    int32_t npass;
+    int32_t nsub, cps, ds, ds_mode, sub_dtype;
+    int64_t nds, out_stride;
+    int32_t sg;               // subbands per workgroup (block = 64*sg threads)
+    int32_t to;               // output samples per tile
+    int32_t dmax;             // max channel delay over the passes
+    int32_t rs;               // LDS bytes per raw row (multiple of 4, odd dword count)
+    int32_t ntiles, ngroups;
+    const int32_t* dly[kMaxPass];   // per-pass idispdt [nchan]
+    void* out[kMaxPass];            // per-pass subbands [nsub][out_stride]
+    int32_t* maxabs[kMaxPass];      // per-pass max |subband|
+};
+
 struct Stage2Args {
     const void* sub;          // [nsub][sub_stride]
     int32_t sub_dtype, nsub, numdms, _pad;
@@ -49,6 +68,10 @@ struct Stage2Args {
 };
 
 hipError_t launch_stage1_direct(const Stage1Args& a, hipStream_t st);
+size_t stage1_tiled_lds_bytes(const Stage1Multi& a);
+hipError_t launch_stage1_tiled(const Stage1Multi& a, int vw, hipStream_t st);
+bool stage1_tiled_supports_cps(int cps);
+hipError_t stage1_tiled_set_lds_limit(size_t bytes);
 hipError_t launch_stage2_direct(const Stage2Args& a, hipStream_t st);
 hipError_t launch_stage2_lds(const Stage2Args& a, int q, hipStream_t st);
 hipError_t launch_pad(float* out, int64_t out_stride, int numdms, int64_t nds, int64_t numout,

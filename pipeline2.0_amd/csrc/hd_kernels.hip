@@ -67,6 +67,14 @@ __device__ __forceinline__ int16_t quant_i16(float x)
     return (int16_t)r;
 }
 
+// Blocks b, b+8, b+16, ... share an XCD (round-robin dispatch; speed only, never
+// correctness): give each XCD a contiguous range of logical block ids (bijective).
+__device__ __forceinline__ int xcd_remap(int b, int nb)
+{
+    const int xcd = b & 7, q = nb >> 3, r = nb & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
 __device__ __forceinline__ int wave_max_i32(int v)
 {
 #pragma unroll
@@ -112,6 +120,297 @@ hipError_t launch_stage1_direct(const Stage1Args& a, hipStream_t st)
     dim3 grid((unsigned)((a.nds + 255) / 256), (unsigned)a.nsub);
     hipLaunchKernelGGL(k_stage1_direct, grid, dim3(256), 0, st, a);
     return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------
+// stage 1, tiled + multi-pass
+// ------------------------------------------------------------------------------------
+//
+// Workgroup = 64*sg threads = one time tile of `to` output samples x sg subbands
+// (G = sg*cps channels, contiguous in the raw row for either band order).
+//  fill : raw rows [to*ds*tile, +to*ds+dmax) of the group's G channels are copied verbatim
+//         into LDS (16/8/4-byte global loads, dword LDS stores, row stride rs with an odd
+//         dword count so the per-row byte reads below are bank-conflict-free at ds = 1);
+//  form : wave w owns subband sl = w, so its CPS channel delays, calibration and zap flags
+//         are wave-uniform registers; lane l owns outputs l, l+64, ...  For every pass the
+//         decoded samples are summed in the oracle's order (k outer, channel inner, from
+//         0.0f), quantised and stored coalesced.
+// Mask: on real data a tile (<= ~1.5k spectra) lies inside one rfifind interval
+// (ptsperint ~ 32k), so each channel is either zapped for the whole tile (its samples are
+// the constant pad value: one add, no LDS read) or not: mode FAST.  Tiles that straddle an
+// interval boundary (mode TWO: per-row select between two flags), tiny test intervals
+// (mode GEN: per-row interval table) and the last tile (reads past the end = pad) take
+// per-sample paths.
+
+constexpr int kModeFast = 0, kModeTwo = 1, kModeGen = 2;
+
+template <int NBITS>
+__device__ __forceinline__ float lds_decode(const uint8_t* p, int lrc, int nibble_hi_first, int be16)
+{
+    if (NBITS == 8) {
+        return (float)p[0];
+    } else if (NBITS == 4) {
+        const uint8_t b = p[0];
+        const bool first = (lrc & 1) == 0;
+        const bool hi = nibble_hi_first ? first : !first;
+        return (float)(hi ? (b >> 4) : (b & 15));
+    } else {
+        const uint16_t w = *(const uint16_t*)p;   // file bytes p[0], p[1]
+        const uint16_t u = be16 ? (uint16_t)((w << 8) | (w >> 8)) : w;
+        return (float)(int16_t)u;
+    }
+}
+
+// Per-channel, wave-uniform state of one subband for one pass.
+template <int CPS>
+struct SubState {
+    int off[CPS];      // LDS byte offset of (row 0 + delay, channel) for this channel
+    int dly[CPS];      // channel delay (rows)
+    float scl[CPS], offs[CPS], wts[CPS], pad[CPS];
+    int zap[CPS];      // FAST: 1 = whole tile zapped;  TWO: bit0 first interval, bit1 second
+};
+
+template <int NBITS, int CPS, bool CALIB, int MODE, bool TAIL>
+__device__ __forceinline__ void form_outputs(const Stage1Multi& a, const uint8_t* lraw, const SubState<CPS>& st,
+                                             const int* livr, int c_first, int64_t brow, int64_t rows_valid,
+                                             int64_t tO0, int lane, int s, int p, int& amax)
+{
+    for (int j = lane; j < a.to; j += 64) {
+        const int64_t tp = tO0 + j;
+        if (tp >= a.nds) break;
+        const int jrow = j * a.ds;
+        float acc = 0.0f;
+        for (int k = 0; k < a.ds; k++) {
+            const uint8_t* rowp = lraw + (jrow + k) * a.rs;
+            float sk = 0.0f;
+#pragma unroll
+            for (int cc = 0; cc < CPS; cc++) {
+                float x;
+                if (MODE == kModeFast && !TAIL && st.zap[cc]) {
+                    x = st.pad[cc];
+                } else {
+                    x = lds_decode<NBITS>(rowp + st.off[cc], c_first + cc, a.rd.nibble_hi_first, a.rd.be16);
+                    if (CALIB) {
+                        x = x * st.scl[cc];
+                        x = x + st.offs[cc];
+                        x = x * st.wts[cc];
+                    }
+                    const int row = jrow + k + st.dly[cc];
+                    if (MODE == kModeFast) {
+                        if (st.zap[cc]) x = st.pad[cc];
+                    } else if (MODE == kModeTwo) {
+                        const int bit = row < brow ? 1 : 2;
+                        if (st.zap[cc] & bit) x = st.pad[cc];
+                    } else {
+                        const int iv = livr[row];
+                        if (iv < a.rd.numint && a.rd.mask[(int64_t)iv * a.rd.nchan + st.zap[cc]]) x = st.pad[cc];
+                    }
+                    if (TAIL && row >= rows_valid) x = st.pad[cc];
+                }
+                sk += x;
+            }
+            acc += sk;
+        }
+        if (a.ds_mode == 1) acc = acc / (float)a.ds;
+        if (a.sub_dtype == 0) {
+            const int16_t q = quant_i16(acc);
+            ((int16_t*)a.out[p])[(int64_t)s * a.out_stride + tp] = q;
+            amax = max(amax, q < 0 ? -(int)q : (int)q);
+        } else {
+            ((float*)a.out[p])[(int64_t)s * a.out_stride + tp] = acc;
+        }
+    }
+}
+
+template <int NBITS, int CPS, bool CALIB, int VW>
+__global__ __launch_bounds__(512) void k_stage1_tiled(Stage1Multi a)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int G = a.sg * CPS;
+    const int logical = xcd_remap(blockIdx.x, gridDim.x);
+    const int tile = logical / a.ngroups;
+    const int g = logical - tile * a.ngroups;
+    const int64_t tO0 = (int64_t)tile * a.to;
+    const int64_t tR0 = tO0 * a.ds;
+    const int rows = a.to * a.ds + a.dmax;
+    const int c0 = g * G;
+    const int rc_lo = a.rd.flip ? a.rd.nchan - c0 - G : c0;
+    const int gbytes = G * NBITS / 8;
+    const int64_t boff = (int64_t)rc_lo * NBITS / 8;
+    uint8_t* lraw = (uint8_t*)smem;
+    int* livr = (int*)(smem + ((rows * a.rs + 15) & ~15));
+
+    // ---- tile mode (uniform)
+    int mode = kModeFast;
+    int64_t iv0 = 0, brow = 0;
+    if (a.rd.mask) {
+        iv0 = tR0 / a.rd.ptsperint;
+        const int64_t iv_last = (tR0 + rows - 1) / a.rd.ptsperint;
+        brow = (iv0 + 1) * a.rd.ptsperint - tR0;
+        mode = iv_last == iv0 ? kModeFast : (iv_last == iv0 + 1 ? kModeTwo : kModeGen);
+        if (mode == kModeGen)
+            for (int r = threadIdx.x; r < rows; r += blockDim.x) livr[r] = (int)((tR0 + r) / a.rd.ptsperint);
+    }
+    const int64_t rows_valid = a.rd.N - tR0;
+    const bool tail = rows_valid < rows;
+
+    // ---- fill: VW-byte global loads, dword LDS stores
+    {
+        const int vpr = gbytes / VW;                 // vectors per row
+        const int nthr = blockDim.x;
+        int r = threadIdx.x / vpr, w = threadIdx.x - (threadIdx.x / vpr) * vpr;
+        const int dr = nthr / vpr, dw = nthr - dr * vpr;
+        for (; r < rows; r += dr) {
+            const int64_t t = tR0 + r;
+            uint32_t v[VW / 4];
+#pragma unroll
+            for (int i = 0; i < VW / 4; i++) v[i] = 0;
+            if (t < a.rd.N) {
+                const uint8_t* src = a.rd.raw + t * a.rd.rowbytes + boff + VW * w;
+                if constexpr (VW == 16) {
+                    const uint4 x = *(const uint4*)src;
+                    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+                } else if constexpr (VW == 8) {
+                    const uint2 x = *(const uint2*)src;
+                    v[0] = x.x; v[1] = x.y;
+                } else {
+                    v[0] = *(const uint32_t*)src;
+                }
+            }
+            uint32_t* dst = (uint32_t*)(lraw + r * a.rs + VW * w);
+#pragma unroll
+            for (int i = 0; i < VW / 4; i++) dst[i] = v[i];
+            w += dw;
+            if (w >= vpr) { w -= vpr; r++; }
+        }
+    }
+    __syncthreads();
+
+    const int sl = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave = subband
+    const int lane = threadIdx.x & 63;
+    const int s = g * a.sg + sl;
+    const int cl0 = sl * CPS;
+    SubState<CPS> st;
+#pragma unroll
+    for (int cc = 0; cc < CPS; cc++) {
+        const int c = c0 + cl0 + cc;
+        const int rc = a.rd.flip ? a.rd.nchan - 1 - c : c;
+        if (CALIB) {
+            st.scl[cc] = a.rd.scl ? a.rd.scl[rc] : 1.0f;
+            st.offs[cc] = a.rd.offs ? a.rd.offs[rc] : 0.0f;
+            st.wts[cc] = a.rd.wts ? a.rd.wts[rc] : 1.0f;
+        }
+        st.pad[cc] = a.rd.padvals ? a.rd.padvals[c] : 0.0f;
+        int z = 0;
+        if (a.rd.mask) {
+            if (mode == kModeGen) {
+                z = c;   // GEN mode looks the mask up per row; keep the channel index here
+            } else {
+                const int z0 = iv0 < a.rd.numint ? a.rd.mask[iv0 * a.rd.nchan + c] : 0;
+                const int z1 = iv0 + 1 < a.rd.numint ? a.rd.mask[(iv0 + 1) * a.rd.nchan + c] : 0;
+                z = mode == kModeFast ? z0 : (z0 ? 1 : 0) | (z1 ? 2 : 0);
+            }
+        }
+        st.zap[cc] = z;
+    }
+    const int lrc0 = a.rd.flip ? G - 1 - cl0 : cl0;   // local raw index of channel cc=0
+    for (int p = 0; p < a.npass; p++) {
+#pragma unroll
+        for (int cc = 0; cc < CPS; cc++) {
+            const int lrc = a.rd.flip ? lrc0 - cc : lrc0 + cc;
+            st.dly[cc] = a.dly[p][c0 + cl0 + cc];
+            st.off[cc] = st.dly[cc] * a.rs + lrc * NBITS / 8;
+        }
+        int amax = 0;
+        if (!tail) {
+            if (mode == kModeFast)
+                form_outputs<NBITS, CPS, CALIB, kModeFast, false>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax);
+            else if (mode == kModeTwo)
+                form_outputs<NBITS, CPS, CALIB, kModeTwo, false>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax);
+            else
+                form_outputs<NBITS, CPS, CALIB, kModeGen, false>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax);
+        } else {
+            if (mode == kModeFast)
+                form_outputs<NBITS, CPS, CALIB, kModeFast, true>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax);
+            else if (mode == kModeTwo)
+                form_outputs<NBITS, CPS, CALIB, kModeTwo, true>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax);
+            else
+                form_outputs<NBITS, CPS, CALIB, kModeGen, true>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax);
+        }
+        if (a.sub_dtype == 0) {
+            amax = wave_max_i32(amax);
+            if (lane == 0 && amax > 0) atomicMax(a.maxabs[p], amax);
+        }
+    }
+}
+
+size_t stage1_tiled_lds_bytes(const Stage1Multi& a)
+{
+    const int rows = a.to * a.ds + a.dmax;
+    size_t b = ((size_t)rows * a.rs + 15) & ~(size_t)15;
+    b += (size_t)rows * sizeof(int);     // GEN-mode row -> interval table
+    return b;
+}
+
+template <int NBITS, int CPS, bool CALIB>
+static hipError_t launch_s1(const Stage1Multi& a, int vw, size_t lds, hipStream_t st)
+{
+    const dim3 grid((unsigned)(a.ntiles * a.ngroups)), block((unsigned)(64 * a.sg));
+    if (vw == 16) hipLaunchKernelGGL((k_stage1_tiled<NBITS, CPS, CALIB, 16>), grid, block, lds, st, a);
+    else if (vw == 8) hipLaunchKernelGGL((k_stage1_tiled<NBITS, CPS, CALIB, 8>), grid, block, lds, st, a);
+    else hipLaunchKernelGGL((k_stage1_tiled<NBITS, CPS, CALIB, 4>), grid, block, lds, st, a);
+    return hipGetLastError();
+}
+
+template <int NBITS, int CPS, bool CALIB>
+static hipError_t set_lds_cps(int bytes)
+{
+    hipError_t e;
+    if ((e = hipFuncSetAttribute((const void*)k_stage1_tiled<NBITS, CPS, CALIB, 16>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes)) != hipSuccess) return e;
+    if ((e = hipFuncSetAttribute((const void*)k_stage1_tiled<NBITS, CPS, CALIB, 8>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes)) != hipSuccess) return e;
+    return hipFuncSetAttribute((const void*)k_stage1_tiled<NBITS, CPS, CALIB, 4>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
+
+#define HD_S1_FOR_CPS(X) X(10) X(8) X(16) X(1)
+
+bool stage1_tiled_supports_cps(int cps) { return cps == 10 || cps == 8 || cps == 16 || cps == 1; }
+
+hipError_t stage1_tiled_set_lds_limit(size_t bytes)
+{
+    hipError_t e = hipSuccess;
+    const int b = (int)bytes;
+#define HD_SET(C)                                                                 \
+    if (e == hipSuccess) e = set_lds_cps<8, C, false>(b);                          \
+    if (e == hipSuccess) e = set_lds_cps<8, C, true>(b);                           \
+    if (e == hipSuccess) e = set_lds_cps<4, C, false>(b);                          \
+    if (e == hipSuccess) e = set_lds_cps<4, C, true>(b);                           \
+    if (e == hipSuccess) e = set_lds_cps<16, C, false>(b);                         \
+    if (e == hipSuccess) e = set_lds_cps<16, C, true>(b);
+    HD_S1_FOR_CPS(HD_SET)
+#undef HD_SET
+    return e;
+}
+
+hipError_t launch_stage1_tiled(const Stage1Multi& a, int vw, hipStream_t st)
+{
+    if (a.nds <= 0 || a.npass <= 0) return hipSuccess;
+    const size_t lds = stage1_tiled_lds_bytes(a);
+    const bool calib = a.rd.scl || a.rd.offs || a.rd.wts;
+#define HD_DISPATCH(C)                                                                                      \
+    if (a.cps == C) {                                                                                       \
+        switch (a.rd.nbits) {                                                                               \
+        case 8: return calib ? launch_s1<8, C, true>(a, vw, lds, st) : launch_s1<8, C, false>(a, vw, lds, st);   \
+        case 4: return calib ? launch_s1<4, C, true>(a, vw, lds, st) : launch_s1<4, C, false>(a, vw, lds, st);   \
+        case 16: return calib ? launch_s1<16, C, true>(a, vw, lds, st) : launch_s1<16, C, false>(a, vw, lds, st);\
+        default: return hipErrorInvalidValue;                                                               \
+        }                                                                                                   \
+    }
+    HD_S1_FOR_CPS(HD_DISPATCH)
+#undef HD_DISPATCH
+    return hipErrorInvalidValue;
 }
 
 // ------------------------------------------------------------------------------------
@@ -185,11 +484,6 @@ constexpr int kSC = 8;     // subbands per LDS stage
 
 typedef short short2v __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ int xcd_remap(int b, int nb)
-{
-    const int xcd = b & 7, q = nb >> 3, r = nb & 7;
-    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
-}
 
 template <int Q>
 __global__ __launch_bounds__(256) void k_stage2_lds(Stage2Args a, const int32_t* __restrict__ boff)

@@ -180,6 +180,12 @@ class Engine:
     def plan(self, pp: PassParams):
         return Plan(self, pp)
 
+    def run_subband_multi(self, plans):
+        """Stage 1 of several passes of one DDplan stage from one read of the raw block."""
+        arr = (ctypes.c_void_p * len(plans))(*[p._p.value for p in plans])
+        self._chk(self._L.hd_run_subband_multi(arr, len(plans)),
+                  "prepsubband -sub (x%d passes)" % len(plans))
+
 
 class Plan:
     """One DDplan pass on a context (hd_plan)."""

@@ -1,0 +1,183 @@
+"""Drop-in replacement for the dedispersion stage of PALFA2_presto_search.search_job().
+
+Reference (pipeline2.0, lib/python/PALFA2_presto_search.py):
+  :444-465  set_up_job: obs_info(filenms) + tempdir in config.processing.base_tmp_dir
+  :494-529  for ddplan in job.ddplans: for passnum: two `prepsubband` calls via
+            timed_execute(), accumulating job.subbanding_time / job.dedispersing_time
+  :531-537  per-DM names  <tempdir>/<base>_DM<dm %.2f>.dat/.inf
+  :352-358  the two timers go to the .report
+
+`run_pass(job, ddplan, passnum, maskfilenm, tempdir)` replaces the body of :500-529 one for
+one: it leaves the same .dat/.inf files (and, with keep_subbands, the same .subNN/.sub.inf
+files) and returns (t_sub, t_dd) wall seconds, which it also adds to the job's timers.
+Failures raise PrestoError, the reference's exception for a failed prepsubband.
+`dedisperse_job(job, per_dm=None)` is the whole loop of :494-537, calling `per_dm(job,
+dmstr, basenm)` where the reference runs single_pulse_search/realfft/accelsearch.
+"""
+import os
+import socket
+import tempfile
+import time
+
+import numpy as np
+
+from . import plan as P
+from .engine import Engine, Opts, PassParams, PrestoError
+from .formats import psrfits
+from .formats.inf import InfoData
+from .formats.mask import read_mask
+from .formats.series import write_dats, write_subbands
+
+
+class DedispJob:
+    """The part of obs_info (PALFA2_presto_search.py:231-294) the dedispersion stage uses."""
+
+    def __init__(self, filenms, resultsdir=".", tmpdir_base=None, device=0, opts=None,
+                 use_subbands=True, keep_subbands=False, backend=None, voverc=0.0):
+        self.filenms = list(filenms)
+        self.filenmstr = " ".join(self.filenms)
+        self.outputdir = resultsdir
+        base = os.path.split(self.filenms[0])[1]
+        self.basefilenm = base[:-5] if base.endswith(".fits") else base
+        self.specinfo = psrfits.SpectraInfo(self.filenms)
+        si = self.specinfo
+        self.backend = backend or si.backend
+        self.MJD = si.start_MJD[0]
+        self.ra_string, self.dec_string = si.ra_str, si.dec_str
+        self.orig_N = si.N                      # float64, as in the reference
+        self.dt = si.dt
+        self.BW = si.BW
+        self.N = self.orig_N
+        self.T = self.N * self.dt
+        self.nchan = si.num_channels
+        self.samp_per_row = si.spectra_per_subint
+        self.fctr = si.fctr
+        self.baryv = voverc                     # TEMPO barycentring is out of scope: -nobary equivalent
+        self.hostname = socket.gethostname()
+        self.use_subbands = use_subbands
+        self.keep_subbands = keep_subbands
+        self.subbanding_time = 0.0
+        self.dedispersing_time = 0.0
+        self.ddplans = P.ddplans_for(self.backend)
+        self.tempdir = tempfile.mkdtemp(suffix="_tmp", prefix=self.basefilenm,
+                                        dir=tmpdir_base or ("/dev/shm" if os.path.isdir("/dev/shm") else None))
+        self.workdir = os.getcwd()
+        self.opts = opts or Opts()
+        self.engine = None
+        self.device = device
+        self._mask_loaded = None
+
+    # -- engine state ------------------------------------------------------------------
+    def open_engine(self):
+        if self.engine is None:
+            self.engine = Engine(self.device)
+            self.obs = self.specinfo.obs_params(self.baryv)
+            self.engine.set_obs(self.obs, self.opts)
+            scl, offs, wts = self.specinfo.read_calib()
+            if scl is not None or offs is not None or wts is not None:
+                self.engine.set_calib(scl, offs, wts)
+            self.engine.push_raw(self.specinfo.read_spectra())
+        return self.engine
+
+    def load_mask(self, maskfilenm):
+        if maskfilenm == self._mask_loaded:
+            return
+        eng = self.open_engine()
+        if maskfilenm and os.path.exists(maskfilenm):
+            m = read_mask(maskfilenm)
+            if m.numchan != self.nchan:
+                raise PrestoError("mask %s has %d channels, data %d" % (maskfilenm, m.numchan, self.nchan))
+            padvals = self._padvals(maskfilenm)
+            eng.set_mask(m.bitmap, m.ptsperint, padvals)
+        else:
+            eng.set_mask(None, 0, None)
+        self._mask_loaded = maskfilenm
+
+    def _padvals(self, maskfilenm):
+        """rfifind pad values [PRESTO-ext]: per-channel levels from <base>_rfifind.stats when
+        present; this build reads a plain-text side file `<mask>.padvals` (one float per
+        channel) if it exists, else uses 0 (mask row)."""
+        side = maskfilenm + ".padvals"
+        if os.path.exists(side):
+            return np.loadtxt(side, dtype=np.float32)
+        return None
+
+    def close(self):
+        if self.engine is not None:
+            self.engine.close()
+            self.engine = None
+
+    def info_template(self, nsub, lofreq, chanwid, dt):
+        return InfoData(name="", telescope=self.specinfo.telescope or "Arecibo",
+                        instrument=self.backend, object=self.specinfo.source or "Unknown",
+                        ra=self.ra_string, dec=self.dec_string, observer=self.specinfo.observer or "Unknown",
+                        mjd=float(self.MJD), bary=0, dt=dt, freq=lofreq, freqband=nsub * chanwid,
+                        num_chan=nsub, chan_wid=chanwid)
+
+
+def pass_params(job, ddplan, passnum):
+    """The parameters of the two prepsubband command lines (PALFA2_presto_search.py:506-520),
+    parsed the way prepsubband parses them (DM strings are "%.2f" text)."""
+    return PassParams(subdm=float(ddplan.subdmlist[passnum]), lodm=float(ddplan.lodm_arg(passnum)),
+                      dmstep=float(ddplan.dmstep_arg()), numdms=ddplan.dmsperpass, nsub=ddplan.numsub,
+                      ds=ddplan.sub_downsamp * (1 if job.use_subbands else ddplan.dd_downsamp),
+                      numout=P.choose_N(job.orig_N / ddplan.downsamp))
+
+
+def run_pass(job, ddplan, passnum, maskfilenm, tempdir):
+    """PALFA2_presto_search.py:498-529 for one pass: subbands (stage 1) then the DM sweep
+    (stage 2); writes <tempdir>/<base>_DM<dm>.dat/.inf; returns (t_sub, t_dd)."""
+    if not job.use_subbands:
+        raise PrestoError("use_subbands=False (PALFA2_presto_search.py:522-529) is not built yet")
+    subbasenm = "%s_DM%s" % (job.basefilenm, ddplan.subdmlist[passnum])
+    eng = job.open_engine()
+    job.load_mask(maskfilenm)
+    pp = pass_params(job, ddplan, passnum)
+    plan = eng.plan(pp)
+    try:
+        t0 = time.time()
+        plan.run_subband()
+        eng.sync()
+        if job.keep_subbands:
+            os.makedirs(os.path.join(tempdir, "subbands"), exist_ok=True)
+            info = job.info_template(pp.nsub, plan.sub_lofreq, plan.sub_chanwid, plan.sub_dt)
+            info.name, info.dm, info.N = subbasenm, pp.subdm, plan.nds
+            write_subbands(os.path.join(tempdir, "subbands", subbasenm), plan.get_subbands(), info)
+        t_sub = time.time() - t0
+        t0 = time.time()
+        series = plan.run_dedisp(to_host=True)
+        info = job.info_template(pp.nsub, plan.sub_lofreq, plan.sub_chanwid, plan.sub_dt)
+        write_dats(os.path.join(tempdir, job.basefilenm), ddplan.dmlist[passnum], series, info, plan.nds)
+        t_dd = time.time() - t0
+    finally:
+        plan.destroy()
+    job.subbanding_time += t_sub
+    job.dedispersing_time += t_dd
+    return t_sub, t_dd
+
+
+def dedisperse_job(job, maskfilenm=None, per_dm=None, remove_dat=False):
+    """The loop of PALFA2_presto_search.py:494-537: every pass of every DDplan stage, then
+    `per_dm(job, dmstr, basenm)` for each new DM (the reference's downstream tools)."""
+    dmstrs = []
+    for ddplan in job.ddplans:
+        for passnum in range(ddplan.numpasses):
+            run_pass(job, ddplan, passnum, maskfilenm, job.tempdir)
+            for dmstr in ddplan.dmlist[passnum]:
+                dmstrs.append(dmstr)
+                basenm = os.path.join(job.tempdir, job.basefilenm + "_DM" + dmstr)
+                if per_dm is not None:
+                    per_dm(job, dmstr, basenm)
+                if remove_dat:
+                    try:
+                        os.remove(basenm + ".dat")
+                    except OSError:
+                        pass
+    return dmstrs
+
+
+def report_lines(job, total_time):
+    """The two .report lines of the stage (PALFA2_presto_search.py:352-358)."""
+    tt = total_time if total_time > 0 else 1.0
+    return ["       subbanding time = %7.1f sec (%5.2f%%)" % (job.subbanding_time, job.subbanding_time / tt * 100.0),
+            "     dedispersing time = %7.1f sec (%5.2f%%)" % (job.dedispersing_time, job.dedispersing_time / tt * 100.0)]

@@ -40,11 +40,13 @@ def test_device_synth_bytes_equal_host(engine):
 
 @pytest.mark.parametrize("nbits,flip,ds", [(8, True, 1), (8, False, 2), (4, True, 3), (16, True, 5),
                                           (8, True, 10), (4, False, 6)])
-def test_stage1_bitexact(engine, nbits, flip, ds):
-    obs = palfa_obs(N=12288, nbits=nbits, flip=flip)
+@pytest.mark.parametrize("s1", [0, 1])
+def test_stage1_bitexact(engine, nbits, flip, ds, s1):
+    obs = palfa_obs(N=12288 + 37, nbits=nbits, flip=flip)
     raw = load_beam(engine, obs)
     pp = PassParams(subdm=612.0, lodm=600.0, dmstep=0.5, numdms=8, nsub=96, ds=ds)
     p = engine.plan(pp)
+    p.set_variant(s1 << 8)
     p.run_subband()
     got = p.get_subbands()
     want = OR.stage1(obs, Opts(), raw, 96, ds, 612.0)
@@ -93,6 +95,29 @@ def test_stage2_bitexact(engine, numdms, ds, numout_mode, variant):
     sub, want = OR.run_pass(obs, Opts(), raw, pp)
     assert got.shape == want.shape
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("mask_pts", [0, 256, 32768])
+def test_stage1_multipass_bitexact(engine, mask_pts):
+    """One launch forms the subbands of many passes (a DDplan stage) from one raw read;
+    every pass must equal its own oracle run.  mask_pts=256 takes the per-row interval path,
+    32768 the two-interval path."""
+    obs = palfa_obs(N=40000, nbits=8)
+    s = palfa_synth()
+    raw = load_beam(engine, obs, synth=s)
+    mask = pad = None
+    if mask_pts:
+        mask, pad = synth_mask(obs, s, mask_pts, frac=0.05)
+        engine.set_mask(mask, mask_pts, pad)
+    d = plan.ddplans_for("pdev")[1]     # 12 passes, ds 2
+    pps = [PassParams(subdm=float(d.subdmlist[i]), lodm=float(d.lodm_arg(i)), dmstep=d.dmstep,
+                      numdms=d.dmsperpass, nsub=96, ds=d.sub_downsamp) for i in range(d.numpasses)]
+    plans = [engine.plan(pp) for pp in pps]
+    engine.run_subband_multi(plans)
+    for pp, p in zip(pps, plans):
+        want = OR.stage1(obs, Opts(), raw, 96, pp.ds, pp.subdm, mask=mask, ptsperint=mask_pts, padvals=pad)
+        assert np.array_equal(p.get_subbands(), want), pp.subdm
+    engine.set_mask()
 
 
 def test_stage2_f32_subbands(engine):
@@ -182,7 +207,11 @@ def test_injected_single_pulse_recovered(engine):
     p = engine.plan(pp)
     p.run_subband()
     out = p.run_dedisp().astype(np.float64)
-    z = (out - np.median(out, axis=1, keepdims=True)) / out.std(axis=1, keepdims=True)
+    _, off = p.delays()
+    out = out[:, : p.nds - int(off.max()) - 1]          # drop the tail whose reads run past the end
+    med = np.median(out, axis=1, keepdims=True)
+    mad = 1.4826 * np.median(np.abs(out - med), axis=1, keepdims=True)
+    z = (out - med) / mad
     d, t = np.unravel_index(np.argmax(z), z.shape)
     assert abs((pp.lodm + d * pp.dmstep) - 350.0) <= 1.0
     t0 = int(round(4.0 / obs.dt))
