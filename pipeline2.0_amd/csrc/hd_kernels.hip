@@ -142,7 +142,7 @@ hipError_t launch_stage1_direct(const Stage1Args& a, hipStream_t st)
 // (mode GEN: per-row interval table) and the last tile (reads past the end = pad) take
 // per-sample paths.
 
-constexpr int kModeFast = 0, kModeTwo = 1, kModeGen = 2;
+constexpr int kModeFast = 0, kModeTwo = 1, kModeGen = 2, kModeClean = 3;
 
 template <int NBITS>
 __device__ __forceinline__ float lds_decode(const uint8_t* p, int lrc, int nibble_hi_first, int be16)
@@ -172,12 +172,13 @@ struct SubState {
 
 template <int NBITS, int CPS, bool CALIB, int MODE, bool TAIL>
 __device__ __forceinline__ void form_outputs(const Stage1Multi& a, const uint8_t* lraw, const SubState<CPS>& st,
-                                             const int* livr, int c_first, int64_t brow, int64_t rows_valid,
+                                             const int* livr, int c_first, int brow, int rows_valid,
                                              int64_t tO0, int lane, int s, int p, int& amax)
 {
-    for (int j = lane; j < a.to; j += 64) {
+    // uniform trip count; only the last iteration can diverge
+    const int jmax = (int)min((int64_t)a.to, a.nds - tO0);
+    for (int j = lane; j < jmax; j += 64) {
         const int64_t tp = tO0 + j;
-        if (tp >= a.nds) break;
         const int jrow = j * a.ds;
         float acc = 0.0f;
         for (int k = 0; k < a.ds; k++) {
@@ -185,27 +186,31 @@ __device__ __forceinline__ void form_outputs(const Stage1Multi& a, const uint8_t
             float sk = 0.0f;
 #pragma unroll
             for (int cc = 0; cc < CPS; cc++) {
-                float x;
-                if (MODE == kModeFast && !TAIL && st.zap[cc]) {
-                    x = st.pad[cc];
-                } else {
-                    x = lds_decode<NBITS>(rowp + st.off[cc], c_first + cc, a.rd.nibble_hi_first, a.rd.be16);
-                    if (CALIB) {
-                        x = x * st.scl[cc];
-                        x = x + st.offs[cc];
-                        x = x * st.wts[cc];
-                    }
+                // branch-free: every sample is read and decoded, then selected
+                float x = lds_decode<NBITS>(rowp + st.off[cc], c_first + cc, a.rd.nibble_hi_first, a.rd.be16);
+                // keep the read unconditional: otherwise hipcc sinks it under a uniform
+                // branch on the zap flag and splits the channel loop into CPS basic blocks
+                if (MODE != kModeClean) asm volatile("" : "+v"(x));
+                if (CALIB) {
+                    x = x * st.scl[cc];
+                    x = x + st.offs[cc];
+                    x = x * st.wts[cc];
+                }
+                if (MODE == kModeFast) {
+                    x = st.zap[cc] ? st.pad[cc] : x;
+                } else if (MODE == kModeTwo) {
                     const int row = jrow + k + st.dly[cc];
-                    if (MODE == kModeFast) {
-                        if (st.zap[cc]) x = st.pad[cc];
-                    } else if (MODE == kModeTwo) {
-                        const int bit = row < brow ? 1 : 2;
-                        if (st.zap[cc] & bit) x = st.pad[cc];
-                    } else {
-                        const int iv = livr[row];
-                        if (iv < a.rd.numint && a.rd.mask[(int64_t)iv * a.rd.nchan + st.zap[cc]]) x = st.pad[cc];
-                    }
-                    if (TAIL && row >= rows_valid) x = st.pad[cc];
+                    const int bit = row < brow ? 1 : 2;
+                    x = (st.zap[cc] & bit) ? st.pad[cc] : x;
+                } else if (MODE == kModeGen) {
+                    const int row = jrow + k + st.dly[cc];
+                    const int iv = livr[row];
+                    if (a.rd.mask && iv < a.rd.numint && a.rd.mask[(int64_t)iv * a.rd.nchan + st.zap[cc]])
+                        x = st.pad[cc];
+                }   // kModeClean: no mask logic at all
+                if (TAIL) {
+                    const int row = jrow + k + st.dly[cc];
+                    x = row >= rows_valid ? st.pad[cc] : x;
                 }
                 sk += x;
             }
@@ -242,16 +247,17 @@ __global__ __launch_bounds__(512) void k_stage1_tiled(Stage1Multi a)
 
     // ---- tile mode (uniform)
     int mode = kModeFast;
-    int64_t iv0 = 0, brow = 0;
+    int64_t iv0 = 0;
+    int brow = 0;
     if (a.rd.mask) {
         iv0 = tR0 / a.rd.ptsperint;
         const int64_t iv_last = (tR0 + rows - 1) / a.rd.ptsperint;
-        brow = (iv0 + 1) * a.rd.ptsperint - tR0;
+        brow = (int)min((iv0 + 1) * a.rd.ptsperint - tR0, (int64_t)rows);
         mode = iv_last == iv0 ? kModeFast : (iv_last == iv0 + 1 ? kModeTwo : kModeGen);
         if (mode == kModeGen)
             for (int r = threadIdx.x; r < rows; r += blockDim.x) livr[r] = (int)((tR0 + r) / a.rd.ptsperint);
     }
-    const int64_t rows_valid = a.rd.N - tR0;
+    const int rows_valid = (int)min(a.rd.N - tR0, (int64_t)rows);
     const bool tail = rows_valid < rows;
 
     // ---- fill: VW-byte global loads, dword LDS stores
@@ -291,6 +297,7 @@ __global__ __launch_bounds__(512) void k_stage1_tiled(Stage1Multi a)
     const int s = g * a.sg + sl;
     const int cl0 = sl * CPS;
     SubState<CPS> st;
+    int any_zap = 0;
 #pragma unroll
     for (int cc = 0; cc < CPS; cc++) {
         const int c = c0 + cl0 + cc;
@@ -312,6 +319,7 @@ __global__ __launch_bounds__(512) void k_stage1_tiled(Stage1Multi a)
             }
         }
         st.zap[cc] = z;
+        any_zap |= z;
     }
     const int lrc0 = a.rd.flip ? G - 1 - cl0 : cl0;   // local raw index of channel cc=0
     for (int p = 0; p < a.npass; p++) {
@@ -323,7 +331,9 @@ __global__ __launch_bounds__(512) void k_stage1_tiled(Stage1Multi a)
         }
         int amax = 0;
         if (!tail) {
-            if (mode == kModeFast)
+            if (mode == kModeFast && !any_zap)
+                form_outputs<NBITS, CPS, CALIB, kModeClean, false>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax);
+            else if (mode == kModeFast)
                 form_outputs<NBITS, CPS, CALIB, kModeFast, false>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax);
             else if (mode == kModeTwo)
                 form_outputs<NBITS, CPS, CALIB, kModeTwo, false>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax);

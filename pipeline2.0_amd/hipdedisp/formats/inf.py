@@ -96,12 +96,16 @@ def read_inf(path) -> InfoData:
     vals, onoff = {}, []
     with open(path) as f:
         lines = f.read().splitlines()
-    inv = {v.split("=")[0].strip(): k for k, v in _LABELS.items()}
+    inv = {v[:40].strip(): k for k, v in _LABELS.items()}
     for ln in lines:
-        if "=" not in ln:
+        # fixed layout: 40-character label, '=', value (labels may contain '=' themselves)
+        if len(ln) > 40 and ln[40] == "=":
+            lab, val = ln[:40].strip(), ln[41:].strip()
+        elif "=" in ln:
+            lab, _, val = ln.partition("=")
+            lab, val = lab.strip(), val.strip()
+        else:
             continue
-        lab, _, val = ln.partition("=")
-        lab, val = lab.strip(), val.strip()
         if lab.startswith("On/Off bin pair"):
             a, b = val.split(",")
             onoff += [float(a), float(b)]
