@@ -9,7 +9,7 @@
  * numbers.  This oracle is therefore pinned by
  *   (1) the reference's own plan code, run to produce tests/golden/ddplan_ref.json;
  *   (2) analytic known-answer tests (impulses, constants) in tests/test_oracle.py;
- *   (3) an independent numpy restatement (tests/oracle_np.py) that must agree bit for bit.
+ *   (3) an independent numpy restatement (oracle/oracle_np.py) that must agree bit for bit.
  * Against PRESTO itself it is "parity unpinned"; each PRESTO-derived rule below is
  * tagged [PRESTO-ext] and has a switch in or_opts.
  */

@@ -34,6 +34,9 @@ struct hd_ctx {
     int32_t numint = 0, ptsperint = 0;
     float* d_padvals = nullptr;
     size_t lds_attr_set = 64 * 1024;   // dynamic-LDS limit already granted to the tiled kernels
+    int* d_special = nullptr;          // stage-1 special-tile list (device) and its host copy
+    int special_cap = 0;
+    std::vector<int> h_special;
     double* d_partial = nullptr;    // shared per-tile partial sums
     size_t partial_bytes = 0;
 };
@@ -184,6 +187,7 @@ extern "C" int hd_close(hd_ctx* c)
     (void)hipStreamSynchronize(c->stream);
     free_obs_buffers(c);
     dfree(c->d_partial);
+    dfree(c->d_special);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return HD_OK;
@@ -743,7 +747,7 @@ static bool stage1_tiling(const hd_ctx* c, int nsub, int ds, int dmax, hd::Stage
     const int G = sg * cps;
     const int gbytes = G * nbits / 8;
     vw = 4;
-    for (int cand : {16, 8}) {
+    for (int cand : {16}) {
         // every group's byte offset (g*G or nchan-(g+1)*G channels) and the row pitch must align
         if (gbytes % cand == 0 && c->rowbytes % cand == 0 && ((int64_t)nchan * nbits / 8) % cand == 0) { vw = cand; break; }
     }
@@ -795,7 +799,26 @@ static int run_subband_chunk(hd_ctx* c, hd_plan** plans, int n)
             HIPCHK(c, hd::stage1_tiled_set_lds_limit(lds));
             c->lds_attr_set = lds;
         }
-        HIPCHK(c, hd::launch_stage1_tiled(m, vw, c->stream));
+        const int nsp = hd::stage1_special_tiles(m, nullptr);
+        int* d_sp = nullptr;
+        if (nsp) {
+            if (c->special_cap < nsp) {
+                HIPCHK(c, hipStreamSynchronize(c->stream));
+                dfree(c->d_special);
+                c->d_special = nullptr;
+                c->special_cap = 0;
+                HIPCHK(c, hipMalloc(&c->d_special, sizeof(int) * nsp));
+                c->special_cap = nsp;
+            }
+            c->h_special.resize(nsp);
+            hd::stage1_special_tiles(m, c->h_special.data());
+            // stream-ordered; the host vector is not touched again before the stream sync of
+            // the next resize, and hipMemcpyAsync from pageable memory stages the bytes.
+            HIPCHK(c, hipMemcpyAsync(c->d_special, c->h_special.data(), sizeof(int) * nsp, hipMemcpyHostToDevice,
+                                     c->stream));
+            d_sp = c->d_special;
+        }
+        HIPCHK(c, hd::launch_stage1_tiled(m, vw, d_sp, nsp, c->stream));
     } else {
         for (int i = 0; i < n; i++) {
             hd_plan* p = plans[i];

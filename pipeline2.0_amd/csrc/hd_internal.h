@@ -69,7 +69,8 @@ struct Stage2Args {
 
 hipError_t launch_stage1_direct(const Stage1Args& a, hipStream_t st);
 size_t stage1_tiled_lds_bytes(const Stage1Multi& a);
-hipError_t launch_stage1_tiled(const Stage1Multi& a, int vw, hipStream_t st);
+int stage1_special_tiles(const Stage1Multi& a, int* out);
+hipError_t launch_stage1_tiled(const Stage1Multi& a, int vw, const int* special, int nspecial, hipStream_t st);
 bool stage1_tiled_supports_cps(int cps);
 hipError_t stage1_tiled_set_lds_limit(size_t bytes);
 hipError_t launch_stage2_direct(const Stage2Args& a, hipStream_t st);

@@ -170,74 +170,111 @@ struct SubState {
     int zap[CPS];      // FAST: 1 = whole tile zapped;  TWO: bit0 first interval, bit1 second
 };
 
+// One decoded, calibrated, masked sample of channel cc at tile row jrow + k (+ delay).
+template <int NBITS, int CPS, bool CALIB, int MODE, bool TAIL>
+__device__ __forceinline__ float s1_sample(const Stage1Multi& a, const uint8_t* rowp, const SubState<CPS>& st,
+                                          const int* livr, int c_first, int brow, int rows_valid, int jk, int cc)
+{
+    // branch-free: every sample is read and decoded, then selected
+    float x = lds_decode<NBITS>(rowp + st.off[cc], c_first + cc, a.rd.nibble_hi_first, a.rd.be16);
+    // keep the read unconditional: otherwise hipcc sinks it under a uniform
+    // branch on the zap flag and splits the channel loop into CPS basic blocks
+    if (MODE != kModeClean) asm volatile("" : "+v"(x));
+    if (CALIB) {
+        x = x * st.scl[cc];
+        x = x + st.offs[cc];
+        x = x * st.wts[cc];
+    }
+    if (MODE == kModeFast) {
+        x = st.zap[cc] ? st.pad[cc] : x;
+    } else if (MODE == kModeTwo) {
+        const int row = jk + st.dly[cc];
+        const int bit = row < brow ? 1 : 2;
+        x = (st.zap[cc] & bit) ? st.pad[cc] : x;
+    } else if (MODE == kModeGen) {
+        const int row = jk + st.dly[cc];
+        const int iv = livr[row];
+        if (a.rd.mask && iv < a.rd.numint && a.rd.mask[(int64_t)iv * a.rd.nchan + st.zap[cc]]) x = st.pad[cc];
+    }   // kModeClean: no mask logic at all
+    if (TAIL) {
+        const int row = jk + st.dly[cc];
+        x = row >= rows_valid ? st.pad[cc] : x;
+    }
+    return x;
+}
+
 template <int NBITS, int CPS, bool CALIB, int MODE, bool TAIL>
 __device__ __forceinline__ void form_outputs(const Stage1Multi& a, const uint8_t* lraw, const SubState<CPS>& st,
                                              const int* livr, int c_first, int brow, int rows_valid,
                                              int64_t tO0, int lane, int s, int p, int& amax)
 {
-    // uniform trip count; only the last iteration can diverge
+    // Two outputs per lane per iteration (j, j+64): two independent add chains for ILP.
+    // Uniform trip count; only the last iteration can diverge.
     const int jmax = (int)min((int64_t)a.to, a.nds - tO0);
-    for (int j = lane; j < jmax; j += 64) {
-        const int64_t tp = tO0 + j;
-        const int jrow = j * a.ds;
-        float acc = 0.0f;
+    for (int j0 = lane; j0 < jmax; j0 += 128) {
+        const bool has1 = j0 + 64 < jmax;
+        const int j1 = has1 ? j0 + 64 : j0;          // duplicate work, result discarded
+        const int jr0 = j0 * a.ds, jr1 = j1 * a.ds;
+        float acc0 = 0.0f, acc1 = 0.0f;
         for (int k = 0; k < a.ds; k++) {
-            const uint8_t* rowp = lraw + (jrow + k) * a.rs;
-            float sk = 0.0f;
+            const uint8_t* rp0 = lraw + (jr0 + k) * a.rs;
+            const uint8_t* rp1 = lraw + (jr1 + k) * a.rs;
+            float sk0 = 0.0f, sk1 = 0.0f;
 #pragma unroll
             for (int cc = 0; cc < CPS; cc++) {
-                // branch-free: every sample is read and decoded, then selected
-                float x = lds_decode<NBITS>(rowp + st.off[cc], c_first + cc, a.rd.nibble_hi_first, a.rd.be16);
-                // keep the read unconditional: otherwise hipcc sinks it under a uniform
-                // branch on the zap flag and splits the channel loop into CPS basic blocks
-                if (MODE != kModeClean) asm volatile("" : "+v"(x));
-                if (CALIB) {
-                    x = x * st.scl[cc];
-                    x = x + st.offs[cc];
-                    x = x * st.wts[cc];
-                }
-                if (MODE == kModeFast) {
-                    x = st.zap[cc] ? st.pad[cc] : x;
-                } else if (MODE == kModeTwo) {
-                    const int row = jrow + k + st.dly[cc];
-                    const int bit = row < brow ? 1 : 2;
-                    x = (st.zap[cc] & bit) ? st.pad[cc] : x;
-                } else if (MODE == kModeGen) {
-                    const int row = jrow + k + st.dly[cc];
-                    const int iv = livr[row];
-                    if (a.rd.mask && iv < a.rd.numint && a.rd.mask[(int64_t)iv * a.rd.nchan + st.zap[cc]])
-                        x = st.pad[cc];
-                }   // kModeClean: no mask logic at all
-                if (TAIL) {
-                    const int row = jrow + k + st.dly[cc];
-                    x = row >= rows_valid ? st.pad[cc] : x;
-                }
-                sk += x;
+                sk0 += s1_sample<NBITS, CPS, CALIB, MODE, TAIL>(a, rp0, st, livr, c_first, brow, rows_valid, jr0 + k, cc);
+                sk1 += s1_sample<NBITS, CPS, CALIB, MODE, TAIL>(a, rp1, st, livr, c_first, brow, rows_valid, jr1 + k, cc);
             }
-            acc += sk;
+            acc0 += sk0;
+            acc1 += sk1;
         }
-        if (a.ds_mode == 1) acc = acc / (float)a.ds;
+        if (a.ds_mode == 1) {
+            acc0 = acc0 / (float)a.ds;
+            acc1 = acc1 / (float)a.ds;
+        }
+        const int64_t tp0 = tO0 + j0, tp1 = tO0 + j1;
         if (a.sub_dtype == 0) {
-            const int16_t q = quant_i16(acc);
-            ((int16_t*)a.out[p])[(int64_t)s * a.out_stride + tp] = q;
-            amax = max(amax, q < 0 ? -(int)q : (int)q);
+            const int16_t q0 = quant_i16(acc0), q1 = quant_i16(acc1);
+            int16_t* o = (int16_t*)a.out[p] + (int64_t)s * a.out_stride;
+            o[tp0] = q0;
+            amax = max(amax, q0 < 0 ? -(int)q0 : (int)q0);
+            if (has1) {
+                o[tp1] = q1;
+                amax = max(amax, q1 < 0 ? -(int)q1 : (int)q1);
+            }
         } else {
-            ((float*)a.out[p])[(int64_t)s * a.out_stride + tp] = acc;
+            float* o = (float*)a.out[p] + (int64_t)s * a.out_stride;
+            o[tp0] = acc0;
+            if (has1) o[tp1] = acc1;
         }
     }
 }
 
-template <int NBITS, int CPS, bool CALIB, int VW>
-__global__ __launch_bounds__(512) void k_stage1_tiled(Stage1Multi a)
+// A tile is "special" when it is the last one (reads past the end of the data) or its
+// rows straddle an rfifind interval boundary.  The hot kernel (SPECIAL = false) skips those
+// tiles and runs only the CLEAN / FAST paths, which keeps its register footprint at two
+// 8-wave workgroups per CU; the few special tiles (host-built list) get a second launch.
+__device__ __forceinline__ bool s1_special(const Stage1Multi& a, int64_t tR0, int rows)
+{
+    if (tR0 + rows > a.rd.N) return true;
+    if (a.rd.mask && tR0 / a.rd.ptsperint != (tR0 + rows - 1) / a.rd.ptsperint) return true;
+    return false;
+}
+
+template <int NBITS, int CPS, bool CALIB, int VW, bool SPECIAL>
+__global__ __launch_bounds__(512, SPECIAL ? 1 : 4)   // hot: 2 x 8-wave WGs per CU -> <= 128 VGPRs
+void k_stage1_tiled(Stage1Multi a, const int* __restrict__ special_tiles)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int G = a.sg * CPS;
     const int logical = xcd_remap(blockIdx.x, gridDim.x);
-    const int tile = logical / a.ngroups;
-    const int g = logical - tile * a.ngroups;
+    const int ti = logical / a.ngroups;
+    const int g = logical - ti * a.ngroups;
+    const int tile = SPECIAL ? special_tiles[ti] : ti;
     const int64_t tO0 = (int64_t)tile * a.to;
     const int64_t tR0 = tO0 * a.ds;
     const int rows = a.to * a.ds + a.dmax;
+    if (!SPECIAL && s1_special(a, tR0, rows)) return;      // uniform: handled by the second launch
     const int c0 = g * G;
     const int rc_lo = a.rd.flip ? a.rd.nchan - c0 - G : c0;
     const int gbytes = G * NBITS / 8;
@@ -254,7 +291,7 @@ __global__ __launch_bounds__(512) void k_stage1_tiled(Stage1Multi a)
         const int64_t iv_last = (tR0 + rows - 1) / a.rd.ptsperint;
         brow = (int)min((iv0 + 1) * a.rd.ptsperint - tR0, (int64_t)rows);
         mode = iv_last == iv0 ? kModeFast : (iv_last == iv0 + 1 ? kModeTwo : kModeGen);
-        if (mode == kModeGen)
+        if (SPECIAL && mode == kModeGen)
             for (int r = threadIdx.x; r < rows; r += blockDim.x) livr[r] = (int)((tR0 + r) / a.rd.ptsperint);
     }
     const int rows_valid = (int)min(a.rd.N - tR0, (int64_t)rows);
@@ -276,9 +313,6 @@ __global__ __launch_bounds__(512) void k_stage1_tiled(Stage1Multi a)
                 if constexpr (VW == 16) {
                     const uint4 x = *(const uint4*)src;
                     v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
-                } else if constexpr (VW == 8) {
-                    const uint2 x = *(const uint2*)src;
-                    v[0] = x.x; v[1] = x.y;
                 } else {
                     v[0] = *(const uint32_t*)src;
                 }
@@ -330,10 +364,13 @@ __global__ __launch_bounds__(512) void k_stage1_tiled(Stage1Multi a)
             st.off[cc] = st.dly[cc] * a.rs + lrc * NBITS / 8;
         }
         int amax = 0;
-        if (!tail) {
-            if (mode == kModeFast && !any_zap)
+        if (!SPECIAL) {
+            if (!any_zap)
                 form_outputs<NBITS, CPS, CALIB, kModeClean, false>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax);
-            else if (mode == kModeFast)
+            else
+                form_outputs<NBITS, CPS, CALIB, kModeFast, false>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax);
+        } else if (!tail) {
+            if (mode == kModeFast)
                 form_outputs<NBITS, CPS, CALIB, kModeFast, false>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax);
             else if (mode == kModeTwo)
                 form_outputs<NBITS, CPS, CALIB, kModeTwo, false>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax);
@@ -362,26 +399,52 @@ size_t stage1_tiled_lds_bytes(const Stage1Multi& a)
     return b;
 }
 
-template <int NBITS, int CPS, bool CALIB>
-static hipError_t launch_s1(const Stage1Multi& a, int vw, size_t lds, hipStream_t st)
+int stage1_special_tiles(const Stage1Multi& a, int* out)
 {
-    const dim3 grid((unsigned)(a.ntiles * a.ngroups)), block((unsigned)(64 * a.sg));
-    if (vw == 16) hipLaunchKernelGGL((k_stage1_tiled<NBITS, CPS, CALIB, 16>), grid, block, lds, st, a);
-    else if (vw == 8) hipLaunchKernelGGL((k_stage1_tiled<NBITS, CPS, CALIB, 8>), grid, block, lds, st, a);
-    else hipLaunchKernelGGL((k_stage1_tiled<NBITS, CPS, CALIB, 4>), grid, block, lds, st, a);
+    int n = 0;
+    const int rows = a.to * a.ds + a.dmax;
+    for (int t = 0; t < a.ntiles; t++) {
+        const int64_t tR0 = (int64_t)t * a.to * a.ds;
+        bool sp = tR0 + rows > a.rd.N;
+        if (a.rd.mask && tR0 / a.rd.ptsperint != (tR0 + rows - 1) / a.rd.ptsperint) sp = true;
+        if (sp) {
+            if (out) out[n] = t;
+            n++;
+        }
+    }
+    return n;
+}
+
+template <int NBITS, int CPS, bool CALIB>
+static hipError_t launch_s1(const Stage1Multi& a, int vw, size_t lds, const int* special, int nspecial,
+                            hipStream_t st)
+{
+    const dim3 block((unsigned)(64 * a.sg));
+    const dim3 grid((unsigned)(a.ntiles * a.ngroups)), grid_sp((unsigned)(nspecial * a.ngroups));
+    if (vw == 16) {
+        hipLaunchKernelGGL((k_stage1_tiled<NBITS, CPS, CALIB, 16, false>), grid, block, lds, st, a, special);
+        if (nspecial)
+            hipLaunchKernelGGL((k_stage1_tiled<NBITS, CPS, CALIB, 16, true>), grid_sp, block, lds, st, a, special);
+    } else {
+        hipLaunchKernelGGL((k_stage1_tiled<NBITS, CPS, CALIB, 4, false>), grid, block, lds, st, a, special);
+        if (nspecial)
+            hipLaunchKernelGGL((k_stage1_tiled<NBITS, CPS, CALIB, 4, true>), grid_sp, block, lds, st, a, special);
+    }
     return hipGetLastError();
 }
 
 template <int NBITS, int CPS, bool CALIB>
 static hipError_t set_lds_cps(int bytes)
 {
-    hipError_t e;
-    if ((e = hipFuncSetAttribute((const void*)k_stage1_tiled<NBITS, CPS, CALIB, 16>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes)) != hipSuccess) return e;
-    if ((e = hipFuncSetAttribute((const void*)k_stage1_tiled<NBITS, CPS, CALIB, 8>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes)) != hipSuccess) return e;
-    return hipFuncSetAttribute((const void*)k_stage1_tiled<NBITS, CPS, CALIB, 4>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    const void* fns[4] = {(const void*)k_stage1_tiled<NBITS, CPS, CALIB, 16, false>,
+                          (const void*)k_stage1_tiled<NBITS, CPS, CALIB, 16, true>,
+                          (const void*)k_stage1_tiled<NBITS, CPS, CALIB, 4, false>,
+                          (const void*)k_stage1_tiled<NBITS, CPS, CALIB, 4, true>};
+    for (const void* f : fns) {
+        hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 #define HD_S1_FOR_CPS(X) X(10) X(8) X(16) X(1)
@@ -404,7 +467,7 @@ hipError_t stage1_tiled_set_lds_limit(size_t bytes)
     return e;
 }
 
-hipError_t launch_stage1_tiled(const Stage1Multi& a, int vw, hipStream_t st)
+hipError_t launch_stage1_tiled(const Stage1Multi& a, int vw, const int* special, int nspecial, hipStream_t st)
 {
     if (a.nds <= 0 || a.npass <= 0) return hipSuccess;
     const size_t lds = stage1_tiled_lds_bytes(a);
@@ -412,9 +475,12 @@ hipError_t launch_stage1_tiled(const Stage1Multi& a, int vw, hipStream_t st)
 #define HD_DISPATCH(C)                                                                                      \
     if (a.cps == C) {                                                                                       \
         switch (a.rd.nbits) {                                                                               \
-        case 8: return calib ? launch_s1<8, C, true>(a, vw, lds, st) : launch_s1<8, C, false>(a, vw, lds, st);   \
-        case 4: return calib ? launch_s1<4, C, true>(a, vw, lds, st) : launch_s1<4, C, false>(a, vw, lds, st);   \
-        case 16: return calib ? launch_s1<16, C, true>(a, vw, lds, st) : launch_s1<16, C, false>(a, vw, lds, st);\
+        case 8: return calib ? launch_s1<8, C, true>(a, vw, lds, special, nspecial, st)                      \
+                             : launch_s1<8, C, false>(a, vw, lds, special, nspecial, st);                    \
+        case 4: return calib ? launch_s1<4, C, true>(a, vw, lds, special, nspecial, st)                      \
+                             : launch_s1<4, C, false>(a, vw, lds, special, nspecial, st);                    \
+        case 16: return calib ? launch_s1<16, C, true>(a, vw, lds, special, nspecial, st)                    \
+                              : launch_s1<16, C, false>(a, vw, lds, special, nspecial, st);                  \
         default: return hipErrorInvalidValue;                                                               \
         }                                                                                                   \
     }
@@ -531,31 +597,72 @@ __global__ __launch_bounds__(256) void k_stage2_lds(Stage2Args a, const int32_t*
     int gcount = 0;
     const uint32_t lane_byte = (uint32_t)lane * 8u;
 
+    // The wave's LDS offsets for a whole chunk (kSC subbands x Q DMs) are fetched with one
+    // vector load per register before the fill, and read back with v_readlane inside the
+    // accumulate loop: no scalar-memory wait sits between the LDS reads.
+    constexpr int NR = (kSC * Q + 63) / 64;
     for (int sc0 = 0; sc0 < a.nsub; sc0 += kSC) {
         const int nsc = (a.nsub - sc0) < kSC ? (a.nsub - sc0) : kSC;
-        __syncthreads();
-        // ---- fill: element m of subband window -> copies j with i = m - j
-        const int welems = ws + 3;
-        for (int e = threadIdx.x; e < nsc * welems; e += 256) {
-            const int sl = e / welems;
-            const int m = e - sl * welems;
-            const int s = sc0 + sl;
-            const int64_t gi = t0 + omin[s] + m;
-            const int16_t v = gi < a.nds ? sub[(int64_t)s * a.sub_stride + gi] : (int16_t)0;
-            int16_t* base = lds + (sl * 4) * ws;
+        int voff[NR];
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int i = m - j;
-                if (i >= 0 && i < ws) base[j * ws + i] = v;
+        for (int r = 0; r < NR; r++) {
+            const int e = r * 64 + lane;
+            const int sl = e / Q, q = e - (e / Q) * Q;
+            voff[r] = (sl < nsc) ? bo[(int64_t)(sc0 + sl) * dpb + q] : 0;
+        }
+        __syncthreads();
+        // ---- fill: thread unit u writes positions 4u..4u+3 of all 4 shifted copies
+        //      (copy j, position i = window element i + j) from 4 aligned dword loads:
+        //      elements g0-p .. g0-p+7 with g0 = window start + 4u, p = g0 & 1 (uniform
+        //      per subband), then v_alignbit for odd element offsets, one ds_write_b64 per copy.
+        const int units = ws >> 2;
+        for (int sl = 0; sl < nsc; sl++) {
+            const int s = sc0 + sl;
+            const int64_t wbeg = t0 + omin[s];
+            const int p = (int)(wbeg & 1);
+            const int16_t* srow = sub + (int64_t)s * a.sub_stride;
+            uint2* dst0 = (uint2*)(lds + (sl * 4) * ws);
+            for (int u = threadIdx.x; u < units; u += 256) {
+                const int64_t g0 = wbeg + 4 * u;
+                uint32_t D[4];
+                if (g0 - p + 8 <= a.nds) {
+                    const uint32_t* src = (const uint32_t*)(srow + (g0 - p));
+#pragma unroll
+                    for (int i = 0; i < 4; i++) D[i] = src[i];
+                } else {   // past the end of the subbands: zeros
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const int64_t e0 = g0 - p + 2 * i;
+                        const uint32_t lo = e0 < a.nds ? (uint16_t)srow[e0] : 0u;
+                        const uint32_t hi = e0 + 1 < a.nds ? (uint16_t)srow[e0 + 1] : 0u;
+                        D[i] = lo | (hi << 16);
+                    }
+                }
+                // copy j needs elements j..j+3 of g0, i.e. D-space halves (p+j) .. (p+j+3)
+#define HD_PAIR(h) (((h) & 1) ? __builtin_amdgcn_alignbit(D[((h) + 1) >> 1], D[(h) >> 1], 16) : D[(h) >> 1])
+                if (p == 0) {
+                    dst0[u] = make_uint2(HD_PAIR(0), HD_PAIR(2));
+                    dst0[(ws >> 2) + u] = make_uint2(HD_PAIR(1), HD_PAIR(3));
+                    dst0[2 * (ws >> 2) + u] = make_uint2(HD_PAIR(2), HD_PAIR(4));
+                    dst0[3 * (ws >> 2) + u] = make_uint2(HD_PAIR(3), HD_PAIR(5));
+                } else {
+                    dst0[u] = make_uint2(HD_PAIR(1), HD_PAIR(3));
+                    dst0[(ws >> 2) + u] = make_uint2(HD_PAIR(2), HD_PAIR(4));
+                    dst0[2 * (ws >> 2) + u] = make_uint2(HD_PAIR(3), HD_PAIR(5));
+                    dst0[3 * (ws >> 2) + u] = make_uint2(HD_PAIR(4), HD_PAIR(6));
+                }
+#undef HD_PAIR
             }
         }
         __syncthreads();
         // ---- accumulate
-        for (int sl = 0; sl < nsc; sl++) {
-            const int32_t* bs = bo + (int64_t)(sc0 + sl) * dpb;
+#pragma unroll
+        for (int sl = 0; sl < kSC; sl++) {
+            if (sl >= nsc) break;
 #pragma unroll
             for (int q = 0; q < Q; q++) {
-                const uint32_t addr = (uint32_t)bs[q] + lane_byte;
+                const int e = sl * Q + q;
+                const uint32_t addr = (uint32_t)__builtin_amdgcn_readlane(voff[e >> 6], e & 63) + lane_byte;
                 const uint2 v = *(const uint2*)(lds_raw + addr);
                 acc16[q][0] += __builtin_bit_cast(short2v, v.x);
                 acc16[q][1] += __builtin_bit_cast(short2v, v.y);
