@@ -191,8 +191,10 @@ HD_API int hd_set_subbands(hd_plan* plan, const void* host);
 HD_API int hd_run_dedisp(hd_plan* plan, float* host_out);
 /* Device-time of the last hd_run_subband / hd_run_dedisp of this plan, ms.           */
 HD_API int hd_plan_last_ms(const hd_plan* plan, float* ms_subband, float* ms_dedisp);
-/* Kernel variants: (s1 << 8) | s2.  s2: 0 auto, 1 direct, 2 LDS-tiled; s1: 0 auto (tiled,
- * multi-pass), 1 direct (one thread per subband sample, for cross-checks).           */
+/* Kernel variants: (s1 << 8) | s2.  s2: 0 auto, 1 direct, 2 LDS-tiled (4 waves x 256 samples),
+ * 3 wide LDS tiles (up to 16 waves share one window); s1: 0 auto, 1 direct
+ * (one thread per subband sample, for cross-checks), 2 float tiled multi-pass, 3 8-bit
+ * integer tiled multi-pass (8-bit data without calibration only; HD_E_INVAL otherwise). */
 HD_API int hd_plan_set_variant(hd_plan* plan, int32_t variant);
 
 #ifdef __cplusplus

@@ -34,9 +34,12 @@ struct hd_ctx {
     int32_t numint = 0, ptsperint = 0;
     float* d_padvals = nullptr;
     size_t lds_attr_set = 64 * 1024;   // dynamic-LDS limit already granted to the tiled kernels
-    int* d_special = nullptr;          // stage-1 special-tile list (device) and its host copy
-    int special_cap = 0;
-    std::vector<int> h_special;
+    size_t lds_attr_q8 = 64 * 1024;    // ... and to the 8-bit integer stage-1 kernels
+    struct SpecialList {               // stage-1 special-tile list per tile geometry (device)
+        int to, ds, dmax, ntiles, two_ok, n;
+        int* d;
+    };
+    std::vector<SpecialList> special_cache;
     double* d_partial = nullptr;    // shared per-tile partial sums
     size_t partial_bytes = 0;
 };
@@ -57,17 +60,23 @@ struct hd_plan {
     bool lds_ok = false;
     int32_t* d_omin = nullptr;
     int32_t* d_boff = nullptr;
+    // wide-tile variant tables (k_stage2_wide)
+    int32_t wq = 0, wr = 0, wnw = 0, wdpb = 0, wws = 0, wsc = 0;
+    bool wide_ok = false;
+    int32_t* d_womin = nullptr;
+    int32_t* d_wboff = nullptr;
     int32_t variant = 0;
     float* d_out = nullptr;
     void* d_sub = nullptr;          // this pass's subbands [nsub][sub_stride]
     size_t sub_bytes = 0;
     bool sub_valid = false;
-    int32_t s1_variant = 0;         // stage 1: 0 auto (tiled), 1 direct
+    int32_t s1_variant = 0;         // stage 1: 0 auto, 1 direct, 2 float tiled, 3 8-bit integer
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     bool ran_sub = false, ran_dd = false;
 };
 
 static thread_local std::string g_err;
+static void clear_special_cache(hd_ctx* c);
 
 static int fail(hd_ctx* ctx, int code, const char* fmt, ...)
 {
@@ -176,6 +185,7 @@ static void free_obs_buffers(hd_ctx* c)
     dfree(c->d_wts); c->d_wts = nullptr;
     dfree(c->d_mask); c->d_mask = nullptr;
     dfree(c->d_padvals); c->d_padvals = nullptr;
+    clear_special_cache(c);
     c->raw_ready = false;
     c->numint = c->ptsperint = 0;
 }
@@ -187,7 +197,7 @@ extern "C" int hd_close(hd_ctx* c)
     (void)hipStreamSynchronize(c->stream);
     free_obs_buffers(c);
     dfree(c->d_partial);
-    dfree(c->d_special);
+    clear_special_cache(c);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return HD_OK;
@@ -284,6 +294,7 @@ extern "C" int hd_set_mask(hd_ctx* c, const uint8_t* mask, int32_t numint, int32
     dfree(c->d_mask);
     c->d_mask = nullptr;
     c->numint = c->ptsperint = 0;
+    clear_special_cache(c);
     if (mask) {
         const size_t n = (size_t)numint * c->obs.nchan;
         HIPCHK(c, hipMalloc(&c->d_mask, n));
@@ -486,6 +497,8 @@ static void plan_free(hd_plan* p)
     dfree(p->d_maxabs);
     dfree(p->d_omin);
     dfree(p->d_boff);
+    dfree(p->d_womin);
+    dfree(p->d_wboff);
     dfree(p->d_out);
     dfree(p->d_sub);
     for (auto& e : p->ev)
@@ -628,8 +641,67 @@ extern "C" int hd_plan_create(hd_ctx* c, const hd_pass* ps, hd_plan** out)
                 boff[((size_t)yb * nsub + s) * p->dpb + k] = ((sl * 4 + (o2 & 3)) * p->wstride + (o2 & ~3)) * 2;
             }
 
+    // wide-tile variant: one y-block of up to 80 DMs (8 waves x Q), T = 256*R samples per tile,
+    // sc subbands per LDS chunk (the largest of 8, 4, 2 whose two buffers fit 160 KiB)
+    std::vector<int32_t> womin, wboff;
+    {
+        int nyb = (ps->numdms + 79) / 80;
+        const int per = (ps->numdms + nyb - 1) / nyb;
+        const int qneed = (per + hd::kWideWaves - 1) / hd::kWideWaves;
+        int Q = 2, R = 4;
+        if (qneed > 8) { Q = 10; R = 3; }
+        else if (qneed > 6) { Q = 8; R = 3; }
+        else if (qneed > 4) { Q = 6; R = 4; }
+        else if (qneed > 2) { Q = 4; R = 4; }
+        const int nw = (per + Q - 1) / Q;
+        const int dpb = nw * Q;
+        nyb = (ps->numdms + dpb - 1) / dpb;
+        womin.assign((size_t)nyb * nsub, 0);
+        int32_t span = 0;
+        for (int yb = 0; yb < nyb; yb++)
+            for (int s = 0; s < nsub; s++) {
+                int32_t lo = INT32_MAX, hi = INT32_MIN;
+                for (int k = 0; k < dpb; k++) {
+                    const int dm = std::min(yb * dpb + k, ps->numdms - 1);
+                    const int32_t v = p->off[(size_t)dm * nsub + s];
+                    lo = std::min(lo, v);
+                    hi = std::max(hi, v);
+                }
+                womin[(size_t)yb * nsub + s] = lo;
+                span = std::max(span, hi - lo);
+            }
+        const int ws = (int)round_up((size_t)(256 * R + span + 4), 4);
+        int sc = 0;
+        for (int cand : {8, 4, 2})
+            if (hd::stage2_wide_lds_bytes(ws, cand) <= 160 * 1024) { sc = cand; break; }
+        p->wide_ok = c->opts.sub_dtype == HD_SUB_I16 && nw <= hd::kWideWaves && hd::stage2_wide_supports(Q, R) && sc > 0;
+        if (p->wide_ok) {
+            p->wq = Q;
+            p->wr = R;
+            p->wnw = nw;
+            p->wdpb = dpb;
+            p->wws = ws;
+            p->wsc = sc;
+            wboff.resize((size_t)nyb * nsub * dpb);
+            for (int yb = 0; yb < nyb; yb++)
+                for (int s = 0; s < nsub; s++)
+                    for (int k = 0; k < dpb; k++) {
+                        const int dm = std::min(yb * dpb + k, ps->numdms - 1);
+                        const int32_t o2 = p->off[(size_t)dm * nsub + s] - womin[(size_t)yb * nsub + s];
+                        const int32_t buf = (s / sc) & 1, sl = s % sc;
+                        wboff[((size_t)yb * nsub + s) * dpb + k] = (((buf * sc + sl) * 4 + (o2 & 3)) * ws + (o2 & ~3)) * 2;
+                    }
+        }
+    }
+
     int rc = HD_OK;
     hipError_t e = hipSetDevice(c->device);
+    if (e == hipSuccess && p->wide_ok) e = hipMalloc(&p->d_womin, sizeof(int32_t) * womin.size());
+    if (e == hipSuccess && p->wide_ok)
+        e = hipMemcpy(p->d_womin, womin.data(), sizeof(int32_t) * womin.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess && p->wide_ok) e = hipMalloc(&p->d_wboff, sizeof(int32_t) * wboff.size());
+    if (e == hipSuccess && p->wide_ok)
+        e = hipMemcpy(p->d_wboff, wboff.data(), sizeof(int32_t) * wboff.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&p->d_idispdt, sizeof(int32_t) * nchan);
     if (e == hipSuccess) e = hipMemcpy(p->d_idispdt, p->idispdt.data(), sizeof(int32_t) * nchan, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&p->d_off, sizeof(int32_t) * p->off.size());
@@ -683,12 +755,14 @@ extern "C" int hd_plan_sub_params(const hd_plan* p, double* lof, double* cw, dou
 extern "C" int hd_plan_set_variant(hd_plan* p, int32_t v)
 {
     if (!p) return fail(nullptr, HD_E_INVAL, "hd_plan_set_variant: NULL plan");
-    // bits 0-7: stage-2 variant (0 auto, 1 direct, 2 LDS); bits 8-15: stage-1 (0 auto/tiled, 1 direct)
+    // bits 0-7: stage-2 variant (0 auto, 1 direct, 2 LDS, 3 wide LDS); bits 8-15: stage-1 (0 auto, 1 direct,
+    // 2 float tiled, 3 8-bit integer tiled)
     const int32_t v1 = (v >> 8) & 0xFF;
     v &= 0xFF;
-    if (v < 0 || v > 2 || v1 > 1) return fail(p->ctx, HD_E_INVAL, "variant must be (s1<<8)|s2 with s1 in 0..1, s2 in 0..2");
+    if (v < 0 || v > 3 || v1 > 3) return fail(p->ctx, HD_E_INVAL, "variant must be (s1<<8)|s2 with s1 in 0..3, s2 in 0..3");
     p->s1_variant = v1;
     if (v == 2 && !p->lds_ok) return fail(p->ctx, HD_E_INVAL, "LDS variant unavailable for this plan (needs int16 subbands and a window that fits 64 KiB)");
+    if (v == 3 && !p->wide_ok) return fail(p->ctx, HD_E_INVAL, "wide-tile variant unavailable for this plan (needs int16 subbands and a window that fits 160 KiB)");
     p->variant = v;
     return HD_OK;
 }
@@ -768,17 +842,161 @@ static bool stage1_tiling(const hd_ctx* c, int nsub, int ds, int dmax, hd::Stage
     return true;
 }
 
+// Float tiled kernel over tiles of a fixed `to` (the 8-bit integer path's special tiles):
+// the widest channel group whose LDS tile fits 160 KiB.
+static bool stage1_tiling_fixed(const hd_ctx* c, int nsub, int ds, int dmax, int to, hd::Stage1Multi& a, int& vw)
+{
+    const int nbits = c->obs.nbits, nchan = c->obs.nchan, cps = nchan / nsub;
+    if (c->rowbytes % 4 || !hd::stage1_tiled_supports_cps(cps)) return false;
+    for (int cand : {8, 4, 2, 1}) {
+        if (nsub % cand || ((int64_t)cand * cps * nbits) % 32) continue;
+        const int gbytes = cand * cps * nbits / 8;
+        int rs = (gbytes + 3) & ~3;
+        if (((rs / 4) & 1) == 0) rs += 4;
+        hd::Stage1Multi t = a;
+        t.sg = cand;
+        t.to = to;
+        t.rs = rs;
+        t.ds = ds;
+        t.dmax = dmax;
+        if (hd::stage1_tiled_lds_bytes(t) > 160 * 1024) continue;
+        vw = (gbytes % 16 == 0 && c->rowbytes % 16 == 0) ? 16 : 4;
+        a.sg = cand;
+        a.rs = rs;
+        a.ngroups = nsub / cand;
+        return true;
+    }
+    return false;
+}
+
+// 8-bit integer path (k_stage1_q8): sg subbands per workgroup, quarter geometry fixed by ds;
+// the first sg in {4, 2, 1} whose LDS tile fits 64 KiB (two or more workgroups per CU),
+// else the smallest tile that fits 160 KiB.
+static bool stage1_q8_tiling(const hd_ctx* c, int nsub, int ds, int dmax, hd::Stage1Multi& a, int& vb)
+{
+    const int nchan = c->obs.nchan, cps = nchan / nsub;
+    if (c->obs.nbits != 8 || c->d_scl || c->d_offs || c->d_wts) return false;
+    if (!hd::stage1_q8_supports(cps, ds)) return false;
+    const int S = hd::stage1_q8_quarter_rows(ds);
+    const int W = S + dmax;
+    int sg = 0, v = 0;
+    size_t best = 0;
+    for (int cand : {4, 2, 1}) {
+        if (nsub % cand) continue;
+        const int G = cand * cps;
+        const int cv = (G % 8 == 0 && nchan % 8 == 0) ? 8 : (G % 4 == 0 && nchan % 4 == 0) ? 4 : 0;
+        if (!cv) continue;
+        const size_t lds = (size_t)G * W * 4;
+        if (lds > 160 * 1024) continue;
+        if (lds <= 64 * 1024) {
+            sg = cand;
+            v = cv;
+            break;
+        }
+        if (!sg || lds < best) {
+            sg = cand;
+            v = cv;
+            best = lds;
+        }
+    }
+    if (!sg) return false;
+    a.sg = sg;
+    a.to = 4 * S / ds;
+    a.dmax = dmax;
+    a.W = W;
+    a.rs = 0;
+    a.two_ok = 1;
+    a.ngroups = nsub / sg;
+    vb = v;
+    return true;
+}
+
+// Host-built list of a launch's special tiles (last tile / interval-straddling), on device.
+// The list depends only on the tile geometry and the mask, so it is built and uploaded once
+// per geometry (synchronous copy) and cached on the context until the mask or obs change.
+static int special_tiles(hd_ctx* c, const hd::Stage1Multi& m, int** d_sp, int* nsp_out)
+{
+    *d_sp = nullptr;
+    *nsp_out = 0;
+    for (const auto& e : c->special_cache)
+        if (e.to == m.to && e.ds == m.ds && e.dmax == m.dmax && e.ntiles == m.ntiles && e.two_ok == m.two_ok) {
+            *d_sp = e.d;
+            *nsp_out = e.n;
+            return HD_OK;
+        }
+    const int nsp = hd::stage1_special_tiles(m, nullptr);
+    hd_ctx::SpecialList e{m.to, m.ds, m.dmax, m.ntiles, m.two_ok, nsp, nullptr};
+    if (nsp) {
+        std::vector<int> h(nsp);
+        hd::stage1_special_tiles(m, h.data());
+        HIPCHK(c, hipMalloc(&e.d, sizeof(int) * nsp));
+        HIPCHK(c, hipMemcpy(e.d, h.data(), sizeof(int) * nsp, hipMemcpyHostToDevice));
+    }
+    c->special_cache.push_back(e);
+    *d_sp = e.d;
+    *nsp_out = nsp;
+    return HD_OK;
+}
+
+static void clear_special_cache(hd_ctx* c)
+{
+    if (!c->special_cache.empty()) (void)hipStreamSynchronize(c->stream);
+    for (auto& e : c->special_cache) dfree(e.d);
+    c->special_cache.clear();
+}
+
 static int run_subband_chunk(hd_ctx* c, hd_plan** plans, int n)
 {
     hd_plan* p0 = plans[0];
     int dmax = 0;
     for (int i = 0; i < n; i++) dmax = std::max(dmax, plans[i]->maxdelay);
     hd::Stage1Multi m{};
-    int vw = 4;
-    const bool tiled = p0->s1_variant != 1 && stage1_tiling(c, p0->pass.nsub, p0->pass.ds, dmax, m, vw);
+    int vw = 4, vb = 4;
+    const int v1 = p0->s1_variant;
+    const bool q8 = (v1 == 0 || v1 == 3) && stage1_q8_tiling(c, p0->pass.nsub, p0->pass.ds, dmax, m, vb);
+    if (v1 == 3 && !q8)
+        return fail(c, HD_E_INVAL, "stage-1 variant 3 (8-bit integer path) does not apply to this pass");
+    const bool tiled = !q8 && (v1 == 0 || v1 == 2) && stage1_tiling(c, p0->pass.nsub, p0->pass.ds, dmax, m, vw);
     for (int i = 0; i < n; i++) HIPCHK(c, hipMemsetAsync(plans[i]->d_maxabs, 0, sizeof(int32_t), c->stream));
     HIPCHK(c, hipEventRecord(p0->ev[0], c->stream));
-    if (tiled) {
+    if (q8) {
+        m.rd = raw_desc(c);
+        m.npass = n;
+        m.nsub = p0->pass.nsub;
+        m.cps = c->obs.nchan / p0->pass.nsub;
+        m.ds = p0->pass.ds;
+        m.ds_mode = c->opts.ds_mode;
+        m.sub_dtype = c->opts.sub_dtype;
+        m.nds = p0->nds;
+        m.out_stride = p0->sub_stride;
+        m.ntiles = (int)((p0->nds + m.to - 1) / m.to);
+        for (int i = 0; i < n; i++) {
+            m.dly[i] = plans[i]->d_idispdt;
+            m.out[i] = plans[i]->d_sub;
+            m.maxabs[i] = plans[i]->d_maxabs;
+        }
+        int nsp = 0, *d_sp = nullptr;
+        int rc = special_tiles(c, m, &d_sp, &nsp);
+        if (rc) return rc;
+        const size_t lds = hd::stage1_q8_lds_bytes(m);
+        if (lds > c->lds_attr_q8) {
+            HIPCHK(c, hd::stage1_q8_set_lds_limit(lds));
+            c->lds_attr_q8 = lds;
+        }
+        HIPCHK(c, hd::launch_stage1_q8(m, vb, c->stream));
+        if (nsp) {
+            hd::Stage1Multi f = m;
+            int fvw = 4;
+            if (!stage1_tiling_fixed(c, m.nsub, m.ds, dmax, m.to, f, fvw))
+                return fail(c, HD_E_INVAL, "stage 1: no float tiling for the integer path's special tiles");
+            const size_t flds = hd::stage1_tiled_lds_bytes(f);
+            if (flds > c->lds_attr_set) {
+                HIPCHK(c, hd::stage1_tiled_set_lds_limit(flds));
+                c->lds_attr_set = flds;
+            }
+            HIPCHK(c, hd::launch_stage1_tiled(f, fvw, d_sp, nsp, true, c->stream));
+        }
+    } else if (tiled) {
         m.rd = raw_desc(c);
         m.npass = n;
         m.nsub = p0->pass.nsub;
@@ -799,26 +1017,10 @@ static int run_subband_chunk(hd_ctx* c, hd_plan** plans, int n)
             HIPCHK(c, hd::stage1_tiled_set_lds_limit(lds));
             c->lds_attr_set = lds;
         }
-        const int nsp = hd::stage1_special_tiles(m, nullptr);
-        int* d_sp = nullptr;
-        if (nsp) {
-            if (c->special_cap < nsp) {
-                HIPCHK(c, hipStreamSynchronize(c->stream));
-                dfree(c->d_special);
-                c->d_special = nullptr;
-                c->special_cap = 0;
-                HIPCHK(c, hipMalloc(&c->d_special, sizeof(int) * nsp));
-                c->special_cap = nsp;
-            }
-            c->h_special.resize(nsp);
-            hd::stage1_special_tiles(m, c->h_special.data());
-            // stream-ordered; the host vector is not touched again before the stream sync of
-            // the next resize, and hipMemcpyAsync from pageable memory stages the bytes.
-            HIPCHK(c, hipMemcpyAsync(c->d_special, c->h_special.data(), sizeof(int) * nsp, hipMemcpyHostToDevice,
-                                     c->stream));
-            d_sp = c->d_special;
-        }
-        HIPCHK(c, hd::launch_stage1_tiled(m, vw, d_sp, nsp, c->stream));
+        int nsp = 0, *d_sp = nullptr;
+        int rc = special_tiles(c, m, &d_sp, &nsp);
+        if (rc) return rc;
+        HIPCHK(c, hd::launch_stage1_tiled(m, vw, d_sp, nsp, false, c->stream));
     } else {
         for (int i = 0; i < n; i++) {
             hd_plan* p = plans[i];
@@ -927,7 +1129,10 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         }
     }
     const bool pad = p->numout > p->nds;
-    const int ntiles = (int)((p->nvalid + kTT - 1) / kTT);
+    const bool use_wide = p->variant == 3 || (p->variant == 0 && p->wide_ok);
+    const bool use_lds = !use_wide && (p->variant == 2 || (p->variant == 0 && p->lds_ok));
+    const int tile = use_wide ? 256 * p->wr : kTT;
+    const int ntiles = (int)((p->nvalid + tile - 1) / tile);
     double* partial = nullptr;
     if (pad && c->opts.pad_mode == HD_PAD_MEAN) {
         const size_t need = sizeof(double) * (size_t)p->pass.numdms * std::max(ntiles, 1);
@@ -953,14 +1158,20 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
     a.out_stride = p->out_stride;
     a.partial = partial;
     a.ntiles = ntiles;
-    a.tile = kTT;
+    a.tile = tile;
     a.maxabs = p->d_maxabs;
     a.omin = p->d_omin;
     a.wstride = p->wstride;
     a.dms_per_blk = p->dpb;
-    const bool use_lds = p->variant == 2 || (p->variant == 0 && p->lds_ok);
     HIPCHK(c, hipEventRecord(p->ev[2], c->stream));
-    if (use_lds) {
+    if (use_wide) {
+        a.off = p->d_wboff;
+        a.omin = p->d_womin;
+        a.wstride = p->wws;
+        a.dms_per_blk = p->wdpb;
+        a.sc = p->wsc;
+        HIPCHK(c, hd::launch_stage2_wide(a, p->wq, p->wr, p->wnw, c->stream));
+    } else if (use_lds) {
         a.off = p->d_boff;
         HIPCHK(c, hd::launch_stage2_lds(a, p->q, c->stream));
     } else {

@@ -44,6 +44,8 @@ struct Stage1Multi {
     int32_t to;               // output samples per tile
     int32_t dmax;             // max channel delay over the passes
     int32_t rs;               // LDS bytes per raw row (multiple of 4, odd dword count)
+    int32_t W;                // 8-bit integer path: LDS dwords per channel row (>= S + dmax)
+    int32_t two_ok;           // tiles straddling one mask-interval boundary are not special
     int32_t ntiles, ngroups;
     const int32_t* dly[kMaxPass];   // per-pass idispdt [nchan]
     void* out[kMaxPass];            // per-pass subbands [nsub][out_stride]
@@ -65,14 +67,29 @@ struct Stage2Args {
     const int32_t* omin;      // [nyblk][nsub] min offset of the y-block's DMs
     int32_t wstride;          // LDS window stride (elements) per copy
     int32_t dms_per_blk;      // DMs per y-block
+    int32_t sc, _pad2;        // wide variant: subbands per LDS chunk
 };
 
 hipError_t launch_stage1_direct(const Stage1Args& a, hipStream_t st);
 size_t stage1_tiled_lds_bytes(const Stage1Multi& a);
 int stage1_special_tiles(const Stage1Multi& a, int* out);
-hipError_t launch_stage1_tiled(const Stage1Multi& a, int vw, const int* special, int nspecial, hipStream_t st);
+hipError_t launch_stage1_tiled(const Stage1Multi& a, int vw, const int* special, int nspecial, bool special_only,
+                               hipStream_t st);
+int stage1_q8_quarter_rows(int ds);
+bool stage1_q8_supports(int cps, int ds);
+size_t stage1_q8_lds_bytes(const Stage1Multi& a);
+hipError_t stage1_q8_set_lds_limit(size_t bytes);
+hipError_t launch_stage1_q8(const Stage1Multi& a, int vb, hipStream_t st);
 bool stage1_tiled_supports_cps(int cps);
 hipError_t stage1_tiled_set_lds_limit(size_t bytes);
+// wide stage-2 tiles: at most kSC2 subbands staged per chunk, kUMax prefetched fill units
+// per thread per chunk, at most kWideWaves waves per workgroup
+constexpr int kSC2 = 8;
+constexpr int kUMax = 4;
+constexpr int kWideWaves = 8;
+size_t stage2_wide_lds_bytes(int wstride, int sc);
+bool stage2_wide_supports(int q, int r);
+hipError_t launch_stage2_wide(const Stage2Args& a, int q, int r, int nw, hipStream_t st);
 hipError_t launch_stage2_direct(const Stage2Args& a, hipStream_t st);
 hipError_t launch_stage2_lds(const Stage2Args& a, int q, hipStream_t st);
 hipError_t launch_pad(float* out, int64_t out_stride, int numdms, int64_t nds, int64_t numout,

@@ -82,6 +82,16 @@ __device__ __forceinline__ int wave_max_i32(int v)
     return v;
 }
 
+// Raise *addr to v.  Every wave of a pass targets the same word, and same-address atomics
+// serialise at the memory side, so read first (a stale value only costs an extra atomic;
+// atomicMax is monotone, so the result is exact) and publish only a new maximum.
+__device__ __forceinline__ void publish_max(int32_t* addr, int v)
+{
+    if (v <= 0) return;
+    const int cur = __hip_atomic_load(addr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v > cur) atomicMax(addr, v);
+}
+
 __global__ __launch_bounds__(256) void k_stage1_direct(Stage1Args a)
 {
     const int s = blockIdx.y;
@@ -110,7 +120,7 @@ __global__ __launch_bounds__(256) void k_stage1_direct(Stage1Args a)
     }
     if (a.sub_dtype == 0 && a.maxabs) {
         amax = wave_max_i32(amax);
-        if ((threadIdx.x & 63) == 0 && amax > 0) atomicMax(a.maxabs, amax);
+        if ((threadIdx.x & 63) == 0) publish_max(a.maxabs, amax);
     }
 }
 
@@ -254,10 +264,13 @@ __device__ __forceinline__ void form_outputs(const Stage1Multi& a, const uint8_t
 // rows straddle an rfifind interval boundary.  The hot kernel (SPECIAL = false) skips those
 // tiles and runs only the CLEAN / FAST paths, which keeps its register footprint at two
 // 8-wave workgroups per CU; the few special tiles (host-built list) get a second launch.
-__device__ __forceinline__ bool s1_special(const Stage1Multi& a, int64_t tR0, int rows)
+__device__ __host__ __forceinline__ bool s1_special(const Stage1Multi& a, int64_t tR0, int rows)
 {
     if (tR0 + rows > a.rd.N) return true;
-    if (a.rd.mask && tR0 / a.rd.ptsperint != (tR0 + rows - 1) / a.rd.ptsperint) return true;
+    if (a.rd.mask) {
+        const int64_t iv0 = tR0 / a.rd.ptsperint, iv1 = (tR0 + rows - 1) / a.rd.ptsperint;
+        if (iv1 > iv0 + (a.two_ok ? 1 : 0)) return true;   // the integer path takes two-interval tiles
+    }
     return false;
 }
 
@@ -386,7 +399,7 @@ void k_stage1_tiled(Stage1Multi a, const int* __restrict__ special_tiles)
         }
         if (a.sub_dtype == 0) {
             amax = wave_max_i32(amax);
-            if (lane == 0 && amax > 0) atomicMax(a.maxabs[p], amax);
+            if (lane == 0) publish_max(a.maxabs[p], amax);
         }
     }
 }
@@ -405,8 +418,7 @@ int stage1_special_tiles(const Stage1Multi& a, int* out)
     const int rows = a.to * a.ds + a.dmax;
     for (int t = 0; t < a.ntiles; t++) {
         const int64_t tR0 = (int64_t)t * a.to * a.ds;
-        bool sp = tR0 + rows > a.rd.N;
-        if (a.rd.mask && tR0 / a.rd.ptsperint != (tR0 + rows - 1) / a.rd.ptsperint) sp = true;
+        const bool sp = s1_special(a, tR0, rows);
         if (sp) {
             if (out) out[n] = t;
             n++;
@@ -417,16 +429,18 @@ int stage1_special_tiles(const Stage1Multi& a, int* out)
 
 template <int NBITS, int CPS, bool CALIB>
 static hipError_t launch_s1(const Stage1Multi& a, int vw, size_t lds, const int* special, int nspecial,
-                            hipStream_t st)
+                            bool special_only, hipStream_t st)
 {
     const dim3 block((unsigned)(64 * a.sg));
     const dim3 grid((unsigned)(a.ntiles * a.ngroups)), grid_sp((unsigned)(nspecial * a.ngroups));
     if (vw == 16) {
-        hipLaunchKernelGGL((k_stage1_tiled<NBITS, CPS, CALIB, 16, false>), grid, block, lds, st, a, special);
+        if (!special_only)
+            hipLaunchKernelGGL((k_stage1_tiled<NBITS, CPS, CALIB, 16, false>), grid, block, lds, st, a, special);
         if (nspecial)
             hipLaunchKernelGGL((k_stage1_tiled<NBITS, CPS, CALIB, 16, true>), grid_sp, block, lds, st, a, special);
     } else {
-        hipLaunchKernelGGL((k_stage1_tiled<NBITS, CPS, CALIB, 4, false>), grid, block, lds, st, a, special);
+        if (!special_only)
+            hipLaunchKernelGGL((k_stage1_tiled<NBITS, CPS, CALIB, 4, false>), grid, block, lds, st, a, special);
         if (nspecial)
             hipLaunchKernelGGL((k_stage1_tiled<NBITS, CPS, CALIB, 4, true>), grid_sp, block, lds, st, a, special);
     }
@@ -467,7 +481,8 @@ hipError_t stage1_tiled_set_lds_limit(size_t bytes)
     return e;
 }
 
-hipError_t launch_stage1_tiled(const Stage1Multi& a, int vw, const int* special, int nspecial, hipStream_t st)
+hipError_t launch_stage1_tiled(const Stage1Multi& a, int vw, const int* special, int nspecial, bool special_only,
+                               hipStream_t st)
 {
     if (a.nds <= 0 || a.npass <= 0) return hipSuccess;
     const size_t lds = stage1_tiled_lds_bytes(a);
@@ -475,17 +490,349 @@ hipError_t launch_stage1_tiled(const Stage1Multi& a, int vw, const int* special,
 #define HD_DISPATCH(C)                                                                                      \
     if (a.cps == C) {                                                                                       \
         switch (a.rd.nbits) {                                                                               \
-        case 8: return calib ? launch_s1<8, C, true>(a, vw, lds, special, nspecial, st)                      \
-                             : launch_s1<8, C, false>(a, vw, lds, special, nspecial, st);                    \
-        case 4: return calib ? launch_s1<4, C, true>(a, vw, lds, special, nspecial, st)                      \
-                             : launch_s1<4, C, false>(a, vw, lds, special, nspecial, st);                    \
-        case 16: return calib ? launch_s1<16, C, true>(a, vw, lds, special, nspecial, st)                    \
-                              : launch_s1<16, C, false>(a, vw, lds, special, nspecial, st);                  \
+        case 8: return calib ? launch_s1<8, C, true>(a, vw, lds, special, nspecial, special_only, st)                      \
+                             : launch_s1<8, C, false>(a, vw, lds, special, nspecial, special_only, st);                    \
+        case 4: return calib ? launch_s1<4, C, true>(a, vw, lds, special, nspecial, special_only, st)                      \
+                             : launch_s1<4, C, false>(a, vw, lds, special, nspecial, special_only, st);                    \
+        case 16: return calib ? launch_s1<16, C, true>(a, vw, lds, special, nspecial, special_only, st)                    \
+                              : launch_s1<16, C, false>(a, vw, lds, special, nspecial, special_only, st);                  \
         default: return hipErrorInvalidValue;                                                               \
         }                                                                                                   \
     }
     HD_S1_FOR_CPS(HD_DISPATCH)
 #undef HD_DISPATCH
+    return hipErrorInvalidValue;
+}
+
+// ------------------------------------------------------------------------------------
+// stage 1, 8-bit integer path (quarter-interleaved LDS tile)
+// ------------------------------------------------------------------------------------
+//
+// For 8-bit data without calibration every stage-1 sum is a sum of small integers, exact
+// in float32, so an integer summation in any order is bit-identical to the oracle's
+// float fold.  The tile of a workgroup (sg subbands = G = sg*CPS channels) holds, per
+// channel, K = S + dmax dwords; dword k packs the bytes of raw rows k, k+S, k+2S, k+3S
+// (one per "quarter" of the tile).  Any delay d then reads whole, aligned dwords: the
+// lane that owns quarter-position j reads dword j*DS + k + d and gets 4 samples, one per
+// quarter, with one ds_read_b32.  Bytes are widened into two packed u16 accumulators
+// (quarters 0/2 and 1/3; the host guarantees CPS*DS*255 < 32768, so no half can carry):
+// ~3 VALU per 4 channel-samples instead of ~2 per sample on the float path.
+// Subbands with masked channels in the tile (rfifind FAST mode) take an exact path: the
+// integer prefix up to the first zapped channel, then the oracle's float fold.  Tiles
+// straddling a mask interval boundary, and the last tile, are left to the float kernel
+// above (its SPECIAL launch over the same tiles).
+
+template <int DS>
+struct Q8Geom {
+    static constexpr int M = DS == 1 ? 4 : DS == 2 ? 2 : 1;   // outputs per lane per quarter
+    static constexpr int JQ = 64 * M;                          // outputs per quarter
+    static constexpr int S = JQ * DS;                          // dwords (raw rows) per quarter
+};
+
+int stage1_q8_quarter_rows(int ds)
+{
+    switch (ds) {
+    case 1: return Q8Geom<1>::S;
+    case 2: return Q8Geom<2>::S;
+    case 3: return Q8Geom<3>::S;
+    case 5: return Q8Geom<5>::S;
+    case 6: return Q8Geom<6>::S;
+    case 10: return Q8Geom<10>::S;
+    default: return 0;
+    }
+}
+
+__device__ __forceinline__ float q8_finish(const Stage1Multi& a, uint32_t v)
+{
+    float x = (float)v;
+    if (a.ds_mode == 1) x = x / (float)a.ds;
+    return x;
+}
+
+// Store the 4 quarter outputs of quarter-position j (integral: exact sums qv; else qf).
+template <int DS>
+__device__ __forceinline__ void q8_store(const Stage1Multi& a, int p, int s, int64_t tO0, int j,
+                                         const uint32_t* qv, const float* qf, bool integral, int& amax)
+{
+    constexpr int JQ = Q8Geom<DS>::JQ;
+    if (a.sub_dtype == 0) {
+        int16_t* o = (int16_t*)a.out[p] + (int64_t)s * a.out_stride + tO0 + j;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            int16_t v;
+            if (integral && a.ds_mode == 0) v = (int16_t)qv[q];     // < 32768 (host check)
+            else v = quant_i16(integral ? q8_finish(a, qv[q]) : qf[q]);
+            o[q * JQ] = v;
+            amax = max(amax, v < 0 ? -(int)v : (int)v);
+        }
+    } else {
+        float* o = (float*)a.out[p] + (int64_t)s * a.out_stride + tO0 + j;
+#pragma unroll
+        for (int q = 0; q < 4; q++) o[q * JQ] = integral ? q8_finish(a, qv[q]) : qf[q];
+    }
+}
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+template <int CPS, int DS, int VB>
+__global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
+{
+    using Gm = Q8Geom<DS>;
+    constexpr int M = Gm::M, JQ = Gm::JQ, S = Gm::S;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    uint32_t* lds = (uint32_t*)smem;
+    const int G = a.sg * CPS;
+    const int logical = xcd_remap(blockIdx.x, gridDim.x);
+    const int tile = logical / a.ngroups;
+    const int g = logical - tile * a.ngroups;
+    const int64_t tO0 = (int64_t)tile * (4 * JQ);
+    const int64_t tR0 = tO0 * DS;
+    if (s1_special(a, tR0, 4 * S + a.dmax)) return;     // uniform: the float kernel's SPECIAL launch
+    const int K = S + a.dmax;
+    const int W = a.W;
+    const int c0 = g * G;
+    const int rc_lo = a.rd.flip ? a.rd.nchan - c0 - G : c0;
+    const int64_t rb = a.rd.rowbytes;
+
+    // ---- fill: unit = (row k, VB-byte chunk): raw rows k + qS (q < 4) -> VB channel dwords;
+    //      two units per iteration so eight row loads are in flight per thread
+    {
+        const uint8_t* src0 = a.rd.raw + tR0 * rb + rc_lo;
+        const int NCH = G / VB;
+        const int units = K * NCH;
+        const int nthr = blockDim.x;
+        for (int u0 = threadIdx.x; u0 < units; u0 += 2 * nthr) {
+            uint32_t r[2][4][VB / 4];
+            int kk[2], cc[2];
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int u = min(u0 + h * nthr, units - 1);     // duplicate (idempotent) tail unit
+                kk[h] = u / NCH;
+                cc[h] = u - kk[h] * NCH;
+                const uint8_t* sp = src0 + (int64_t)kk[h] * rb + cc[h] * VB;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const uint8_t* sq = sp + (int64_t)q * S * rb;
+                    if constexpr (VB == 8) {
+                        const uint2 v = *(const uint2*)sq;
+                        r[h][q][0] = v.x;
+                        r[h][q][1] = v.y;
+                    } else {
+                        r[h][q][0] = *(const uint32_t*)sq;
+                    }
+                }
+            }
+#pragma unroll
+            for (int h = 0; h < 2; h++)
+#pragma unroll
+                for (int i = 0; i < VB / 4; i++) {
+                    // 4x4 byte transpose: dword j of the output = channel 4i+j of rows q = 0..3
+                    const uint32_t ab_lo = __builtin_amdgcn_perm(r[h][1][i], r[h][0][i], 0x05010400u);
+                    const uint32_t ab_hi = __builtin_amdgcn_perm(r[h][1][i], r[h][0][i], 0x07030602u);
+                    const uint32_t cd_lo = __builtin_amdgcn_perm(r[h][3][i], r[h][2][i], 0x05010400u);
+                    const uint32_t cd_hi = __builtin_amdgcn_perm(r[h][3][i], r[h][2][i], 0x07030602u);
+                    uint32_t* d = lds + (cc[h] * VB + 4 * i) * W + kk[h];
+                    d[0] = __builtin_amdgcn_perm(cd_lo, ab_lo, 0x05040100u);
+                    d[W] = __builtin_amdgcn_perm(cd_lo, ab_lo, 0x07060302u);
+                    d[2 * W] = __builtin_amdgcn_perm(cd_hi, ab_hi, 0x05040100u);
+                    d[3 * W] = __builtin_amdgcn_perm(cd_hi, ab_hi, 0x07060302u);
+                }
+        }
+    }
+    __syncthreads();
+
+    // ---- per-wave subband state (wave = subband)
+    const int sl = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int s = g * a.sg + sl;
+    const int cl0 = sl * CPS;
+    int lrb[CPS];
+    float pad[CPS];
+    // rfifind mask: the tile lies in interval iv0, or straddles iv0 | iv0+1 at row brow
+    uint32_t z0 = 0, z1 = 0;
+    int brow = 1 << 30;
+    int64_t iv0 = 0;
+    if (a.rd.mask) {
+        iv0 = tR0 / a.rd.ptsperint;
+        const int64_t b = (iv0 + 1) * a.rd.ptsperint - tR0;
+        if (b < 4 * S + a.dmax) brow = (int)b;
+    }
+#pragma unroll
+    for (int cc = 0; cc < CPS; cc++) {
+        const int c = c0 + cl0 + cc;
+        const int lr = a.rd.flip ? G - 1 - (cl0 + cc) : cl0 + cc;
+        lrb[cc] = lr * W;
+        pad[cc] = a.rd.padvals ? a.rd.padvals[c] : 0.0f;
+        if (a.rd.mask) {
+            if (iv0 < a.rd.numint && a.rd.mask[iv0 * a.rd.nchan + c]) z0 |= 1u << cc;
+            if (brow < (1 << 30) && iv0 + 1 < a.rd.numint && a.rd.mask[(iv0 + 1) * a.rd.nchan + c]) z1 |= 1u << cc;
+        }
+    }
+    if (brow >= (1 << 30)) z1 = z0;
+    z0 = __builtin_amdgcn_readfirstlane(z0);
+    z1 = __builtin_amdgcn_readfirstlane(z1);
+    const uint32_t zany = z0 | z1, zall = z0 & z1, zsplit = z0 ^ z1;
+    const int fz = zany ? __builtin_ctz(zany) : CPS;      // first channel off the integer path
+    const uint32_t* lbase = lds + lane * DS;
+    const bool fast_out = a.sub_dtype == 0 && a.ds_mode == 0;
+    // channel delays of pass p live in lanes 0..CPS-1 of vd; pass p+1's are loaded while
+    // pass p is formed, so no global-load latency sits at the head of a pass
+    int vd = lane < CPS ? a.dly[0][c0 + cl0 + lane] : 0;
+
+    for (int p = 0; p < a.npass; p++) {
+        const int vd_next = (lane < CPS && p + 1 < a.npass) ? a.dly[p + 1][c0 + cl0 + lane] : 0;
+        int dl[CPS];
+#pragma unroll
+        for (int cc = 0; cc < CPS; cc++) dl[cc] = __builtin_amdgcn_readlane(vd, cc);
+        int amax = 0;
+        if (zany == 0) {
+            uint32_t ae[M], ao[M];
+#pragma unroll
+            for (int m = 0; m < M; m++) ae[m] = ao[m] = 0;
+#pragma unroll
+            for (int cc = 0; cc < CPS; cc++) {
+                const uint32_t* b = lbase + lrb[cc] + dl[cc];
+#pragma unroll
+                for (int m = 0; m < M; m++)
+#pragma unroll
+                    for (int k = 0; k < DS; k++) {
+                        const uint32_t x = b[m * 64 * DS + k];
+                        ae[m] += x & 0x00FF00FFu;                              // quarters 0, 2
+                        ao[m] += __builtin_amdgcn_perm(0u, x, 0x0c030c01u);    // quarters 1, 3
+                    }
+            }
+            if (fast_out) {   // int16 sums (< 32768: host check): store the u16 halves directly
+                u16x2 mx = {0, 0};
+                int16_t* o = (int16_t*)a.out[p] + (int64_t)s * a.out_stride + tO0 + lane;
+#pragma unroll
+                for (int m = 0; m < M; m++) {
+                    o[64 * m] = (int16_t)(ae[m] & 0xFFFFu);
+                    o[64 * m + JQ] = (int16_t)(ao[m] & 0xFFFFu);
+                    o[64 * m + 2 * JQ] = (int16_t)(ae[m] >> 16);
+                    o[64 * m + 3 * JQ] = (int16_t)(ao[m] >> 16);
+                    mx = __builtin_elementwise_max(mx, __builtin_bit_cast(u16x2, ae[m]));
+                    mx = __builtin_elementwise_max(mx, __builtin_bit_cast(u16x2, ao[m]));
+                }
+                amax = max((int)mx.x, (int)mx.y);
+            } else {
+#pragma unroll
+                for (int m = 0; m < M; m++) {
+                    const uint32_t qv[4] = {ae[m] & 0xFFFFu, ao[m] & 0xFFFFu, ae[m] >> 16, ao[m] >> 16};
+                    q8_store<DS>(a, p, s, tO0, lane + 64 * m, qv, nullptr, true, amax);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int m = 0; m < M; m++) {
+                float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+                for (int k = 0; k < DS; k++) {
+                    // oracle order: sk folds the channels from 0.0f; integer (exact) until the
+                    // first masked channel, then the float fold
+                    const int t = (lane + 64 * m) * DS + k;    // quarter-relative raw row
+                    uint32_t pe = 0, po = 0;
+                    float sk[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+                    for (int cc = 0; cc < CPS; cc++) {
+                        if (cc < fz) {
+                            const uint32_t x = lbase[lrb[cc] + dl[cc] + m * 64 * DS + k];
+                            pe += x & 0x00FF00FFu;
+                            po += __builtin_amdgcn_perm(0u, x, 0x0c030c01u);
+                        } else {
+                            if (cc == fz) {
+                                sk[0] = (float)(pe & 0xFFFFu);
+                                sk[1] = (float)(po & 0xFFFFu);
+                                sk[2] = (float)(pe >> 16);
+                                sk[3] = (float)(po >> 16);
+                            }
+                            if (zall & (1u << cc)) {
+#pragma unroll
+                                for (int q = 0; q < 4; q++) sk[q] += pad[cc];
+                            } else {
+                                const uint32_t x = lbase[lrb[cc] + dl[cc] + m * 64 * DS + k];
+                                float v[4] = {(float)(x & 0xFFu), (float)((x >> 8) & 0xFFu),
+                                              (float)((x >> 16) & 0xFFu), (float)(x >> 24)};
+                                if (zsplit & (1u << cc)) {   // zapped on one side of the interval boundary
+                                    const bool zlo = (z0 >> cc) & 1;
+#pragma unroll
+                                    for (int q = 0; q < 4; q++)
+                                        if ((t + q * S + dl[cc] < brow) == zlo) v[q] = pad[cc];
+                                }
+#pragma unroll
+                                for (int q = 0; q < 4; q++) sk[q] += v[q];
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int q = 0; q < 4; q++) acc[q] += sk[q];
+                }
+                if (a.ds_mode == 1)
+#pragma unroll
+                    for (int q = 0; q < 4; q++) acc[q] = acc[q] / (float)DS;
+                q8_store<DS>(a, p, s, tO0, lane + 64 * m, nullptr, acc, false, amax);
+            }
+        }
+        if (a.sub_dtype == 0) {
+            amax = wave_max_i32(amax);
+            if (lane == 0) publish_max(a.maxabs[p], amax);
+        }
+        vd = vd_next;
+    }
+}
+
+size_t stage1_q8_lds_bytes(const Stage1Multi& a) { return (size_t)a.sg * a.cps * a.W * 4; }
+
+template <int CPS, int DS>
+static hipError_t launch_q8_ds(const Stage1Multi& a, int vb, size_t lds, hipStream_t st)
+{
+    const dim3 block((unsigned)(64 * a.sg)), grid((unsigned)(a.ntiles * a.ngroups));
+    if (vb == 8) hipLaunchKernelGGL((k_stage1_q8<CPS, DS, 8>), grid, block, lds, st, a);
+    else hipLaunchKernelGGL((k_stage1_q8<CPS, DS, 4>), grid, block, lds, st, a);
+    return hipGetLastError();
+}
+
+template <int CPS, int DS>
+static hipError_t set_lds_q8_ds(int bytes)
+{
+    hipError_t e = hipFuncSetAttribute((const void*)k_stage1_q8<CPS, DS, 8>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute((const void*)k_stage1_q8<CPS, DS, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                bytes);
+    return e;
+}
+
+#define HD_Q8_FOR_CPS(X) X(10) X(8) X(16)
+#define HD_Q8_FOR_DS(C, X) X(C, 1) X(C, 2) X(C, 3) X(C, 5) X(C, 6) X(C, 10)
+
+bool stage1_q8_supports(int cps, int ds)
+{
+    return (cps == 10 || cps == 8 || cps == 16) && stage1_q8_quarter_rows(ds) > 0 && cps * ds * 255 < 32768;
+}
+
+hipError_t stage1_q8_set_lds_limit(size_t bytes)
+{
+    hipError_t e = hipSuccess;
+    const int b = (int)bytes;
+#define HD_SETQ(C, D) \
+    if (e == hipSuccess) e = set_lds_q8_ds<C, D>(b);
+#define HD_SETQC(C) HD_Q8_FOR_DS(C, HD_SETQ)
+    HD_Q8_FOR_CPS(HD_SETQC)
+#undef HD_SETQC
+#undef HD_SETQ
+    return e;
+}
+
+hipError_t launch_stage1_q8(const Stage1Multi& a, int vb, hipStream_t st)
+{
+    if (a.nds <= 0 || a.npass <= 0 || a.ntiles <= 0) return hipSuccess;
+    const size_t lds = stage1_q8_lds_bytes(a);
+#define HD_LQ(C, D) \
+    if (a.cps == C && a.ds == D) return launch_q8_ds<C, D>(a, vb, lds, st);
+#define HD_LQC(C) HD_Q8_FOR_DS(C, HD_LQ)
+    HD_Q8_FOR_CPS(HD_LQC)
+#undef HD_LQC
+#undef HD_LQ
     return hipErrorInvalidValue;
 }
 
@@ -735,6 +1082,274 @@ hipError_t launch_stage2_lds(const Stage2Args& a, int q, hipStream_t st)
     case 24: return launch_lds_q<24>(a, a.off, nyblk, st);
     default: return hipErrorInvalidValue;
     }
+}
+
+// ------------------------------------------------------------------------------------
+// stage 2, wide LDS tiles (int16 subbands)
+// ------------------------------------------------------------------------------------
+//
+// Workgroup = NW <= 8 waves; wave w owns DMs w*Q .. w*Q+Q-1 of the y-block and all waves
+// share one tile of T = 256*R output samples, so every subband window staged in LDS (the
+// same 4 shifted copies as k_stage2_lds) serves NW*Q DMs -- up to 80, a whole PALFA pass.
+// Lane l owns samples t0 + 256r + 4l + i (r < R, i < 4): for one (subband, DM) its R
+// ds_read_b64 share one address at immediate offsets 512r, so the per-pair address work
+// (v_readlane of the host-built byte offset + v_add) is paid once per R reads.  Eight waves
+// of up to 256 VGPRs (two per SIMD) rather than sixteen of 128: the accumulators of Q*R*4
+// samples stay in registers with room left for several LDS reads in flight.  Subbands are
+// staged sc (<= kSC2) at a time into one of two LDS buffers: chunk c+1's global loads are
+// issued before chunk c is accumulated and written to the other buffer after it (one barrier
+// per chunk).  Accumulation is packed int16 widened to int32 every G subbands, as above.
+
+template <int Q, int R>
+__global__ __launch_bounds__(512) void k_stage2_wide(Stage2Args a, const int32_t* __restrict__ boff)
+{
+    extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+    int16_t* lds = (int16_t*)lds_raw;
+    constexpr int T = 256 * R;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t t0 = (int64_t)tile * T;
+    const int yb = blockIdx.y;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nthr = blockDim.x;
+    const int dpb = a.dms_per_blk;
+    const int dblk0 = yb * dpb;
+    const int ws = a.wstride;        // elements per shifted copy (multiple of 4)
+    const int upw = ws >> 2;         // fill units (4 window positions) per subband
+    const int sc = a.sc;             // subbands per chunk (<= kSC2)
+    const int16_t* sub = (const int16_t*)a.sub;
+    const int32_t* omin = a.omin + (int64_t)yb * a.nsub;
+    const int32_t* bo = boff + (int64_t)yb * a.nsub * dpb + wave * Q;
+    const int nchunk = (a.nsub + sc - 1) / sc;
+
+    int maxabs = *a.maxabs;
+    maxabs = maxabs < 1 ? 1 : maxabs;
+    int G = 32767 / maxabs;
+    G = G < 1 ? 1 : (G > 64 ? 64 : G);
+    G = __builtin_amdgcn_readfirstlane(G);
+
+    int acc32[Q][R][4];
+    short2v acc16[Q][R][2];
+#pragma unroll
+    for (int q = 0; q < Q; q++)
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) acc32[q][r][j] = 0;
+            acc16[q][r][0] = short2v{0, 0};
+            acc16[q][r][1] = short2v{0, 0};
+        }
+    int gcount = 0;
+    const uint32_t lane_byte = (uint32_t)lane * 8u;
+
+    // fill unit u = sl * upw + uu of a chunk: 4 window positions of subband sl, from 8
+    // subband samples (4 dwords); the first kUMax units of a thread are prefetched
+    int usl[kUMax], uuu[kUMax];
+#pragma unroll
+    for (int i = 0; i < kUMax; i++) {
+        const int u = threadIdx.x + i * nthr;
+        usl[i] = u / upw;
+        uuu[i] = u - usl[i] * upw;
+    }
+    auto load_unit = [&](int s, int uu, uint32_t* D) -> int {
+        const int64_t wbeg = t0 + omin[s];
+        const int p = (int)(wbeg & 1);
+        const int16_t* srow = sub + (int64_t)s * a.sub_stride;
+        const int64_t e0 = wbeg + 4 * uu - p;
+        if (e0 + 8 <= a.nds) {
+            const uint32_t* src = (const uint32_t*)(srow + e0);
+#pragma unroll
+            for (int j = 0; j < 4; j++) D[j] = src[j];
+        } else {   // past the end of the subbands: zeros
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int64_t e = e0 + 2 * j;
+                const uint32_t lo = e < a.nds ? (uint16_t)srow[e] : 0u;
+                const uint32_t hi = e + 1 < a.nds ? (uint16_t)srow[e + 1] : 0u;
+                D[j] = lo | (hi << 16);
+            }
+        }
+        return p;
+    };
+    auto store_unit = [&](int16_t* buf, int sl, int u, const uint32_t* Di, int p) {
+        uint2* dst0 = (uint2*)(buf + (sl * 4) * ws);
+#define HD_PAIR(h) (((h) & 1) ? __builtin_amdgcn_alignbit(Di[((h) + 1) >> 1], Di[(h) >> 1], 16) : Di[(h) >> 1])
+        if (p == 0) {
+            dst0[u] = make_uint2(HD_PAIR(0), HD_PAIR(2));
+            dst0[upw + u] = make_uint2(HD_PAIR(1), HD_PAIR(3));
+            dst0[2 * upw + u] = make_uint2(HD_PAIR(2), HD_PAIR(4));
+            dst0[3 * upw + u] = make_uint2(HD_PAIR(3), HD_PAIR(5));
+        } else {
+            dst0[u] = make_uint2(HD_PAIR(1), HD_PAIR(3));
+            dst0[upw + u] = make_uint2(HD_PAIR(2), HD_PAIR(4));
+            dst0[2 * upw + u] = make_uint2(HD_PAIR(3), HD_PAIR(5));
+            dst0[3 * upw + u] = make_uint2(HD_PAIR(4), HD_PAIR(6));
+        }
+#undef HD_PAIR
+    };
+    uint32_t D[kUMax][4];
+    int pbit = 0;
+    auto fetch = [&](int c) {
+        const int s0 = c * sc;
+        const int nsc = min(sc, a.nsub - s0);
+        pbit = 0;
+#pragma unroll
+        for (int i = 0; i < kUMax; i++)
+            if (usl[i] < nsc) pbit |= load_unit(s0 + usl[i], uuu[i], D[i]) << i;
+    };
+    auto put = [&](int c) {
+        const int s0 = c * sc;
+        const int nsc = min(sc, a.nsub - s0);
+        int16_t* buf = lds + (c & 1) * (sc * 4 * ws);
+#pragma unroll
+        for (int i = 0; i < kUMax; i++)
+            if (usl[i] < nsc) store_unit(buf, usl[i], uuu[i], D[i], (pbit >> i) & 1);
+        // units beyond the prefetched ones (wide windows only): synchronous
+        for (int u = threadIdx.x + kUMax * nthr; u < nsc * upw; u += nthr) {
+            const int sl = u / upw, uu = u - (u / upw) * upw;
+            uint32_t E[4];
+            const int p = load_unit(s0 + sl, uu, E);
+            store_unit(buf, sl, uu, E, p);
+        }
+    };
+    // the chunk's (subband, DM) byte offsets: entry e = sl*Q + q in lane e&63 of voff[e>>6]
+    constexpr int NR = (kSC2 * Q + 63) / 64;
+    auto load_voff = [&](int c, int (&v)[NR]) {
+        const int s0 = c * sc;
+        const int nsc = min(sc, a.nsub - s0);
+#pragma unroll
+        for (int i = 0; i < NR; i++) {
+            const int e = i * 64 + lane;
+            const int sl = e / Q, q = e - (e / Q) * Q;
+            v[i] = (sl < nsc) ? bo[(int64_t)(s0 + sl) * dpb + q] : 0;
+        }
+    };
+
+    int voff[NR], voff_nxt[NR];
+    load_voff(0, voff);
+    fetch(0);
+    put(0);
+    __syncthreads();
+    for (int c = 0; c < nchunk; c++) {
+        const bool more = c + 1 < nchunk;
+#pragma unroll
+        for (int i = 0; i < NR; i++) voff_nxt[i] = 0;
+        if (more) {
+            load_voff(c + 1, voff_nxt);
+            fetch(c + 1);
+        }
+        const int nsc = min(sc, a.nsub - c * sc);
+#pragma unroll
+        for (int sl = 0; sl < kSC2; sl++) {
+            if (sl < nsc) {
+#pragma unroll
+                for (int q = 0; q < Q; q++) {
+                    const int e = sl * Q + q;
+                    const uint32_t addr = (uint32_t)__builtin_amdgcn_readlane(voff[e >> 6], e & 63) + lane_byte;
+#pragma unroll
+                    for (int r = 0; r < R; r++) {
+                        const uint2 v = *(const uint2*)(lds_raw + addr + 512 * r);
+                        acc16[q][r][0] += __builtin_bit_cast(short2v, v.x);
+                        acc16[q][r][1] += __builtin_bit_cast(short2v, v.y);
+                    }
+                }
+                if (++gcount == G) {
+                    gcount = 0;
+#pragma unroll
+                    for (int q = 0; q < Q; q++)
+#pragma unroll
+                        for (int r = 0; r < R; r++) {
+                            acc32[q][r][0] += acc16[q][r][0].x;
+                            acc32[q][r][1] += acc16[q][r][0].y;
+                            acc32[q][r][2] += acc16[q][r][1].x;
+                            acc32[q][r][3] += acc16[q][r][1].y;
+                            acc16[q][r][0] = short2v{0, 0};
+                            acc16[q][r][1] = short2v{0, 0};
+                        }
+                }
+            }
+        }
+        if (more) put(c + 1);
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < NR; i++) voff[i] = voff_nxt[i];
+    }
+
+    // ---- finish, store, per-tile partial sums
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+        const int dl = wave * Q + q;
+        const int d = dblk0 + dl;
+        const bool dv = dl < dpb && d < a.numdms;
+        int64_t part = 0;
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            acc32[q][r][0] += acc16[q][r][0].x;
+            acc32[q][r][1] += acc16[q][r][0].y;
+            acc32[q][r][2] += acc16[q][r][1].x;
+            acc32[q][r][3] += acc16[q][r][1].y;
+            const int64_t tl = t0 + 256 * r + 4 * lane;
+            if (dv) {
+                float* o = a.out + (int64_t)d * a.out_stride + tl;
+                if (tl + 3 < a.nvalid) {
+                    *(float4*)o = make_float4((float)acc32[q][r][0], (float)acc32[q][r][1], (float)acc32[q][r][2],
+                                              (float)acc32[q][r][3]);
+                    part += (int64_t)acc32[q][r][0] + acc32[q][r][1] + acc32[q][r][2] + acc32[q][r][3];
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        if (tl + j < a.nvalid) {
+                            o[j] = (float)acc32[q][r][j];
+                            part += acc32[q][r][j];
+                        }
+                }
+            }
+        }
+        if (dv && a.partial) {
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) part += __shfl_xor(part, m, 64);
+            if (lane == 0) a.partial[(int64_t)d * a.ntiles + tile] = (double)part;
+        }
+    }
+}
+
+size_t stage2_wide_lds_bytes(int wstride, int sc) { return (size_t)2 * sc * 4 * wstride * sizeof(int16_t); }
+
+template <int Q, int R>
+static hipError_t launch_wide_qr(const Stage2Args& a, int nw, int nyblk, hipStream_t st)
+{
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_stage2_wide<Q, R>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           160 * 1024);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    const unsigned ntiles = (unsigned)((a.nvalid + 256 * R - 1) / (256 * R));
+    hipLaunchKernelGGL((k_stage2_wide<Q, R>), dim3(ntiles, (unsigned)nyblk), dim3((unsigned)(64 * nw)),
+                       stage2_wide_lds_bytes(a.wstride, a.sc), st, a, a.off);
+    return hipGetLastError();
+}
+
+#define HD_WIDE_QR(X) X(10, 3) X(8, 3) X(6, 4) X(4, 4) X(2, 4)
+
+bool stage2_wide_supports(int q, int r)
+{
+#define HD_WS(QQ, RR) if (q == QQ && r == RR) return true;
+    HD_WIDE_QR(HD_WS)
+#undef HD_WS
+    return false;
+}
+
+// boff is passed through Stage2Args.off (host-built [nyblk][nsub][nw*Q] byte offsets).
+hipError_t launch_stage2_wide(const Stage2Args& a, int q, int r, int nw, hipStream_t st)
+{
+    if (a.nvalid <= 0) return hipSuccess;
+    const int nyblk = (a.numdms + a.dms_per_blk - 1) / a.dms_per_blk;
+#define HD_WL(QQ, RR) if (q == QQ && r == RR) return launch_wide_qr<QQ, RR>(a, nw, nyblk, st);
+    HD_WIDE_QR(HD_WL)
+#undef HD_WL
+    return hipErrorInvalidValue;
 }
 
 // ------------------------------------------------------------------------------------

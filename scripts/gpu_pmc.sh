@@ -1,17 +1,18 @@
 #!/bin/bash
-# PMC passes (each its own rocprofv3 run; counters only with --kernel-trace, never with sys/runtime traces).
+# PMC passes (each its own rocprofv3 run; counters only with --kernel-trace, never with
+# sys/runtime traces).  Stops at the first failing pass.
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out/pmc
 B="python3 bench.py --steps 1 --warmup 0 --no-cpu"
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pmc/sq -o sq \
-  --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES \
-  -- $B > gpurun_out/pmc/sq.log 2>&1 && \
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pmc/sq2 -o sq2 \
-  --pmc SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_LDS SQ_INSTS_SMEM \
-  -- $B > gpurun_out/pmc/sq2.log 2>&1 && \
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pmc/fetch -o fetch --pmc FETCH_SIZE \
-  -- $B > gpurun_out/pmc/fetch.log 2>&1 && \
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pmc/write -o write --pmc WRITE_SIZE \
-  -- $B > gpurun_out/pmc/write.log 2>&1
-echo "pmc rc=$?"
+run() {  # name counters...
+  local n=$1; shift
+  timeout -s KILL 240 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pmc/$n -o $n --pmc "$@" -- $B \
+    > gpurun_out/pmc/$n.log 2>&1 || { echo "pmc pass $n failed"; exit 1; }
+}
+run sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES
+run sq2 SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_LDS SQ_INSTS_SMEM
+run sq3 SQ_LDS_IDX_ACTIVE SQ_LDS_UNALIGNED_STALL SQ_WAIT_INST_ANY SQ_INSTS_VALU_ADD_F32 SQ_INST_CYCLES_VMEM_WR SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH
+run fetch FETCH_SIZE
+run write WRITE_SIZE
+echo "pmc done"

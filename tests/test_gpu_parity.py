@@ -40,7 +40,7 @@ def test_device_synth_bytes_equal_host(engine):
 
 @pytest.mark.parametrize("nbits,flip,ds", [(8, True, 1), (8, False, 2), (4, True, 3), (16, True, 5),
                                           (8, True, 10), (4, False, 6)])
-@pytest.mark.parametrize("s1", [0, 1])
+@pytest.mark.parametrize("s1", [0, 1, 2])
 def test_stage1_bitexact(engine, nbits, flip, ds, s1):
     obs = palfa_obs(N=12288 + 37, nbits=nbits, flip=flip)
     raw = load_beam(engine, obs)
@@ -79,7 +79,7 @@ def test_stage1_calib_mask_bitexact(engine, sub_dtype, ds_mode):
 
 @pytest.mark.parametrize("numdms,ds,numout_mode", [(76, 1, "none"), (64, 2, "none"), (76, 3, "pad"),
                                                    (5, 1, "trunc"), (100, 5, "pad"), (76, 10, "pad")])
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3])
 def test_stage2_bitexact(engine, numdms, ds, numout_mode, variant):
     obs = palfa_obs(N=3 * 8192, nbits=8)
     raw = load_beam(engine, obs)
@@ -98,10 +98,11 @@ def test_stage2_bitexact(engine, numdms, ds, numout_mode, variant):
 
 
 @pytest.mark.parametrize("mask_pts", [0, 256, 32768])
-def test_stage1_multipass_bitexact(engine, mask_pts):
+@pytest.mark.parametrize("s1", [0, 2])
+def test_stage1_multipass_bitexact(engine, mask_pts, s1):
     """One launch forms the subbands of many passes (a DDplan stage) from one raw read;
     every pass must equal its own oracle run.  mask_pts=256 takes the per-row interval path,
-    32768 the two-interval path."""
+    32768 the two-interval path; s1=0 picks the 8-bit integer kernel, 2 the float one."""
     obs = palfa_obs(N=40000, nbits=8)
     s = palfa_synth()
     raw = load_beam(engine, obs, synth=s)
@@ -113,11 +114,50 @@ def test_stage1_multipass_bitexact(engine, mask_pts):
     pps = [PassParams(subdm=float(d.subdmlist[i]), lodm=float(d.lodm_arg(i)), dmstep=d.dmstep,
                       numdms=d.dmsperpass, nsub=96, ds=d.sub_downsamp) for i in range(d.numpasses)]
     plans = [engine.plan(pp) for pp in pps]
+    for p in plans:
+        p.set_variant(s1 << 8)
     engine.run_subband_multi(plans)
     for pp, p in zip(pps, plans):
         want = OR.stage1(obs, Opts(), raw, 96, pp.ds, pp.subdm, mask=mask, ptsperint=mask_pts, padvals=pad)
         assert np.array_equal(p.get_subbands(), want), pp.subdm
     engine.set_mask()
+
+
+@pytest.mark.parametrize("ds", [1, 2, 3, 5, 6, 10])
+@pytest.mark.parametrize("flip,sub_dtype,ds_mode,masked", [(True, 0, 0, True), (False, 0, 1, False),
+                                                          (False, 1, 0, True), (True, 1, 1, True)])
+def test_stage1_int8_path_bitexact(engine, ds, flip, sub_dtype, ds_mode, masked):
+    """8-bit integer stage-1 kernel (variant 3) over 3 passes of one launch: exact integer sums,
+    the integer-prefix + float fold of subbands with zapped channels, and the special tiles
+    (mask-interval straddles, last tile) on the float kernel -- all equal to the oracle."""
+    obs = palfa_obs(N=65536 + 777, nbits=8, flip=flip)
+    opts = Opts(sub_dtype=sub_dtype, ds_mode=ds_mode)
+    s = palfa_synth()
+    raw = load_beam(engine, obs, opts, synth=s)
+    mask = pad = None
+    pts = 16384
+    if masked:
+        mask, pad = synth_mask(obs, s, pts, frac=0.1)
+        engine.set_mask(mask, pts, pad)
+    pps = [PassParams(subdm=sd, lodm=sd - 5.0, dmstep=0.5, numdms=4, nsub=96, ds=ds) for sd in (40.0, 350.0, 1020.0)]
+    plans = [engine.plan(pp) for pp in pps]
+    for p in plans:
+        p.set_variant(3 << 8)
+    engine.run_subband_multi(plans)
+    for pp, p in zip(pps, plans):
+        want = OR.stage1(obs, opts, raw, 96, ds, pp.subdm, mask=mask, ptsperint=pts if masked else 0, padvals=pad)
+        assert np.array_equal(p.get_subbands(), want), pp.subdm
+        p.destroy()
+    engine.set_mask()
+
+
+def test_stage1_int8_variant_rejects_other_data(engine):
+    obs = palfa_obs(N=8192, nbits=4)
+    load_beam(engine, obs)
+    p = engine.plan(PassParams(subdm=10.0, lodm=0.0, dmstep=1.0, numdms=4, nsub=96, ds=1))
+    p.set_variant(3 << 8)
+    with pytest.raises(PrestoError, match="integer path"):
+        p.run_subband()
 
 
 def test_stage2_f32_subbands(engine):
