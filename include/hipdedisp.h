@@ -194,7 +194,10 @@ HD_API int hd_plan_last_ms(const hd_plan* plan, float* ms_subband, float* ms_ded
 /* Kernel variants: (s1 << 8) | s2.  s2: 0 auto, 1 direct, 2 LDS-tiled (4 waves x 256 samples),
  * 3 wide LDS tiles (up to 16 waves share one window); s1: 0 auto, 1 direct
  * (one thread per subband sample, for cross-checks), 2 float tiled multi-pass, 3 8-bit
- * integer tiled multi-pass (8-bit data without calibration only; HD_E_INVAL otherwise). */
+ * integer tiled multi-pass (8-bit data without calibration only; HD_E_INVAL otherwise).
+ * Bits 16-23 are profiling probes that skip parts of the tiled kernels (results are then
+ * invalid; never set them in production): 1 skip the sums, 2 skip the LDS fill, 4 skip
+ * the stage-2 stores. */
 HD_API int hd_plan_set_variant(hd_plan* plan, int32_t variant);
 
 #ifdef __cplusplus

@@ -33,6 +33,7 @@ struct hd_ctx {
     uint8_t* d_mask = nullptr;
     int32_t numint = 0, ptsperint = 0;
     float* d_padvals = nullptr;
+    std::vector<float> h_padvals;      // host copy (bounds for the integer stage-1 path)
     size_t lds_attr_set = 64 * 1024;   // dynamic-LDS limit already granted to the tiled kernels
     size_t lds_attr_q8 = 64 * 1024;    // ... and to the 8-bit integer stage-1 kernels
     struct SpecialList {               // stage-1 special-tile list per tile geometry (device)
@@ -60,17 +61,21 @@ struct hd_plan {
     bool lds_ok = false;
     int32_t* d_omin = nullptr;
     int32_t* d_boff = nullptr;
-    // wide-tile variant tables (k_stage2_wide)
-    int32_t wq = 0, wr = 0, wnw = 0, wdpb = 0, wws = 0, wsc = 0;
-    bool wide_ok = false;
-    int32_t* d_womin = nullptr;
-    int32_t* d_wboff = nullptr;
+    // wide-tile variant tables: [0] k_stage2_wide (16 waves, double-buffered), [1] k_stage2_wide2
+    // (8 waves, two workgroups per CU)
+    struct Wide {
+        bool ok = false;
+        int32_t q = 0, r = 0, nw = 0, dpb = 0, ws = 0, sc = 0;
+        int32_t* d_omin = nullptr;
+        int32_t* d_boff = nullptr;
+    } wide[2];
     int32_t variant = 0;
     float* d_out = nullptr;
     void* d_sub = nullptr;          // this pass's subbands [nsub][sub_stride]
     size_t sub_bytes = 0;
     bool sub_valid = false;
     int32_t s1_variant = 0;         // stage 1: 0 auto, 1 direct, 2 float tiled, 3 8-bit integer
+    int32_t probe = 0;              // profiling switches (hd_plan_set_variant bits 16-23)
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     bool ran_sub = false, ran_dd = false;
 };
@@ -185,6 +190,7 @@ static void free_obs_buffers(hd_ctx* c)
     dfree(c->d_wts); c->d_wts = nullptr;
     dfree(c->d_mask); c->d_mask = nullptr;
     dfree(c->d_padvals); c->d_padvals = nullptr;
+    c->h_padvals.clear();
     clear_special_cache(c);
     c->raw_ready = false;
     c->numint = c->ptsperint = 0;
@@ -302,6 +308,8 @@ extern "C" int hd_set_mask(hd_ctx* c, const uint8_t* mask, int32_t numint, int32
         c->numint = numint;
         c->ptsperint = ptsperint;
     }
+    if (padvals) c->h_padvals.assign(padvals, padvals + c->obs.nchan);
+    else c->h_padvals.clear();
     int rc = upload(c, &c->d_padvals, padvals, c->obs.nchan);
     return rc;
 }
@@ -497,8 +505,10 @@ static void plan_free(hd_plan* p)
     dfree(p->d_maxabs);
     dfree(p->d_omin);
     dfree(p->d_boff);
-    dfree(p->d_womin);
-    dfree(p->d_wboff);
+    for (auto& w : p->wide) {
+        dfree(w.d_omin);
+        dfree(w.d_boff);
+    }
     dfree(p->d_out);
     dfree(p->d_sub);
     for (auto& e : p->ev)
@@ -583,6 +593,69 @@ extern "C" int hd_plan_tables(const hd_obs* o, const hd_opts* opts, const hd_pas
     return HD_OK;
 }
 
+// Tables of a wide-tile stage-2 variant: y-blocks of up to nwmax*5 DMs (nw waves x Q DMs),
+// T = 256*R samples per tile, windows of ws elements per shifted copy, sc subbands per chunk;
+// boff[yb][s][k] = LDS byte offset of DM k's 4 samples for subband s (lane 0).
+static void wide_tables(hd_plan* p, int nwmax, bool dbuf, bool i16, hd_plan::Wide& w, std::vector<int32_t>& omin,
+                        std::vector<int32_t>& boff)
+{
+    const int nsub = p->pass.nsub, numdms = p->pass.numdms;
+    int nyb = (numdms + 5 * nwmax - 1) / (5 * nwmax);
+    const int per = (numdms + nyb - 1) / nyb;
+    const int qneed = (per + nwmax - 1) / nwmax;
+    int Q = 2, R = 4;
+    if (qneed > 4) { Q = 5; R = 3; }
+    else if (qneed > 3) { Q = 4; R = 4; }
+    else if (qneed > 2) { Q = 3; R = 4; }
+    const int nw = (per + Q - 1) / Q;
+    const int dpb = nw * Q;
+    nyb = (numdms + dpb - 1) / dpb;
+    omin.assign((size_t)nyb * nsub, 0);
+    int32_t span = 0;
+    for (int yb = 0; yb < nyb; yb++)
+        for (int s = 0; s < nsub; s++) {
+            int32_t lo = INT32_MAX, hi = INT32_MIN;
+            for (int k = 0; k < dpb; k++) {
+                const int dm = std::min(yb * dpb + k, numdms - 1);
+                const int32_t v = p->off[(size_t)dm * nsub + s];
+                lo = std::min(lo, v);
+                hi = std::max(hi, v);
+            }
+            omin[(size_t)yb * nsub + s] = lo;
+            span = std::max(span, hi - lo);
+        }
+    const int ws = (int)round_up((size_t)(256 * R + span + 4), 4);
+    int sc = 0;
+    for (int pass = 0; pass < 2 && !sc; pass++)
+        for (int cand : {8, 4}) {
+            if (nsub % cand) continue;
+            const size_t lds = dbuf ? hd::stage2_wide_lds_bytes(ws, cand) : hd::stage2_wide2_lds_bytes(ws, cand, nsub);
+            const bool fits = lds <= (size_t)(dbuf || pass ? 160 : 80) * 1024;
+            const bool units = !dbuf || (size_t)cand * (ws / 4) <= (size_t)hd::kUMax * nw * 64;
+            // double-buffered: prefer chunks whose fill units are all prefetched (the overflow is
+            // filled synchronously)
+            if (fits && (units || pass)) { sc = cand; break; }
+        }
+    w = hd_plan::Wide{};
+    w.ok = i16 && nw <= nwmax && hd::stage2_wide_supports(Q, R) && sc > 0;
+    if (!w.ok) return;
+    w.q = Q;
+    w.r = R;
+    w.nw = nw;
+    w.dpb = dpb;
+    w.ws = ws;
+    w.sc = sc;
+    boff.resize((size_t)nyb * nsub * dpb);
+    for (int yb = 0; yb < nyb; yb++)
+        for (int s = 0; s < nsub; s++)
+            for (int k = 0; k < dpb; k++) {
+                const int dm = std::min(yb * dpb + k, numdms - 1);
+                const int32_t o2 = p->off[(size_t)dm * nsub + s] - omin[(size_t)yb * nsub + s];
+                const int32_t buf = dbuf ? (s / sc) & 1 : 0, sl = s % sc;
+                boff[((size_t)yb * nsub + s) * dpb + k] = (((buf * sc + sl) * 4 + (o2 & 3)) * ws + (o2 & ~3)) * 2;
+            }
+}
+
 extern "C" int hd_plan_create(hd_ctx* c, const hd_pass* ps, hd_plan** out)
 {
     if (!c) return fail(nullptr, HD_E_INVAL, "hd_plan_create: NULL context");
@@ -641,67 +714,20 @@ extern "C" int hd_plan_create(hd_ctx* c, const hd_pass* ps, hd_plan** out)
                 boff[((size_t)yb * nsub + s) * p->dpb + k] = ((sl * 4 + (o2 & 3)) * p->wstride + (o2 & ~3)) * 2;
             }
 
-    // wide-tile variant: one y-block of up to 80 DMs (8 waves x Q), T = 256*R samples per tile,
-    // sc subbands per LDS chunk (the largest of 8, 4, 2 whose two buffers fit 160 KiB)
-    std::vector<int32_t> womin, wboff;
-    {
-        int nyb = (ps->numdms + 79) / 80;
-        const int per = (ps->numdms + nyb - 1) / nyb;
-        const int qneed = (per + hd::kWideWaves - 1) / hd::kWideWaves;
-        int Q = 2, R = 4;
-        if (qneed > 8) { Q = 10; R = 3; }
-        else if (qneed > 6) { Q = 8; R = 3; }
-        else if (qneed > 4) { Q = 6; R = 4; }
-        else if (qneed > 2) { Q = 4; R = 4; }
-        const int nw = (per + Q - 1) / Q;
-        const int dpb = nw * Q;
-        nyb = (ps->numdms + dpb - 1) / dpb;
-        womin.assign((size_t)nyb * nsub, 0);
-        int32_t span = 0;
-        for (int yb = 0; yb < nyb; yb++)
-            for (int s = 0; s < nsub; s++) {
-                int32_t lo = INT32_MAX, hi = INT32_MIN;
-                for (int k = 0; k < dpb; k++) {
-                    const int dm = std::min(yb * dpb + k, ps->numdms - 1);
-                    const int32_t v = p->off[(size_t)dm * nsub + s];
-                    lo = std::min(lo, v);
-                    hi = std::max(hi, v);
-                }
-                womin[(size_t)yb * nsub + s] = lo;
-                span = std::max(span, hi - lo);
-            }
-        const int ws = (int)round_up((size_t)(256 * R + span + 4), 4);
-        int sc = 0;
-        for (int cand : {8, 4, 2})
-            if (hd::stage2_wide_lds_bytes(ws, cand) <= 160 * 1024) { sc = cand; break; }
-        p->wide_ok = c->opts.sub_dtype == HD_SUB_I16 && nw <= hd::kWideWaves && hd::stage2_wide_supports(Q, R) && sc > 0;
-        if (p->wide_ok) {
-            p->wq = Q;
-            p->wr = R;
-            p->wnw = nw;
-            p->wdpb = dpb;
-            p->wws = ws;
-            p->wsc = sc;
-            wboff.resize((size_t)nyb * nsub * dpb);
-            for (int yb = 0; yb < nyb; yb++)
-                for (int s = 0; s < nsub; s++)
-                    for (int k = 0; k < dpb; k++) {
-                        const int dm = std::min(yb * dpb + k, ps->numdms - 1);
-                        const int32_t o2 = p->off[(size_t)dm * nsub + s] - womin[(size_t)yb * nsub + s];
-                        const int32_t buf = (s / sc) & 1, sl = s % sc;
-                        wboff[((size_t)yb * nsub + s) * dpb + k] = (((buf * sc + sl) * 4 + (o2 & 3)) * ws + (o2 & ~3)) * 2;
-                    }
-        }
-    }
+    std::vector<int32_t> womin[2], wboff[2];
+    for (int k = 0; k < 2; k++)
+        wide_tables(p, k == 0 ? 16 : 8, k == 0, c->opts.sub_dtype == HD_SUB_I16, p->wide[k], womin[k], wboff[k]);
 
     int rc = HD_OK;
     hipError_t e = hipSetDevice(c->device);
-    if (e == hipSuccess && p->wide_ok) e = hipMalloc(&p->d_womin, sizeof(int32_t) * womin.size());
-    if (e == hipSuccess && p->wide_ok)
-        e = hipMemcpy(p->d_womin, womin.data(), sizeof(int32_t) * womin.size(), hipMemcpyHostToDevice);
-    if (e == hipSuccess && p->wide_ok) e = hipMalloc(&p->d_wboff, sizeof(int32_t) * wboff.size());
-    if (e == hipSuccess && p->wide_ok)
-        e = hipMemcpy(p->d_wboff, wboff.data(), sizeof(int32_t) * wboff.size(), hipMemcpyHostToDevice);
+    for (int k = 0; k < 2 && e == hipSuccess; k++) {
+        hd_plan::Wide& w = p->wide[k];
+        if (!w.ok) continue;
+        e = hipMalloc(&w.d_omin, sizeof(int32_t) * womin[k].size());
+        if (e == hipSuccess) e = hipMemcpy(w.d_omin, womin[k].data(), sizeof(int32_t) * womin[k].size(), hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMalloc(&w.d_boff, sizeof(int32_t) * wboff[k].size());
+        if (e == hipSuccess) e = hipMemcpy(w.d_boff, wboff[k].data(), sizeof(int32_t) * wboff[k].size(), hipMemcpyHostToDevice);
+    }
     if (e == hipSuccess) e = hipMalloc(&p->d_idispdt, sizeof(int32_t) * nchan);
     if (e == hipSuccess) e = hipMemcpy(p->d_idispdt, p->idispdt.data(), sizeof(int32_t) * nchan, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&p->d_off, sizeof(int32_t) * p->off.size());
@@ -758,11 +784,13 @@ extern "C" int hd_plan_set_variant(hd_plan* p, int32_t v)
     // bits 0-7: stage-2 variant (0 auto, 1 direct, 2 LDS, 3 wide LDS); bits 8-15: stage-1 (0 auto, 1 direct,
     // 2 float tiled, 3 8-bit integer tiled)
     const int32_t v1 = (v >> 8) & 0xFF;
+    p->probe = (v >> 16) & 0xFF;     // profiling only (results invalid): see hipdedisp.h
     v &= 0xFF;
-    if (v < 0 || v > 3 || v1 > 3) return fail(p->ctx, HD_E_INVAL, "variant must be (s1<<8)|s2 with s1 in 0..3, s2 in 0..3");
+    if (v < 0 || v > 4 || v1 > 3) return fail(p->ctx, HD_E_INVAL, "variant must be (s1<<8)|s2 with s1 in 0..3, s2 in 0..4");
     p->s1_variant = v1;
     if (v == 2 && !p->lds_ok) return fail(p->ctx, HD_E_INVAL, "LDS variant unavailable for this plan (needs int16 subbands and a window that fits 64 KiB)");
-    if (v == 3 && !p->wide_ok) return fail(p->ctx, HD_E_INVAL, "wide-tile variant unavailable for this plan (needs int16 subbands and a window that fits 160 KiB)");
+    if ((v == 3 && !p->wide[0].ok) || (v == 4 && !p->wide[1].ok))
+        return fail(p->ctx, HD_E_INVAL, "wide-tile variant unavailable for this plan (needs int16 subbands and a window that fits LDS)");
     p->variant = v;
     return HD_OK;
 }
@@ -906,6 +934,16 @@ static bool stage1_q8_tiling(const hd_ctx* c, int nsub, int ds, int dmax, hd::St
     a.W = W;
     a.rs = 0;
     a.two_ok = 1;
+    // bound on the rounding of the oracle's float fold (CPS channel adds per ds step, then
+    // ds adds of the steps) for sums of 8-bit samples and pad values: each add errs by at most
+    // half an ulp of its result; ulps are over-estimated 2x by taking 2^(floor(log2 x) - 22)
+    {
+        double maxpad = 255.0;
+        for (float v : c->h_padvals) maxpad = std::max(maxpad, (double)fabsf(v));
+        const double smax = cps * maxpad, amax = ds * smax;
+        auto ulp2 = [](double x) { return ldexp(1.0, (int)floor(log2(x)) - 22); };
+        a.tie_eps = ds * cps * 0.5 * ulp2(smax) + ds * 0.5 * ulp2(amax);
+    }
     a.ngroups = nsub / sg;
     vb = v;
     return true;
@@ -960,6 +998,7 @@ static int run_subband_chunk(hd_ctx* c, hd_plan** plans, int n)
     for (int i = 0; i < n; i++) HIPCHK(c, hipMemsetAsync(plans[i]->d_maxabs, 0, sizeof(int32_t), c->stream));
     HIPCHK(c, hipEventRecord(p0->ev[0], c->stream));
     if (q8) {
+        m.probe = p0->probe;
         m.rd = raw_desc(c);
         m.npass = n;
         m.nsub = p0->pass.nsub;
@@ -1129,9 +1168,13 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         }
     }
     const bool pad = p->numout > p->nds;
-    const bool use_wide = p->variant == 3 || (p->variant == 0 && p->wide_ok);
+    int wk = -1;                       // wide variant in use (index into p->wide), or -1
+    if (p->variant == 3) wk = 0;
+    else if (p->variant == 4) wk = 1;
+    else if (p->variant == 0) wk = p->wide[0].ok ? 0 : (p->wide[1].ok ? 1 : -1);
+    const bool use_wide = wk >= 0;
     const bool use_lds = !use_wide && (p->variant == 2 || (p->variant == 0 && p->lds_ok));
-    const int tile = use_wide ? 256 * p->wr : kTT;
+    const int tile = use_wide ? 256 * p->wide[wk].r : kTT;
     const int ntiles = (int)((p->nvalid + tile - 1) / tile);
     double* partial = nullptr;
     if (pad && c->opts.pad_mode == HD_PAD_MEAN) {
@@ -1165,12 +1208,15 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
     a.dms_per_blk = p->dpb;
     HIPCHK(c, hipEventRecord(p->ev[2], c->stream));
     if (use_wide) {
-        a.off = p->d_wboff;
-        a.omin = p->d_womin;
-        a.wstride = p->wws;
-        a.dms_per_blk = p->wdpb;
-        a.sc = p->wsc;
-        HIPCHK(c, hd::launch_stage2_wide(a, p->wq, p->wr, p->wnw, c->stream));
+        const hd_plan::Wide& w = p->wide[wk];
+        a.off = w.d_boff;
+        a.omin = w.d_omin;
+        a.wstride = w.ws;
+        a.dms_per_blk = w.dpb;
+        a.sc = w.sc;
+        a.probe = p->probe;
+        if (wk == 0) HIPCHK(c, hd::launch_stage2_wide(a, w.q, w.r, w.nw, c->stream));
+        else HIPCHK(c, hd::launch_stage2_wide2(a, w.q, w.r, w.nw, c->stream));
     } else if (use_lds) {
         a.off = p->d_boff;
         HIPCHK(c, hd::launch_stage2_lds(a, p->q, c->stream));

@@ -46,6 +46,8 @@ struct Stage1Multi {
     int32_t rs;               // LDS bytes per raw row (multiple of 4, odd dword count)
     int32_t W;                // 8-bit integer path: LDS dwords per channel row (>= S + dmax)
     int32_t two_ok;           // tiles straddling one mask-interval boundary are not special
+    int32_t probe;            // profiling only: bit0 skip subband formation, bit1 skip fill
+    double tie_eps;           // 8-bit integer path: bound on |float fold - exact sum| (masked channels)
     int32_t ntiles, ngroups;
     const int32_t* dly[kMaxPass];   // per-pass idispdt [nchan]
     void* out[kMaxPass];            // per-pass subbands [nsub][out_stride]
@@ -67,7 +69,8 @@ struct Stage2Args {
     const int32_t* omin;      // [nyblk][nsub] min offset of the y-block's DMs
     int32_t wstride;          // LDS window stride (elements) per copy
     int32_t dms_per_blk;      // DMs per y-block
-    int32_t sc, _pad2;        // wide variant: subbands per LDS chunk
+    int32_t sc;               // wide variant: subbands per LDS chunk
+    int32_t probe;            // profiling only: bit0 skip accumulation, bit1 skip fill, bit2 skip stores
 };
 
 hipError_t launch_stage1_direct(const Stage1Args& a, hipStream_t st);
@@ -85,11 +88,13 @@ hipError_t stage1_tiled_set_lds_limit(size_t bytes);
 // wide stage-2 tiles: at most kSC2 subbands staged per chunk, kUMax prefetched fill units
 // per thread per chunk, at most kWideWaves waves per workgroup
 constexpr int kSC2 = 8;
-constexpr int kUMax = 4;
-constexpr int kWideWaves = 8;
+constexpr int kUMax = 2;
+constexpr int kWideWaves = 16;
 size_t stage2_wide_lds_bytes(int wstride, int sc);
 bool stage2_wide_supports(int q, int r);
 hipError_t launch_stage2_wide(const Stage2Args& a, int q, int r, int nw, hipStream_t st);
+size_t stage2_wide2_lds_bytes(int wstride, int sc, int nsub);
+hipError_t launch_stage2_wide2(const Stage2Args& a, int q, int r, int nw, hipStream_t st);
 hipError_t launch_stage2_direct(const Stage2Args& a, hipStream_t st);
 hipError_t launch_stage2_lds(const Stage2Args& a, int q, hipStream_t st);
 hipError_t launch_pad(float* out, int64_t out_stride, int numdms, int64_t nds, int64_t numout,

@@ -58,13 +58,15 @@ __device__ __forceinline__ float chan_value(const RawDesc& rd, int64_t t, int c)
 }
 
 // PRESTO NEAREST_LONG, saturated to int16.
+// Evaluated in float, exactly: for a float x, (double)x +- 0.5 is exact, so floor/ceil of
+// it is trunc(x) stepped by one when the (exact) fraction x - trunc(x) reaches +-0.5.
 __device__ __forceinline__ int16_t quant_i16(float x)
 {
-    const double d = (double)x;
-    double r = d < 0 ? ceil(d - 0.5) : floor(d + 0.5);
-    r = r > 32767.0 ? 32767.0 : r;
-    r = r < -32768.0 ? -32768.0 : r;
-    return (int16_t)r;
+    const float t = truncf(x);
+    const float f = x - t;
+    float r = x >= 0.0f ? (f >= 0.5f ? t + 1.0f : t) : (f <= -0.5f ? t - 1.0f : t);
+    r = fminf(fmaxf(r, -32768.0f), 32767.0f);
+    return (int16_t)(int)r;
 }
 
 // Blocks b, b+8, b+16, ... share an XCD (round-robin dispatch; speed only, never
@@ -369,6 +371,7 @@ void k_stage1_tiled(Stage1Multi a, const int* __restrict__ special_tiles)
         any_zap |= z;
     }
     const int lrc0 = a.rd.flip ? G - 1 - cl0 : cl0;   // local raw index of channel cc=0
+    int pmax = 0;                                      // lane p: max |subband| of pass p
     for (int p = 0; p < a.npass; p++) {
 #pragma unroll
         for (int cc = 0; cc < CPS; cc++) {
@@ -399,9 +402,12 @@ void k_stage1_tiled(Stage1Multi a, const int* __restrict__ special_tiles)
         }
         if (a.sub_dtype == 0) {
             amax = wave_max_i32(amax);
-            if (lane == 0) publish_max(a.maxabs[p], amax);
+            pmax = lane == p ? amax : pmax;
         }
     }
+    // one publication per pass at the end: a load-tested atomic inside the pass loop would
+    // make the wave wait for all of its outstanding stores every pass
+    if (a.sub_dtype == 0 && lane < a.npass) publish_max(a.maxabs[lane], pmax);
 }
 
 size_t stage1_tiled_lds_bytes(const Stage1Multi& a)
@@ -573,6 +579,7 @@ __device__ __forceinline__ void q8_store(const Stage1Multi& a, int p, int s, int
 }
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <int CPS, int DS, int VB>
 __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
@@ -595,17 +602,19 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
     const int64_t rb = a.rd.rowbytes;
 
     // ---- fill: unit = (row k, VB-byte chunk): raw rows k + qS (q < 4) -> VB channel dwords;
-    //      two units per iteration so eight row loads are in flight per thread
-    {
+    //      U units per iteration, all their row loads issued before the first is used (the
+    //      fill is latency-bound: a CU needs tens of KB of loads in flight)
+    if (!(a.probe & 2)) {
+        constexpr int U = 32 / VB;
         const uint8_t* src0 = a.rd.raw + tR0 * rb + rc_lo;
         const int NCH = G / VB;
         const int units = K * NCH;
         const int nthr = blockDim.x;
-        for (int u0 = threadIdx.x; u0 < units; u0 += 2 * nthr) {
-            uint32_t r[2][4][VB / 4];
-            int kk[2], cc[2];
+        for (int u0 = threadIdx.x; u0 < units; u0 += U * nthr) {
+            uint32_t r[U][4][VB / 4];
+            int kk[U], cc[U];
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
+            for (int h = 0; h < U; h++) {
                 const int u = min(u0 + h * nthr, units - 1);     // duplicate (idempotent) tail unit
                 kk[h] = u / NCH;
                 cc[h] = u - kk[h] * NCH;
@@ -623,7 +632,7 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
                 }
             }
 #pragma unroll
-            for (int h = 0; h < 2; h++)
+            for (int h = 0; h < U; h++)
 #pragma unroll
                 for (int i = 0; i < VB / 4; i++) {
                     // 4x4 byte transpose: dword j of the output = channel 4i+j of rows q = 0..3
@@ -675,22 +684,57 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
     const int fz = zany ? __builtin_ctz(zany) : CPS;      // first channel off the integer path
     const uint32_t* lbase = lds + lane * DS;
     const bool fast_out = a.sub_dtype == 0 && a.ds_mode == 0;
+    // Masked channels without a float fold.  With int16 sums (sum mode), a subband whose
+    // masked channels are masked for the whole tile outputs NEAREST(F), F = the oracle's float
+    // fold of integers and pad values.  The exact sum is R = I + DS*P (I: integer sum of the
+    // unmasked channels, P: sum of the masked channels' pads, exact in double) and
+    // |F - R| <= a.tie_eps (host bound on the fold's rounding), so while frac(DS*P) stays
+    // further than tie_eps from 1/2, NEAREST(F) = I + floor(DS*P + 1/2) (R >= 0): the integer
+    // path plus a per-tile constant.  Near-ties, split (two-interval) channels, negative pads
+    // and the other output modes take the exact float fold below.
+    int cadd = 0;
+    bool intpath = zany == 0;
+    if (zany && zsplit == 0 && fast_out) {
+        double P = 0.0;
+        bool neg = false;
+#pragma unroll
+        for (int cc = 0; cc < CPS; cc++)
+            if (zall & (1u << cc)) {
+                P += (double)pad[cc];
+                neg |= pad[cc] < 0.0f;
+            }
+        const double Rp = (double)DS * P;
+        const double fr = Rp - floor(Rp);
+        const double cd = floor(Rp + 0.5);
+        if (!neg && fabs(fr - 0.5) > a.tie_eps && cd + (double)(CPS * DS * 255) <= 32767.0) {
+            intpath = true;
+            cadd = (int)cd;
+        }
+    }
+    intpath = __builtin_amdgcn_readfirstlane((int)intpath) != 0;
+    cadd = __builtin_amdgcn_readfirstlane(cadd);
+    const uint32_t cpack = (uint32_t)cadd * 0x00010001u;
     // channel delays of pass p live in lanes 0..CPS-1 of vd; pass p+1's are loaded while
     // pass p is formed, so no global-load latency sits at the head of a pass
-    int vd = lane < CPS ? a.dly[0][c0 + cl0 + lane] : 0;
+    // (unconditional, clamped loads: a branch around them would cost a vmcnt(0) drain)
+    const int dlane = c0 + cl0 + min(lane, CPS - 1);
+    int vd = a.dly[0][dlane];
+    int pmax = 0;                                         // lane p: max |subband| of pass p
 
-    for (int p = 0; p < a.npass; p++) {
-        const int vd_next = (lane < CPS && p + 1 < a.npass) ? a.dly[p + 1][c0 + cl0 + lane] : 0;
+    const int npass = (a.probe & 1) ? 0 : a.npass;
+    for (int p = 0; p < npass; p++) {
+        const int vd_next = a.dly[min(p + 1, a.npass - 1)][dlane];
         int dl[CPS];
 #pragma unroll
         for (int cc = 0; cc < CPS; cc++) dl[cc] = __builtin_amdgcn_readlane(vd, cc);
         int amax = 0;
-        if (zany == 0) {
+        if (intpath) {
             uint32_t ae[M], ao[M];
 #pragma unroll
-            for (int m = 0; m < M; m++) ae[m] = ao[m] = 0;
+            for (int m = 0; m < M; m++) ae[m] = ao[m] = cpack;
 #pragma unroll
             for (int cc = 0; cc < CPS; cc++) {
+                if (zall & (1u << cc)) continue;       // masked channel: its pads are in cpack
                 const uint32_t* b = lbase + lrb[cc] + dl[cc];
 #pragma unroll
                 for (int m = 0; m < M; m++)
@@ -731,7 +775,7 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
                     // first masked channel, then the float fold
                     const int t = (lane + 64 * m) * DS + k;    // quarter-relative raw row
                     uint32_t pe = 0, po = 0;
-                    float sk[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+                    f32x2 sk01 = {0.0f, 0.0f}, sk23 = {0.0f, 0.0f};   // quarters (0,1), (2,3): v_pk_add_f32
 #pragma unroll
                     for (int cc = 0; cc < CPS; cc++) {
                         if (cc < fz) {
@@ -740,31 +784,34 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
                             po += __builtin_amdgcn_perm(0u, x, 0x0c030c01u);
                         } else {
                             if (cc == fz) {
-                                sk[0] = (float)(pe & 0xFFFFu);
-                                sk[1] = (float)(po & 0xFFFFu);
-                                sk[2] = (float)(pe >> 16);
-                                sk[3] = (float)(po >> 16);
+                                sk01 = f32x2{(float)(pe & 0xFFFFu), (float)(po & 0xFFFFu)};
+                                sk23 = f32x2{(float)(pe >> 16), (float)(po >> 16)};
                             }
                             if (zall & (1u << cc)) {
-#pragma unroll
-                                for (int q = 0; q < 4; q++) sk[q] += pad[cc];
+                                const f32x2 pp = {pad[cc], pad[cc]};
+                                sk01 += pp;
+                                sk23 += pp;
                             } else {
                                 const uint32_t x = lbase[lrb[cc] + dl[cc] + m * 64 * DS + k];
-                                float v[4] = {(float)(x & 0xFFu), (float)((x >> 8) & 0xFFu),
-                                              (float)((x >> 16) & 0xFFu), (float)(x >> 24)};
+                                f32x2 v01 = {(float)(x & 0xFFu), (float)((x >> 8) & 0xFFu)};
+                                f32x2 v23 = {(float)((x >> 16) & 0xFFu), (float)(x >> 24)};
                                 if (zsplit & (1u << cc)) {   // zapped on one side of the interval boundary
                                     const bool zlo = (z0 >> cc) & 1;
-#pragma unroll
-                                    for (int q = 0; q < 4; q++)
-                                        if ((t + q * S + dl[cc] < brow) == zlo) v[q] = pad[cc];
+                                    const int rr = t + dl[cc];
+                                    if ((rr < brow) == zlo) v01.x = pad[cc];
+                                    if ((rr + S < brow) == zlo) v01.y = pad[cc];
+                                    if ((rr + 2 * S < brow) == zlo) v23.x = pad[cc];
+                                    if ((rr + 3 * S < brow) == zlo) v23.y = pad[cc];
                                 }
-#pragma unroll
-                                for (int q = 0; q < 4; q++) sk[q] += v[q];
+                                sk01 += v01;
+                                sk23 += v23;
                             }
                         }
                     }
-#pragma unroll
-                    for (int q = 0; q < 4; q++) acc[q] += sk[q];
+                    acc[0] += sk01.x;
+                    acc[1] += sk01.y;
+                    acc[2] += sk23.x;
+                    acc[3] += sk23.y;
                 }
                 if (a.ds_mode == 1)
 #pragma unroll
@@ -774,10 +821,11 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
         }
         if (a.sub_dtype == 0) {
             amax = wave_max_i32(amax);
-            if (lane == 0) publish_max(a.maxabs[p], amax);
+            pmax = lane == p ? amax : pmax;
         }
         vd = vd_next;
     }
+    if (a.sub_dtype == 0 && lane < a.npass) publish_max(a.maxabs[lane], pmax);
 }
 
 size_t stage1_q8_lds_bytes(const Stage1Multi& a) { return (size_t)a.sg * a.cps * a.W * 4; }
@@ -1088,20 +1136,49 @@ hipError_t launch_stage2_lds(const Stage2Args& a, int q, hipStream_t st)
 // stage 2, wide LDS tiles (int16 subbands)
 // ------------------------------------------------------------------------------------
 //
-// Workgroup = NW <= 8 waves; wave w owns DMs w*Q .. w*Q+Q-1 of the y-block and all waves
+// Workgroup = NW <= 16 waves; wave w owns DMs w*Q .. w*Q+Q-1 of the y-block and all waves
 // share one tile of T = 256*R output samples, so every subband window staged in LDS (the
 // same 4 shifted copies as k_stage2_lds) serves NW*Q DMs -- up to 80, a whole PALFA pass.
 // Lane l owns samples t0 + 256r + 4l + i (r < R, i < 4): for one (subband, DM) its R
 // ds_read_b64 share one address at immediate offsets 512r, so the per-pair address work
-// (v_readlane of the host-built byte offset + v_add) is paid once per R reads.  Eight waves
-// of up to 256 VGPRs (two per SIMD) rather than sixteen of 128: the accumulators of Q*R*4
-// samples stay in registers with room left for several LDS reads in flight.  Subbands are
-// staged sc (<= kSC2) at a time into one of two LDS buffers: chunk c+1's global loads are
-// issued before chunk c is accumulated and written to the other buffer after it (one barrier
-// per chunk).  Accumulation is packed int16 widened to int32 every G subbands, as above.
+// (v_readlane of the host-built byte offset + v_add) is paid once per R reads.  The reads
+// are issued by inline asm one (subband, DM) step ahead of their use, with an explicit
+// lgkmcnt wait: hipcc would otherwise fuse them into ds_read2st64_b64 (8 LDS cycles
+// instead of 2 x 2) and wait for each one right after issuing it.  Subbands are staged sc
+// (<= kSC2) at a time into one of two LDS buffers: chunk c+1's global loads are issued
+// before chunk c is accumulated and written to the other buffer after it (one barrier per
+// chunk).  Accumulation is packed int16 widened to int32 every G subbands, as above.
 
-template <int Q, int R>
-__global__ __launch_bounds__(512) void k_stage2_wide(Stage2Args a, const int32_t* __restrict__ boff)
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+template <int R>
+__device__ __forceinline__ void lds_read_r(uint64_t (&b)[R], uint32_t addr)
+{
+#pragma unroll
+    for (int r = 0; r < R; r++) asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(b[r]) : "v"(addr), "i"(512 * r));
+}
+
+template <int R>
+__device__ __forceinline__ void lds_wait_keep(uint64_t (&b)[R])
+{
+    // wait until at most R LDS operations are outstanding (the next step's reads): the reads
+    // into b are then complete; b is an in/out operand so its uses stay after the wait
+    if constexpr (R == 3) asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]));
+    else if constexpr (R == 4) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]));
+    else if constexpr (R == 2) asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(b[0]), "+v"(b[1]));
+    else static_assert(R == 2 || R == 3 || R == 4, "R");
+}
+
+template <int R>
+__device__ __forceinline__ void lds_wait_all(uint64_t (&b)[R])
+{
+    if constexpr (R == 3) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]));
+    else if constexpr (R == 4) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]));
+    else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b[0]), "+v"(b[1]));
+}
+
+template <int Q, int R, int SC>
+__global__ __launch_bounds__(1024) void k_stage2_wide(Stage2Args a, const int32_t* __restrict__ boff)
 {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
     int16_t* lds = (int16_t*)lds_raw;
@@ -1116,7 +1193,7 @@ __global__ __launch_bounds__(512) void k_stage2_wide(Stage2Args a, const int32_t
     const int dblk0 = yb * dpb;
     const int ws = a.wstride;        // elements per shifted copy (multiple of 4)
     const int upw = ws >> 2;         // fill units (4 window positions) per subband
-    const int sc = a.sc;             // subbands per chunk (<= kSC2)
+    constexpr int sc = SC;           // subbands per chunk (nsub % SC == 0: every chunk is full)
     const int16_t* sub = (const int16_t*)a.sub;
     const int32_t* omin = a.omin + (int64_t)yb * a.nsub;
     const int32_t* bo = boff + (int64_t)yb * a.nsub * dpb + wave * Q;
@@ -1156,10 +1233,12 @@ __global__ __launch_bounds__(512) void k_stage2_wide(Stage2Args a, const int32_t
         const int p = (int)(wbeg & 1);
         const int16_t* srow = sub + (int64_t)s * a.sub_stride;
         const int64_t e0 = wbeg + 4 * uu - p;
-        if (e0 + 8 <= a.nds) {
-            const uint32_t* src = (const uint32_t*)(srow + e0);
-#pragma unroll
-            for (int j = 0; j < 4; j++) D[j] = src[j];
+        if (e0 + 8 <= a.nds) {   // one dwordx4 load (4-byte aligned: e0 is even)
+            const u32x4a4 v = *(const u32x4a4*)(srow + e0);
+            D[0] = v.x;
+            D[1] = v.y;
+            D[2] = v.z;
+            D[3] = v.w;
         } else {   // past the end of the subbands: zeros
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -1197,10 +1276,10 @@ __global__ __launch_bounds__(512) void k_stage2_wide(Stage2Args a, const int32_t
         for (int i = 0; i < kUMax; i++)
             if (usl[i] < nsc) pbit |= load_unit(s0 + usl[i], uuu[i], D[i]) << i;
     };
-    auto put = [&](int c) {
+    auto put_buf = [&](int c, int b) {
         const int s0 = c * sc;
         const int nsc = min(sc, a.nsub - s0);
-        int16_t* buf = lds + (c & 1) * (sc * 4 * ws);
+        int16_t* buf = lds + b * (sc * 4 * ws);
 #pragma unroll
         for (int i = 0; i < kUMax; i++)
             if (usl[i] < nsc) store_unit(buf, usl[i], uuu[i], D[i], (pbit >> i) & 1);
@@ -1213,7 +1292,7 @@ __global__ __launch_bounds__(512) void k_stage2_wide(Stage2Args a, const int32_t
         }
     };
     // the chunk's (subband, DM) byte offsets: entry e = sl*Q + q in lane e&63 of voff[e>>6]
-    constexpr int NR = (kSC2 * Q + 63) / 64;
+    constexpr int NR = (SC * Q + 63) / 64;
     auto load_voff = [&](int c, int (&v)[NR]) {
         const int s0 = c * sc;
         const int nsc = min(sc, a.nsub - s0);
@@ -1228,48 +1307,56 @@ __global__ __launch_bounds__(512) void k_stage2_wide(Stage2Args a, const int32_t
     int voff[NR], voff_nxt[NR];
     load_voff(0, voff);
     fetch(0);
-    put(0);
+    put_buf(0, 0);
     __syncthreads();
     for (int c = 0; c < nchunk; c++) {
-        const bool more = c + 1 < nchunk;
+        // next chunk's loads, unconditionally (the last iteration re-loads the last chunk
+        // into the idle buffer): a branch around them would make the compiler drain vmcnt
+        // before the accumulation instead of after it
+        const int cn = min(c + 1, nchunk - 1);
+        load_voff(cn, voff_nxt);
+        if (!(a.probe & 2)) fetch(cn);
+        constexpr int nsteps = SC * Q;   // (subband, DM) steps of a chunk; straight-line code,
+                                         // so the in-flight read registers are never copied
+        uint64_t b0[R], b1[R];
+        if (!(a.probe & 1)) {
+        lds_read_r<R>(b0, (uint32_t)__builtin_amdgcn_readlane(voff[0], 0) + lane_byte);
 #pragma unroll
-        for (int i = 0; i < NR; i++) voff_nxt[i] = 0;
-        if (more) {
-            load_voff(c + 1, voff_nxt);
-            fetch(c + 1);
-        }
-        const int nsc = min(sc, a.nsub - c * sc);
-#pragma unroll
-        for (int sl = 0; sl < kSC2; sl++) {
-            if (sl < nsc) {
-#pragma unroll
-                for (int q = 0; q < Q; q++) {
-                    const int e = sl * Q + q;
-                    const uint32_t addr = (uint32_t)__builtin_amdgcn_readlane(voff[e >> 6], e & 63) + lane_byte;
-#pragma unroll
-                    for (int r = 0; r < R; r++) {
-                        const uint2 v = *(const uint2*)(lds_raw + addr + 512 * r);
-                        acc16[q][r][0] += __builtin_bit_cast(short2v, v.x);
-                        acc16[q][r][1] += __builtin_bit_cast(short2v, v.y);
-                    }
+        for (int e = 0; e < nsteps; e++) {
+            {
+                uint64_t (&cur)[R] = (e & 1) ? b1 : b0;
+                uint64_t (&nxt)[R] = (e & 1) ? b0 : b1;
+                if (e + 1 < nsteps) {
+                    const int e1 = e + 1;
+                    lds_read_r<R>(nxt, (uint32_t)__builtin_amdgcn_readlane(voff[e1 >> 6], e1 & 63) + lane_byte);
+                    lds_wait_keep<R>(cur);
+                } else {
+                    lds_wait_all<R>(cur);
                 }
-                if (++gcount == G) {
+                const int q = e % Q;
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    acc16[q][r][0] += __builtin_bit_cast(short2v, (uint32_t)cur[r]);
+                    acc16[q][r][1] += __builtin_bit_cast(short2v, (uint32_t)(cur[r] >> 32));
+                }
+                if (q == Q - 1 && ++gcount == G) {
                     gcount = 0;
 #pragma unroll
-                    for (int q = 0; q < Q; q++)
+                    for (int qq = 0; qq < Q; qq++)
 #pragma unroll
                         for (int r = 0; r < R; r++) {
-                            acc32[q][r][0] += acc16[q][r][0].x;
-                            acc32[q][r][1] += acc16[q][r][0].y;
-                            acc32[q][r][2] += acc16[q][r][1].x;
-                            acc32[q][r][3] += acc16[q][r][1].y;
-                            acc16[q][r][0] = short2v{0, 0};
-                            acc16[q][r][1] = short2v{0, 0};
+                            acc32[qq][r][0] += acc16[qq][r][0].x;
+                            acc32[qq][r][1] += acc16[qq][r][0].y;
+                            acc32[qq][r][2] += acc16[qq][r][1].x;
+                            acc32[qq][r][3] += acc16[qq][r][1].y;
+                            acc16[qq][r][0] = short2v{0, 0};
+                            acc16[qq][r][1] = short2v{0, 0};
                         }
                 }
             }
         }
-        if (more) put(c + 1);
+        }
+        if (!(a.probe & 2)) put_buf(cn, (c + 1) & 1);
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < NR; i++) voff[i] = voff_nxt[i];
@@ -1289,7 +1376,7 @@ __global__ __launch_bounds__(512) void k_stage2_wide(Stage2Args a, const int32_t
             acc32[q][r][2] += acc16[q][r][1].x;
             acc32[q][r][3] += acc16[q][r][1].y;
             const int64_t tl = t0 + 256 * r + 4 * lane;
-            if (dv) {
+            if (dv && !(a.probe & 4)) {
                 float* o = a.out + (int64_t)d * a.out_stride + tl;
                 if (tl + 3 < a.nvalid) {
                     *(float4*)o = make_float4((float)acc32[q][r][0], (float)acc32[q][r][1], (float)acc32[q][r][2],
@@ -1313,25 +1400,257 @@ __global__ __launch_bounds__(512) void k_stage2_wide(Stage2Args a, const int32_t
     }
 }
 
-size_t stage2_wide_lds_bytes(int wstride, int sc) { return (size_t)2 * sc * 4 * wstride * sizeof(int16_t); }
+#define HD_WIDE_QR(X) X(5, 3) X(4, 4) X(3, 4) X(2, 4)
 
-template <int Q, int R>
-static hipError_t launch_wide_qr(const Stage2Args& a, int nw, int nyblk, hipStream_t st)
+// Two workgroups per CU: 8 waves x Q DMs (<= 40) per workgroup, one LDS window buffer, no
+// register prefetch.  While one workgroup waits for its chunk's loads and barriers, the other
+// accumulates; the subband windows of a tile are filled once per 40-DM y-block.
+template <int Q, int R, int SC>
+__global__ __launch_bounds__(512, 2) void k_stage2_wide2(Stage2Args a, const int32_t* __restrict__ boff)
+{
+    extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+    int16_t* lds = (int16_t*)lds_raw;
+    constexpr int T = 256 * R;
+    constexpr int UM = 4;                       // fill units per thread per chunk (host check)
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t t0 = (int64_t)tile * T;
+    const int yb = blockIdx.y;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nthr = blockDim.x;
+    const int dpb = a.dms_per_blk;
+    const int dblk0 = yb * dpb;
+    const int ws = a.wstride;
+    const int upw = ws >> 2;
+    const int16_t* sub = (const int16_t*)a.sub;
+    const int32_t* bo = boff + (int64_t)yb * a.nsub * dpb + wave * Q;
+    const int nchunk = a.nsub / SC;
+    int32_t* lomin = (int32_t*)(lds_raw + (size_t)SC * 4 * ws * 2);
+    for (int i = threadIdx.x; i < a.nsub; i += nthr) lomin[i] = a.omin[(int64_t)yb * a.nsub + i];
+
+    int maxabs = *a.maxabs;
+    maxabs = maxabs < 1 ? 1 : maxabs;
+    int G = 32767 / maxabs;
+    G = G < 1 ? 1 : (G > 64 ? 64 : G);
+    G = __builtin_amdgcn_readfirstlane(G);
+
+    int acc32[Q][R][4];
+    short2v acc16[Q][R][2];
+#pragma unroll
+    for (int q = 0; q < Q; q++)
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) acc32[q][r][j] = 0;
+            acc16[q][r][0] = short2v{0, 0};
+            acc16[q][r][1] = short2v{0, 0};
+        }
+    int gcount = 0;
+    const uint32_t lane_byte = (uint32_t)lane * 8u;
+    constexpr int NR = (SC * Q + 63) / 64;
+    __syncthreads();
+
+    for (int c = 0; c < nchunk; c++) {
+        const int s0 = c * SC;
+        int voff[NR];
+#pragma unroll
+        for (int i = 0; i < NR; i++) {
+            const int e = i * 64 + lane;
+            const int sl = e / Q, q = e - (e / Q) * Q;
+            voff[i] = (sl < SC) ? bo[(int64_t)(s0 + sl) * dpb + q] : 0;
+        }
+        // ---- fill: UM units per thread per round, all loads first, then the 4 shifted copies
+        for (int ub = 0; ub < SC * upw && !(a.probe & 2); ub += UM * nthr) {
+            uint32_t D[UM][4];
+            int pb[UM], usl[UM], uuu[UM];
+#pragma unroll
+            for (int i = 0; i < UM; i++) {
+                const int u = ub + threadIdx.x + i * nthr;
+                usl[i] = u < SC * upw ? u / upw : SC;
+                uuu[i] = u - usl[i] * upw;
+                pb[i] = 0;
+                if (usl[i] < SC) {
+                    const int s = s0 + usl[i];
+                    const int64_t wbeg = t0 + lomin[s];
+                    const int p = (int)(wbeg & 1);
+                    pb[i] = p;
+                    const int16_t* srow = sub + (int64_t)s * a.sub_stride;
+                    const int64_t e0 = wbeg + 4 * uuu[i] - p;
+                    if (e0 + 8 <= a.nds) {
+                        const u32x4a4 v = *(const u32x4a4*)(srow + e0);
+                        D[i][0] = v.x;
+                        D[i][1] = v.y;
+                        D[i][2] = v.z;
+                        D[i][3] = v.w;
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 4; j++) {
+                            const int64_t e = e0 + 2 * j;
+                            const uint32_t lo = e < a.nds ? (uint16_t)srow[e] : 0u;
+                            const uint32_t hi = e + 1 < a.nds ? (uint16_t)srow[e + 1] : 0u;
+                            D[i][j] = lo | (hi << 16);
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < UM; i++) {
+                if (usl[i] < SC) {
+                    uint2* dst0 = (uint2*)(lds + (usl[i] * 4) * ws);
+                    const int u = uuu[i];
+                    const uint32_t* Di = D[i];
+#define HD_PAIR(h) (((h) & 1) ? __builtin_amdgcn_alignbit(Di[((h) + 1) >> 1], Di[(h) >> 1], 16) : Di[(h) >> 1])
+                    if (pb[i] == 0) {
+                        dst0[u] = make_uint2(HD_PAIR(0), HD_PAIR(2));
+                        dst0[upw + u] = make_uint2(HD_PAIR(1), HD_PAIR(3));
+                        dst0[2 * upw + u] = make_uint2(HD_PAIR(2), HD_PAIR(4));
+                        dst0[3 * upw + u] = make_uint2(HD_PAIR(3), HD_PAIR(5));
+                    } else {
+                        dst0[u] = make_uint2(HD_PAIR(1), HD_PAIR(3));
+                        dst0[upw + u] = make_uint2(HD_PAIR(2), HD_PAIR(4));
+                        dst0[2 * upw + u] = make_uint2(HD_PAIR(3), HD_PAIR(5));
+                        dst0[3 * upw + u] = make_uint2(HD_PAIR(4), HD_PAIR(6));
+                    }
+#undef HD_PAIR
+                }
+            }
+        }
+        __syncthreads();
+        if (!(a.probe & 1)) {
+            constexpr int nsteps = SC * Q;
+            uint64_t b0[R], b1[R];
+            lds_read_r<R>(b0, (uint32_t)__builtin_amdgcn_readlane(voff[0], 0) + lane_byte);
+#pragma unroll
+            for (int e = 0; e < nsteps; e++) {
+                uint64_t (&cur)[R] = (e & 1) ? b1 : b0;
+                uint64_t (&nxt)[R] = (e & 1) ? b0 : b1;
+                if (e + 1 < nsteps) {
+                    const int e1 = e + 1;
+                    lds_read_r<R>(nxt, (uint32_t)__builtin_amdgcn_readlane(voff[e1 >> 6], e1 & 63) + lane_byte);
+                    lds_wait_keep<R>(cur);
+                } else {
+                    lds_wait_all<R>(cur);
+                }
+                const int q = e % Q;
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    acc16[q][r][0] += __builtin_bit_cast(short2v, (uint32_t)cur[r]);
+                    acc16[q][r][1] += __builtin_bit_cast(short2v, (uint32_t)(cur[r] >> 32));
+                }
+                if (q == Q - 1 && ++gcount == G) {
+                    gcount = 0;
+#pragma unroll
+                    for (int qq = 0; qq < Q; qq++)
+#pragma unroll
+                        for (int r = 0; r < R; r++) {
+                            acc32[qq][r][0] += acc16[qq][r][0].x;
+                            acc32[qq][r][1] += acc16[qq][r][0].y;
+                            acc32[qq][r][2] += acc16[qq][r][1].x;
+                            acc32[qq][r][3] += acc16[qq][r][1].y;
+                            acc16[qq][r][0] = short2v{0, 0};
+                            acc16[qq][r][1] = short2v{0, 0};
+                        }
+                }
+            }
+        }
+        __syncthreads();
+    }
+
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+        const int dl = wave * Q + q;
+        const int d = dblk0 + dl;
+        const bool dv = dl < dpb && d < a.numdms;
+        int64_t part = 0;
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            acc32[q][r][0] += acc16[q][r][0].x;
+            acc32[q][r][1] += acc16[q][r][0].y;
+            acc32[q][r][2] += acc16[q][r][1].x;
+            acc32[q][r][3] += acc16[q][r][1].y;
+            const int64_t tl = t0 + 256 * r + 4 * lane;
+            if (dv && !(a.probe & 4)) {
+                float* o = a.out + (int64_t)d * a.out_stride + tl;
+                if (tl + 3 < a.nvalid) {
+                    *(float4*)o = make_float4((float)acc32[q][r][0], (float)acc32[q][r][1], (float)acc32[q][r][2],
+                                              (float)acc32[q][r][3]);
+                    part += (int64_t)acc32[q][r][0] + acc32[q][r][1] + acc32[q][r][2] + acc32[q][r][3];
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        if (tl + j < a.nvalid) {
+                            o[j] = (float)acc32[q][r][j];
+                            part += acc32[q][r][j];
+                        }
+                }
+            }
+        }
+        if (dv && a.partial) {
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) part += __shfl_xor(part, m, 64);
+            if (lane == 0) a.partial[(int64_t)d * a.ntiles + tile] = (double)part;
+        }
+    }
+}
+
+size_t stage2_wide2_lds_bytes(int wstride, int sc, int nsub) { return (size_t)sc * 4 * wstride * 2 + (size_t)nsub * 4; }
+
+template <int Q, int R, int SC>
+static hipError_t launch_wide2_qrs(const Stage2Args& a, int nw, int nyblk, hipStream_t st)
 {
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_stage2_wide<Q, R>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           160 * 1024);
+        hipError_t e = hipFuncSetAttribute((const void*)k_stage2_wide2<Q, R, SC>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attr = true;
     }
     const unsigned ntiles = (unsigned)((a.nvalid + 256 * R - 1) / (256 * R));
-    hipLaunchKernelGGL((k_stage2_wide<Q, R>), dim3(ntiles, (unsigned)nyblk), dim3((unsigned)(64 * nw)),
-                       stage2_wide_lds_bytes(a.wstride, a.sc), st, a, a.off);
+    hipLaunchKernelGGL((k_stage2_wide2<Q, R, SC>), dim3(ntiles, (unsigned)nyblk), dim3((unsigned)(64 * nw)),
+                       stage2_wide2_lds_bytes(a.wstride, SC, a.nsub), st, a, a.off);
     return hipGetLastError();
 }
 
-#define HD_WIDE_QR(X) X(10, 3) X(8, 3) X(6, 4) X(4, 4) X(2, 4)
+hipError_t launch_stage2_wide2(const Stage2Args& a, int q, int r, int nw, hipStream_t st)
+{
+    if (a.nvalid <= 0) return hipSuccess;
+    const int nyblk = (a.numdms + a.dms_per_blk - 1) / a.dms_per_blk;
+#define HD_W2(QQ, RR)                                                                   \
+    if (q == QQ && r == RR) {                                                           \
+        if (a.sc == 8) return launch_wide2_qrs<QQ, RR, 8>(a, nw, nyblk, st);            \
+        if (a.sc == 4) return launch_wide2_qrs<QQ, RR, 4>(a, nw, nyblk, st);            \
+    }
+    HD_WIDE_QR(HD_W2)
+#undef HD_W2
+    return hipErrorInvalidValue;
+}
+
+size_t stage2_wide_lds_bytes(int wstride, int sc) { return (size_t)2 * sc * 4 * wstride * sizeof(int16_t); }
+
+template <int Q, int R, int SC>
+static hipError_t launch_wide_qrs(const Stage2Args& a, int nw, int nyblk, hipStream_t st)
+{
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_stage2_wide<Q, R, SC>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    const unsigned ntiles = (unsigned)((a.nvalid + 256 * R - 1) / (256 * R));
+    hipLaunchKernelGGL((k_stage2_wide<Q, R, SC>), dim3(ntiles, (unsigned)nyblk), dim3((unsigned)(64 * nw)),
+                       stage2_wide_lds_bytes(a.wstride, SC), st, a, a.off);
+    return hipGetLastError();
+}
+
+template <int Q, int R>
+static hipError_t launch_wide_qr(const Stage2Args& a, int nw, int nyblk, hipStream_t st)
+{
+    if (a.sc == 8) return launch_wide_qrs<Q, R, 8>(a, nw, nyblk, st);
+    if (a.sc == 4) return launch_wide_qrs<Q, R, 4>(a, nw, nyblk, st);
+    return hipErrorInvalidValue;
+}
+
 
 bool stage2_wide_supports(int q, int r)
 {
