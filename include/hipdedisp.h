@@ -162,6 +162,10 @@ HD_API int hd_synth_host(const hd_obs* obs, const hd_synth* s, int64_t start, in
 
 /* Copy device spectra [start, start+count) back to host (file layout). */
 HD_API int hd_get_raw(hd_ctx* ctx, void* out, int64_t start, int64_t count);
+/* Multi-GPU (hipdedisp.sharding): raw spectra already in device memory of the context's
+ * GPU -- e.g. a block another rank broadcast over RCCL -- in / out, device-to-device.      */
+HD_API int hd_push_raw_device(hd_ctx* ctx, const void* dev_spectra, int64_t start, int64_t nspectra);
+HD_API int hd_get_raw_device(hd_ctx* ctx, void* dev_out, int64_t start, int64_t count);
 
 /* ---- passes --------------------------------------------------------------------- */
 /* Host-only: the integer tables and subband-level parameters a plan would use, without

@@ -65,10 +65,10 @@ struct hd_plan {
     // (8 waves, two workgroups per CU)
     struct Wide {
         bool ok = false;
-        int32_t q = 0, r = 0, nw = 0, dpb = 0, ws = 0, sc = 0;
+        int32_t q = 0, r = 0, nw = 0, dpb = 0, ws = 0, sc = 0, npw = 0, nbp = 0;
         int32_t* d_omin = nullptr;
         int32_t* d_boff = nullptr;
-    } wide[2];
+    } wide[3];                      // [2]: k_stage2_ring (16 waves, LDS-DMA staging ring)
     int32_t variant = 0;
     float* d_out = nullptr;
     void* d_sub = nullptr;          // this pass's subbands [nsub][sub_stride]
@@ -328,6 +328,36 @@ extern "C" int hd_push_raw(hd_ctx* c, const void* spectra, int64_t start, int64_
                              hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->raw_ready = true;
+    return HD_OK;
+}
+
+// Device-resident raw spectra (multi-GPU: the block another rank broadcast over RCCL).
+extern "C" int hd_push_raw_device(hd_ctx* c, const void* dev_spectra, int64_t start, int64_t n)
+{
+    if (!c) return fail(nullptr, HD_E_INVAL, "hd_push_raw_device: NULL context");
+    if (!c->have_obs) return fail(c, HD_E_STATE, "hd_push_raw_device before hd_set_obs");
+    if (!dev_spectra || start < 0 || n < 0 || start + n > c->obs.N)
+        return fail(c, HD_E_INVAL, "hd_push_raw_device: range [%lld, %lld) outside [0, %lld)", (long long)start,
+                    (long long)(start + n), (long long)c->obs.N);
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc = ensure_raw(c);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->d_raw + (size_t)start * c->rowbytes, dev_spectra, (size_t)n * c->rowbytes,
+                             hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->raw_ready = true;
+    return HD_OK;
+}
+
+extern "C" int hd_get_raw_device(hd_ctx* c, void* dev_out, int64_t start, int64_t n)
+{
+    if (!c) return fail(nullptr, HD_E_INVAL, "hd_get_raw_device: NULL context");
+    if (!c->raw_ready || !c->d_raw) return fail(c, HD_E_STATE, "hd_get_raw_device: no raw data");
+    if (!dev_out || start < 0 || n < 0 || start + n > c->obs.N) return fail(c, HD_E_INVAL, "hd_get_raw_device: bad range");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpyAsync(dev_out, c->d_raw + (size_t)start * c->rowbytes, (size_t)n * c->rowbytes,
+                             hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     return HD_OK;
 }
 
@@ -597,7 +627,7 @@ extern "C" int hd_plan_tables(const hd_obs* o, const hd_opts* opts, const hd_pas
 // T = 256*R samples per tile, windows of ws elements per shifted copy, sc subbands per chunk;
 // boff[yb][s][k] = LDS byte offset of DM k's 4 samples for subband s (lane 0).
 static void wide_tables(hd_plan* p, int nwmax, bool dbuf, bool i16, hd_plan::Wide& w, std::vector<int32_t>& omin,
-                        std::vector<int32_t>& boff)
+                        std::vector<int32_t>& boff, bool ring = false)
 {
     const int nsub = p->pass.nsub, numdms = p->pass.numdms;
     int nyb = (numdms + 5 * nwmax - 1) / (5 * nwmax);
@@ -607,7 +637,7 @@ static void wide_tables(hd_plan* p, int nwmax, bool dbuf, bool i16, hd_plan::Wid
     if (qneed > 4) { Q = 5; R = 3; }
     else if (qneed > 3) { Q = 4; R = 4; }
     else if (qneed > 2) { Q = 3; R = 4; }
-    const int nw = (per + Q - 1) / Q;
+    const int nw = ring ? 16 : (per + Q - 1) / Q;   // the ring needs all 16 waves as DMA loaders
     const int dpb = nw * Q;
     nyb = (numdms + dpb - 1) / dpb;
     omin.assign((size_t)nyb * nsub, 0);
@@ -626,7 +656,15 @@ static void wide_tables(hd_plan* p, int nwmax, bool dbuf, bool i16, hd_plan::Wid
         }
     const int ws = (int)round_up((size_t)(256 * R + span + 4), 4);
     int sc = 0;
-    for (int pass = 0; pass < 2 && !sc; pass++)
+    int npw = 0, nbp = 0;
+    if (ring) {   // 4-subband chunks, every loader piece from one of the 16 waves, LDS fits
+        npw = (int)((((size_t)ws + 8) * 2 + 1023) / 1024);
+        nbp = (int)(((size_t)hd::kRingSC * dpb * 4 + 1023) / 1024);
+        if (nsub % hd::kRingSC == 0 && nw == 16 && hd::kRingSC * npw + nbp <= 16 &&
+            hd::stage2_ring_lds_bytes(ws, npw, nbp, nsub) <= 160 * 1024)
+            sc = hd::kRingSC;
+    }
+    for (int pass = 0; pass < 2 && !sc && !ring; pass++)
         for (int cand : {8, 4}) {
             if (nsub % cand) continue;
             const size_t lds = dbuf ? hd::stage2_wide_lds_bytes(ws, cand) : hd::stage2_wide2_lds_bytes(ws, cand, nsub);
@@ -645,7 +683,9 @@ static void wide_tables(hd_plan* p, int nwmax, bool dbuf, bool i16, hd_plan::Wid
     w.dpb = dpb;
     w.ws = ws;
     w.sc = sc;
-    boff.resize((size_t)nyb * nsub * dpb);
+    w.npw = npw;
+    w.nbp = nbp;
+    boff.resize((size_t)nyb * nsub * dpb + (ring ? 256 : 0));   // ring: the last DMA piece may over-read
     for (int yb = 0; yb < nyb; yb++)
         for (int s = 0; s < nsub; s++)
             for (int k = 0; k < dpb; k++) {
@@ -673,7 +713,12 @@ extern "C" int hd_plan_create(hd_ctx* c, const hd_pass* ps, hd_plan** out)
     p->nds = o.N / ps->ds;
     p->numout = ps->numout > 0 ? ps->numout : p->nds;
     p->nvalid = std::min(p->nds, p->numout);
-    p->sub_stride = (int64_t)round_up((size_t)std::max<int64_t>(p->nds, 1), 64);
+    {
+        int32_t maxoff = 0;
+        for (int32_t v : T.off) maxoff = std::max(maxoff, v);
+        // zero tail after N/ds: stage-2 windows (tile + offsets + DMA pieces) may read into it
+        p->sub_stride = (int64_t)round_up((size_t)std::max<int64_t>(p->nds, 1) + (size_t)maxoff + 4096, 64);
+    }
     p->out_stride = (int64_t)round_up((size_t)p->numout, 64);
     const int nchan = o.nchan, nsub = ps->nsub;
     p->idispdt = std::move(T.idispdt);
@@ -714,13 +759,13 @@ extern "C" int hd_plan_create(hd_ctx* c, const hd_pass* ps, hd_plan** out)
                 boff[((size_t)yb * nsub + s) * p->dpb + k] = ((sl * 4 + (o2 & 3)) * p->wstride + (o2 & ~3)) * 2;
             }
 
-    std::vector<int32_t> womin[2], wboff[2];
-    for (int k = 0; k < 2; k++)
-        wide_tables(p, k == 0 ? 16 : 8, k == 0, c->opts.sub_dtype == HD_SUB_I16, p->wide[k], womin[k], wboff[k]);
+    std::vector<int32_t> womin[3], wboff[3];
+    for (int k = 0; k < 3; k++)
+        wide_tables(p, k == 1 ? 8 : 16, k != 1, c->opts.sub_dtype == HD_SUB_I16, p->wide[k], womin[k], wboff[k], k == 2);
 
     int rc = HD_OK;
     hipError_t e = hipSetDevice(c->device);
-    for (int k = 0; k < 2 && e == hipSuccess; k++) {
+    for (int k = 0; k < 3 && e == hipSuccess; k++) {
         hd_plan::Wide& w = p->wide[k];
         if (!w.ok) continue;
         e = hipMalloc(&w.d_omin, sizeof(int32_t) * womin[k].size());
@@ -786,10 +831,10 @@ extern "C" int hd_plan_set_variant(hd_plan* p, int32_t v)
     const int32_t v1 = (v >> 8) & 0xFF;
     p->probe = (v >> 16) & 0xFF;     // profiling only (results invalid): see hipdedisp.h
     v &= 0xFF;
-    if (v < 0 || v > 4 || v1 > 3) return fail(p->ctx, HD_E_INVAL, "variant must be (s1<<8)|s2 with s1 in 0..3, s2 in 0..4");
+    if (v < 0 || v > 5 || v1 > 3) return fail(p->ctx, HD_E_INVAL, "variant must be (s1<<8)|s2 with s1 in 0..3, s2 in 0..5");
     p->s1_variant = v1;
     if (v == 2 && !p->lds_ok) return fail(p->ctx, HD_E_INVAL, "LDS variant unavailable for this plan (needs int16 subbands and a window that fits 64 KiB)");
-    if ((v == 3 && !p->wide[0].ok) || (v == 4 && !p->wide[1].ok))
+    if ((v == 3 && !p->wide[0].ok) || (v == 4 && !p->wide[1].ok) || (v == 5 && !p->wide[2].ok))
         return fail(p->ctx, HD_E_INVAL, "wide-tile variant unavailable for this plan (needs int16 subbands and a window that fits LDS)");
     p->variant = v;
     return HD_OK;
@@ -810,6 +855,7 @@ static int ensure_sub(hd_ctx* c, hd_plan* p)
         p->d_sub = nullptr;
         return fail(c, HD_E_NOMEM, "cannot allocate %zu bytes of subbands", need);
     }
+    HIPCHK(c, hipMemsetAsync(p->d_sub, 0, need, c->stream));   // the zero tail of every row
     p->sub_bytes = need;
     return HD_OK;
 }
@@ -1013,6 +1059,7 @@ static int run_subband_chunk(hd_ctx* c, hd_plan** plans, int n)
             m.dly[i] = plans[i]->d_idispdt;
             m.out[i] = plans[i]->d_sub;
             m.maxabs[i] = plans[i]->d_maxabs;
+            m.ostride[i] = plans[i]->sub_stride;
         }
         int nsp = 0, *d_sp = nullptr;
         int rc = special_tiles(c, m, &d_sp, &nsp);
@@ -1050,6 +1097,7 @@ static int run_subband_chunk(hd_ctx* c, hd_plan** plans, int n)
             m.dly[i] = plans[i]->d_idispdt;
             m.out[i] = plans[i]->d_sub;
             m.maxabs[i] = plans[i]->d_maxabs;
+            m.ostride[i] = plans[i]->sub_stride;
         }
         const size_t lds = hd::stage1_tiled_lds_bytes(m);
         if (lds > c->lds_attr_set) {
@@ -1169,9 +1217,8 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
     }
     const bool pad = p->numout > p->nds;
     int wk = -1;                       // wide variant in use (index into p->wide), or -1
-    if (p->variant == 3) wk = 0;
-    else if (p->variant == 4) wk = 1;
-    else if (p->variant == 0) wk = p->wide[0].ok ? 0 : (p->wide[1].ok ? 1 : -1);
+    if (p->variant >= 3) wk = p->variant - 3;
+    else if (p->variant == 0) wk = p->wide[2].ok ? 2 : p->wide[0].ok ? 0 : (p->wide[1].ok ? 1 : -1);
     const bool use_wide = wk >= 0;
     const bool use_lds = !use_wide && (p->variant == 2 || (p->variant == 0 && p->lds_ok));
     const int tile = use_wide ? 256 * p->wide[wk].r : kTT;
@@ -1215,8 +1262,11 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         a.dms_per_blk = w.dpb;
         a.sc = w.sc;
         a.probe = p->probe;
+        a.ring_npw = w.npw;
+        a.ring_nbp = w.nbp;
         if (wk == 0) HIPCHK(c, hd::launch_stage2_wide(a, w.q, w.r, w.nw, c->stream));
-        else HIPCHK(c, hd::launch_stage2_wide2(a, w.q, w.r, w.nw, c->stream));
+        else if (wk == 1) HIPCHK(c, hd::launch_stage2_wide2(a, w.q, w.r, w.nw, c->stream));
+        else HIPCHK(c, hd::launch_stage2_ring(a, w.q, w.r, c->stream));
     } else if (use_lds) {
         a.off = p->d_boff;
         HIPCHK(c, hd::launch_stage2_lds(a, p->q, c->stream));

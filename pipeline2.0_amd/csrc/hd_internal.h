@@ -52,6 +52,7 @@ struct Stage1Multi {
     const int32_t* dly[kMaxPass];   // per-pass idispdt [nchan]
     void* out[kMaxPass];            // per-pass subbands [nsub][out_stride]
     int32_t* maxabs[kMaxPass];      // per-pass max |subband|
+    int64_t ostride[kMaxPass];      // per-pass subband row stride (elements; rows carry a zero tail)
 };
 
 struct Stage2Args {
@@ -70,6 +71,7 @@ struct Stage2Args {
     int32_t wstride;          // LDS window stride (elements) per copy
     int32_t dms_per_blk;      // DMs per y-block
     int32_t sc;               // wide variant: subbands per LDS chunk
+    int32_t ring_npw, ring_nbp;   // ring variant: 1 KiB DMA pieces per window / per offset block
     int32_t probe;            // profiling only: bit0 skip accumulation, bit1 skip fill, bit2 skip stores
 };
 
@@ -94,6 +96,9 @@ size_t stage2_wide_lds_bytes(int wstride, int sc);
 bool stage2_wide_supports(int q, int r);
 hipError_t launch_stage2_wide(const Stage2Args& a, int q, int r, int nw, hipStream_t st);
 size_t stage2_wide2_lds_bytes(int wstride, int sc, int nsub);
+constexpr int kRingSC = 4, kRingNS = 5;   // ring variant: subbands per chunk, staging slots
+size_t stage2_ring_lds_bytes(int wstride, int npw, int nbp, int nsub);
+hipError_t launch_stage2_ring(const Stage2Args& a, int q, int r, hipStream_t st);
 hipError_t launch_stage2_wide2(const Stage2Args& a, int q, int r, int nw, hipStream_t st);
 hipError_t launch_stage2_direct(const Stage2Args& a, hipStream_t st);
 hipError_t launch_stage2_lds(const Stage2Args& a, int q, hipStream_t st);

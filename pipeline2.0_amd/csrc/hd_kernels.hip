@@ -247,7 +247,7 @@ __device__ __forceinline__ void form_outputs(const Stage1Multi& a, const uint8_t
         const int64_t tp0 = tO0 + j0, tp1 = tO0 + j1;
         if (a.sub_dtype == 0) {
             const int16_t q0 = quant_i16(acc0), q1 = quant_i16(acc1);
-            int16_t* o = (int16_t*)a.out[p] + (int64_t)s * a.out_stride;
+            int16_t* o = (int16_t*)a.out[p] + (int64_t)s * a.ostride[p];
             o[tp0] = q0;
             amax = max(amax, q0 < 0 ? -(int)q0 : (int)q0);
             if (has1) {
@@ -255,7 +255,7 @@ __device__ __forceinline__ void form_outputs(const Stage1Multi& a, const uint8_t
                 amax = max(amax, q1 < 0 ? -(int)q1 : (int)q1);
             }
         } else {
-            float* o = (float*)a.out[p] + (int64_t)s * a.out_stride;
+            float* o = (float*)a.out[p] + (int64_t)s * a.ostride[p];
             o[tp0] = acc0;
             if (has1) o[tp1] = acc1;
         }
@@ -562,7 +562,7 @@ __device__ __forceinline__ void q8_store(const Stage1Multi& a, int p, int s, int
 {
     constexpr int JQ = Q8Geom<DS>::JQ;
     if (a.sub_dtype == 0) {
-        int16_t* o = (int16_t*)a.out[p] + (int64_t)s * a.out_stride + tO0 + j;
+        int16_t* o = (int16_t*)a.out[p] + (int64_t)s * a.ostride[p] + tO0 + j;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             int16_t v;
@@ -572,7 +572,7 @@ __device__ __forceinline__ void q8_store(const Stage1Multi& a, int p, int s, int
             amax = max(amax, v < 0 ? -(int)v : (int)v);
         }
     } else {
-        float* o = (float*)a.out[p] + (int64_t)s * a.out_stride + tO0 + j;
+        float* o = (float*)a.out[p] + (int64_t)s * a.ostride[p] + tO0 + j;
 #pragma unroll
         for (int q = 0; q < 4; q++) o[q * JQ] = integral ? q8_finish(a, qv[q]) : qf[q];
     }
@@ -747,7 +747,7 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
             }
             if (fast_out) {   // int16 sums (< 32768: host check): store the u16 halves directly
                 u16x2 mx = {0, 0};
-                int16_t* o = (int16_t*)a.out[p] + (int64_t)s * a.out_stride + tO0 + lane;
+                int16_t* o = (int16_t*)a.out[p] + (int64_t)s * a.ostride[p] + tO0 + lane;
 #pragma unroll
                 for (int m = 0; m < M; m++) {
                     o[64 * m] = (int16_t)(ae[m] & 0xFFFFu);
@@ -1402,6 +1402,253 @@ __global__ __launch_bounds__(1024) void k_stage2_wide(Stage2Args a, const int32_
 
 #define HD_WIDE_QR(X) X(5, 3) X(4, 4) X(3, 4) X(2, 4)
 
+// ------------------------------------------------------------------------------------
+// stage 2, wide tiles fed by an LDS-DMA staging ring
+// ------------------------------------------------------------------------------------
+//
+// As k_stage2_wide (16 waves x Q DMs share a tile of T = 256*R samples; asm-pipelined LDS
+// reads), but each 4-subband chunk's raw windows and (subband, DM) offsets are copied
+// global -> LDS by LDS-DMA (global_load_lds_dwordx4, inline asm so hipcc neither waits for
+// it nor drains it at barriers) into a ring of NS staging slots, NS-3 chunks ahead of
+// their expansion.  No register holds data in flight -- the accumulators keep their VGPRs --
+// and the global latency is covered by two chunks of accumulation.  Iteration c: DMA of
+// chunk c+NS-1 (one 1 KiB piece per loader wave); expand chunk c+1 (staging -> the 4 shifted
+// copies); accumulate chunk c; wait for this wave's DMA of chunk c+2; one barrier.
+// Subband rows carry a zero tail (plan allocation), so windows never need bounds checks.
+
+template <int R>
+__device__ __forceinline__ void ring_wait_vm()
+{
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kRingNS - 3) : "memory");
+}
+
+__device__ __forceinline__ void ring_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_dst)
+{
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_dst)
+                 : "memory");
+}
+
+template <int Q, int R>
+__global__ __launch_bounds__(1024) void k_stage2_ring(Stage2Args a, const int32_t* __restrict__ boff)
+{
+    extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+    constexpr int SC = kRingSC, NS = kRingNS, T = 256 * R;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t t0 = (int64_t)tile * T;
+    const int yb = blockIdx.y;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nthr = blockDim.x;
+    const int dpb = a.dms_per_blk;
+    const int dblk0 = yb * dpb;
+    const int ws = a.wstride;
+    const int upw = ws >> 2;
+    const int npw = a.ring_npw;                       // 1 KiB DMA pieces per window
+    const int nbp = a.ring_nbp;                       // pieces of a chunk's offset block
+    const int slot_bytes = (SC * npw + nbp) * 1024;
+    const int omin_bytes = (a.nsub * 4 + 15) & ~15;
+    // LDS: [omin: nsub ints][NS staging slots][2 x SC x 4 copies x ws int16]
+    int32_t* lomin = (int32_t*)lds_raw;
+    const uint32_t ring0 = (uint32_t)omin_bytes;
+    const uint32_t exp0 = ring0 + (uint32_t)(NS * slot_bytes);
+    const uint32_t lane_byte = exp0 + (uint32_t)lane * 8u;   // host offsets are relative to exp0
+    const int16_t* sub = (const int16_t*)a.sub;
+    const int32_t* bo_g = boff + (int64_t)yb * a.nsub * dpb;
+    const int nchunk = a.nsub / SC;
+
+    for (int i = threadIdx.x; i < a.nsub; i += nthr) lomin[i] = a.omin[(int64_t)yb * a.nsub + i];
+    __syncthreads();
+
+    int maxabs = *a.maxabs;
+    maxabs = maxabs < 1 ? 1 : maxabs;
+    int G = 32767 / maxabs;
+    G = G < 1 ? 1 : (G > 64 ? 64 : G);
+    G = __builtin_amdgcn_readfirstlane(G);
+
+    int acc32[Q][R][4];
+    short2v acc16[Q][R][2];
+#pragma unroll
+    for (int q = 0; q < Q; q++)
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) acc32[q][r][j] = 0;
+            acc16[q][r][0] = short2v{0, 0};
+            acc16[q][r][1] = short2v{0, 0};
+        }
+    int gcount = 0;
+    const bool loader = wave < SC * npw + nbp;
+
+    // one DMA piece per loader wave per chunk (chunks past the end re-load the last one into
+    // a consumed slot, so every loader wave issues exactly one DMA per iteration)
+    auto dma = [&](int cc) {
+        if (!loader) return;
+        const int c2 = min(cc, nchunk - 1);
+        const int s0 = c2 * SC;
+        const uint32_t slot = ring0 + (uint32_t)((cc % NS) * slot_bytes);
+        if (wave < SC * npw) {
+            const int sl = wave / npw, pc = wave - (wave / npw) * npw;
+            const int s = s0 + sl;
+            const int om = lomin[s];
+            const int64_t e0 = t0 + om - (om & 1);
+            const char* src = (const char*)(sub + (int64_t)s * a.sub_stride + e0) + pc * 1024 + lane * 16;
+            dma16(src, slot + (uint32_t)((sl * npw + pc) * 1024));
+        } else {
+            const int bp = wave - SC * npw;
+            const char* src = (const char*)(bo_g + (int64_t)s0 * dpb) + bp * 1024 + lane * 16;
+            dma16(src, slot + (uint32_t)((SC * npw + bp) * 1024));
+        }
+    };
+    // staging slot of chunk cc -> its 4 shifted copies in expanded buffer cc & 1
+    auto expand = [&](int cc) {
+        const char* slot = lds_raw + ring0 + (cc % NS) * slot_bytes;
+        int16_t* buf = (int16_t*)(lds_raw + exp0) + (cc & 1) * (SC * 4 * ws);
+        for (int u = threadIdx.x; u < SC * upw; u += nthr) {
+            const int sl = u / upw, uu = u - (u / upw) * upw;
+            const uint2 lo = *(const uint2*)(slot + sl * npw * 1024 + uu * 8);
+            const uint2 hi = *(const uint2*)(slot + sl * npw * 1024 + uu * 8 + 8);
+            const uint32_t Di[4] = {lo.x, lo.y, hi.x, hi.y};
+            const int p = lomin[cc * SC + sl] & 1;
+            uint2* dst0 = (uint2*)(buf + (sl * 4) * ws);
+#define HD_PAIR(h) (((h) & 1) ? __builtin_amdgcn_alignbit(Di[((h) + 1) >> 1], Di[(h) >> 1], 16) : Di[(h) >> 1])
+            if (p == 0) {
+                dst0[uu] = make_uint2(HD_PAIR(0), HD_PAIR(2));
+                dst0[upw + uu] = make_uint2(HD_PAIR(1), HD_PAIR(3));
+                dst0[2 * upw + uu] = make_uint2(HD_PAIR(2), HD_PAIR(4));
+                dst0[3 * upw + uu] = make_uint2(HD_PAIR(3), HD_PAIR(5));
+            } else {
+                dst0[uu] = make_uint2(HD_PAIR(1), HD_PAIR(3));
+                dst0[upw + uu] = make_uint2(HD_PAIR(2), HD_PAIR(4));
+                dst0[2 * upw + uu] = make_uint2(HD_PAIR(3), HD_PAIR(5));
+                dst0[3 * upw + uu] = make_uint2(HD_PAIR(4), HD_PAIR(6));
+            }
+#undef HD_PAIR
+        }
+    };
+
+    // prologue: chunks 0 .. NS-2 in flight; chunks 0 and 1 landed; chunk 0 expanded
+#pragma unroll
+    for (int cc = 0; cc < NS - 1; cc++) dma(cc);
+    ring_wait_vm<R>();
+    ring_barrier();
+    expand(0);
+    ring_barrier();
+
+    for (int c = 0; c < nchunk; c++) {
+        dma(c + NS - 1);
+        if (c + 1 < nchunk) expand(c + 1);
+        // this chunk's (subband, DM) byte offsets: entry e = sl*Q + q in lane e
+        const int32_t* sboff = (const int32_t*)(lds_raw + ring0 + (c % NS) * slot_bytes + SC * npw * 1024);
+        const int esl = lane / Q, eq = lane - (lane / Q) * Q;
+        const int voff = esl < SC ? sboff[esl * dpb + wave * Q + eq] : 0;
+        if (!(a.probe & 1)) {
+            constexpr int nsteps = SC * Q;
+            uint64_t b0[R], b1[R];
+            lds_read_r<R>(b0, (uint32_t)__builtin_amdgcn_readlane(voff, 0) + lane_byte);
+#pragma unroll
+            for (int e = 0; e < nsteps; e++) {
+                uint64_t (&cur)[R] = (e & 1) ? b1 : b0;
+                uint64_t (&nxt)[R] = (e & 1) ? b0 : b1;
+                if (e + 1 < nsteps) {
+                    lds_read_r<R>(nxt, (uint32_t)__builtin_amdgcn_readlane(voff, e + 1) + lane_byte);
+                    lds_wait_keep<R>(cur);
+                } else {
+                    lds_wait_all<R>(cur);
+                }
+                const int q = e % Q;
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    acc16[q][r][0] += __builtin_bit_cast(short2v, (uint32_t)cur[r]);
+                    acc16[q][r][1] += __builtin_bit_cast(short2v, (uint32_t)(cur[r] >> 32));
+                }
+                if (q == Q - 1 && ++gcount == G) {
+                    gcount = 0;
+#pragma unroll
+                    for (int qq = 0; qq < Q; qq++)
+#pragma unroll
+                        for (int r = 0; r < R; r++) {
+                            acc32[qq][r][0] += acc16[qq][r][0].x;
+                            acc32[qq][r][1] += acc16[qq][r][0].y;
+                            acc32[qq][r][2] += acc16[qq][r][1].x;
+                            acc32[qq][r][3] += acc16[qq][r][1].y;
+                            acc16[qq][r][0] = short2v{0, 0};
+                            acc16[qq][r][1] = short2v{0, 0};
+                        }
+                }
+            }
+        }
+        ring_wait_vm<R>();
+        ring_barrier();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may land after the workgroup ends
+
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+        const int dl = wave * Q + q;
+        const int d = dblk0 + dl;
+        const bool dv = dl < dpb && d < a.numdms;
+        int64_t part = 0;
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            acc32[q][r][0] += acc16[q][r][0].x;
+            acc32[q][r][1] += acc16[q][r][0].y;
+            acc32[q][r][2] += acc16[q][r][1].x;
+            acc32[q][r][3] += acc16[q][r][1].y;
+            const int64_t tl = t0 + 256 * r + 4 * lane;
+            if (dv && !(a.probe & 4)) {
+                float* o = a.out + (int64_t)d * a.out_stride + tl;
+                if (tl + 3 < a.nvalid) {
+                    *(float4*)o = make_float4((float)acc32[q][r][0], (float)acc32[q][r][1], (float)acc32[q][r][2],
+                                              (float)acc32[q][r][3]);
+                    part += (int64_t)acc32[q][r][0] + acc32[q][r][1] + acc32[q][r][2] + acc32[q][r][3];
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        if (tl + j < a.nvalid) {
+                            o[j] = (float)acc32[q][r][j];
+                            part += acc32[q][r][j];
+                        }
+                }
+            }
+        }
+        if (dv && a.partial) {
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) part += __shfl_xor(part, m, 64);
+            if (lane == 0) a.partial[(int64_t)d * a.ntiles + tile] = (double)part;
+        }
+    }
+}
+
+size_t stage2_ring_lds_bytes(int wstride, int npw, int nbp, int nsub)
+{
+    return (size_t)((nsub * 4 + 15) & ~15) + (size_t)kRingNS * (kRingSC * npw + nbp) * 1024 +
+           (size_t)2 * kRingSC * 4 * wstride * 2;
+}
+
+template <int Q, int R>
+static hipError_t launch_ring_qr(const Stage2Args& a, int nyblk, hipStream_t st)
+{
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_stage2_ring<Q, R>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           160 * 1024);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    const unsigned ntiles = (unsigned)((a.nvalid + 256 * R - 1) / (256 * R));
+    hipLaunchKernelGGL((k_stage2_ring<Q, R>), dim3(ntiles, (unsigned)nyblk), dim3(1024),
+                       stage2_ring_lds_bytes(a.wstride, a.ring_npw, a.ring_nbp, a.nsub), st, a, a.off);
+    return hipGetLastError();
+}
+
 // Two workgroups per CU: 8 waves x Q DMs (<= 40) per workgroup, one LDS window buffer, no
 // register prefetch.  While one workgroup waits for its chunk's loads and barriers, the other
 // accumulates; the subband windows of a tile are filled once per 40-DM y-block.
@@ -1622,6 +1869,17 @@ hipError_t launch_stage2_wide2(const Stage2Args& a, int q, int r, int nw, hipStr
     }
     HD_WIDE_QR(HD_W2)
 #undef HD_W2
+    return hipErrorInvalidValue;
+}
+
+// ring variant: 16 waves (nw is fixed by the host to 16 whenever the ring applies)
+hipError_t launch_stage2_ring(const Stage2Args& a, int q, int r, hipStream_t st)
+{
+    if (a.nvalid <= 0) return hipSuccess;
+    const int nyblk = (a.numdms + a.dms_per_blk - 1) / a.dms_per_blk;
+#define HD_RL(QQ, RR) if (q == QQ && r == RR) return launch_ring_qr<QQ, RR>(a, nyblk, st);
+    HD_WIDE_QR(HD_RL)
+#undef HD_RL
     return hipErrorInvalidValue;
 }
 

@@ -34,7 +34,7 @@ EXPORTED = [
     "hd_push_raw", "hd_synth_device", "hd_synth_host", "hd_plan_create", "hd_plan_destroy",
     "hd_plan_get_delays", "hd_plan_sub_params", "hd_run_subband", "hd_get_subbands",
     "hd_set_subbands", "hd_run_dedisp", "hd_plan_last_ms", "hd_plan_set_variant",
-    "hd_get_raw", "hd_plan_tables", "hd_run_subband_multi",
+    "hd_get_raw", "hd_plan_tables", "hd_run_subband_multi", "hd_push_raw_device", "hd_get_raw_device",
 ]
 
 
@@ -125,6 +125,8 @@ def load():
         "hd_plan_set_variant": (ctypes.c_int, [vp, i32]),
         "hd_get_raw": (ctypes.c_int, [vp, vp, i64, i64]),
         "hd_run_subband_multi": (ctypes.c_int, [P(vp), i32]),
+        "hd_push_raw_device": (ctypes.c_int, [vp, vp, i64, i64]),
+        "hd_get_raw_device": (ctypes.c_int, [vp, vp, i64, i64]),
         "hd_plan_tables": (ctypes.c_int, [P(hd_obs), P(hd_opts), P(hd_pass), P(ctypes.c_int32),
                                           P(ctypes.c_int32), P(ctypes.c_double), P(ctypes.c_double),
                                           P(ctypes.c_double)]),

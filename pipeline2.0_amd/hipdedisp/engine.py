@@ -167,6 +167,18 @@ class Engine:
         self._chk(self._L.hd_push_raw(self._ctx, a.ctypes.data_as(ctypes.c_void_p), int(start), int(n)),
                   "hd_push_raw")
 
+    def push_raw_device(self, dev_ptr, start=0, count=None):
+        """Raw spectra from device memory of this context's GPU (an int address, e.g. a
+        torch tensor's data_ptr() after an RCCL broadcast)."""
+        count = self.obs.N - start if count is None else count
+        self._chk(self._L.hd_push_raw_device(self._ctx, ctypes.c_void_p(int(dev_ptr)), int(start), int(count)),
+                  "hd_push_raw_device")
+
+    def get_raw_device(self, dev_ptr, start=0, count=None):
+        count = self.obs.N - start if count is None else count
+        self._chk(self._L.hd_get_raw_device(self._ctx, ctypes.c_void_p(int(dev_ptr)), int(start), int(count)),
+                  "hd_get_raw_device")
+
     def get_raw(self, start=0, count=None):
         count = self.obs.N - start if count is None else count
         out = np.empty((count, self.obs.rowbytes), np.uint8)

@@ -29,7 +29,7 @@ for pp in (PassParams(subdm=3.80, lodm=0.0, dmstep=0.1, numdms=76, nsub=96, ds=1
             print("ds=%d stage1 variant %d: %s (bad %d)" % (pp.ds, s1, np.array_equal(got, want_sub),
                                                              int((got != want_sub).sum())), flush=True)
             p.destroy()
-        for s2 in (1, 2, 3, 4):
+        for s2 in (1, 2, 3, 4, 5):
             p = eng.plan(pp)
             p.set_variant((1 << 8) | s2)
             p.run_subband()

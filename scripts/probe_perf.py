@@ -36,7 +36,7 @@ with Engine(0) as eng:
         for p in plans:
             p.set_variant(0)
         eng.run_subband_multi(plans)
-        for v2, probe in ((3, 0), (3, 1), (3, 2), (4, 0), (4, 1), (4, 2), (4, 3), (2, 0)):
+        for v2, probe in ((5, 0), (5, 1), (5, 2), (5, 3), (3, 0), (4, 0), (2, 0)):
             p = plans[0]
             p.set_variant((probe << 16) | v2)
             t = []

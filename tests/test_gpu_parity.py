@@ -79,7 +79,7 @@ def test_stage1_calib_mask_bitexact(engine, sub_dtype, ds_mode):
 
 @pytest.mark.parametrize("numdms,ds,numout_mode", [(76, 1, "none"), (64, 2, "none"), (76, 3, "pad"),
                                                    (5, 1, "trunc"), (100, 5, "pad"), (76, 10, "pad")])
-@pytest.mark.parametrize("variant", [1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5])
 def test_stage2_bitexact(engine, numdms, ds, numout_mode, variant):
     obs = palfa_obs(N=3 * 8192, nbits=8)
     raw = load_beam(engine, obs)
