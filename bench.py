@@ -35,6 +35,9 @@ def parse():
     ap.add_argument("--variant", type=int, default=0, help="stage-2 kernel: 0 auto, 1 direct, 2 LDS")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU-baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU work for the baseline sample")
+    ap.add_argument("--mode", choices=["beam", "shard"], default="beam",
+                    help="beam: one beam per rank (weak scaling, configs[4]); shard: ONE beam's 57 passes "
+                         "LPT-sharded over the ranks after an RCCL broadcast of the raw block (strong, configs[2])")
     return ap.parse_args()
 
 
@@ -45,8 +48,11 @@ def dist_setup(args):
     if world > 1:
         import torch
         import torch.distributed as dist
+        # one rank per GPU; HD_DIST_BACKEND=gloo (and ranks sharing a GPU) only to rehearse the
+        # multi-rank logic on a one-GPU box -- the node run is RCCL ("nccl" on ROCm) over xGMI
+        local = local % max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group(os.environ.get("HD_DIST_BACKEND", "nccl"), init_method="env://")
         return world, rank, local, dist, torch
     return 1, 0, 0, None, None
 
@@ -86,10 +92,40 @@ def run_step(eng, stages):
     """One beam: per DDplan stage, stage 1 for all its passes from one raw read, then the
     stage-2 sweep of each pass."""
     for plans in stages:
+        if not plans:
+            continue
         eng.run_subband_multi(plans)
         for p in plans:
             p.run_dedisp(to_host=False)
     eng.sync()
+
+
+def shard_stages(eng, obs, ddplans, rank, world, variant):
+    """This rank's LPT share of the beam's passes (hipdedisp.sharding), grouped by stage."""
+    from hipdedisp import sharding as S
+    sb = S.ShardedBeam(ddplans, obs, rank, world)
+    stages = [[] for _ in ddplans]
+    for stage, passnums in sb.my_groups():
+        for i in passnums:
+            p = eng.plan(sb.pass_params(stage, i))
+            if variant:
+                p.set_variant(variant)
+            stages[stage].append(p)
+    return stages
+
+
+def broadcast_beam(eng, obs, rank, dist, torch):
+    """Rank 0's raw block to every rank over RCCL (xGMI), then into each engine."""
+    from hipdedisp import sharding as S
+    t = torch.empty(obs.N * obs.rowbytes, dtype=torch.uint8, device="cuda")
+    if rank == 0:
+        eng.get_raw_device(t.data_ptr())
+    torch.cuda.synchronize()
+    S.broadcast_raw(t, src=0)
+    torch.cuda.synchronize()
+    if rank != 0:
+        eng.push_raw_device(t.data_ptr())
+    del t
 
 
 def cpu_baseline(obs, synth, ddplans, target_s):
@@ -144,27 +180,46 @@ def main():
     obs = palfa_obs(N=args.nspec, nbits=args.nbits)
     synth = palfa_synth(beam=rank, nbits=args.nbits)
     ddplans = P.ddplans_for("pdev")
+    shard = args.mode == "shard"
+    if shard:
+        synth = palfa_synth(beam=0, nbits=args.nbits)       # one beam for the whole node
     eng = Engine(local)
     eng.set_obs(obs, Opts())
-    eng.synth_device(synth)
+    if not shard or rank == 0:
+        eng.synth_device(synth)
     pts = rfifind_ptsperint(obs.dt)
     mask, pad = synth_mask(obs, synth, pts)
     eng.set_mask(mask, pts, pad)
-    stages = build_plans(eng, obs, ddplans, args.variant)
+    if shard:
+        stages = shard_stages(eng, obs, ddplans, rank, world, args.variant)
+    else:
+        stages = build_plans(eng, obs, ddplans, args.variant)
     plans = [p for st in stages for p in st]
-    out_per_step = sum(p.pp.numdms * p.nds for p in plans)
+    out_per_step = sum(p.pp.numdms * p.nds for p in plans)          # this rank's samples
+    if shard and world > 1:
+        broadcast_beam(eng, obs, rank, dist, torch)                 # untimed: makes warmup valid
 
+    bcast_s = 0.0
     for _ in range(args.warmup):
         run_step(eng, stages)
     barrier(dist, torch)
     eng.sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        if shard and world > 1:      # the exchange is part of every sharded beam
+            tb = time.perf_counter()
+            broadcast_beam(eng, obs, rank, dist, torch)
+            bcast_s += time.perf_counter() - tb
         run_step(eng, stages)
     eng.sync()
     barrier(dist, torch)
     dt = time.perf_counter() - t0
     dt_max = max_over_ranks(dt, dist, torch)
+    total_out = out_per_step
+    if dist is not None:
+        tt = torch.tensor([float(out_per_step)], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt)
+        total_out = tt.item()
 
     # per-kernel device time of the last step (hipEvents on the engine's stream)
     ms1 = ms2 = 0.0
@@ -196,21 +251,23 @@ def main():
     step_s = dt_max / args.steps
     line = {
         "metric": METRIC,
-        "value": world * out_per_step * args.steps / dt_max,
+        "value": total_out * args.steps / dt_max,
         "unit": "samples/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": step_s * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if shard else "weak",
         "vs_baseline": None,
         "dtype": "u8->f32 subbanding, i16 subbands, i16x2/i32 exact sums, f32 out",
         "data": "synthetic",
         "config": {"workload": "C2: full PALFA Mock beam per GPU (960 ch x 2^22 x %d-bit, 65.476 us), "
                                "57-pass DDplan = 4188 DM trials, rfifind-style mask" % args.nbits,
                    "nchan": obs.nchan, "nspec": obs.N, "nbits": obs.nbits, "dm_trials": 4188, "passes": len(plans),
-                   "out_samples_per_beam": out_per_step, "parallelism": "beam-per-GPU x%d" % world},
+                   "out_samples_per_beam": sum(d.numpasses * d.dmsperpass * (obs.N // d.sub_downsamp) for d in ddplans),
+                   "parallelism": ("1 beam, passes LPT-sharded x%d, RCCL raw broadcast" % world) if shard
+                   else "beam-per-GPU x%d" % world},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "avg_launch_ms": launch_ms, "bytes_per_unit": b_unit},
@@ -218,6 +275,8 @@ def main():
         "step_compulsory_hbm_frac": (raw_bytes + 4.0 * out_per_step) / step_s / (HBM_PEAK_GBS * 1e9),
         "stage2_valu_frac": adds2 / (ms2 * 1e-3) / VALU_ADD_PEAK if ms2 > 0 else None,
     }
+    if shard:
+        line["broadcast_ms_per_step"] = 1e3 * bcast_s / args.steps
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(obs, synth, ddplans, args.cpu_seconds)
     if rank == 0:
