@@ -153,6 +153,25 @@ HD_API int hd_set_mask(hd_ctx* ctx, const uint8_t* mask, int32_t numint, int32_t
 /* Copy nspectra raw spectra (file layout, rows of nchan*nbits/8 bytes) to device
  * spectra [start, start + nspectra).  Host memory may be pageable or pinned.       */
 HD_API int hd_push_raw(hd_ctx* ctx, const void* spectra, int64_t start, int64_t nspectra);
+/* Streaming PSRFITS ingest (north_star (b); replaces the whole-file read PRESTO's
+ * prepsubband does through psrfits.c before the loops of
+ * lib/python/PALFA2_presto_search.py:506-511).  Reads the DATA column of rows
+ * [row0, row0 + nrows) of one SUBINT binary table straight from the file into two pinned
+ * host buffers in turn (pread), each handed to the device with hipMemcpyAsync on the
+ * context's stream, so the disk read of block k+1 overlaps the PCIe copy of block k.
+ * The DATA column must hold whole spectra (npol 1: col_bytes = nsblk*nchan*nbits/8);
+ * spectra land at device spectra [start, ...).  Optional stats: seconds spent in pread,
+ * seconds for the whole call (both may be NULL).                                      */
+typedef struct {
+    int64_t table_offset;   /* byte offset of the table's first row in the file          */
+    int64_t row_bytes;      /* NAXIS1                                                      */
+    int64_t col_offset;     /* byte offset of the DATA column inside a row                 */
+    int64_t col_bytes;      /* DATA bytes per row                                          */
+    int64_t row0, nrows;    /* rows to read                                                */
+    int64_t block_bytes;    /* pinned block size (0: 32 MiB; at least one row)             */
+} hd_rows_src;
+HD_API int hd_push_raw_file(hd_ctx* ctx, const char* path, const hd_rows_src* src, int64_t start,
+                            double* io_seconds, double* total_seconds);
 /* Fill the device raw block with the synthetic beam (bit-identical to hd_synth_host). */
 HD_API int hd_synth_device(hd_ctx* ctx, const hd_synth* s);
 /* Host generator: spectra [start, start+count) of the same beam into out (file layout).

@@ -9,7 +9,11 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <fcntl.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <chrono>
 #include <string>
 #include <thread>
 #include <vector>
@@ -43,6 +47,11 @@ struct hd_ctx {
     std::vector<SpecialList> special_cache;
     double* d_partial = nullptr;    // shared per-tile partial sums
     size_t partial_bytes = 0;
+    // streaming ingest (hd_push_raw_file): two pinned host blocks, each guarded by the event
+    // of the last copy that read it
+    void* pin[2] = {nullptr, nullptr};
+    size_t pin_bytes = 0;
+    hipEvent_t pin_ev[2] = {nullptr, nullptr};
 };
 
 struct hd_plan {
@@ -203,6 +212,10 @@ extern "C" int hd_close(hd_ctx* c)
     (void)hipStreamSynchronize(c->stream);
     free_obs_buffers(c);
     dfree(c->d_partial);
+    for (int b = 0; b < 2; b++) {
+        if (c->pin[b]) (void)hipHostFree(c->pin[b]);
+        if (c->pin_ev[b]) (void)hipEventDestroy(c->pin_ev[b]);
+    }
     clear_special_cache(c);
     (void)hipStreamDestroy(c->stream);
     delete c;
@@ -328,6 +341,97 @@ extern "C" int hd_push_raw(hd_ctx* c, const void* spectra, int64_t start, int64_
                              hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->raw_ready = true;
+    return HD_OK;
+}
+
+// Streaming PSRFITS ingest: pread of the DATA column of row blocks into two pinned host
+// buffers in turn, each followed by hipMemcpyAsync on the context stream; before a buffer is
+// refilled its previous copy is waited for (its event), so reading block k+1 from the file
+// overlaps the PCIe copy of block k.
+static int read_full(int fd, void* dst, size_t n, off_t off)
+{
+    char* p = (char*)dst;
+    while (n) {
+        const ssize_t got = pread(fd, p, n, off);
+        if (got <= 0) return -1;
+        p += got;
+        n -= (size_t)got;
+        off += got;
+    }
+    return 0;
+}
+
+extern "C" int hd_push_raw_file(hd_ctx* c, const char* path, const hd_rows_src* src, int64_t start,
+                                double* io_seconds, double* total_seconds)
+{
+    using clk = std::chrono::steady_clock;
+    const auto t_all = clk::now();
+    if (!c) return fail(nullptr, HD_E_INVAL, "hd_push_raw_file: NULL context");
+    if (!c->have_obs) return fail(c, HD_E_STATE, "hd_push_raw_file before hd_set_obs");
+    if (!path || !src) return fail(c, HD_E_INVAL, "hd_push_raw_file: NULL argument");
+    const int64_t rb = c->rowbytes;
+    if (src->col_bytes <= 0 || src->col_bytes % rb || src->row_bytes < src->col_offset + src->col_bytes ||
+        src->row0 < 0 || src->nrows < 0 || src->table_offset < 0)
+        return fail(c, HD_E_INVAL, "hd_push_raw_file: DATA column of %lld bytes is not whole spectra of %lld bytes "
+                    "(or bad row geometry)", (long long)src->col_bytes, (long long)rb);
+    const int64_t spr = src->col_bytes / rb;   // spectra per row (NSBLK)
+    if (start < 0 || start + src->nrows * spr > c->obs.N)
+        return fail(c, HD_E_INVAL, "hd_push_raw_file: spectra [%lld, %lld) outside [0, %lld)", (long long)start,
+                    (long long)(start + src->nrows * spr), (long long)c->obs.N);
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc = ensure_raw(c);
+    if (rc) return rc;
+    const size_t want = src->block_bytes > 0 ? (size_t)src->block_bytes : (size_t)32 << 20;
+    const int64_t rows_blk = std::max<int64_t>(1, (int64_t)(want / (size_t)src->col_bytes));
+    const size_t blk_bytes = (size_t)rows_blk * (size_t)src->col_bytes;
+    if (c->pin_bytes < blk_bytes) {
+        for (int b = 0; b < 2; b++) {
+            if (c->pin[b]) HIPCHK(c, hipHostFree(c->pin[b]));
+            c->pin[b] = nullptr;
+        }
+        c->pin_bytes = 0;
+        for (int b = 0; b < 2; b++) HIPCHK(c, hipHostMalloc(&c->pin[b], blk_bytes, hipHostMallocDefault));
+        c->pin_bytes = blk_bytes;
+    }
+    for (int b = 0; b < 2; b++)
+        if (!c->pin_ev[b]) HIPCHK(c, hipEventCreateWithFlags(&c->pin_ev[b], hipEventDisableTiming));
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) return fail(c, HD_E_IO, "hd_push_raw_file: cannot open %s", path);
+    double io = 0.0;
+    int err = 0;
+    bool used[2] = {false, false};
+    for (int64_t r = 0, k = 0; r < src->nrows && !err; r += rows_blk, k++) {
+        const int b = (int)(k & 1);
+        const int64_t nr = std::min(rows_blk, src->nrows - r);
+        if (used[b] && hipEventSynchronize(c->pin_ev[b]) != hipSuccess) { err = HD_E_HIP; break; }
+        const auto t0 = clk::now();
+        char* dst = (char*)c->pin[b];
+        if (src->col_offset == 0 && src->col_bytes == src->row_bytes) {
+            if (read_full(fd, dst, (size_t)(nr * src->col_bytes), (off_t)(src->table_offset + (src->row0 + r) * src->row_bytes)))
+                err = HD_E_IO;
+        } else {
+            for (int64_t i = 0; i < nr && !err; i++)
+                if (read_full(fd, dst + i * src->col_bytes, (size_t)src->col_bytes,
+                              (off_t)(src->table_offset + (src->row0 + r + i) * src->row_bytes + src->col_offset)))
+                    err = HD_E_IO;
+        }
+        io += std::chrono::duration<double>(clk::now() - t0).count();
+        if (err) break;
+        if (hipMemcpyAsync(c->d_raw + (size_t)(start + r * spr) * rb, dst, (size_t)(nr * src->col_bytes),
+                           hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+            hipEventRecord(c->pin_ev[b], c->stream) != hipSuccess) {
+            err = HD_E_HIP;
+            break;
+        }
+        used[b] = true;
+    }
+    close(fd);
+    const hipError_t se = hipStreamSynchronize(c->stream);
+    if (err == HD_E_IO) return fail(c, HD_E_IO, "hd_push_raw_file: short read from %s", path);
+    if (err || se != hipSuccess) return fail(c, HD_E_HIP, "hd_push_raw_file: HIP copy failed");
+    c->raw_ready = true;
+    if (io_seconds) *io_seconds = io;
+    if (total_seconds) *total_seconds = std::chrono::duration<double>(clk::now() - t_all).count();
     return HD_OK;
 }
 
@@ -634,8 +738,9 @@ static void wide_tables(hd_plan* p, int nwmax, bool dbuf, bool i16, hd_plan::Wid
     const int per = (numdms + nyb - 1) / nyb;
     const int qneed = (per + nwmax - 1) / nwmax;
     int Q = 2, R = 4;
-    if (qneed > 4) { Q = 5; R = 3; }
-    else if (qneed > 3) { Q = 4; R = 4; }
+    static const int ring_r5 = getenv("HD_RING_R5") ? atoi(getenv("HD_RING_R5")) : 3;   // experiment
+    if (qneed > 4) { Q = 5; R = ring ? ring_r5 : 3; }
+    else if (qneed > 3) { Q = 4; R = ring ? 3 : 4; }
     else if (qneed > 2) { Q = 3; R = 4; }
     const int nw = ring ? 16 : (per + Q - 1) / Q;   // the ring needs all 16 waves as DMA loaders
     const int dpb = nw * Q;
@@ -675,7 +780,7 @@ static void wide_tables(hd_plan* p, int nwmax, bool dbuf, bool i16, hd_plan::Wid
             if (fits && (units || pass)) { sc = cand; break; }
         }
     w = hd_plan::Wide{};
-    w.ok = i16 && nw <= nwmax && hd::stage2_wide_supports(Q, R) && sc > 0;
+    w.ok = i16 && nw <= nwmax && (ring ? hd::stage2_ring_supports(Q, R) : hd::stage2_wide_supports(Q, R)) && sc > 0;
     if (!w.ok) return;
     w.q = Q;
     w.r = R;

@@ -94,6 +94,7 @@ constexpr int kUMax = 2;
 constexpr int kWideWaves = 16;
 size_t stage2_wide_lds_bytes(int wstride, int sc);
 bool stage2_wide_supports(int q, int r);
+bool stage2_ring_supports(int q, int r);
 hipError_t launch_stage2_wide(const Stage2Args& a, int q, int r, int nw, hipStream_t st);
 size_t stage2_wide2_lds_bytes(int wstride, int sc, int nsub);
 constexpr int kRingSC = 4, kRingNS = 5;   // ring variant: subbands per chunk, staging slots

@@ -1177,6 +1177,29 @@ __device__ __forceinline__ void lds_wait_all(uint64_t (&b)[R])
     else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b[0]), "+v"(b[1]));
 }
 
+
+// wait until at most N LDS operations are outstanding; b (the buffer about to be consumed)
+// is an in/out operand so its uses stay after the wait
+template <int N, int R>
+__device__ __forceinline__ void lds_wait_n(uint64_t (&b)[R])
+{
+    if constexpr (R == 2) asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(b[0]), "+v"(b[1]) : "i"(N));
+    else if constexpr (R == 3) asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]) : "i"(N));
+    else if constexpr (R == 4)
+        asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]) : "i"(N));
+    else static_assert(R >= 2 && R <= 4, "R");
+}
+
+// LDS read lookahead of the ring kernel (in (subband, DM) steps): as deep as the 128-VGPR
+// budget of 4 waves per SIMD allows next to the Q*R*6 accumulator registers
+template <int Q, int R>
+constexpr int ring_la()
+{
+    const int spare = 128 - 26 - Q * R * 6;
+    const int la = spare / (2 * R) - 1;
+    return la < 1 ? 1 : (la > 3 ? 3 : la);
+}
+
 template <int Q, int R, int SC>
 __global__ __launch_bounds__(1024) void k_stage2_wide(Stage2Args a, const int32_t* __restrict__ boff)
 {
@@ -1401,6 +1424,9 @@ __global__ __launch_bounds__(1024) void k_stage2_wide(Stage2Args a, const int32_
 }
 
 #define HD_WIDE_QR(X) X(5, 3) X(4, 4) X(3, 4) X(2, 4)
+// ring: every (Q, R) keeps its accumulators, two read buffers and the loop addresses in 128
+// VGPRs without spilling (Q=4 takes R=3: at R=4 the loop spilled to scratch)
+#define HD_RING_QR(X) X(5, 3) X(5, 2) X(4, 3) X(3, 4) X(2, 4)
 
 // ------------------------------------------------------------------------------------
 // stage 2, wide tiles fed by an LDS-DMA staging ring
@@ -1433,6 +1459,17 @@ __device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_dst)
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
                  : "v"(gsrc), "s"(lds_dst)
+                 : "memory");
+}
+
+// The same with a wave-uniform 64-bit base in SGPRs and a 32-bit per-lane byte offset
+// (saddr form): one VGPR per lane instead of a 64-bit pointer kept live across the loop.
+__device__ __forceinline__ void dma16s(const void* sbase, uint32_t voff, uint32_t lds_dst)
+{
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(sbase), "s"(lds_dst)
                  : "memory");
 }
 
@@ -1497,14 +1534,14 @@ __global__ __launch_bounds__(1024) void k_stage2_ring(Stage2Args a, const int32_
         if (wave < SC * npw) {
             const int sl = wave / npw, pc = wave - (wave / npw) * npw;
             const int s = s0 + sl;
-            const int om = lomin[s];
+            const int om = __builtin_amdgcn_readfirstlane(lomin[s]);
             const int64_t e0 = t0 + om - (om & 1);
-            const char* src = (const char*)(sub + (int64_t)s * a.sub_stride + e0) + pc * 1024 + lane * 16;
-            dma16(src, slot + (uint32_t)((sl * npw + pc) * 1024));
+            const char* src = (const char*)(sub + (int64_t)s * a.sub_stride + e0) + pc * 1024;
+            dma16s(src, (uint32_t)lane * 16u, slot + (uint32_t)((sl * npw + pc) * 1024));
         } else {
             const int bp = wave - SC * npw;
-            const char* src = (const char*)(bo_g + (int64_t)s0 * dpb) + bp * 1024 + lane * 16;
-            dma16(src, slot + (uint32_t)((SC * npw + bp) * 1024));
+            const char* src = (const char*)(bo_g + (int64_t)s0 * dpb) + bp * 1024;
+            dma16s(src, (uint32_t)lane * 16u, slot + (uint32_t)((SC * npw + bp) * 1024));
         }
     };
     // staging slot of chunk cc -> its 4 shifted copies in expanded buffer cc & 1
@@ -1544,24 +1581,32 @@ __global__ __launch_bounds__(1024) void k_stage2_ring(Stage2Args a, const int32_
 
     for (int c = 0; c < nchunk; c++) {
         dma(c + NS - 1);
-        if (c + 1 < nchunk) expand(c + 1);
+        if (c + 1 < nchunk && !(a.probe & 8)) expand(c + 1);
         // this chunk's (subband, DM) byte offsets: entry e = sl*Q + q in lane e
         const int32_t* sboff = (const int32_t*)(lds_raw + ring0 + (c % NS) * slot_bytes + SC * npw * 1024);
         const int esl = lane / Q, eq = lane - (lane / Q) * Q;
         const int voff = esl < SC ? sboff[esl * dpb + wave * Q + eq] : 0;
         if (!(a.probe & 1)) {
-            constexpr int nsteps = SC * Q;
-            uint64_t b0[R], b1[R];
-            lds_read_r<R>(b0, (uint32_t)__builtin_amdgcn_readlane(voff, 0) + lane_byte);
+            // (subband, DM) steps of this chunk; the reads of step e+LA are issued before
+            // step e's sums, so LA steps of R reads stay in flight per wave
+            constexpr int nsteps = SC * Q, LA = ring_la<Q, R>();
+            uint64_t bb[LA + 1][R];
+#pragma unroll
+            for (int e = 0; e < LA; e++)
+                lds_read_r<R>(bb[e], (uint32_t)__builtin_amdgcn_readlane(voff, e) + lane_byte);
 #pragma unroll
             for (int e = 0; e < nsteps; e++) {
-                uint64_t (&cur)[R] = (e & 1) ? b1 : b0;
-                uint64_t (&nxt)[R] = (e & 1) ? b0 : b1;
-                if (e + 1 < nsteps) {
-                    lds_read_r<R>(nxt, (uint32_t)__builtin_amdgcn_readlane(voff, e + 1) + lane_byte);
-                    lds_wait_keep<R>(cur);
+                uint64_t (&cur)[R] = bb[e % (LA + 1)];
+                if (e + LA < nsteps) {
+                    lds_read_r<R>(bb[(e + LA) % (LA + 1)],
+                                  (uint32_t)__builtin_amdgcn_readlane(voff, e + LA) + lane_byte);
+                    lds_wait_n<LA * R>(cur);
+                } else if (e + 3 == nsteps && LA >= 2) {
+                    lds_wait_n<2 * R>(cur);
+                } else if (e + 2 == nsteps && LA >= 1) {
+                    lds_wait_n<R>(cur);
                 } else {
-                    lds_wait_all<R>(cur);
+                    lds_wait_n<0>(cur);
                 }
                 const int q = e % Q;
 #pragma unroll
@@ -1878,9 +1923,17 @@ hipError_t launch_stage2_ring(const Stage2Args& a, int q, int r, hipStream_t st)
     if (a.nvalid <= 0) return hipSuccess;
     const int nyblk = (a.numdms + a.dms_per_blk - 1) / a.dms_per_blk;
 #define HD_RL(QQ, RR) if (q == QQ && r == RR) return launch_ring_qr<QQ, RR>(a, nyblk, st);
-    HD_WIDE_QR(HD_RL)
+    HD_RING_QR(HD_RL)
 #undef HD_RL
     return hipErrorInvalidValue;
+}
+
+bool stage2_ring_supports(int q, int r)
+{
+#define HD_RS(QQ, RR) if (q == QQ && r == RR) return true;
+    HD_RING_QR(HD_RS)
+#undef HD_RS
+    return false;
 }
 
 size_t stage2_wide_lds_bytes(int wstride, int sc) { return (size_t)2 * sc * 4 * wstride * sizeof(int16_t); }

@@ -35,6 +35,7 @@ EXPORTED = [
     "hd_plan_get_delays", "hd_plan_sub_params", "hd_run_subband", "hd_get_subbands",
     "hd_set_subbands", "hd_run_dedisp", "hd_plan_last_ms", "hd_plan_set_variant",
     "hd_get_raw", "hd_plan_tables", "hd_run_subband_multi", "hd_push_raw_device", "hd_get_raw_device",
+    "hd_push_raw_file",
 ]
 
 
@@ -63,6 +64,12 @@ class hd_pass(ctypes.Structure):
 
 
 _NPSR = 8
+
+
+class hd_rows_src(ctypes.Structure):
+    _fields_ = [("table_offset", ctypes.c_int64), ("row_bytes", ctypes.c_int64), ("col_offset", ctypes.c_int64),
+                ("col_bytes", ctypes.c_int64), ("row0", ctypes.c_int64), ("nrows", ctypes.c_int64),
+                ("block_bytes", ctypes.c_int64)]
 
 
 class hd_synth(ctypes.Structure):
@@ -127,6 +134,8 @@ def load():
         "hd_run_subband_multi": (ctypes.c_int, [P(vp), i32]),
         "hd_push_raw_device": (ctypes.c_int, [vp, vp, i64, i64]),
         "hd_get_raw_device": (ctypes.c_int, [vp, vp, i64, i64]),
+        "hd_push_raw_file": (ctypes.c_int, [vp, ctypes.c_char_p, P(hd_rows_src), i64, P(ctypes.c_double),
+                                            P(ctypes.c_double)]),
         "hd_plan_tables": (ctypes.c_int, [P(hd_obs), P(hd_opts), P(hd_pass), P(ctypes.c_int32),
                                           P(ctypes.c_int32), P(ctypes.c_double), P(ctypes.c_double),
                                           P(ctypes.c_double)]),

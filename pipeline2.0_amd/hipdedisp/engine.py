@@ -5,6 +5,7 @@ raises when a PRESTO program fails (lib/python/PALFA2_presto_search.py:740-744,
 raised at :123-128), so callers' retry/cleanup semantics are unchanged.
 """
 import ctypes
+import os
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -166,6 +167,19 @@ class Engine:
         n = a.size // self.obs.rowbytes
         self._chk(self._L.hd_push_raw(self._ctx, a.ctypes.data_as(ctypes.c_void_p), int(start), int(n)),
                   "hd_push_raw")
+
+    def push_raw_file(self, path, table_offset, row_bytes, col_offset, col_bytes, row0, nrows, start=0,
+                      block_bytes=0):
+        """Stream the DATA column of rows [row0, row0+nrows) of a PSRFITS SUBINT table from
+        `path` into device spectra [start, ...) through two pinned host blocks
+        (hd_push_raw_file).  Returns (seconds in pread, seconds for the call)."""
+        src = _lib.hd_rows_src(table_offset=int(table_offset), row_bytes=int(row_bytes), col_offset=int(col_offset),
+                               col_bytes=int(col_bytes), row0=int(row0), nrows=int(nrows),
+                               block_bytes=int(block_bytes))
+        io, tot = ctypes.c_double(), ctypes.c_double()
+        self._chk(self._L.hd_push_raw_file(self._ctx, os.fsencode(path), ctypes.byref(src), int(start),
+                                           ctypes.byref(io), ctypes.byref(tot)), "hd_push_raw_file(%s)" % path)
+        return io.value, tot.value
 
     def push_raw_device(self, dev_ptr, start=0, count=None):
         """Raw spectra from device memory of this context's GPU (an int address, e.g. a

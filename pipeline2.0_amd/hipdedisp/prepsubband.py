@@ -85,7 +85,7 @@ def run(argv):
             scl, offs, wts = si.read_calib()
             if scl is not None or offs is not None or wts is not None:
                 eng.set_calib(scl, offs, wts)
-            eng.push_raw(si.read_spectra())
+            si.stream_to(eng)
             _mask_state(eng, a.mask, obs.nchan)
             if a.sub:
                 if a.subdm is None:

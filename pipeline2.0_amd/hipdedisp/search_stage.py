@@ -76,7 +76,7 @@ class DedispJob:
             scl, offs, wts = self.specinfo.read_calib()
             if scl is not None or offs is not None or wts is not None:
                 self.engine.set_calib(scl, offs, wts)
-            self.engine.push_raw(self.specinfo.read_spectra())
+            self.ingest = self.specinfo.stream_to(self.engine)   # (pread s, total s, bytes)
         return self.engine
 
     def load_mask(self, maskfilenm):

@@ -120,3 +120,27 @@ def test_report_lines():
     lines = report_lines(J(), 100.0)
     assert lines[0] == "       subbanding time =    12.5 sec (12.50%)"
     assert lines[1] == "     dedispersing time =    30.2 sec (30.25%)"
+
+
+def test_psrfits_stream_geometry(tmp_path):
+    """SpectraInfo.stream_to hands hd_push_raw_file the DATA column geometry of each SUBINT
+    table; reading the file with exactly that geometry (as the C reader does) gives the
+    spectra read_spectra() gives.  CPU: the engine is a recorder."""
+    obs = palfa_obs(N=4096, nbits=8, nsblk=512)
+    spectra = host_spectra(obs, palfa_synth())
+    fn = str(tmp_path / "beam.fits")
+    psrfits.write_psrfits(fn, spectra, obs)
+    si = psrfits.SpectraInfo([fn])
+
+    class Rec:
+        def push_raw_file(self, path, table_offset, row_bytes, col_offset, col_bytes, row0, nrows, start=0,
+                          block_bytes=0):
+            raw = np.fromfile(path, np.uint8)
+            rows = [raw[table_offset + (row0 + i) * row_bytes + col_offset:][:col_bytes] for i in range(nrows)]
+            self.got = (start, np.concatenate(rows).reshape(-1, obs.rowbytes))
+            return 0.0, 0.0
+
+    rec = Rec()
+    _, _, nbytes = si.stream_to(rec)
+    assert nbytes == spectra.size
+    assert rec.got[0] == 0 and np.array_equal(rec.got[1], spectra)

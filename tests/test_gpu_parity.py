@@ -258,3 +258,36 @@ def test_injected_single_pulse_recovered(engine):
     w = int(round(0.002 / obs.dt))
     assert t0 - 2 <= t <= t0 + w + 2
     assert z[d, t] > 8.0
+
+
+@pytest.mark.parametrize("nbits,flip,block", [(8, True, 0), (4, True, 700000), (16, False, 1 << 20)])
+def test_psrfits_stream_ingest(engine, tmp_path, nbits, flip, block):
+    """hd_push_raw_file (pinned double-buffered pread -> hipMemcpyAsync): the device raw block
+    equals the file's spectra byte for byte, for one block and for many blocks (small block
+    sizes force the two pinned buffers to alternate), and a pass run on it matches the oracle."""
+    from hipdedisp.formats import psrfits
+    obs = palfa_obs(N=8192, nbits=nbits, nsblk=512, flip=flip)
+    spectra = host_spectra(obs, palfa_synth(nbits=nbits))
+    fn = str(tmp_path / "beam.fits")
+    psrfits.write_psrfits(fn, spectra, obs)
+    si = psrfits.SpectraInfo([fn])
+    engine.set_obs(si.obs_params(), Opts())
+    io_s, tot_s, nbytes = si.stream_to(engine, block_bytes=block)
+    assert nbytes == spectra.size and 0.0 <= io_s <= tot_s
+    assert np.array_equal(engine.get_raw(), spectra)
+    pp = PassParams(subdm=30.0, lodm=26.2, dmstep=0.1, numdms=76, nsub=96, ds=1, numout=0)
+    p = engine.plan(pp)
+    p.run_subband()
+    got = p.run_dedisp()
+    p.destroy()
+    _, want = OR.run_pass(obs, Opts(), spectra, pp)
+    assert np.array_equal(got, want)
+
+
+def test_psrfits_stream_ingest_errors(engine, tmp_path):
+    obs = palfa_obs(N=2048, nbits=8, nsblk=512)
+    engine.set_obs(obs, Opts())
+    with pytest.raises(PrestoError):
+        engine.push_raw_file(str(tmp_path / "missing.fits"), 0, obs.rowbytes * 512, 0, obs.rowbytes * 512, 0, 4)
+    with pytest.raises(PrestoError):   # DATA column that is not whole spectra
+        engine.push_raw_file(str(tmp_path / "missing.fits"), 0, 1000, 0, 999, 0, 4)
