@@ -215,12 +215,15 @@ HD_API int hd_run_dedisp(hd_plan* plan, float* host_out);
 /* Device-time of the last hd_run_subband / hd_run_dedisp of this plan, ms.           */
 HD_API int hd_plan_last_ms(const hd_plan* plan, float* ms_subband, float* ms_dedisp);
 /* Kernel variants: (s1 << 8) | s2.  s2: 0 auto, 1 direct, 2 LDS-tiled (4 waves x 256 samples),
- * 3 wide LDS tiles (up to 16 waves share one window); s1: 0 auto, 1 direct
+ * 3 wide LDS tiles (up to 16 waves share one window), 4 two workgroups per CU, 5 LDS-DMA
+ * ring, 6 ring over subband-pair partials (the auto choice when 2*max|subband| <= 32767 is
+ * known on the host: 8/4-bit data without calibration, or uploaded int16 subbands; forcing
+ * it otherwise fails in hd_run_dedisp with HD_E_INVAL); s1: 0 auto, 1 direct
  * (one thread per subband sample, for cross-checks), 2 float tiled multi-pass, 3 8-bit
  * integer tiled multi-pass (8-bit data without calibration only; HD_E_INVAL otherwise).
  * Bits 16-23 are profiling probes that skip parts of the tiled kernels (results are then
  * invalid; never set them in production): 1 skip the sums, 2 skip the LDS fill, 4 skip
- * the stage-2 stores. */
+ * the stage-2 stores, 8 skip the stage-2 expand. */
 HD_API int hd_plan_set_variant(hd_plan* plan, int32_t variant);
 
 #ifdef __cplusplus

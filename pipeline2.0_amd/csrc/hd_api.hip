@@ -75,9 +75,13 @@ struct hd_plan {
     struct Wide {
         bool ok = false;
         int32_t q = 0, r = 0, nw = 0, dpb = 0, ws = 0, sc = 0, npw = 0, nbp = 0;
-        int32_t* d_omin = nullptr;
+        int32_t umax = 0;               // [3] only: largest pattern count of a subband pair
+        int32_t* d_omin = nullptr;      // [3]: the pair table (kPairTab ints per y-block and pair)
         int32_t* d_boff = nullptr;
-    } wide[3];                      // [2]: k_stage2_ring (16 waves, LDS-DMA staging ring)
+    } wide[4];                      // [2]: k_stage2_ring (16 waves, LDS-DMA staging ring);
+                                    // [3]: k_stage2_pair (the ring over subband-pair partials)
+    int32_t sub_bound = -1;         // bound on |subband| known on the host (-1: none), set when
+                                    // the subbands are formed or uploaded (pair variant gate)
     int32_t variant = 0;
     float* d_out = nullptr;
     void* d_sub = nullptr;          // this pass's subbands [nsub][sub_stride]
@@ -801,6 +805,103 @@ static void wide_tables(hd_plan* p, int nwmax, bool dbuf, bool i16, hd_plan::Wid
             }
 }
 
+// Tables of the pair variant (k_stage2_pair): the ring's y-blocks (16 waves x Q DMs), one
+// subband pair (2c, 2c+1) per chunk.  Per y-block and pair: the distinct relative offsets
+// r = off[d][2c+1] - off[d][2c] of the block's DMs (sorted; at most kPairUMax, else the
+// variant does not apply), base0 = min off[d][2c], b1 = base0 + min r, and the S1 staging
+// index k1[u] = r_u - min r + (b1 & 1) of pattern u.  boff[yb][c][k] = LDS byte offset
+// (from the expanded area) of DM k's 4 samples: buffer (c & 1), pattern u(k), copy o2 & 3.
+static void pair_tables(hd_plan* p, bool i16, hd_plan::Wide& w, std::vector<int32_t>& ptab,
+                        std::vector<int32_t>& boff)
+{
+    w = hd_plan::Wide{};
+    const int nsub = p->pass.nsub, numdms = p->pass.numdms;
+    if (!i16 || nsub % 2 || numdms < 1) return;
+    int nyb = (numdms + 80 - 1) / 80;
+    const int per = (numdms + nyb - 1) / nyb;
+    const int qneed = (per + 15) / 16;
+    int Q = 2, R = 4;
+    if (qneed > 4) { Q = 5; R = 3; }
+    else if (qneed > 3) { Q = 4; R = 3; }
+    else if (qneed > 2) { Q = 3; R = 4; }
+    const int dpb = 16 * Q;
+    nyb = (numdms + dpb - 1) / dpb;
+    const int npair = nsub / 2;
+    ptab.assign((size_t)nyb * npair * hd::kPairTab, 0);
+    std::vector<std::vector<int32_t>> rs((size_t)nyb * npair);
+    int32_t span0 = 0, k1max = 0;
+    int umax = 0;
+    auto dmof = [&](int yb, int k) { return std::min(yb * dpb + k, numdms - 1); };
+    for (int yb = 0; yb < nyb; yb++)
+        for (int c = 0; c < npair; c++) {
+            const int s0 = 2 * c, s1 = s0 + 1;
+            int32_t lo = INT32_MAX, hi = INT32_MIN;
+            std::vector<int32_t>& r = rs[(size_t)yb * npair + c];
+            for (int k = 0; k < dpb; k++) {
+                const int dm = dmof(yb, k);
+                const int32_t o0 = p->off[(size_t)dm * nsub + s0], o1 = p->off[(size_t)dm * nsub + s1];
+                lo = std::min(lo, o0);
+                hi = std::max(hi, o0);
+                r.push_back(o1 - o0);
+            }
+            std::sort(r.begin(), r.end());
+            r.erase(std::unique(r.begin(), r.end()), r.end());
+            if ((int)r.size() > hd::kPairUMax) return;
+            const int32_t b1 = lo + r[0];
+            int32_t* t = &ptab[((size_t)yb * npair + c) * hd::kPairTab];
+            t[0] = lo;
+            t[1] = b1;
+            t[2] = (int32_t)r.size();
+            for (size_t u = 0; u < r.size(); u++) {
+                t[3 + u] = r[u] - r[0] + (b1 & 1);
+                k1max = std::max(k1max, t[3 + u]);
+            }
+            span0 = std::max(span0, hi - lo);
+            umax = std::max(umax, (int)r.size());
+        }
+    const int ws = (int)round_up((size_t)(256 * R + span0 + 4), 4);
+    const int npw = (int)((((size_t)ws + 10 + k1max) * 2 + 1023) / 1024);
+    const int nbp = (int)(((size_t)dpb * 4 + 1023) / 1024);
+    if (2 * npw + nbp > 16 || hd::stage2_pair_lds_bytes(ws, npw, nbp, nsub, umax) > 160 * 1024 ||
+        !hd::stage2_pair_supports(Q, R))
+        return;
+    boff.assign((size_t)nyb * npair * dpb + 256, 0);   // the last DMA piece may over-read
+    for (int yb = 0; yb < nyb; yb++)
+        for (int c = 0; c < npair; c++) {
+            const std::vector<int32_t>& r = rs[(size_t)yb * npair + c];
+            const int32_t base0 = ptab[((size_t)yb * npair + c) * hd::kPairTab];
+            for (int k = 0; k < dpb; k++) {
+                const int dm = dmof(yb, k);
+                const int32_t o0 = p->off[(size_t)dm * nsub + 2 * c], o1 = p->off[(size_t)dm * nsub + 2 * c + 1];
+                const int u = (int)(std::lower_bound(r.begin(), r.end(), o1 - o0) - r.begin());
+                const int32_t o2 = o0 - base0;
+                boff[((size_t)yb * npair + c) * dpb + k] = ((((c & 1) * umax + u) * 4 + (o2 & 3)) * ws + (o2 & ~3)) * 2;
+            }
+        }
+    w.ok = true;
+    w.q = Q;
+    w.r = R;
+    w.nw = 16;
+    w.dpb = dpb;
+    w.ws = ws;
+    w.sc = 2;
+    w.npw = npw;
+    w.nbp = nbp;
+    w.umax = umax;
+}
+
+// Static bound on |subband| for subbands formed by stage 1 on the device (-1: none): integer
+// samples of <= 8 bits, no calibration, int16 sums of cps*ds samples or pad values.
+static int32_t stage1_sub_bound(const hd_ctx* c, const hd_plan* p)
+{
+    if (c->opts.sub_dtype != HD_SUB_I16 || c->d_scl || c->d_offs || c->d_wts || c->obs.nbits > 8) return -1;
+    double amax = (double)((1 << c->obs.nbits) - 1);
+    for (float v : c->h_padvals) amax = std::max(amax, std::fabs((double)v));
+    const int cps = (c->obs.nchan + p->pass.nsub - 1) / p->pass.nsub;
+    const double b = std::ceil((double)cps * (c->opts.ds_mode == HD_DS_SUM ? p->pass.ds : 1) * amax) + 1.0;
+    return b > 32767.0 ? 32767 : (int32_t)b;
+}
+
 extern "C" int hd_plan_create(hd_ctx* c, const hd_pass* ps, hd_plan** out)
 {
     if (!c) return fail(nullptr, HD_E_INVAL, "hd_plan_create: NULL context");
@@ -864,13 +965,14 @@ extern "C" int hd_plan_create(hd_ctx* c, const hd_pass* ps, hd_plan** out)
                 boff[((size_t)yb * nsub + s) * p->dpb + k] = ((sl * 4 + (o2 & 3)) * p->wstride + (o2 & ~3)) * 2;
             }
 
-    std::vector<int32_t> womin[3], wboff[3];
+    std::vector<int32_t> womin[4], wboff[4];
     for (int k = 0; k < 3; k++)
         wide_tables(p, k == 1 ? 8 : 16, k != 1, c->opts.sub_dtype == HD_SUB_I16, p->wide[k], womin[k], wboff[k], k == 2);
+    pair_tables(p, c->opts.sub_dtype == HD_SUB_I16, p->wide[3], womin[3], wboff[3]);
 
     int rc = HD_OK;
     hipError_t e = hipSetDevice(c->device);
-    for (int k = 0; k < 3 && e == hipSuccess; k++) {
+    for (int k = 0; k < 4 && e == hipSuccess; k++) {
         hd_plan::Wide& w = p->wide[k];
         if (!w.ok) continue;
         e = hipMalloc(&w.d_omin, sizeof(int32_t) * womin[k].size());
@@ -936,10 +1038,11 @@ extern "C" int hd_plan_set_variant(hd_plan* p, int32_t v)
     const int32_t v1 = (v >> 8) & 0xFF;
     p->probe = (v >> 16) & 0xFF;     // profiling only (results invalid): see hipdedisp.h
     v &= 0xFF;
-    if (v < 0 || v > 5 || v1 > 3) return fail(p->ctx, HD_E_INVAL, "variant must be (s1<<8)|s2 with s1 in 0..3, s2 in 0..5");
+    if (v < 0 || v > 6 || v1 > 3) return fail(p->ctx, HD_E_INVAL, "variant must be (s1<<8)|s2 with s1 in 0..3, s2 in 0..6");
     p->s1_variant = v1;
     if (v == 2 && !p->lds_ok) return fail(p->ctx, HD_E_INVAL, "LDS variant unavailable for this plan (needs int16 subbands and a window that fits 64 KiB)");
-    if ((v == 3 && !p->wide[0].ok) || (v == 4 && !p->wide[1].ok) || (v == 5 && !p->wide[2].ok))
+    if ((v == 3 && !p->wide[0].ok) || (v == 4 && !p->wide[1].ok) || (v == 5 && !p->wide[2].ok) ||
+        (v == 6 && !p->wide[3].ok))
         return fail(p->ctx, HD_E_INVAL, "wide-tile variant unavailable for this plan (needs int16 subbands and a window that fits LDS)");
     p->variant = v;
     return HD_OK;
@@ -1235,6 +1338,7 @@ static int run_subband_chunk(hd_ctx* c, hd_plan** plans, int n)
     HIPCHK(c, hipEventRecord(p0->ev[1], c->stream));
     for (int i = 0; i < n; i++) {
         plans[i]->sub_valid = true;
+        plans[i]->sub_bound = stage1_sub_bound(c, plans[i]);
         plans[i]->ran_sub = (i == 0);   // the launch's time is attributed to its first plan
     }
     return HD_OK;
@@ -1301,6 +1405,9 @@ extern "C" int hd_set_subbands(hd_plan* p, const void* host)
         const size_t n = (size_t)p->pass.nsub * p->nds;
         for (size_t i = 0; i < n; i++) m = std::max(m, h[i] < 0 ? -(int32_t)h[i] : (int32_t)h[i]);
         HIPCHK(c, hipMemcpyAsync(p->d_maxabs, &m, sizeof m, hipMemcpyHostToDevice, c->stream));
+        p->sub_bound = m;
+    } else {
+        p->sub_bound = -1;
     }
     HIPCHK(c, hipStreamSynchronize(c->stream));
     p->sub_valid = true;
@@ -1321,9 +1428,20 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         }
     }
     const bool pad = p->numout > p->nds;
+    // pair partials need |sub[s0] + sub[s1]| <= 32767 (packed int16), known on the host
+    const bool pair_ok = p->wide[3].ok && p->sub_bound >= 0 && 2 * p->sub_bound <= 32767;
+    if (p->variant == 6 && !pair_ok)
+        return fail(c, HD_E_INVAL, "hd_run_dedisp: pair variant needs 2 * max|subband| <= 32767 known on the host "
+                    "(bound %d)", (int)p->sub_bound);
     int wk = -1;                       // wide variant in use (index into p->wide), or -1
     if (p->variant >= 3) wk = p->variant - 3;
-    else if (p->variant == 0) wk = p->wide[2].ok ? 2 : p->wide[0].ok ? 0 : (p->wide[1].ok ? 1 : -1);
+    else if (p->variant == 0) {
+        // auto: pair partials where they measured faster than the ring (full-resolution passes
+        // of >= 72 DMs: 1.31 vs 1.39 ms per Mock stage-0 pass; at ds >= 2 or 64 DMs the extra
+        // expand work outweighs the halved sums, profiles/r01_stage2_variants.txt)
+        const bool pair_auto = pair_ok && p->pass.ds == 1 && p->pass.numdms >= 72;
+        wk = pair_auto ? 3 : p->wide[2].ok ? 2 : p->wide[0].ok ? 0 : (p->wide[1].ok ? 1 : -1);
+    }
     const bool use_wide = wk >= 0;
     const bool use_lds = !use_wide && (p->variant == 2 || (p->variant == 0 && p->lds_ok));
     const int tile = use_wide ? 256 * p->wide[wk].r : kTT;
@@ -1369,9 +1487,12 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         a.probe = p->probe;
         a.ring_npw = w.npw;
         a.ring_nbp = w.nbp;
+        a.ptab = w.d_omin;
+        a.umax = w.umax;
         if (wk == 0) HIPCHK(c, hd::launch_stage2_wide(a, w.q, w.r, w.nw, c->stream));
         else if (wk == 1) HIPCHK(c, hd::launch_stage2_wide2(a, w.q, w.r, w.nw, c->stream));
-        else HIPCHK(c, hd::launch_stage2_ring(a, w.q, w.r, c->stream));
+        else if (wk == 2) HIPCHK(c, hd::launch_stage2_ring(a, w.q, w.r, c->stream));
+        else HIPCHK(c, hd::launch_stage2_pair(a, w.q, w.r, c->stream));
     } else if (use_lds) {
         a.off = p->d_boff;
         HIPCHK(c, hd::launch_stage2_lds(a, p->q, c->stream));

@@ -73,6 +73,10 @@ struct Stage2Args {
     int32_t sc;               // wide variant: subbands per LDS chunk
     int32_t ring_npw, ring_nbp;   // ring variant: 1 KiB DMA pieces per window / per offset block
     int32_t probe;            // profiling only: bit0 skip accumulation, bit1 skip fill, bit2 skip stores
+    // pair variant: per (y-block, subband pair) {base0, b1, U, k1[0..U)} (kPairTab ints) and
+    // the largest U of the plan (expanded copies per pair = 4*umax)
+    const int32_t* ptab;
+    int32_t umax;
 };
 
 hipError_t launch_stage1_direct(const Stage1Args& a, hipStream_t st);
@@ -100,6 +104,10 @@ size_t stage2_wide2_lds_bytes(int wstride, int sc, int nsub);
 constexpr int kRingSC = 4, kRingNS = 5;   // ring variant: subbands per chunk, staging slots
 size_t stage2_ring_lds_bytes(int wstride, int npw, int nbp, int nsub);
 hipError_t launch_stage2_ring(const Stage2Args& a, int q, int r, hipStream_t st);
+constexpr int kPairUMax = 6, kPairTab = 16;   // pair variant: patterns per pair, table ints per pair
+size_t stage2_pair_lds_bytes(int wstride, int npw, int nbp, int nsub, int umax);
+bool stage2_pair_supports(int q, int r);
+hipError_t launch_stage2_pair(const Stage2Args& a, int q, int r, hipStream_t st);
 hipError_t launch_stage2_wide2(const Stage2Args& a, int q, int r, int nw, hipStream_t st);
 hipError_t launch_stage2_direct(const Stage2Args& a, hipStream_t st);
 hipError_t launch_stage2_lds(const Stage2Args& a, int q, hipStream_t st);

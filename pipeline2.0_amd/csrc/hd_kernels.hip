@@ -1694,6 +1694,250 @@ static hipError_t launch_ring_qr(const Stage2Args& a, int nyblk, hipStream_t st)
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------
+// Pair variant (default where the subband bound allows it): the ring above, one subband PAIR
+// (s0, s1) per chunk.  For every DM d of the y-block, out[d] takes
+//   sub[s0][t + off[d][s0]] + sub[s1][t + off[d][s1]] = P_u[t + off[d][s0] - base0],
+//   P_u[i] = sub[s0][base0 + i] + sub[s1][base0 + r_u + i],  r_u = off[d][s1] - off[d][s0],
+// and a pass's 76 DMs take only 2-6 distinct r_u per pair (host table).  The expand step
+// forms each P_u once per tile (in its 4 shifted copies) and every DM then reads ONE window
+// per pair instead of two: half the LDS reads and half the packed adds of the ring, at the
+// price of U/2 (mean ~1.5) times the expand writes.  All sums are exact integers (int16
+// subbands, |P_u| <= 2 * max|subband| <= 32767 by the host's static bound, packed-int16
+// groups widened to int32 before they can wrap), so the result is bit-identical.
+// Staging slot of a chunk: [s0 window: npw KiB][s1 window: npw KiB][offsets: nbp KiB];
+// expanded buffer: 2 (chunk parity) x umax patterns x 4 copies x ws int16.
+
+__device__ __forceinline__ void load8_shift(const uint32_t* w32, int x, uint32_t (&o)[4])
+{
+    // o = int16 elements x .. x+7 of the staging window (any parity), as 4 packed pairs
+    const uint32_t* q = w32 + (x >> 1);
+    const uint32_t sh = (uint32_t)(x & 1) * 16u;
+    uint32_t w[5];
+#pragma unroll
+    for (int m = 0; m < 5; m++) w[m] = q[m];
+#pragma unroll
+    for (int m = 0; m < 4; m++) o[m] = __builtin_amdgcn_alignbit(w[m + 1], w[m], sh);
+}
+
+template <int Q, int R>
+__global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, const int32_t* __restrict__ boff)
+{
+    extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+    constexpr int NS = kRingNS, T = 256 * R;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t t0 = (int64_t)tile * T;
+    const int yb = blockIdx.y;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nthr = blockDim.x;
+    const int dpb = a.dms_per_blk;
+    const int dblk0 = yb * dpb;
+    const int ws = a.wstride;
+    const int upw = ws >> 2;
+    const int npw = a.ring_npw;                       // 1 KiB DMA pieces per window
+    const int nbp = a.ring_nbp;                       // pieces of a chunk's offset block
+    const int umax = a.umax;
+    const int slot_bytes = (2 * npw + nbp) * 1024;
+    const int npair = a.nsub >> 1;
+    const int tab_bytes = npair * kPairTab * 4;
+    int32_t* ltab = (int32_t*)lds_raw;
+    const uint32_t ring0 = (uint32_t)tab_bytes;
+    const uint32_t exp0 = ring0 + (uint32_t)(NS * slot_bytes);
+    const uint32_t lane_byte = exp0 + (uint32_t)lane * 8u;   // host offsets are relative to exp0
+    const int16_t* sub = (const int16_t*)a.sub;
+    const int32_t* bo_g = boff + (int64_t)yb * npair * dpb;
+    const int nchunk = npair;
+
+    for (int i = threadIdx.x; i < npair * kPairTab; i += nthr) ltab[i] = a.ptab[(int64_t)yb * npair * kPairTab + i];
+    __syncthreads();
+
+    int maxabs = *a.maxabs;
+    maxabs = maxabs < 1 ? 1 : maxabs;
+    int G = 32767 / (2 * maxabs);                      // pairs per packed-int16 group
+    G = G < 1 ? 1 : (G > 64 ? 64 : G);
+    G = __builtin_amdgcn_readfirstlane(G);
+
+    int acc32[Q][R][4];
+    short2v acc16[Q][R][2];
+#pragma unroll
+    for (int q = 0; q < Q; q++)
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) acc32[q][r][j] = 0;
+            acc16[q][r][0] = short2v{0, 0};
+            acc16[q][r][1] = short2v{0, 0};
+        }
+    int gcount = 0;
+    const bool loader = wave < 2 * npw + nbp;
+
+    auto dma = [&](int cc) {
+        if (!loader) return;
+        const int c2 = min(cc, nchunk - 1);
+        const uint32_t slot = ring0 + (uint32_t)((cc % NS) * slot_bytes);
+        if (wave < 2 * npw) {
+            const int sl = wave >= npw ? 1 : 0, pc = wave - sl * npw;
+            const int s = 2 * c2 + sl;
+            const int b = __builtin_amdgcn_readfirstlane(ltab[c2 * kPairTab + sl]);   // base0 | b1
+            const int64_t e0 = t0 + b - (b & 1);
+            const char* src = (const char*)(sub + (int64_t)s * a.sub_stride + e0) + pc * 1024;
+            dma16s(src, (uint32_t)lane * 16u, slot + (uint32_t)((sl * npw + pc) * 1024));
+        } else {
+            const int bp = wave - 2 * npw;
+            const char* src = (const char*)(bo_g + (int64_t)c2 * dpb) + bp * 1024;
+            dma16s(src, (uint32_t)lane * 16u, slot + (uint32_t)((2 * npw + bp) * 1024));
+        }
+    };
+    // staging slot of chunk cc -> the 4 shifted copies of each pattern partial, buffer cc & 1
+    auto expand = [&](int cc) {
+        const char* slot = lds_raw + ring0 + (cc % NS) * slot_bytes;
+        const uint32_t* S0 = (const uint32_t*)slot;
+        const uint32_t* S1 = (const uint32_t*)(slot + npw * 1024);
+        const int32_t* pt = ltab + cc * kPairTab;
+        const int k0 = pt[0] & 1;
+        const int U = pt[2];
+        int16_t* buf = (int16_t*)(lds_raw + exp0) + (cc & 1) * (umax * 4 * ws);
+        for (int idx = threadIdx.x; idx < U * upw; idx += nthr) {
+            int u = 0, uu = idx;
+#pragma unroll
+            for (int k = 1; k < kPairUMax; k++)
+                if (uu >= upw) { uu -= upw; u++; }
+            uint32_t A[4], B[4], P[4];
+            load8_shift(S0, k0 + 4 * uu, A);
+            load8_shift(S1, pt[3 + u] + 4 * uu, B);
+#pragma unroll
+            for (int m = 0; m < 4; m++)
+                P[m] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(short2v, A[m]) + __builtin_bit_cast(short2v, B[m]));
+            uint2* dst0 = (uint2*)(buf + (u * 4) * ws);
+            const uint32_t h1 = __builtin_amdgcn_alignbit(P[1], P[0], 16);
+            const uint32_t h3 = __builtin_amdgcn_alignbit(P[2], P[1], 16);
+            const uint32_t h5 = __builtin_amdgcn_alignbit(P[3], P[2], 16);
+            dst0[uu] = make_uint2(P[0], P[1]);
+            dst0[upw + uu] = make_uint2(h1, h3);
+            dst0[2 * upw + uu] = make_uint2(P[1], P[2]);
+            dst0[3 * upw + uu] = make_uint2(h3, h5);
+        }
+    };
+
+#pragma unroll
+    for (int cc = 0; cc < NS - 1; cc++) dma(cc);
+    ring_wait_vm<R>();
+    ring_barrier();
+    expand(0);
+    ring_barrier();
+
+    for (int c = 0; c < nchunk; c++) {
+        dma(c + NS - 1);
+        if (c + 1 < nchunk && !(a.probe & 8)) expand(c + 1);
+        // this chunk's per-DM byte offsets: entry q in lane q
+        const int32_t* sboff = (const int32_t*)(lds_raw + ring0 + (c % NS) * slot_bytes + 2 * npw * 1024);
+        const int voff = lane < Q ? sboff[wave * Q + lane] : 0;
+        if (!(a.probe & 1)) {
+            constexpr int nsteps = Q, LA = ring_la<Q, R>() < Q - 1 ? ring_la<Q, R>() : Q - 1;
+            uint64_t bb[LA + 1][R];
+#pragma unroll
+            for (int e = 0; e < LA; e++)
+                lds_read_r<R>(bb[e], (uint32_t)__builtin_amdgcn_readlane(voff, e) + lane_byte);
+#pragma unroll
+            for (int e = 0; e < nsteps; e++) {
+                uint64_t (&cur)[R] = bb[e % (LA + 1)];
+                if (e + LA < nsteps) {
+                    lds_read_r<R>(bb[(e + LA) % (LA + 1)],
+                                  (uint32_t)__builtin_amdgcn_readlane(voff, e + LA) + lane_byte);
+                    lds_wait_n<LA * R>(cur);
+                } else if (e + 3 == nsteps && LA >= 2) {
+                    lds_wait_n<2 * R>(cur);
+                } else if (e + 2 == nsteps && LA >= 1) {
+                    lds_wait_n<R>(cur);
+                } else {
+                    lds_wait_n<0>(cur);
+                }
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    acc16[e][r][0] += __builtin_bit_cast(short2v, (uint32_t)cur[r]);
+                    acc16[e][r][1] += __builtin_bit_cast(short2v, (uint32_t)(cur[r] >> 32));
+                }
+            }
+            if (++gcount == G) {
+                gcount = 0;
+#pragma unroll
+                for (int qq = 0; qq < Q; qq++)
+#pragma unroll
+                    for (int r = 0; r < R; r++) {
+                        acc32[qq][r][0] += acc16[qq][r][0].x;
+                        acc32[qq][r][1] += acc16[qq][r][0].y;
+                        acc32[qq][r][2] += acc16[qq][r][1].x;
+                        acc32[qq][r][3] += acc16[qq][r][1].y;
+                        acc16[qq][r][0] = short2v{0, 0};
+                        acc16[qq][r][1] = short2v{0, 0};
+                    }
+            }
+        }
+        ring_wait_vm<R>();
+        ring_barrier();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may land after the workgroup ends
+
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+        const int dl = wave * Q + q;
+        const int d = dblk0 + dl;
+        const bool dv = dl < dpb && d < a.numdms;
+        int64_t part = 0;
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            acc32[q][r][0] += acc16[q][r][0].x;
+            acc32[q][r][1] += acc16[q][r][0].y;
+            acc32[q][r][2] += acc16[q][r][1].x;
+            acc32[q][r][3] += acc16[q][r][1].y;
+            const int64_t tl = t0 + 256 * r + 4 * lane;
+            if (dv && !(a.probe & 4)) {
+                float* o = a.out + (int64_t)d * a.out_stride + tl;
+                if (tl + 3 < a.nvalid) {
+                    *(float4*)o = make_float4((float)acc32[q][r][0], (float)acc32[q][r][1], (float)acc32[q][r][2],
+                                              (float)acc32[q][r][3]);
+                    part += (int64_t)acc32[q][r][0] + acc32[q][r][1] + acc32[q][r][2] + acc32[q][r][3];
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        if (tl + j < a.nvalid) {
+                            o[j] = (float)acc32[q][r][j];
+                            part += acc32[q][r][j];
+                        }
+                }
+            }
+        }
+        if (dv && a.partial) {
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) part += __shfl_xor(part, m, 64);
+            if (lane == 0) a.partial[(int64_t)d * a.ntiles + tile] = (double)part;
+        }
+    }
+}
+
+size_t stage2_pair_lds_bytes(int wstride, int npw, int nbp, int nsub, int umax)
+{
+    return (size_t)(nsub / 2) * kPairTab * 4 + (size_t)kRingNS * (2 * npw + nbp) * 1024 +
+           (size_t)2 * umax * 4 * wstride * 2;
+}
+
+template <int Q, int R>
+static hipError_t launch_pair_qr(const Stage2Args& a, int nyblk, hipStream_t st)
+{
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_stage2_pair<Q, R>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           160 * 1024);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    const unsigned ntiles = (unsigned)((a.nvalid + 256 * R - 1) / (256 * R));
+    hipLaunchKernelGGL((k_stage2_pair<Q, R>), dim3(ntiles, (unsigned)nyblk), dim3(1024),
+                       stage2_pair_lds_bytes(a.wstride, a.ring_npw, a.ring_nbp, a.nsub, a.umax), st, a, a.off);
+    return hipGetLastError();
+}
+
 // Two workgroups per CU: 8 waves x Q DMs (<= 40) per workgroup, one LDS window buffer, no
 // register prefetch.  While one workgroup waits for its chunk's loads and barriers, the other
 // accumulates; the subband windows of a tile are filled once per 40-DM y-block.
@@ -1927,6 +2171,18 @@ hipError_t launch_stage2_ring(const Stage2Args& a, int q, int r, hipStream_t st)
 #undef HD_RL
     return hipErrorInvalidValue;
 }
+
+hipError_t launch_stage2_pair(const Stage2Args& a, int q, int r, hipStream_t st)
+{
+    if (a.nvalid <= 0) return hipSuccess;
+    const int nyblk = (a.numdms + a.dms_per_blk - 1) / a.dms_per_blk;
+#define HD_PL(QQ, RR) if (q == QQ && r == RR) return launch_pair_qr<QQ, RR>(a, nyblk, st);
+    HD_RING_QR(HD_PL)
+#undef HD_PL
+    return hipErrorInvalidValue;
+}
+
+bool stage2_pair_supports(int q, int r) { return stage2_ring_supports(q, r); }
 
 bool stage2_ring_supports(int q, int r)
 {

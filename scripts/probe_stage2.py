@@ -11,6 +11,8 @@ from hipdedisp.synth import palfa_obs, palfa_synth  # noqa: E402
 
 obs = palfa_obs(N=1 << 22, nbits=8)
 args = [x for x in sys.argv[1:] if not x.startswith("--probes=")]
+variant = int(next((a[10:] for a in sys.argv[1:] if a.startswith("--variant=")), "0"))
+args = [x for x in args if not x.startswith("--variant=")]
 stages = [int(x) for x in (args or ["0"])]
 probes = [int(x) for x in next((a[9:] for a in sys.argv[1:] if a.startswith("--probes=")), "0,1,4,5,8,9,13,15").split(",")]
 with Engine(0) as eng:
@@ -23,11 +25,11 @@ with Engine(0) as eng:
                                 numout=P.choose_N(obs.N / d.downsamp)))
         p.run_subband()
         for probe in probes:
-            p.set_variant(probe << 16)
+            p.set_variant((probe << 16) | variant)
             t = []
             for _ in range(5):
                 p.run_dedisp(to_host=False)
                 eng.sync()
                 t.append(p.last_ms()[1])
-            print("stage %d stage-2 probe %2d: %.3f ms" % (st, probe, min(t)), flush=True)
+            print("stage %d stage-2 variant %d probe %2d: %.3f ms" % (st, variant, probe, min(t)), flush=True)
         p.destroy()

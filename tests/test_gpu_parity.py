@@ -79,7 +79,7 @@ def test_stage1_calib_mask_bitexact(engine, sub_dtype, ds_mode):
 
 @pytest.mark.parametrize("numdms,ds,numout_mode", [(76, 1, "none"), (64, 2, "none"), (76, 3, "pad"),
                                                    (5, 1, "trunc"), (100, 5, "pad"), (76, 10, "pad")])
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6])
 def test_stage2_bitexact(engine, numdms, ds, numout_mode, variant):
     obs = palfa_obs(N=3 * 8192, nbits=8)
     raw = load_beam(engine, obs)
@@ -89,11 +89,64 @@ def test_stage2_bitexact(engine, numdms, ds, numout_mode, variant):
     lodm = 534.4 if ds > 1 else 12.3
     pp = PassParams(subdm=lodm + 19.0, lodm=lodm, dmstep=0.5, numdms=numdms, nsub=96, ds=ds, numout=numout)
     p = engine.plan(pp)
-    p.set_variant(variant)
+    try:
+        p.set_variant(variant)
+    except PrestoError:
+        if variant == 6:   # wide DM steps: > kPairUMax patterns per pair or LDS (the DDplan passes apply, below)
+            pytest.skip("pair variant not applicable to this plan")
+        raise
     p.run_subband()
-    got = p.run_dedisp()
+    try:
+        got = p.run_dedisp()
+    except PrestoError:
+        if variant == 6 and ds == 10:
+            pytest.skip("pair variant not applicable (subband bound)")
+        raise
     sub, want = OR.run_pass(obs, Opts(), raw, pp)
     assert got.shape == want.shape
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("stage,passnum", [(0, 0), (0, 27), (1, 5), (2, 0), (3, 8), (4, 2)])
+def test_stage2_pair_ddplan_passes(engine, stage, passnum):
+    """The pair-partial kernel (variant 6, the default for 8-bit data) on real Mock DDplan
+    passes, rfifind-style mask, bit-exact against the oracle; the default choice must be
+    the same kernel (same result) and the ring (variant 5) must agree too."""
+    obs = palfa_obs(N=3 * 8192, nbits=8)
+    synth = palfa_synth()
+    raw = load_beam(engine, obs, synth=synth)
+    pts = 2048
+    mask, pad = synth_mask(obs, synth, pts)
+    engine.set_mask(mask, pts, pad)
+    d = plan.ddplans_for("pdev")[stage]
+    pp = PassParams(subdm=float(d.subdmlist[passnum]), lodm=float(d.lodm_arg(passnum)), dmstep=float(d.dmstep_arg()),
+                    numdms=d.dmsperpass, nsub=d.numsub, ds=d.sub_downsamp, numout=plan.choose_N(obs.N / d.downsamp))
+    p = engine.plan(pp)
+    p.run_subband()
+    outs = []
+    for v in (6, 0, 5):
+        p.set_variant(v)
+        outs.append(p.run_dedisp())
+    _, want = OR.run_pass(obs, Opts(), raw, pp, mask=mask, ptsperint=pts, padvals=pad)
+    for v, got in zip((6, 0, 5), outs):
+        assert np.array_equal(got, want), v
+    engine.set_mask()
+
+
+def test_stage2_pair_rejects_unbounded_subbands(engine):
+    """16-bit data: no host bound on |subband| -> the pair variant refuses (HD_E_INVAL) and
+    the default falls back to the ring kernel, still bit-exact."""
+    obs = palfa_obs(N=2 * 8192, nbits=16)
+    raw = load_beam(engine, obs)
+    pp = PassParams(subdm=30.0, lodm=26.2, dmstep=0.1, numdms=76, nsub=96, ds=1, numout=0)
+    p = engine.plan(pp)
+    p.run_subband()
+    p.set_variant(6)
+    with pytest.raises(PrestoError):
+        p.run_dedisp()
+    p.set_variant(0)
+    got = p.run_dedisp()
+    _, want = OR.run_pass(obs, Opts(), raw, pp)
     assert np.array_equal(got, want)
 
 
