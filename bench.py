@@ -34,6 +34,9 @@ def parse():
     ap.add_argument("--nbits", type=int, default=8)
     ap.add_argument("--variant", type=int, default=0, help="stage-2 kernel: 0 auto, 1 direct, 2 LDS")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU-baseline leg")
+    ap.add_argument("--streams", type=int, default=1, choices=(1, 2),
+                    help="stage-2 HIP streams (hd_set_streams): 2 overlaps consecutive passes (no launch tails; "
+                         "per-kernel event times then include the shared time, so the roofline is taken at 1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU work for the baseline sample")
     ap.add_argument("--mode", choices=["beam", "shard"], default="beam",
                     help="beam: one beam per rank (weak scaling, configs[4]); shard: ONE beam's 57 passes "
@@ -185,6 +188,7 @@ def main():
         synth = palfa_synth(beam=0, nbits=args.nbits)       # one beam for the whole node
     eng = Engine(local)
     eng.set_obs(obs, Opts())
+    eng.set_streams(args.streams)
     if not shard or rank == 0:
         eng.synth_device(synth)
     pts = rfifind_ptsperint(obs.dt)
@@ -272,6 +276,7 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "avg_launch_ms": launch_ms, "bytes_per_unit": b_unit},
         "kernel_ms_per_step": {"stage1": ms1, "stage2": ms2},
+        "stage2_streams": args.streams,
         "step_compulsory_hbm_frac": (raw_bytes + 4.0 * out_per_step) / step_s / (HBM_PEAK_GBS * 1e9),
         "stage2_valu_frac": adds2 / (ms2 * 1e-3) / VALU_ADD_PEAK if ms2 > 0 else None,
     }

@@ -138,6 +138,12 @@ HD_API int         hd_open(int device, hd_ctx** out);
 HD_API int         hd_close(hd_ctx* ctx);
 HD_API const char* hd_last_error(const hd_ctx* ctx);
 HD_API int         hd_sync(hd_ctx* ctx);
+/* Streams for stage 2 (default 1).  With 2, consecutive hd_run_dedisp calls alternate
+ * between two HIP streams, so one pass's last tiles share the GPU with the next pass's
+ * first ones (no launch tail); stage 1 and hd_set_subbands wait for the second stream's
+ * passes, hd_sync waits for both.  Per-plan device times (hd_plan_last_ms) then include
+ * the time a kernel shared the GPU with its neighbour.                                */
+HD_API int         hd_set_streams(hd_ctx* ctx, int32_t n);
 
 /* Observation + switches.  The device raw block (N * nchan * nbits/8 bytes) is allocated
  * on the first hd_push_raw / hd_synth_device. */

@@ -52,7 +52,37 @@ struct hd_ctx {
     void* pin[2] = {nullptr, nullptr};
     size_t pin_bytes = 0;
     hipEvent_t pin_ev[2] = {nullptr, nullptr};
+    // stage 2 alternates between the main stream and stream2, so one pass's last tiles and
+    // the next pass's first ones share the GPU (no tail between launches).  ev_fork orders
+    // stream2 after the main stream's work so far; ev_join (after each stream2 pass) orders
+    // main-stream work that rewrites subbands after it; each stream has its own partials.
+    hipStream_t stream2 = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    bool s2_pending = false;
+    bool dual = false;              // hd_set_streams(ctx, 2)
+    uint32_t dd_count = 0;
+    double* d_partial2 = nullptr;
+    size_t partial_bytes2 = 0;
 };
+
+// main-stream work from here on runs after every stage-2 pass queued on stream2
+static hipError_t join_stream2(hd_ctx* c)
+{
+    if (!c->s2_pending) return hipSuccess;
+    c->s2_pending = false;
+    return hipStreamWaitEvent(c->stream, c->ev_join, 0);
+}
+
+static hipError_t sync_all(hd_ctx* c)
+{
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (c->stream2) {
+        const hipError_t e2 = hipStreamSynchronize(c->stream2);
+        if (e == hipSuccess) e = e2;
+    }
+    c->s2_pending = false;
+    return e;
+}
 
 struct hd_plan {
     hd_ctx* ctx = nullptr;
@@ -91,6 +121,7 @@ struct hd_plan {
     int32_t probe = 0;              // profiling switches (hd_plan_set_variant bits 16-23)
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     bool ran_sub = false, ran_dd = false;
+    hipStream_t dd_stream = nullptr;  // stream of the last hd_run_dedisp (its ev[3] marks the end)
 };
 
 static thread_local std::string g_err;
@@ -187,7 +218,10 @@ extern "C" int hd_open(int device, hd_ctx** out)
         return fail(nullptr, HD_E_NODEV, "hd_open: device %d out of range (have %d)", device, n);
     hd_ctx* c = new hd_ctx();
     c->device = device;
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
         delete c;
         return fail(nullptr, HD_E_HIP, "hd_open: cannot initialise device %d", device);
     }
@@ -213,9 +247,13 @@ extern "C" int hd_close(hd_ctx* c)
 {
     if (!c) return HD_OK;
     (void)hipSetDevice(c->device);
-    (void)hipStreamSynchronize(c->stream);
+    (void)sync_all(c);
     free_obs_buffers(c);
     dfree(c->d_partial);
+    dfree(c->d_partial2);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     for (int b = 0; b < 2; b++) {
         if (c->pin[b]) (void)hipHostFree(c->pin[b]);
         if (c->pin_ev[b]) (void)hipEventDestroy(c->pin_ev[b]);
@@ -226,13 +264,24 @@ extern "C" int hd_close(hd_ctx* c)
     return HD_OK;
 }
 
+extern "C" int hd_set_streams(hd_ctx* c, int32_t n)
+{
+    if (!c) return fail(nullptr, HD_E_INVAL, "hd_set_streams: NULL context");
+    if (n != 1 && n != 2) return fail(c, HD_E_INVAL, "hd_set_streams: n must be 1 or 2");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, sync_all(c));
+    c->dual = n == 2;
+    c->dd_count = 0;
+    return HD_OK;
+}
+
 extern "C" const char* hd_last_error(const hd_ctx* c) { return c ? c->err.c_str() : g_err.c_str(); }
 
 extern "C" int hd_sync(hd_ctx* c)
 {
     if (!c) return fail(nullptr, HD_E_INVAL, "hd_sync: NULL context");
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, sync_all(c));
     return HD_OK;
 }
 
@@ -263,7 +312,7 @@ extern "C" int hd_set_obs(hd_ctx* c, const hd_obs* o, const hd_opts* opts)
     if (op.clip_sigma != 0.0f)
         return fail(c, HD_E_INVAL, "clip_sigma != 0 is not implemented yet (see DESIGN.md, clipping row)");
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, sync_all(c));
     free_obs_buffers(c);
     c->obs = *o;
     c->opts = op;
@@ -1006,7 +1055,7 @@ extern "C" int hd_plan_destroy(hd_plan* p)
     if (!p) return HD_OK;
     hd_ctx* c = p->ctx;
     (void)hipSetDevice(c->device);
-    (void)hipStreamSynchronize(c->stream);
+    (void)sync_all(c);
     plan_free(p);
     delete p;
     return HD_OK;
@@ -1359,6 +1408,7 @@ extern "C" int hd_run_subband_multi(hd_plan** plans, int32_t n)
     }
     if (!c->raw_ready) return fail(c, HD_E_STATE, "hd_run_subband: no raw data (hd_push_raw / hd_synth_device)");
     HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, join_stream2(c));          // a stage-2 pass on stream2 may still read these subbands
     for (int i = 0; i < n; i++) {
         int rc = ensure_sub(c, plans[i]);
         if (rc) return rc;
@@ -1394,6 +1444,7 @@ extern "C" int hd_set_subbands(hd_plan* p, const void* host)
     if (!p || !host) return fail(p ? p->ctx : nullptr, HD_E_INVAL, "hd_set_subbands: NULL argument");
     hd_ctx* c = p->ctx;
     HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, join_stream2(c));
     int rc = ensure_sub(c, p);
     if (rc) return rc;
     const size_t es = sub_elem(c);
@@ -1428,6 +1479,15 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         }
     }
     const bool pad = p->numout > p->nds;
+    // alternate streams between passes (see hd_ctx::stream2); a plan re-run on the other
+    // stream first waits for its previous run, which wrote the same series
+    const bool alt = c->dual && (c->dd_count++ & 1u) != 0;
+    hipStream_t st = alt ? c->stream2 : c->stream;
+    if (alt) {
+        HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
+        HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
+    }
+    if (p->ran_dd && p->dd_stream != st) HIPCHK(c, hipStreamWaitEvent(st, p->ev[3], 0));
     // pair partials need |sub[s0] + sub[s1]| <= 32767 (packed int16), known on the host
     const bool pair_ok = p->wide[3].ok && p->sub_bound >= 0 && 2 * p->sub_bound <= 32767;
     if (p->variant == 6 && !pair_ok)
@@ -1449,15 +1509,17 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
     double* partial = nullptr;
     if (pad && c->opts.pad_mode == HD_PAD_MEAN) {
         const size_t need = sizeof(double) * (size_t)p->pass.numdms * std::max(ntiles, 1);
-        if (c->partial_bytes < need) {
-            HIPCHK(c, hipStreamSynchronize(c->stream));
-            dfree(c->d_partial);
-            c->d_partial = nullptr;
-            c->partial_bytes = 0;
-            HIPCHK(c, hipMalloc(&c->d_partial, need));
-            c->partial_bytes = need;
+        double*& buf = alt ? c->d_partial2 : c->d_partial;
+        size_t& have = alt ? c->partial_bytes2 : c->partial_bytes;
+        if (have < need) {
+            HIPCHK(c, hipStreamSynchronize(st));
+            dfree(buf);
+            buf = nullptr;
+            have = 0;
+            HIPCHK(c, hipMalloc(&buf, need));
+            have = need;
         }
-        partial = c->d_partial;
+        partial = buf;
     }
     hd::Stage2Args a{};
     a.sub = p->d_sub;
@@ -1476,7 +1538,7 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
     a.omin = p->d_omin;
     a.wstride = p->wstride;
     a.dms_per_blk = p->dpb;
-    HIPCHK(c, hipEventRecord(p->ev[2], c->stream));
+    HIPCHK(c, hipEventRecord(p->ev[2], st));
     if (use_wide) {
         const hd_plan::Wide& w = p->wide[wk];
         a.off = w.d_boff;
@@ -1489,26 +1551,31 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         a.ring_nbp = w.nbp;
         a.ptab = w.d_omin;
         a.umax = w.umax;
-        if (wk == 0) HIPCHK(c, hd::launch_stage2_wide(a, w.q, w.r, w.nw, c->stream));
-        else if (wk == 1) HIPCHK(c, hd::launch_stage2_wide2(a, w.q, w.r, w.nw, c->stream));
-        else if (wk == 2) HIPCHK(c, hd::launch_stage2_ring(a, w.q, w.r, c->stream));
-        else HIPCHK(c, hd::launch_stage2_pair(a, w.q, w.r, c->stream));
+        if (wk == 0) HIPCHK(c, hd::launch_stage2_wide(a, w.q, w.r, w.nw, st));
+        else if (wk == 1) HIPCHK(c, hd::launch_stage2_wide2(a, w.q, w.r, w.nw, st));
+        else if (wk == 2) HIPCHK(c, hd::launch_stage2_ring(a, w.q, w.r, st));
+        else HIPCHK(c, hd::launch_stage2_pair(a, w.q, w.r, st));
     } else if (use_lds) {
         a.off = p->d_boff;
-        HIPCHK(c, hd::launch_stage2_lds(a, p->q, c->stream));
+        HIPCHK(c, hd::launch_stage2_lds(a, p->q, st));
     } else {
         a.off = p->d_off;
-        HIPCHK(c, hd::launch_stage2_direct(a, c->stream));
+        HIPCHK(c, hd::launch_stage2_direct(a, st));
     }
     if (pad)
         HIPCHK(c, hd::launch_pad(p->d_out, p->out_stride, p->pass.numdms, p->nds, p->numout, partial, ntiles,
-                                 c->opts.pad_mode, c->stream));
-    HIPCHK(c, hipEventRecord(p->ev[3], c->stream));
+                                 c->opts.pad_mode, st));
+    HIPCHK(c, hipEventRecord(p->ev[3], st));
+    if (alt) {
+        HIPCHK(c, hipEventRecord(c->ev_join, st));
+        c->s2_pending = true;
+    }
     p->ran_dd = true;
+    p->dd_stream = st;
     if (host_out) {
         HIPCHK(c, hipMemcpy2DAsync(host_out, sizeof(float) * p->numout, p->d_out, sizeof(float) * p->out_stride,
-                                   sizeof(float) * p->numout, p->pass.numdms, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
+                                   sizeof(float) * p->numout, p->pass.numdms, hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipStreamSynchronize(st));
     }
     return HD_OK;
 }

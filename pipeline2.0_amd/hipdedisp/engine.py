@@ -141,6 +141,10 @@ class Engine:
     def sync(self):
         self._chk(self._L.hd_sync(self._ctx), "hd_sync")
 
+    def set_streams(self, n):
+        """1 (default) or 2 HIP streams for stage 2 (hd_set_streams)."""
+        self._chk(self._L.hd_set_streams(self._ctx, int(n)), "hd_set_streams")
+
     # -- observation state --
     def set_obs(self, obs: ObsParams, opts: Optional[Opts] = None):
         opts = opts or Opts()

@@ -388,3 +388,31 @@ def test_candidate_lists_identical_on_injected_sources(engine):
     best_dm = pp.lodm + max(hits, key=lambda c: c[3])[0] * pp.dmstep
     assert abs(best_dm - 71.0) <= 1.5
     engine.set_mask()
+
+
+def test_dual_stream_stage2_matches(engine):
+    """hd_set_streams(2): consecutive passes alternate between two streams (and a plan re-run
+    on the other stream, and stage 1 rewriting subbands a stream-2 pass still reads, are
+    ordered) -- every series equals the single-stream result, over repeated beams."""
+    obs = palfa_obs(N=3 * 8192, nbits=8)
+    load_beam(engine, obs)
+    d = plan.ddplans_for("pdev")[0]
+    pps = [PassParams(subdm=float(d.subdmlist[i]), lodm=float(d.lodm_arg(i)), dmstep=float(d.dmstep_arg()),
+                      numdms=d.dmsperpass, nsub=d.numsub, ds=1, numout=plan.choose_N(obs.N)) for i in range(5)]
+    plans = [engine.plan(pp) for pp in pps]
+    engine.run_subband_multi(plans)
+    want = [p.run_dedisp() for p in plans]
+    engine.set_streams(2)
+    try:
+        for _ in range(3):
+            engine.run_subband_multi(plans)
+            for p in plans:
+                p.run_dedisp(to_host=False)
+            got = [p.run_dedisp() for p in plans]          # host copies, alternating streams again
+            for g, w in zip(got, want):
+                assert np.array_equal(g, w)
+        engine.sync()
+    finally:
+        engine.set_streams(1)
+        for p in plans:
+            p.destroy()
