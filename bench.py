@@ -93,7 +93,9 @@ def build_plans(eng, obs, ddplans, variant):
 
 def run_step(eng, stages):
     """One beam: per DDplan stage, stage 1 for all its passes from one raw read, then the
-    stage-2 sweep of each pass."""
+    stage-2 sweep of each pass.  Every step is a new beam for the engine (hd_touch_raw), so
+    the per-beam channel-major copy of the raw block is rebuilt and timed in each step."""
+    eng.touch_raw()
     for plans in stages:
         if not plans:
             continue

@@ -144,6 +144,10 @@ HD_API int         hd_sync(hd_ctx* ctx);
  * passes, hd_sync waits for both.  Per-plan device times (hd_plan_last_ms) then include
  * the time a kernel shared the GPU with its neighbour.                                */
 HD_API int         hd_set_streams(hd_ctx* ctx, int32_t n);
+/* Declare the raw block changed outside the library (e.g. written in place through a device
+ * pointer): derived layouts (the channel-major copy the 8-bit stage-1 fill reads, built once
+ * per raw block inside the first stage-1 launch) are rebuilt by the next stage-1 launch.  */
+HD_API int         hd_touch_raw(hd_ctx* ctx);
 
 /* Observation + switches.  The device raw block (N * nchan * nbits/8 bytes) is allocated
  * on the first hd_push_raw / hd_synth_device. */

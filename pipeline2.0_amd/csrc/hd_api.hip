@@ -33,6 +33,9 @@ struct hd_ctx {
     int32_t rowbytes = 0;
     uint8_t* d_raw = nullptr;
     bool raw_ready = false;
+    uint8_t* d_rawT = nullptr;         // channel-major copy for the 8-bit stage-1 fill (lazy)
+    int64_t rawT_stride = 0;
+    bool rawT_valid = false;           // false whenever the raw block changes
     float *d_scl = nullptr, *d_offs = nullptr, *d_wts = nullptr;
     uint8_t* d_mask = nullptr;
     int32_t numint = 0, ptsperint = 0;
@@ -232,6 +235,8 @@ extern "C" int hd_open(int device, hd_ctx** out)
 static void free_obs_buffers(hd_ctx* c)
 {
     dfree(c->d_raw); c->d_raw = nullptr;
+    dfree(c->d_rawT); c->d_rawT = nullptr;
+    c->rawT_valid = false;
     dfree(c->d_scl); c->d_scl = nullptr;
     dfree(c->d_offs); c->d_offs = nullptr;
     dfree(c->d_wts); c->d_wts = nullptr;
@@ -273,6 +278,44 @@ extern "C" int hd_set_streams(hd_ctx* c, int32_t n)
     c->dual = n == 2;
     c->dd_count = 0;
     return HD_OK;
+}
+
+extern "C" int hd_touch_raw(hd_ctx* c)
+{
+    if (!c) return fail(nullptr, HD_E_INVAL, "hd_touch_raw: NULL context");
+    c->rawT_valid = false;
+    return HD_OK;
+}
+
+// Channel-major copy of the 8-bit raw block for k_stage1_q8's fill, rebuilt on the stream
+// (and charged to the stage-1 launch that needs it) once per raw block.  nullptr when it
+// does not apply (the kernel then fills from the row-major block).
+static const uint8_t* ensure_rawT(hd_ctx* c, int dmax)
+{
+    if (c->obs.nbits != 8 || c->obs.nchan % 4 || c->obs.N % 4 || (int64_t)dmax + 8 > hd::kRawTPad) return nullptr;
+    if (!c->d_rawT) {
+        const int64_t stride = (int64_t)round_up((size_t)(c->obs.N + hd::kRawTPad), 256);
+        const size_t bytes = (size_t)stride * c->obs.nchan;
+        if (hipMalloc(&c->d_rawT, bytes) != hipSuccess) {
+            c->d_rawT = nullptr;
+            (void)hipGetLastError();
+            return nullptr;                // no room: row-major fill
+        }
+        if (hipMemsetAsync(c->d_rawT, 0, bytes, c->stream) != hipSuccess) {
+            dfree(c->d_rawT);
+            c->d_rawT = nullptr;
+            return nullptr;
+        }
+        c->rawT_stride = stride;
+        c->rawT_valid = false;
+    }
+    if (!c->rawT_valid) {
+        if (hd::launch_raw_transpose8(c->d_raw, c->obs.N, c->obs.nchan, c->d_rawT, c->rawT_stride, c->stream) !=
+            hipSuccess)
+            return nullptr;
+        c->rawT_valid = true;
+    }
+    return c->d_rawT;
 }
 
 extern "C" const char* hd_last_error(const hd_ctx* c) { return c ? c->err.c_str() : g_err.c_str(); }
@@ -394,6 +437,7 @@ extern "C" int hd_push_raw(hd_ctx* c, const void* spectra, int64_t start, int64_
                              hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->raw_ready = true;
+    c->rawT_valid = false;
     return HD_OK;
 }
 
@@ -483,6 +527,7 @@ extern "C" int hd_push_raw_file(hd_ctx* c, const char* path, const hd_rows_src* 
     if (err == HD_E_IO) return fail(c, HD_E_IO, "hd_push_raw_file: short read from %s", path);
     if (err || se != hipSuccess) return fail(c, HD_E_HIP, "hd_push_raw_file: HIP copy failed");
     c->raw_ready = true;
+    c->rawT_valid = false;
     if (io_seconds) *io_seconds = io;
     if (total_seconds) *total_seconds = std::chrono::duration<double>(clk::now() - t_all).count();
     return HD_OK;
@@ -503,6 +548,7 @@ extern "C" int hd_push_raw_device(hd_ctx* c, const void* dev_spectra, int64_t st
                              hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->raw_ready = true;
+    c->rawT_valid = false;
     return HD_OK;
 }
 
@@ -677,6 +723,7 @@ extern "C" int hd_synth_device(hd_ctx* c, const hd_synth* s)
     if (e != hipSuccess || e2 != hipSuccess)
         return fail(c, HD_E_HIP, "synth kernel failed: %s", hipGetErrorString(e != hipSuccess ? e : e2));
     c->raw_ready = true;
+    c->rawT_valid = false;
     return HD_OK;
 }
 
@@ -1303,6 +1350,8 @@ static int run_subband_chunk(hd_ctx* c, hd_plan** plans, int n)
     if (q8) {
         m.probe = p0->probe;
         m.rd = raw_desc(c);
+        m.rawT = (p0->probe & 4) ? nullptr : ensure_rawT(c, dmax);   // probe bit 2: row-major fill
+        m.tstride = c->rawT_stride;
         m.npass = n;
         m.nsub = p0->pass.nsub;
         m.cps = c->obs.nchan / p0->pass.nsub;

@@ -53,6 +53,10 @@ struct Stage1Multi {
     void* out[kMaxPass];            // per-pass subbands [nsub][out_stride]
     int32_t* maxabs[kMaxPass];      // per-pass max |subband|
     int64_t ostride[kMaxPass];      // per-pass subband row stride (elements; rows carry a zero tail)
+    // 8-bit integer path: channel-major copy of the raw block ([nchan][tstride] bytes, file
+    // channel order, zero tail) or nullptr (row-major fill from rd.raw)
+    const uint8_t* rawT;
+    int64_t tstride;
 };
 
 struct Stage2Args {
@@ -113,6 +117,9 @@ hipError_t launch_stage2_direct(const Stage2Args& a, hipStream_t st);
 hipError_t launch_stage2_lds(const Stage2Args& a, int q, hipStream_t st);
 hipError_t launch_pad(float* out, int64_t out_stride, int numdms, int64_t nds, int64_t numout,
                       const double* partial, int ntiles, int pad_mode, hipStream_t st);
+constexpr int64_t kRawTPad = 65536;   // zero rows after N in each channel-major raw row
+hipError_t launch_raw_transpose8(const uint8_t* raw, int64_t N, int32_t nchan, uint8_t* rawT, int64_t tstride,
+                                 hipStream_t st);
 hipError_t launch_synth(uint8_t* raw, int64_t N, int32_t rowbytes, const hd_synth_tab* tab_dev,
                         hipStream_t st);
 

@@ -604,7 +604,54 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
     // ---- fill: unit = (row k, VB-byte chunk): raw rows k + qS (q < 4) -> VB channel dwords;
     //      U units per iteration, all their row loads issued before the first is used (the
     //      fill is latency-bound: a CU needs tens of KB of loads in flight)
-    if (!(a.probe & 2)) {
+    if (!(a.probe & 2) && a.rawT) {
+        // channel-major raw (k_raw_transpose8): unit = (local channel lc, 16-row block kb);
+        // the 4 quarter runs of a channel are contiguous bytes, so each lane loads 16 B per
+        // quarter and a wave's loads are 1-KiB coalesced runs (the row-major fill below uses G
+        // of every 960-B row: 3-7x more L2->L1 traffic than bytes kept, and 4-8x the loads).
+        // Same LDS image: dword kk of channel lc packs rows kk + q*S (q = 0..3).
+        constexpr int U = 4;
+        const int nkb = (K + 15) >> 4;
+        const int units = G * nkb;
+        const int nthr = blockDim.x;
+        const uint8_t* t0p = a.rawT + (int64_t)rc_lo * a.tstride + tR0;
+        for (int u0 = threadIdx.x; u0 < units; u0 += U * nthr) {
+            uint4 r[U][4];
+            int lcs[U], kbs[U];
+#pragma unroll
+            for (int h = 0; h < U; h++) {
+                const int u = min(u0 + h * nthr, units - 1);     // duplicate (idempotent) tail unit
+                lcs[h] = u / nkb;
+                kbs[h] = u - lcs[h] * nkb;
+                const uint8_t* sp = t0p + (int64_t)lcs[h] * a.tstride + 16 * kbs[h];
+#pragma unroll
+                for (int q = 0; q < 4; q++) r[h][q] = *(const uint4*)(sp + (int64_t)q * S);
+            }
+#pragma unroll
+            for (int h = 0; h < U; h++) {
+                uint32_t* d = lds + lcs[h] * W + 16 * kbs[h];
+#pragma unroll
+                for (int w = 0; w < 4; w++) {
+                    const uint32_t x0 = w == 0 ? r[h][0].x : w == 1 ? r[h][0].y : w == 2 ? r[h][0].z : r[h][0].w;
+                    const uint32_t x1 = w == 0 ? r[h][1].x : w == 1 ? r[h][1].y : w == 2 ? r[h][1].z : r[h][1].w;
+                    const uint32_t x2 = w == 0 ? r[h][2].x : w == 1 ? r[h][2].y : w == 2 ? r[h][2].z : r[h][2].w;
+                    const uint32_t x3 = w == 0 ? r[h][3].x : w == 1 ? r[h][3].y : w == 2 ? r[h][3].z : r[h][3].w;
+                    // 4x4 byte transpose: dword j = row 16kb+4w+j of quarters q = 0..3
+                    const uint32_t ab_lo = __builtin_amdgcn_perm(x1, x0, 0x05010400u);
+                    const uint32_t ab_hi = __builtin_amdgcn_perm(x1, x0, 0x07030602u);
+                    const uint32_t cd_lo = __builtin_amdgcn_perm(x3, x2, 0x05010400u);
+                    const uint32_t cd_hi = __builtin_amdgcn_perm(x3, x2, 0x07030602u);
+                    const uint32_t o4[4] = {__builtin_amdgcn_perm(cd_lo, ab_lo, 0x05040100u),
+                                            __builtin_amdgcn_perm(cd_lo, ab_lo, 0x07060302u),
+                                            __builtin_amdgcn_perm(cd_hi, ab_hi, 0x05040100u),
+                                            __builtin_amdgcn_perm(cd_hi, ab_hi, 0x07060302u)};
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        if (16 * kbs[h] + 4 * w + j < K) d[4 * w + j] = o4[j];
+                }
+            }
+        }
+    } else if (!(a.probe & 2)) {
         constexpr int U = 32 / VB;
         const uint8_t* src0 = a.rd.raw + tR0 * rb + rc_lo;
         const int NCH = G / VB;
@@ -652,6 +699,7 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
 
     // ---- per-wave subband state (wave = subband)
     const int sl = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (sl >= a.sg) return;                               // fill-only waves (no barrier follows)
     const int lane = threadIdx.x & 63;
     const int s = g * a.sg + sl;
     const int cl0 = sl * CPS;
@@ -833,7 +881,8 @@ size_t stage1_q8_lds_bytes(const Stage1Multi& a) { return (size_t)a.sg * a.cps *
 template <int CPS, int DS>
 static hipError_t launch_q8_ds(const Stage1Multi& a, int vb, size_t lds, hipStream_t st)
 {
-    const dim3 block((unsigned)(64 * a.sg)), grid((unsigned)(a.ntiles * a.ngroups));
+    // at least 4 waves fill the tile (the fill is latency-bound); waves past sg then leave
+    const dim3 block((unsigned)(64 * (a.sg < 4 ? 4 : a.sg))), grid((unsigned)(a.ntiles * a.ngroups));
     if (vb == 8) hipLaunchKernelGGL((k_stage1_q8<CPS, DS, 8>), grid, block, lds, st, a);
     else hipLaunchKernelGGL((k_stage1_q8<CPS, DS, 4>), grid, block, lds, st, a);
     return hipGetLastError();
@@ -2236,6 +2285,61 @@ hipError_t launch_stage2_wide(const Stage2Args& a, int q, int r, int nw, hipStre
     HD_WIDE_QR(HD_WL)
 #undef HD_WL
     return hipErrorInvalidValue;
+}
+
+// ------------------------------------------------------------------------------------
+// channel-major copy of an 8-bit raw block (k_stage1_q8's fill source)
+// ------------------------------------------------------------------------------------
+// Tile = 128 rows x 128 channels: coalesced 128-B row reads into LDS, then per thread 4x4
+// byte transposes of 4 rows x 4 channels and 128-B channel runs out.  rawT[c][t] = raw[t][c];
+// the kRawTPad bytes after N in every channel row are zeroed by the host allocation.
+__global__ __launch_bounds__(256) void k_raw_transpose8(const uint8_t* __restrict__ raw, int64_t N, int32_t nchan,
+                                                       uint8_t* __restrict__ rawT, int64_t tstride)
+{
+    __shared__ uint32_t tile[128][33];
+    const int64_t t0 = (int64_t)blockIdx.x * 128;
+    const int c0 = blockIdx.y * 128;
+    const int rb = nchan;                                   // bytes per raw row (8-bit)
+    const int ncw = min(128, nchan - c0) >> 2;              // channel dwords in this tile
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int idx = threadIdx.x + 256 * k;
+        const int row = idx >> 5, col = idx & 31;
+        uint32_t v = 0;
+        if (t0 + row < N && col < ncw) v = *(const uint32_t*)(raw + (t0 + row) * rb + c0 + 4 * col);
+        tile[row][col] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int b = threadIdx.x + 256 * k;
+        const int rbk = b & 31, cb = b >> 5;                // rows 4rbk..4rbk+3, channels 4cb..4cb+3
+        if (cb >= ncw) continue;
+        const uint32_t r0 = tile[4 * rbk][cb], r1 = tile[4 * rbk + 1][cb], r2 = tile[4 * rbk + 2][cb],
+                       r3 = tile[4 * rbk + 3][cb];
+        const uint32_t ab_lo = __builtin_amdgcn_perm(r1, r0, 0x05010400u);
+        const uint32_t ab_hi = __builtin_amdgcn_perm(r1, r0, 0x07030602u);
+        const uint32_t cd_lo = __builtin_amdgcn_perm(r3, r2, 0x05010400u);
+        const uint32_t cd_hi = __builtin_amdgcn_perm(r3, r2, 0x07030602u);
+        const uint32_t o4[4] = {__builtin_amdgcn_perm(cd_lo, ab_lo, 0x05040100u),
+                                __builtin_amdgcn_perm(cd_lo, ab_lo, 0x07060302u),
+                                __builtin_amdgcn_perm(cd_hi, ab_hi, 0x05040100u),
+                                __builtin_amdgcn_perm(cd_hi, ab_hi, 0x07060302u)};
+        const int64_t t = t0 + 4 * rbk;
+        if (t < N) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) *(uint32_t*)(rawT + (int64_t)(c0 + 4 * cb + i) * tstride + t) = o4[i];
+        }
+    }
+}
+
+hipError_t launch_raw_transpose8(const uint8_t* raw, int64_t N, int32_t nchan, uint8_t* rawT, int64_t tstride,
+                                 hipStream_t st)
+{
+    if (nchan % 4 || N % 4) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)((N + 127) / 128), (unsigned)((nchan + 127) / 128));
+    hipLaunchKernelGGL(k_raw_transpose8, grid, dim3(256), 0, st, raw, N, nchan, rawT, tstride);
+    return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------

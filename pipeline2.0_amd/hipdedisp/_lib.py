@@ -35,7 +35,7 @@ EXPORTED = [
     "hd_plan_get_delays", "hd_plan_sub_params", "hd_run_subband", "hd_get_subbands",
     "hd_set_subbands", "hd_run_dedisp", "hd_plan_last_ms", "hd_plan_set_variant",
     "hd_get_raw", "hd_plan_tables", "hd_run_subband_multi", "hd_push_raw_device", "hd_get_raw_device",
-    "hd_push_raw_file", "hd_set_streams",
+    "hd_push_raw_file", "hd_set_streams", "hd_touch_raw",
 ]
 
 
@@ -114,6 +114,7 @@ def load():
         "hd_last_error": (ctypes.c_char_p, [vp]),
         "hd_sync": (ctypes.c_int, [vp]),
         "hd_set_streams": (ctypes.c_int, [vp, i32]),
+        "hd_touch_raw": (ctypes.c_int, [vp]),
         "hd_set_obs": (ctypes.c_int, [vp, P(hd_obs), P(hd_opts)]),
         "hd_set_chan_calib": (ctypes.c_int, [vp, f32p, f32p, f32p]),
         "hd_set_mask": (ctypes.c_int, [vp, P(ctypes.c_uint8), i32, i32, f32p]),

@@ -141,6 +141,10 @@ class Engine:
     def sync(self):
         self._chk(self._L.hd_sync(self._ctx), "hd_sync")
 
+    def touch_raw(self):
+        """The raw block changed outside the library: rebuild derived layouts (hd_touch_raw)."""
+        self._chk(self._L.hd_touch_raw(self._ctx), "hd_touch_raw")
+
     def set_streams(self, n):
         """1 (default) or 2 HIP streams for stage 2 (hd_set_streams)."""
         self._chk(self._L.hd_set_streams(self._ctx, int(n)), "hd_set_streams")

@@ -416,3 +416,28 @@ def test_dual_stream_stage2_matches(engine):
         engine.set_streams(1)
         for p in plans:
             p.destroy()
+
+
+def test_stage1_channel_major_fill(engine):
+    """The 8-bit stage-1 kernel fills its LDS tile from a channel-major copy of the raw block
+    (built once per raw block): results equal the row-major fill (probe bit 2) and the oracle,
+    and a new raw block (hd_push_raw) or hd_touch_raw rebuilds the copy."""
+    obs = palfa_obs(N=3 * 8192, nbits=8)
+    d = plan.ddplans_for("pdev")[3]
+    pp = PassParams(subdm=float(d.subdmlist[2]), lodm=float(d.lodm_arg(2)), dmstep=float(d.dmstep_arg()),
+                    numdms=d.dmsperpass, nsub=96, ds=d.sub_downsamp, numout=0)
+    for beam in (0, 1):
+        raw = load_beam(engine, obs, synth=palfa_synth(beam=beam), device_synth=False)
+        p = engine.plan(pp)
+        p.run_subband()
+        a = p.get_subbands()
+        p.set_variant(4 << 16)            # probe: row-major fill
+        p.run_subband()
+        b = p.get_subbands()
+        p.set_variant(0)
+        engine.touch_raw()
+        p.run_subband()
+        c = p.get_subbands()
+        want, _ = OR.run_pass(obs, Opts(), raw, pp)
+        p.destroy()
+        assert np.array_equal(a, want) and np.array_equal(b, want) and np.array_equal(c, want), beam
