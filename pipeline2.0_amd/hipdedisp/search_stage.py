@@ -62,7 +62,9 @@ class DedispJob:
         self.tempdir = tempfile.mkdtemp(suffix="_tmp", prefix=self.basefilenm,
                                         dir=tmpdir_base or ("/dev/shm" if os.path.isdir("/dev/shm") else None))
         self.workdir = os.getcwd()
-        self.opts = opts or Opts()
+        # without subbands prepsubband dedisperses the channels themselves (nsub = nchan
+        # [PRESTO-ext]) and no .sub int16 file is written, so they stay float32 (:522-529)
+        self.opts = opts or (Opts() if use_subbands else Opts(sub_dtype=1))
         self.engine = None
         self.device = device
         self._mask_loaded = None
@@ -118,17 +120,25 @@ class DedispJob:
 def pass_params(job, ddplan, passnum):
     """The parameters of the two prepsubband command lines (PALFA2_presto_search.py:506-520),
     parsed the way prepsubband parses them (DM strings are "%.2f" text)."""
-    return PassParams(subdm=float(ddplan.subdmlist[passnum]), lodm=float(ddplan.lodm_arg(passnum)),
+    lodm = float(ddplan.lodm_arg(passnum))
+    numout = P.choose_N(job.orig_N / ddplan.downsamp)
+    if not job.use_subbands:
+        # :522-527: no -sub / -subdm / -nsub; -downsamp dd_downsamp*sub_downsamp.  With one
+        # channel per subband every stage-1 channel delay is 0, so subdm is immaterial.
+        return PassParams(subdm=lodm, lodm=lodm, dmstep=float(ddplan.dmstep_arg()), numdms=ddplan.dmsperpass,
+                          nsub=job.nchan, ds=ddplan.sub_downsamp * ddplan.dd_downsamp, numout=numout)
+    return PassParams(subdm=float(ddplan.subdmlist[passnum]), lodm=lodm,
                       dmstep=float(ddplan.dmstep_arg()), numdms=ddplan.dmsperpass, nsub=ddplan.numsub,
-                      ds=ddplan.sub_downsamp * (1 if job.use_subbands else ddplan.dd_downsamp),
-                      numout=P.choose_N(job.orig_N / ddplan.downsamp))
+                      ds=ddplan.sub_downsamp, numout=numout)
 
 
 def run_pass(job, ddplan, passnum, maskfilenm, tempdir):
     """PALFA2_presto_search.py:498-529 for one pass: subbands (stage 1) then the DM sweep
-    (stage 2); writes <tempdir>/<base>_DM<dm>.dat/.inf; returns (t_sub, t_dd)."""
+    (stage 2); writes <tempdir>/<base>_DM<dm>.dat/.inf; returns (t_sub, t_dd).  Without
+    subbands (:522-529) the reference makes one prepsubband call, timed as dedispersing
+    time only: t_sub is 0 and the whole pass goes to t_dd."""
     if not job.use_subbands:
-        raise PrestoError("use_subbands=False (PALFA2_presto_search.py:522-529) is not built yet")
+        return _run_pass_nosub(job, ddplan, passnum, maskfilenm, tempdir)
     subbasenm = "%s_DM%s" % (job.basefilenm, ddplan.subdmlist[passnum])
     eng = job.open_engine()
     job.load_mask(maskfilenm)
@@ -154,6 +164,27 @@ def run_pass(job, ddplan, passnum, maskfilenm, tempdir):
     job.subbanding_time += t_sub
     job.dedispersing_time += t_dd
     return t_sub, t_dd
+
+
+def _run_pass_nosub(job, ddplan, passnum, maskfilenm, tempdir):
+    """PALFA2_presto_search.py:522-529: `prepsubband -mask M -lodm -dmstep -numdms -downsamp
+    (dd*sub) -numout N` straight on the raw data: channels (downsampled, float32) are the
+    subbands of a nsub = nchan pass."""
+    eng = job.open_engine()
+    job.load_mask(maskfilenm)
+    pp = pass_params(job, ddplan, passnum)
+    plan = eng.plan(pp)
+    try:
+        t0 = time.time()
+        plan.run_subband()
+        series = plan.run_dedisp(to_host=True)
+        info = job.info_template(pp.nsub, plan.sub_lofreq, plan.sub_chanwid, plan.sub_dt)
+        write_dats(os.path.join(tempdir, job.basefilenm), ddplan.dmlist[passnum], series, info, plan.nds)
+        t_dd = time.time() - t0
+    finally:
+        plan.destroy()
+    job.dedispersing_time += t_dd
+    return 0.0, t_dd
 
 
 def dedisperse_job(job, maskfilenm=None, per_dm=None, remove_dat=False):

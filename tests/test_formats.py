@@ -114,6 +114,27 @@ def test_pass_params_mirror_command_lines():
             assert "%.2f" % pp.lodm == g["passes"][i]["lodm_arg"]
 
 
+class _JobNoSub:
+    use_subbands = False
+    orig_N = float(1 << 22)
+    nchan = 960
+
+
+def test_pass_params_no_subbands_mirror_command_line():
+    """use_subbands=False: one command per pass (PALFA2_presto_search.py:522-527), no -nsub
+    (channels are the subbands, nsub = nchan [PRESTO-ext]) and -downsamp dd*sub."""
+    for d in P.ddplans_for("pdev"):
+        for i in range(d.numpasses):
+            pp = pass_params(_JobNoSub(), d, i)
+            cmd = "prepsubband -mask %s -lodm %.2f -dmstep %.2f -numdms %d -downsamp %d -numout %d -o %s %s" % (
+                "m.mask", d.lodm + i * d.sub_dmstep, d.dmstep, d.dmsperpass, d.dd_downsamp * d.sub_downsamp,
+                P.choose_N(_JobNoSub.orig_N / d.downsamp), "t/b", "in.fits")
+            a = parse_cli(cmd.split()[1:])
+            assert pp.lodm == a.lodm and pp.dmstep == a.dmstep and pp.numdms == a.numdms
+            assert pp.ds == a.downsamp and pp.numout == a.numout and pp.nsub == 960 and a.nsub == 0
+            assert not a.sub and a.subdm is None
+
+
 def test_report_lines():
     class J:
         subbanding_time, dedispersing_time = 12.5, 30.25

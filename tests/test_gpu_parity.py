@@ -228,6 +228,33 @@ def test_stage2_f32_subbands(engine):
     np.testing.assert_allclose(got[:, nds:], want[:, nds:], rtol=REL_TOL, atol=0)
 
 
+@pytest.mark.parametrize("ds", [1, 3])
+def test_no_subband_pass_nsub_eq_nchan(engine, ds):
+    """use_subbands=False (PALFA2_presto_search.py:522-529): every channel is its own float32
+    subband (nsub = nchan = 960), -downsamp dd*sub; bit-exact against the oracle on the data
+    samples, padding mean within REL_TOL; masked."""
+    obs = palfa_obs(N=12288 + 5, nbits=8)
+    opts = Opts(sub_dtype=1)
+    s = palfa_synth()
+    raw = load_beam(engine, obs, opts, synth=s)
+    pts = 2048
+    mask, pad = synth_mask(obs, s, pts)
+    engine.set_mask(mask, pts, pad)
+    pp = PassParams(subdm=70.0, lodm=70.0, dmstep=0.3, numdms=12, nsub=obs.nchan, ds=ds,
+                    numout=obs.N // ds + 333)
+    p = engine.plan(pp)
+    idd, _ = p.delays()
+    assert not idd.any()
+    p.run_subband()
+    got = p.run_dedisp()
+    p.destroy()
+    engine.set_mask()
+    _, want = OR.run_pass(obs, opts, raw, pp, mask=mask, ptsperint=pts, padvals=pad)
+    nds = obs.N // ds
+    assert np.array_equal(got[:, :nds], want[:, :nds])
+    np.testing.assert_allclose(got[:, nds:], want[:, nds:], rtol=REL_TOL, atol=0)
+
+
 def test_sub_input_mode_matches_one_shot(engine):
     """Stage 2 fed from .subNN data (HD_PASS_SUB_INPUT, .sub.inf values) == one-shot pass."""
     obs = palfa_obs(N=20000, nbits=8)
@@ -441,3 +468,48 @@ def test_stage1_channel_major_fill(engine):
         want, _ = OR.run_pass(obs, Opts(), raw, pp)
         p.destroy()
         assert np.array_equal(a, want) and np.array_equal(b, want) and np.array_equal(c, want), beam
+
+
+@pytest.mark.parametrize("use_subbands", [True, False])
+def test_search_stage_dedisperse_job(engine, tmp_path, use_subbands):
+    """search_stage.dedisperse_job (the loop of PALFA2_presto_search.py:494-537) on a PSRFITS
+    file, with and without subbands: one pass each from DDplan stages 0 and 3; the
+    <base>_DM<dm>.dat files equal the oracle's series for the same command parameters, the
+    .inf records N and DM, and the timers go where the reference puts them."""
+    import copy
+    import os
+    from hipdedisp.formats import psrfits
+    from hipdedisp.formats.inf import read_inf
+    from hipdedisp.search_stage import DedispJob, dedisperse_job, pass_params
+    obs = palfa_obs(N=8192, nbits=8, nsblk=512)
+    spectra = host_spectra(obs, palfa_synth())
+    fn = str(tmp_path / "beam.fits")
+    psrfits.write_psrfits(fn, spectra, obs)
+    job = DedispJob([fn], resultsdir=str(tmp_path), tmpdir_base=str(tmp_path), device=0,
+                    use_subbands=use_subbands, backend="pdev")
+    ddplans = []
+    for st in (0, 3):
+        d = copy.copy(job.ddplans[st])
+        d.numpasses = 1
+        ddplans.append(d)
+    job.ddplans = ddplans
+    try:
+        dmstrs = dedisperse_job(job)
+        assert len(dmstrs) == sum(d.dmsperpass for d in ddplans)
+        sobs = job.specinfo.obs_params(0.0)
+        for d in ddplans:
+            pp = pass_params(job, d, 0)
+            _, want = OR.run_pass(sobs, job.opts, spectra, pp)
+            nds = int(obs.N // pp.ds)
+            for k, dmstr in enumerate(d.dmlist[0]):
+                base = os.path.join(job.tempdir, "%s_DM%s" % (job.basefilenm, dmstr))
+                got = np.fromfile(base + ".dat", np.float32)
+                assert got.size == (pp.numout or nds)      # choose_N < 10000 -> 0: no padding
+                assert np.array_equal(got[:nds], want[k, :nds]), dmstr
+                np.testing.assert_allclose(got[nds:], want[k, nds:], rtol=REL_TOL, atol=0)
+                inf = read_inf(base + ".inf")
+                assert inf.N == got.size and "%.2f" % inf.dm == dmstr
+        assert job.dedispersing_time > 0
+        assert (job.subbanding_time > 0) == use_subbands
+    finally:
+        job.close()
