@@ -513,3 +513,36 @@ def test_search_stage_dedisperse_job(engine, tmp_path, use_subbands):
         assert (job.subbanding_time > 0) == use_subbands
     finally:
         job.close()
+
+
+def test_c4_ddplan2b_passes_to_dm_10000(engine):
+    """Config 4 (BASELINE.json configs[3]): the DDplan2b plan from 0 to 10000 pc cm^-3
+    (PALFA2_presto_search.py:308-317 -> DDplan2b.py), nsub 96, downsampling 1..64; the
+    highest-DM pass of every step, with an rfifind-style mask, bit-exact against the oracle
+    (subbands and series, padding included).  N = 2^18 so the DM-10090 sweep (~10.7 s of
+    delay) still has data under it."""
+    N = 1 << 18
+    obs = palfa_obs(N=N, nbits=8)
+    s = palfa_synth()
+    raw = load_beam(engine, obs, synth=s)
+    pts = rfifind_ptsperint(obs.dt)
+    mask, pad = synth_mask(obs, s, pts)
+    engine.set_mask(mask, pts, pad)
+    steps = plan.ddplan2b_plans(obs.dt, 1375.5, 322.6, obs.nchan, 2048, 0.0, 10000.0, 96, 0.1)
+    assert max(d.downsamp for d in steps) == 64
+    try:
+        for d in steps:
+            i = d.numpasses - 1
+            pp = PassParams(subdm=float(d.subdmlist[i]), lodm=float(d.lodm_arg(i)), dmstep=float(d.dmstep_arg()),
+                            numdms=d.dmsperpass, nsub=d.numsub, ds=d.sub_downsamp,
+                            numout=plan.choose_N(N / d.downsamp))
+            p = engine.plan(pp)
+            p.run_subband()
+            got_sub = p.get_subbands()
+            got = p.run_dedisp()
+            p.destroy()
+            want_sub, want = OR.run_pass(obs, Opts(), raw, pp, mask=mask, ptsperint=pts, padvals=pad, omp=True)
+            assert np.array_equal(got_sub, want_sub), d.downsamp
+            assert np.array_equal(got, want), d.downsamp
+    finally:
+        engine.set_mask()
