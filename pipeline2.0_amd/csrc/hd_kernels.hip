@@ -1629,7 +1629,7 @@ __global__ __launch_bounds__(1024) void k_stage2_ring(Stage2Args a, const int32_
     ring_barrier();
 
     for (int c = 0; c < nchunk; c++) {
-        dma(c + NS - 1);
+        if (!(a.probe & 2)) dma(c + NS - 1);   // probe 2: no window DMA after the prologue
         if (c + 1 < nchunk && !(a.probe & 8)) expand(c + 1);
         // this chunk's (subband, DM) byte offsets: entry e = sl*Q + q in lane e
         const int32_t* sboff = (const int32_t*)(lds_raw + ring0 + (c % NS) * slot_bytes + SC * npw * 1024);
@@ -1877,7 +1877,7 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, const int32_
     ring_barrier();
 
     for (int c = 0; c < nchunk; c++) {
-        dma(c + NS - 1);
+        if (!(a.probe & 2)) dma(c + NS - 1);   // probe 2: no window DMA after the prologue
         if (c + 1 < nchunk && !(a.probe & 8)) expand(c + 1);
         // this chunk's per-DM byte offsets: entry q in lane q
         const int32_t* sboff = (const int32_t*)(lds_raw + ring0 + (c % NS) * slot_bytes + 2 * npw * 1024);
