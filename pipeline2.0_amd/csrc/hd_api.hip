@@ -25,6 +25,7 @@
 
 struct hd_ctx {
     int device = -1;
+    int ncu = 256;                     // compute units (persistent stage-2 workgroups)
     hipStream_t stream = nullptr;
     std::string err;
     bool have_obs = false;
@@ -122,6 +123,7 @@ struct hd_plan {
     bool sub_valid = false;
     int32_t s1_variant = 0;         // stage 1: 0 auto, 1 direct, 2 float tiled, 3 8-bit integer
     int32_t probe = 0;              // profiling switches (hd_plan_set_variant bits 16-23)
+    int32_t pair_persist = 0;       // hd_plan_set_variant bits 24-25 (pair kernel tile scheduling)
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     bool ran_sub = false, ran_dd = false;
     hipStream_t dd_stream = nullptr;  // stream of the last hd_run_dedisp (its ev[3] marks the end)
@@ -228,6 +230,8 @@ extern "C" int hd_open(int device, hd_ctx** out)
         delete c;
         return fail(nullptr, HD_E_HIP, "hd_open: cannot initialise device %d", device);
     }
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0) c->ncu = ncu;
     *out = c;
     return HD_OK;
 }
@@ -1133,6 +1137,7 @@ extern "C" int hd_plan_set_variant(hd_plan* p, int32_t v)
     // 2 float tiled, 3 8-bit integer tiled)
     const int32_t v1 = (v >> 8) & 0xFF;
     p->probe = (v >> 16) & 0xFF;     // profiling only (results invalid): see hipdedisp.h
+    p->pair_persist = (v >> 24) & 0x3;   // pair kernel: 0/1 persistent workgroups (default), 2 one per tile
     v &= 0xFF;
     if (v < 0 || v > 6 || v1 > 3) return fail(p->ctx, HD_E_INVAL, "variant must be (s1<<8)|s2 with s1 in 0..3, s2 in 0..6");
     p->s1_variant = v1;
@@ -1600,6 +1605,7 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         a.ring_nbp = w.nbp;
         a.ptab = w.d_omin;
         a.umax = w.umax;
+        a.nwg = p->pair_persist != 2 ? c->ncu : 0;   // persistent by default (measured 1.29 vs 1.36 ms, stage-0 pass)
         if (wk == 0) HIPCHK(c, hd::launch_stage2_wide(a, w.q, w.r, w.nw, st));
         else if (wk == 1) HIPCHK(c, hd::launch_stage2_wide2(a, w.q, w.r, w.nw, st));
         else if (wk == 2) HIPCHK(c, hd::launch_stage2_ring(a, w.q, w.r, st));

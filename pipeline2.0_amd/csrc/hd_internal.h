@@ -61,7 +61,8 @@ struct Stage1Multi {
 
 struct Stage2Args {
     const void* sub;          // [nsub][sub_stride]
-    int32_t sub_dtype, nsub, numdms, _pad;
+    int32_t sub_dtype, nsub, numdms;
+    int32_t nwg;              // pair variant: workgroups along x (0 = one per tile; else persistent, contiguous tile ranges)
     int64_t nds, sub_stride;
     int64_t nvalid;           // min(nds, numout): samples computed
     const int32_t* off;       // [numdms][nsub]

@@ -1774,8 +1774,18 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, const int32_
 {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
     constexpr int NS = kRingNS, T = 256 * R;
-    const int tile = xcd_remap(blockIdx.x, gridDim.x);
-    const int64_t t0 = (int64_t)tile * T;
+    // one tile per workgroup (nwg == 0), or a persistent workgroup over a contiguous tile
+    // range whose chunks (tile, pair) form one stream through the DMA ring, so the table
+    // load, ring prologue and launch of the next tile overlap the current one
+    int tb, ntl;
+    if (a.nwg == 0) {
+        tb = xcd_remap(blockIdx.x, gridDim.x);
+        ntl = 1;
+    } else {
+        const int nt = (int)((a.nvalid + T - 1) / T);
+        tb = (int)((int64_t)blockIdx.x * nt / gridDim.x);
+        ntl = (int)((int64_t)(blockIdx.x + 1) * nt / gridDim.x) - tb;
+    }
     const int yb = blockIdx.y;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1821,9 +1831,16 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, const int32_
     int gcount = 0;
     const bool loader = wave < 2 * npw + nbp;
 
+    const int ntot = ntl * nchunk;
+    int dpair = 0, dtile = 0, dcount = 0;              // source chunk of the next DMA (clamped at the end)
     auto dma = [&](int cc) {
+        const int c2 = dpair;
+        const int64_t t0 = (int64_t)(tb + dtile) * T;
+        if (dcount + 1 < ntot) {
+            dcount++;
+            if (++dpair == nchunk) { dpair = 0; dtile++; }
+        }
         if (!loader) return;
-        const int c2 = min(cc, nchunk - 1);
         const uint32_t slot = ring0 + (uint32_t)((cc % NS) * slot_bytes);
         if (wave < 2 * npw) {
             const int sl = wave >= npw ? 1 : 0, pc = wave - sl * npw;
@@ -1839,11 +1856,11 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, const int32_
         }
     };
     // staging slot of chunk cc -> the 4 shifted copies of each pattern partial, buffer cc & 1
-    auto expand = [&](int cc) {
+    auto expand = [&](int cc, int pr) {
         const char* slot = lds_raw + ring0 + (cc % NS) * slot_bytes;
         const uint32_t* S0 = (const uint32_t*)slot;
         const uint32_t* S1 = (const uint32_t*)(slot + npw * 1024);
-        const int32_t* pt = ltab + cc * kPairTab;
+        const int32_t* pt = ltab + pr * kPairTab;
         const int k0 = pt[0] & 1;
         const int U = pt[2];
         int16_t* buf = (int16_t*)(lds_raw + exp0) + (cc & 1) * (umax * 4 * ws);
@@ -1869,16 +1886,67 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, const int32_
         }
     };
 
+    auto flush = [&](int tile) {
+        const int64_t t0 = (int64_t)tile * T;
+    #pragma unroll
+        for (int q = 0; q < Q; q++) {
+            const int dl = wave * Q + q;
+            const int d = dblk0 + dl;
+            const bool dv = dl < dpb && d < a.numdms;
+            int64_t part = 0;
+    #pragma unroll
+            for (int r = 0; r < R; r++) {
+                acc32[q][r][0] += acc16[q][r][0].x;
+                acc32[q][r][1] += acc16[q][r][0].y;
+                acc32[q][r][2] += acc16[q][r][1].x;
+                acc32[q][r][3] += acc16[q][r][1].y;
+                const int64_t tl = t0 + 256 * r + 4 * lane;
+                if (dv && !(a.probe & 4)) {
+                    float* o = a.out + (int64_t)d * a.out_stride + tl;
+                    if (tl + 3 < a.nvalid) {
+                        *(float4*)o = make_float4((float)acc32[q][r][0], (float)acc32[q][r][1], (float)acc32[q][r][2],
+                                                  (float)acc32[q][r][3]);
+                        part += (int64_t)acc32[q][r][0] + acc32[q][r][1] + acc32[q][r][2] + acc32[q][r][3];
+                    } else {
+    #pragma unroll
+                        for (int j = 0; j < 4; j++)
+                            if (tl + j < a.nvalid) {
+                                o[j] = (float)acc32[q][r][j];
+                                part += acc32[q][r][j];
+                            }
+                    }
+                }
+            }
+            if (dv && a.partial) {
+    #pragma unroll
+                for (int m = 32; m >= 1; m >>= 1) part += __shfl_xor(part, m, 64);
+                if (lane == 0) a.partial[(int64_t)d * a.ntiles + tile] = (double)part;
+            }
+        }
+        gcount = 0;
+#pragma unroll
+        for (int q = 0; q < Q; q++)
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+#pragma unroll
+                for (int j = 0; j < 4; j++) acc32[q][r][j] = 0;
+                acc16[q][r][0] = short2v{0, 0};
+                acc16[q][r][1] = short2v{0, 0};
+            }
+    };
+
 #pragma unroll
     for (int cc = 0; cc < NS - 1; cc++) dma(cc);
     ring_wait_vm<R>();
     ring_barrier();
-    expand(0);
+    expand(0, 0);
     ring_barrier();
 
-    for (int c = 0; c < nchunk; c++) {
+    int pr = 0, ktile = 0;                             // pair and tile of chunk c
+    for (int c = 0; c < ntot; c++) {
         if (!(a.probe & 2)) dma(c + NS - 1);   // probe 2: no window DMA after the prologue
-        if (c + 1 < nchunk && !(a.probe & 8)) expand(c + 1);
+        const int prn = pr + 1 == nchunk ? 0 : pr + 1;
+        if (c + 1 < ntot && !(a.probe & 8)) expand(c + 1, prn);
         // this chunk's per-DM byte offsets: entry q in lane q
         const int32_t* sboff = (const int32_t*)(lds_raw + ring0 + (c % NS) * slot_bytes + 2 * npw * 1024);
         const int voff = lane < Q ? sboff[wave * Q + lane] : 0;
@@ -1925,44 +1993,12 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, const int32_
         }
         ring_wait_vm<R>();
         ring_barrier();
+        // tile done: its stores go out after this chunk's DMA wait, so they do not hold it up
+        if (pr == nchunk - 1) flush(tb + ktile++);
+        pr = prn;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may land after the workgroup ends
 
-#pragma unroll
-    for (int q = 0; q < Q; q++) {
-        const int dl = wave * Q + q;
-        const int d = dblk0 + dl;
-        const bool dv = dl < dpb && d < a.numdms;
-        int64_t part = 0;
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-            acc32[q][r][0] += acc16[q][r][0].x;
-            acc32[q][r][1] += acc16[q][r][0].y;
-            acc32[q][r][2] += acc16[q][r][1].x;
-            acc32[q][r][3] += acc16[q][r][1].y;
-            const int64_t tl = t0 + 256 * r + 4 * lane;
-            if (dv && !(a.probe & 4)) {
-                float* o = a.out + (int64_t)d * a.out_stride + tl;
-                if (tl + 3 < a.nvalid) {
-                    *(float4*)o = make_float4((float)acc32[q][r][0], (float)acc32[q][r][1], (float)acc32[q][r][2],
-                                              (float)acc32[q][r][3]);
-                    part += (int64_t)acc32[q][r][0] + acc32[q][r][1] + acc32[q][r][2] + acc32[q][r][3];
-                } else {
-#pragma unroll
-                    for (int j = 0; j < 4; j++)
-                        if (tl + j < a.nvalid) {
-                            o[j] = (float)acc32[q][r][j];
-                            part += acc32[q][r][j];
-                        }
-                }
-            }
-        }
-        if (dv && a.partial) {
-#pragma unroll
-            for (int m = 32; m >= 1; m >>= 1) part += __shfl_xor(part, m, 64);
-            if (lane == 0) a.partial[(int64_t)d * a.ntiles + tile] = (double)part;
-        }
-    }
 }
 
 size_t stage2_pair_lds_bytes(int wstride, int npw, int nbp, int nsub, int umax)
@@ -1982,8 +2018,11 @@ static hipError_t launch_pair_qr(const Stage2Args& a, int nyblk, hipStream_t st)
         attr = true;
     }
     const unsigned ntiles = (unsigned)((a.nvalid + 256 * R - 1) / (256 * R));
-    hipLaunchKernelGGL((k_stage2_pair<Q, R>), dim3(ntiles, (unsigned)nyblk), dim3(1024),
-                       stage2_pair_lds_bytes(a.wstride, a.ring_npw, a.ring_nbp, a.nsub, a.umax), st, a, a.off);
+    const unsigned nx = a.nwg > 0 && (unsigned)a.nwg < ntiles ? (unsigned)a.nwg : ntiles;
+    Stage2Args b = a;
+    if (nx == ntiles) b.nwg = 0;
+    hipLaunchKernelGGL((k_stage2_pair<Q, R>), dim3(nx, (unsigned)nyblk), dim3(1024),
+                       stage2_pair_lds_bytes(a.wstride, a.ring_npw, a.ring_nbp, a.nsub, a.umax), st, b, a.off);
     return hipGetLastError();
 }
 

@@ -133,6 +133,34 @@ def test_stage2_pair_ddplan_passes(engine, stage, passnum):
     engine.set_mask()
 
 
+@pytest.mark.parametrize("stage", [0, 1])
+def test_stage2_pair_persistent_bitexact(engine, stage):
+    """Pair kernel with persistent workgroups (variant bits 24-25 = 1: one workgroup per CU,
+    each over a contiguous range of tiles whose chunks stream through one DMA ring): more
+    tiles than CUs and a ragged last tile, masked; bit-exact against the oracle and equal
+    to one workgroup per tile (bits = 2)."""
+    obs = palfa_obs(N=(1 << 19) + 777, nbits=8)
+    synth = palfa_synth()
+    raw = load_beam(engine, obs, synth=synth)
+    pts = 2048
+    mask, pad = synth_mask(obs, synth, pts)
+    engine.set_mask(mask, pts, pad)
+    d = plan.ddplans_for("pdev")[stage]
+    pp = PassParams(subdm=float(d.subdmlist[1]), lodm=float(d.lodm_arg(1)), dmstep=float(d.dmstep_arg()),
+                    numdms=d.dmsperpass, nsub=d.numsub, ds=d.sub_downsamp, numout=plan.choose_N(obs.N / d.downsamp))
+    p = engine.plan(pp)
+    p.run_subband()
+    outs = []
+    for v in (6 | (1 << 24), 6 | (2 << 24)):
+        p.set_variant(v)
+        outs.append(p.run_dedisp())
+    p.destroy()
+    engine.set_mask()
+    _, want = OR.run_pass(obs, Opts(), raw, pp, mask=mask, ptsperint=pts, padvals=pad, omp=True)
+    assert np.array_equal(outs[0], want)
+    assert np.array_equal(outs[1], want)
+
+
 def test_stage2_pair_rejects_unbounded_subbands(engine):
     """16-bit data: no host bound on |subband| -> the pair variant refuses (HD_E_INVAL) and
     the default falls back to the ring kernel, still bit-exact."""
