@@ -1012,6 +1012,8 @@ extern "C" int hd_plan_create(hd_ctx* c, const hd_pass* ps, hd_plan** out)
     Tables T;
     int rc0 = compute_tables(c, o, c->opts, ps, T);
     if (rc0) return rc0;
+    if (o.N / ps->ds < 1)
+        return fail(c, HD_E_INVAL, "hd_plan_create: %lld spectra give no sample at -downsamp %d", (long long)o.N, ps->ds);
 
     hd_plan* p = new hd_plan();
     p->ctx = c;

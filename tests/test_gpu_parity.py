@@ -574,3 +574,28 @@ def test_c4_ddplan2b_passes_to_dm_10000(engine):
             assert np.array_equal(got, want), d.downsamp
     finally:
         engine.set_mask()
+
+
+@pytest.mark.parametrize("N,ds,numdms", [(4096, 1, 76), (4096 + 13, 3, 1), (2000, 2, 64), (1, 1, 4), (3, 5, 4)])
+def test_beam_shorter_than_the_sweep(engine, N, ds, numdms):
+    """Edge sizes: a beam shorter than its own dispersion sweep (DM ~1000: ~1 s = 16k samples
+    of delay across the band, every stage-1 and stage-2 read past the end), a single DM, a
+    ragged length, a one-sample beam, and fewer samples than the downsampling factor (no
+    output: refused).  Bit-exact against the oracle, padding included."""
+    obs = palfa_obs(N=N, nbits=8)
+    raw = load_beam(engine, obs)
+    nds = N // ds
+    pp = PassParams(subdm=1000.0, lodm=990.0, dmstep=0.5, numdms=numdms, nsub=96, ds=ds, numout=nds + 100)
+    if nds == 0:
+        with pytest.raises(PrestoError):
+            engine.plan(pp)
+        return
+    p = engine.plan(pp)
+    p.run_subband()
+    got_sub = p.get_subbands()
+    got = p.run_dedisp()
+    p.destroy()
+    want_sub, want = OR.run_pass(obs, Opts(), raw, pp)
+    assert np.array_equal(got_sub, want_sub)
+    assert np.array_equal(got[:, :nds], want[:, :nds])
+    np.testing.assert_allclose(got[:, nds:], want[:, nds:], rtol=REL_TOL, atol=0)
