@@ -2336,8 +2336,17 @@ __global__ __launch_bounds__(256) void k_raw_transpose8(const uint8_t* __restric
                                                        uint8_t* __restrict__ rawT, int64_t tstride)
 {
     __shared__ uint32_t tile[128][33];
-    const int64_t t0 = (int64_t)blockIdx.x * 128;
-    const int c0 = blockIdx.y * 128;
+    // 1-D grid, XCD-aware: workgroup L runs on XCD L % 8; its s-th workgroup there takes
+    // channel tile s % nct of time block (s / nct) * 8 + L % 8, so the nct channel tiles of
+    // one time block run back to back on one XCD.  Raw rows are 960 B (64-B aligned), so
+    // half the 128-B row pieces straddle two cache lines, which the neighbouring channel
+    // tile then finds in that XCD's L2 instead of fetching from HBM again.
+    const int nct = (nchan + 127) >> 7;
+    const int xcd = blockIdx.x & 7, sl = blockIdx.x >> 3;
+    const int64_t tb = (int64_t)(sl / nct) * 8 + xcd;
+    if (tb * 128 >= N) return;
+    const int64_t t0 = tb * 128;
+    const int c0 = (sl % nct) * 128;
     const int rb = nchan;                                   // bytes per raw row (8-bit)
     const int ncw = min(128, nchan - c0) >> 2;              // channel dwords in this tile
 #pragma unroll
@@ -2376,8 +2385,10 @@ hipError_t launch_raw_transpose8(const uint8_t* raw, int64_t N, int32_t nchan, u
                                  hipStream_t st)
 {
     if (nchan % 4 || N % 4) return hipErrorInvalidValue;
-    const dim3 grid((unsigned)((N + 127) / 128), (unsigned)((nchan + 127) / 128));
-    hipLaunchKernelGGL(k_raw_transpose8, grid, dim3(256), 0, st, raw, N, nchan, rawT, tstride);
+    const int64_t ntb8 = ((N + 127) / 128 + 7) / 8 * 8;          // time blocks, padded to the 8 XCDs
+    const int64_t nwg = ntb8 * ((nchan + 127) / 128);
+    if (nwg > 0x7fffffffLL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_raw_transpose8, dim3((unsigned)nwg), dim3(256), 0, st, raw, N, nchan, rawT, tstride);
     return hipGetLastError();
 }
 
