@@ -599,3 +599,38 @@ def test_beam_shorter_than_the_sweep(engine, N, ds, numdms):
     assert np.array_equal(got_sub, want_sub)
     assert np.array_equal(got[:, :nds], want[:, :nds])
     np.testing.assert_allclose(got[:, nds:], want[:, nds:], rtol=REL_TOL, atol=0)
+
+
+def test_prepsubband_cli_shim_commands(engine, tmp_path):
+    """The reference's three command strings (PALFA2_presto_search.py:506-511, :514-520,
+    :522-527) through the `prepsubband` shim: exit status 0, and the .dat series equal the
+    oracle's for the same parameters (the two-step subband path via .subNN files)."""
+    import glob
+    import os
+    from hipdedisp import prepsubband as cli
+    from hipdedisp.formats import psrfits
+    obs = palfa_obs(N=8192, nbits=8, nsblk=512)
+    spectra = host_spectra(obs, palfa_synth())
+    fn = str(tmp_path / "beam.fits")
+    psrfits.write_psrfits(fn, spectra, obs)
+    sobs = psrfits.SpectraInfo([fn]).obs_params(0.0)
+    os.makedirs(str(tmp_path / "subbands"))
+    dev = ["-device", "0"]
+    assert cli.main(("-psrfits -sub -subdm 30.40 -downsamp 1 -nsub 96 -o %s/subbands/beam %s"
+                     % (tmp_path, fn)).split() + dev) == 0
+    subs = sorted(glob.glob(str(tmp_path / "subbands" / "beam_DM30.40.sub[0-9]*")))
+    assert len(subs) == 96
+    assert cli.main(("-lodm 26.60 -dmstep 0.10 -numdms 76 -downsamp 1 -nsub 96 -numout 0 -o %s/beam"
+                     % tmp_path).split() + subs + dev) == 0
+    pp = PassParams(subdm=30.4, lodm=26.6, dmstep=0.1, numdms=76, nsub=96, ds=1, numout=0)
+    _, want = OR.run_pass(sobs, Opts(), spectra, pp)
+    for k in (0, 37, 75):
+        got = np.fromfile(str(tmp_path / ("beam_DM%.2f.dat" % (26.6 + 0.1 * k))), np.float32)
+        assert np.array_equal(got, want[k]), k
+    assert cli.main(("-mask none -lodm 100.00 -dmstep 1.00 -numdms 8 -downsamp 2 -numout 0 -o %s/nosub %s"
+                     % (tmp_path, fn)).split()[2:] + dev) == 0
+    pp = PassParams(subdm=100.0, lodm=100.0, dmstep=1.0, numdms=8, nsub=obs.nchan, ds=2, numout=0)
+    _, want = OR.run_pass(sobs, Opts(sub_dtype=1), spectra, pp)
+    for k in (0, 7):
+        got = np.fromfile(str(tmp_path / ("nosub_DM%.2f.dat" % (100.0 + k))), np.float32)
+        assert np.array_equal(got, want[k]), k
