@@ -46,12 +46,20 @@ extern "C" {
 /* Subband sample storage (PRESTO writes .subNN as 16-bit ints; f32 keeps them exact). */
 #define HD_SUB_I16   0
 #define HD_SUB_F32   1
-/* Downsampling of subbands: sum of ds samples, or their mean. */
+/* Downsampling of subbands: sum of ds samples, or their mean (prepsubband's get_data
+ * divides the ds-sample sum by -downsamp [PRESTO-ext]; the default). */
 #define HD_DS_SUM    0
 #define HD_DS_MEAN   1
 /* Padding of a DM series from its length N/ds up to numout. */
-#define HD_PAD_MEAN  0   /* mean of the series' data samples (double sum, cast to f32) */
+#define HD_PAD_MEAN  0   /* per-DM mean of the series' data samples (double sum, cast to f32) */
 #define HD_PAD_ZERO  1
+#define HD_PAD_DM0   2   /* prepsubband: the running mean of the FIRST DM's data samples,
+                            for every DM [PRESTO-ext] (the default); computed as the exact
+                            mean (integer sums for int16 subbands), cast to f32          */
+/* int16 subband rounding. */
+#define HD_ROUND_PRESTO  0   /* prepsubband's (short)(x + 0.5) as x86-64 evaluates it: the
+                                double x + 0.5 truncated to int32, low 16 bits (default)  */
+#define HD_ROUND_NEAREST 1   /* nearest, ties away from zero, saturated                    */
 
 typedef struct hd_ctx  hd_ctx;
 typedef struct hd_plan hd_plan;
@@ -75,14 +83,16 @@ typedef struct {
 /* PRESTO-semantics switches.  Defaults: hd_opts_default(). */
 typedef struct {
     int32_t   sub_dtype;       /* HD_SUB_I16 (default) | HD_SUB_F32                      */
-    int32_t   ds_mode;         /* HD_DS_SUM (default)  | HD_DS_MEAN                      */
-    int32_t   pad_mode;        /* HD_PAD_MEAN (default) | HD_PAD_ZERO                    */
+    int32_t   ds_mode;         /* HD_DS_MEAN (default) | HD_DS_SUM                       */
+    int32_t   pad_mode;        /* HD_PAD_DM0 (default) | HD_PAD_MEAN | HD_PAD_ZERO       */
     int32_t   nibble_hi_first; /* 4-bit: first sample in the high nibble (default 1)     */
     int32_t   be16;            /* 16-bit samples big-endian as stored in FITS (default 1)*/
     int32_t   inf_roundtrip;   /* subband-level freq/dt pass through "%.12g"/"%.15g" text,
                                   as they do through the .sub.inf file (default 1)        */
-    float     clip_sigma;      /* time-domain clip threshold; 0 disables  */
-    int32_t   _pad0;
+    float     clip_sigma;      /* PRESTO clip_times threshold on each raw read block (obs
+                                  nsblk spectra); 6.0 = prepsubband's default -clip, which
+                                  the reference's commands leave on; 0 = -noclip           */
+    int32_t   sub_round;       /* HD_ROUND_PRESTO (default) | HD_ROUND_NEAREST           */
 } hd_opts;
 
 /* One prepsubband pass: stage-1 subbanding at subdm + stage-2 sweep over numdms DMs. */
@@ -155,11 +165,26 @@ HD_API int hd_set_obs(hd_ctx* ctx, const hd_obs* obs, const hd_opts* opts);
 /* Per-raw-channel DAT_SCL / DAT_OFFS / DAT_WTS (file channel order); NULL = identity.
  * Value = ((raw * scl) + offs) * wts, as PSRFITS defines.                         */
 HD_API int hd_set_chan_calib(hd_ctx* ctx, const float* scl, const float* offs, const float* wts);
-/* rfifind mask as a dense bitmap mask[numint][nchan] (1 = zapped), ascending-frequency
- * channels; masked samples become padvals[c].  padvals also fill reads past the end
- * of the data.  mask == NULL clears the mask (padvals may still be given).          */
+/* rfifind mask (reference :482-490 makes it, stage 1 reads it with -mask) as PRESTO's
+ * read_mask leaves it: mask[numint][nchan] = the interval's channel list (1 = listed,
+ * ascending-frequency channels), zapint[numint] = 1 for intervals in zap_ints (NULL: a row
+ * listing every channel counts as one), dtint = seconds per interval as stored in the file
+ * (<= 0: ptsperint * dt).  Applied per raw read block (obs nsblk spectra) with check_mask's
+ * rule [PRESTO-ext]: the union of the lists of the block's first and last interval, or
+ * every channel when either is a zap_int.  padvals[nchan] = initial pad values (rfifind
+ * .stats, hd_stats_padvals; NULL = 0); with clipping on, clip_times replaces them block by
+ * block with its running channel levels.  mask == NULL clears the mask.                */
 HD_API int hd_set_mask(hd_ctx* ctx, const uint8_t* mask, int32_t numint, int32_t ptsperint,
-                const float* padvals);
+                       double dtint, const uint8_t* zapint, const float* padvals);
+/* determine_padvals [PRESTO-ext]: pad values from an rfifind .stats file's interval
+ * averages dataavg[numint][numchan] -- per channel, the avg_var mean of the middle 80 % of
+ * its sorted interval averages.  Host-only.                                            */
+HD_API int hd_stats_padvals(const float* dataavg, int32_t numint, int32_t numchan, float* padvals);
+/* Cleaning state of the current raw block (computed by the next stage-1 launch, or now):
+ * pad[nblk][nchan] pad values in force per read block, clipped[N] (1 = spectrum replaced
+ * by clip_times), zap[nblk][nchan] zapped channels per block; any may be NULL.  *nclipped
+ * receives the number of clipped spectra (may be NULL).  nblk = ceil(N / nsblk).        */
+HD_API int hd_get_clean(hd_ctx* ctx, float* pad, uint8_t* clipped, uint8_t* zap, int64_t* nclipped);
 /* Copy nspectra raw spectra (file layout, rows of nchan*nbits/8 bytes) to device
  * spectra [start, start + nspectra).  Host memory may be pageable or pinned.       */
 HD_API int hd_push_raw(hd_ctx* ctx, const void* spectra, int64_t start, int64_t nspectra);
@@ -218,10 +243,15 @@ HD_API int hd_run_subband(hd_plan* plan);
 HD_API int hd_run_subband_multi(hd_plan** plans, int32_t n);
 /* Subbands device <-> host, layout [nsub][N/ds] of int16 or f32 (opts.sub_dtype).   */
 HD_API int hd_get_subbands(hd_plan* plan, void* host);
+/* Samples [t0, t0+count) of every subband, host layout [nsub][count] (t0+count <= N/ds). */
+HD_API int hd_get_subbands_window(hd_plan* plan, int64_t t0, int64_t count, void* host);
 HD_API int hd_set_subbands(hd_plan* plan, const void* host);
 /* Stage 2: subbands -> numdms series of numout f32 samples.  host_out [numdms][numout]
  * receives them when non-NULL; otherwise they stay resident on the device.          */
 HD_API int hd_run_dedisp(hd_plan* plan, float* host_out);
+/* Samples [t0, t0+count) of DMs [dm0, dm0+ndm) of the device-resident series of the last
+ * hd_run_dedisp, host layout [ndm][count] (t0+count <= numout).                        */
+HD_API int hd_get_series(hd_plan* plan, int32_t dm0, int32_t ndm, int64_t t0, int64_t count, float* host);
 /* Device-time of the last hd_run_subband / hd_run_dedisp of this plan, ms.           */
 HD_API int hd_plan_last_ms(const hd_plan* plan, float* ms_subband, float* ms_dedisp);
 /* Kernel variants: (s1 << 8) | s2.  s2: 0 auto, 1 direct, 2 LDS-tiled (4 waves x 256 samples),

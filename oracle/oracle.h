@@ -8,10 +8,25 @@
  * from this image.  The reference holds no tests or fixtures that pin prepsubband's
  * numbers.  This oracle is therefore pinned by
  *   (1) the reference's own plan code, run to produce tests/golden/ddplan_ref.json;
- *   (2) analytic known-answer tests (impulses, constants) in tests/test_oracle.py;
+ *   (2) analytic known-answer tests (impulses, constants, clipping) in tests/test_oracle.py;
  *   (3) an independent numpy restatement (oracle/oracle_np.py) that must agree bit for bit.
  * Against PRESTO itself it is "parity unpinned"; each PRESTO-derived rule below is
- * tagged [PRESTO-ext] and has a switch in or_opts.
+ * tagged [PRESTO-ext], names the PRESTO function it restates from memory, and has a
+ * switch in or_opts where PRESTO versions are known to differ.
+ *
+ * Per-block model (PRESTO reads raw data one PSRFITS subint = nsblk spectra at a time,
+ * backend_common.c read_psrdata [PRESTO-ext]).  For raw block b:
+ *   1. decode (unpack, DAT_SCL/OFFS/WTS, band flip) -> X[t][c], ascending frequency;
+ *   2. check_mask(b*nsblk*dt, nsblk*dt) -> zapped channel set of the block, or ALL when
+ *      the block touches an interval in zap_ints (mask.c check_mask: the union of the
+ *      block's first and last interval only);
+ *   3. if clip_sigma > 0 and the block is not ALL-zapped: clip_times(X, ..., padvals)
+ *      (clipping.c): zero-DM series, block median, "good" spectra within 0.7..1.3 x median,
+ *      their mean/std (avg_var, AS 52) and per-channel means, 30-block running averages;
+ *      spectra with |zdm - running_avg| > clip_sigma * running_std are replaced by the
+ *      running channel averages, which also become the pad values (good_chan_levels);
+ *   4. zapped channels of the block := padvals (as updated by step 3).
+ * Spectra past N read as the last block's pad values.
  */
 #ifndef HD_ORACLE_H
 #define HD_ORACLE_H
@@ -30,15 +45,25 @@ typedef struct {
 } or_obs;   /* same field meaning as hd_obs (include/hipdedisp.h) */
 
 typedef struct {
-    int32_t sub_dtype;        /* 0 int16, 1 f32              */
-    int32_t ds_mode;          /* 0 sum, 1 mean               */
-    int32_t pad_mode;         /* 0 mean, 1 zero              */
+    int32_t sub_dtype;        /* 0 int16, 1 f32                                        */
+    int32_t ds_mode;          /* 0 sum, 1 mean (prepsubband get_data: ftmp / downsamp)  */
+    int32_t pad_mode;         /* 0 per-DM mean, 1 zero, 2 first-DM running mean (PRESTO) */
     int32_t nibble_hi_first;
     int32_t be16;
     int32_t inf_roundtrip;
-    float   clip_sigma;
-    int32_t _pad0;
+    float   clip_sigma;       /* 0: -noclip                                             */
+    int32_t sub_round;        /* 0 PRESTO (short)(x + 0.5) (x86 cvttsd2si, low 16 bits);
+                                 1 nearest, ties away, saturated                       */
 } or_opts;
+
+/* rfifind mask as PRESTO's read_mask leaves it [PRESTO-ext, mask.c] */
+typedef struct {
+    const uint8_t* chans;     /* [numint][nchan], 1 = channel in the interval's list     */
+    const uint8_t* zapint;    /* [numint], 1 = interval in zap_ints; NULL: a row listing
+                                 every channel counts as a zap_int                       */
+    int32_t numint, ptsperint;
+    double  dtint;            /* seconds per interval as stored; <= 0: ptsperint * dt    */
+} or_mask;
 
 /* ---- PRESTO src/dispersion.c restated [PRESTO-ext] ---- */
 double  or_delay_from_dm(double dm, double freq_emitted);
@@ -61,12 +86,26 @@ void or_dm_offsets(const or_obs* obs, const or_opts* opts, int nsub, int ds,
 void or_dm_offsets_sub(int nsub, double lof, double bw, double dsdt, double voverc,
                        double lodm, double dmstep, int numdms, int32_t* off);
 
+/* ---- per-block cleaning (steps 2-4 above) ----
+ * blocks of blk spectra, nblk = ceil(N / blk).
+ * or_check_mask_blocks: zap[nblk][nchan] and allzap[nblk] from the mask (mask.c check_mask).
+ * or_clip_prepare: pad[nblk][nchan] = pad values in force for block b (after its clip),
+ *   clipped[N] = 1 for spectra clip_times replaced; returns the number clipped, or -1.
+ *   padvals0 = initial pad values (determine_padvals; NULL = 0). */
+void    or_check_mask_blocks(const or_obs* obs, const or_mask* mask, int blk, int nblk,
+                             uint8_t* zap, uint8_t* allzap);
+int64_t or_clip_prepare(const or_obs* obs, const or_opts* opts, const uint8_t* raw,
+                        const float* scl, const float* offs, const float* wts,
+                        const uint8_t* allzap, const float* padvals0, int blk, int nblk,
+                        float* pad, uint8_t* clipped);
+
 /* ---- stage 1: raw -> subbands, output samples [t0, t0+count) of every subband ----
  * out: [nsub][out_stride] int16 or f32 (opts->sub_dtype); column index = t - t0.
- * scl/offs/wts: per raw channel or NULL; mask [numint][nchan] or NULL; padvals or NULL. */
+ * scl/offs/wts: per raw channel or NULL.  Cleaning: zap [nblk][nchan] or NULL,
+ * pad [nblk][nchan] or NULL (0), clipped [N] or NULL; blocks of blk spectra. */
 int or_stage1(const or_obs* obs, const or_opts* opts, const uint8_t* raw,
               const float* scl, const float* offs, const float* wts,
-              const uint8_t* mask, int numint, int ptsperint, const float* padvals,
+              const uint8_t* zap, const float* pad, const uint8_t* clipped, int blk, int nblk,
               int nsub, int ds, const int32_t* idispdt,
               int64_t t0, int64_t count, void* out, int64_t out_stride);
 
@@ -80,13 +119,9 @@ int or_stage2(const void* sub, int sub_dtype, int64_t nds, int64_t sub_stride, i
 /* Padding of full series [numdms][numout] whose first nds samples are data. */
 void or_pad(float* out, int numdms, int64_t nds, int64_t numout, int pad_mode);
 
-/* Whole pass, full length: convenience for tests. */
-int or_run_pass(const or_obs* obs, const or_opts* opts, const uint8_t* raw,
-                const float* scl, const float* offs, const float* wts,
-                const uint8_t* mask, int numint, int ptsperint, const float* padvals,
-                double subdm, double lodm, double dmstep, int numdms, int nsub, int ds,
-                int64_t numout, void* sub_out /* [nsub][N/ds] or NULL */,
-                float* dat_out /* [numdms][numout] */);
+/* determine_padvals [PRESTO-ext, mask.c]: per channel, the mean (avg_var) of the middle
+ * 80 % of its sorted interval averages from rfifind's .stats (dataavg [numint][numchan]). */
+void or_stats_padvals(const float* dataavg, int numint, int numchan, float* padvals);
 
 int or_num_threads(void);
 

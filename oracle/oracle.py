@@ -7,6 +7,7 @@ plan code, analytic KATs and an independent numpy restatement, oracle/oracle_np.
 import ctypes
 import os
 import subprocess
+from dataclasses import dataclass
 
 import numpy as np
 
@@ -23,7 +24,12 @@ class or_obs(ctypes.Structure):
 class or_opts(ctypes.Structure):
     _fields_ = [("sub_dtype", ctypes.c_int32), ("ds_mode", ctypes.c_int32), ("pad_mode", ctypes.c_int32),
                 ("nibble_hi_first", ctypes.c_int32), ("be16", ctypes.c_int32),
-                ("inf_roundtrip", ctypes.c_int32), ("clip_sigma", ctypes.c_float), ("_pad0", ctypes.c_int32)]
+                ("inf_roundtrip", ctypes.c_int32), ("clip_sigma", ctypes.c_float), ("sub_round", ctypes.c_int32)]
+
+
+class or_mask(ctypes.Structure):
+    _fields_ = [("chans", ctypes.c_void_p), ("zapint", ctypes.c_void_p), ("numint", ctypes.c_int32),
+                ("ptsperint", ctypes.c_int32), ("dtint", ctypes.c_double)]
 
 
 _libs = {}
@@ -40,19 +46,25 @@ def lib(omp=False):
         if not os.path.exists(path):
             build()
         L = ctypes.CDLL(path)
-        vp, i32, i64, d = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
+        vp, i64, d = ctypes.c_void_p, ctypes.c_int64, ctypes.c_double
         P = ctypes.POINTER
-        L.or_chan_delays.argtypes = [P(or_obs), ctypes.c_int, d, P(ctypes.c_int32)]
-        L.or_sub_params.argtypes = [P(or_obs), P(or_opts), ctypes.c_int, ctypes.c_int, P(d), P(d), P(d)]
-        L.or_dm_offsets.argtypes = [P(or_obs), P(or_opts), ctypes.c_int, ctypes.c_int, d, d, ctypes.c_int,
-                                    P(ctypes.c_int32)]
-        L.or_dm_offsets_sub.argtypes = [ctypes.c_int, d, d, d, d, d, d, ctypes.c_int, P(ctypes.c_int32)]
-        L.or_stage1.argtypes = [P(or_obs), P(or_opts), vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, vp,
-                                ctypes.c_int, ctypes.c_int, vp, i64, i64, vp, i64]
-        L.or_stage2.argtypes = [vp, ctypes.c_int, i64, i64, ctypes.c_int, vp, ctypes.c_int, i64, i64, vp, i64]
-        L.or_pad.argtypes = [vp, ctypes.c_int, i64, i64, ctypes.c_int]
+        ci = ctypes.c_int
+        L.or_chan_delays.argtypes = [P(or_obs), ci, d, P(ctypes.c_int32)]
+        L.or_sub_params.argtypes = [P(or_obs), P(or_opts), ci, ci, P(d), P(d), P(d)]
+        L.or_dm_offsets.argtypes = [P(or_obs), P(or_opts), ci, ci, d, d, ci, P(ctypes.c_int32)]
+        L.or_dm_offsets_sub.argtypes = [ci, d, d, d, d, d, d, ci, P(ctypes.c_int32)]
+        L.or_check_mask_blocks.argtypes = [P(or_obs), P(or_mask), ci, ci, vp, vp]
+        L.or_check_mask_blocks.restype = None
+        L.or_clip_prepare.argtypes = [P(or_obs), P(or_opts), vp, vp, vp, vp, vp, vp, ci, ci, vp, vp]
+        L.or_clip_prepare.restype = i64
+        L.or_stage1.argtypes = [P(or_obs), P(or_opts), vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, vp,
+                                i64, i64, vp, i64]
+        L.or_stage2.argtypes = [vp, ci, i64, i64, ci, vp, ci, i64, i64, vp, i64]
+        L.or_pad.argtypes = [vp, ci, i64, i64, ci]
         L.or_pad.restype = None
-        L.or_num_threads.restype = ctypes.c_int
+        L.or_stats_padvals.argtypes = [vp, ci, ci, vp]
+        L.or_stats_padvals.restype = None
+        L.or_num_threads.restype = ci
         L.or_nearest_long.restype = i64
         L.or_nearest_long.argtypes = [d]
         L.or_delay_from_dm.restype = d
@@ -69,7 +81,7 @@ def _obs(o):
 def _opts(p):
     return or_opts(sub_dtype=p.sub_dtype, ds_mode=p.ds_mode, pad_mode=p.pad_mode,
                    nibble_hi_first=int(p.nibble_hi_first), be16=int(p.be16),
-                   inf_roundtrip=int(p.inf_roundtrip), clip_sigma=p.clip_sigma)
+                   inf_roundtrip=int(p.inf_roundtrip), clip_sigma=p.clip_sigma, sub_round=p.sub_round)
 
 
 def _ptr(a):
@@ -105,23 +117,70 @@ def dm_offsets_sub(nsub, lof, bw, dsdt, lodm, dmstep, numdms, voverc=0.0):
     return out
 
 
+@dataclass
+class Clean:
+    """Per-block cleaning state of a raw block (oracle.h model): blocks of `blk` spectra."""
+    blk: int
+    nblk: int
+    zap: np.ndarray          # uint8 [nblk][nchan]
+    allzap: np.ndarray       # uint8 [nblk]
+    pad: np.ndarray          # float32 [nblk][nchan]
+    clipped: np.ndarray      # uint8 [N]
+    nclipped: int
+
+
+def block_masks(obs, mask, ptsperint, dtint=0.0, zapint=None, blk=None):
+    """mask.c check_mask per read block: (zap [nblk][nchan], allzap [nblk])."""
+    blk = int(blk or obs.nsblk)
+    nblk = (obs.N + blk - 1) // blk
+    zap = np.zeros((nblk, obs.nchan), np.uint8)
+    allzap = np.zeros(nblk, np.uint8)
+    if mask is None:
+        return zap, allzap
+    m = np.ascontiguousarray(mask, np.uint8)
+    zi = None if zapint is None else np.ascontiguousarray(zapint, np.uint8)
+    om = or_mask(chans=_ptr(m), zapint=_ptr(zi), numint=m.shape[0], ptsperint=int(ptsperint), dtint=float(dtint))
+    o = _obs(obs)
+    lib().or_check_mask_blocks(ctypes.byref(o), ctypes.byref(om), blk, nblk, _ptr(zap), _ptr(allzap))
+    return zap, allzap
+
+
+def prepare(obs, opts, raw, calib=(None, None, None), mask=None, ptsperint=0, padvals=None, dtint=0.0,
+            zapint=None, blk=None):
+    """Block masks + clip_times over the whole raw block -> Clean."""
+    blk = int(blk or obs.nsblk)
+    nblk = (obs.N + blk - 1) // blk
+    zap, allzap = block_masks(obs, mask, ptsperint, dtint, zapint, blk)
+    pad = np.zeros((nblk, obs.nchan), np.float32)
+    clipped = np.zeros(obs.N, np.uint8)
+    raw = np.ascontiguousarray(raw, np.uint8)
+    cal = [None if c is None else np.ascontiguousarray(c, np.float32) for c in calib]
+    pv = None if padvals is None else np.ascontiguousarray(padvals, np.float32)
+    o, p = _obs(obs), _opts(opts)
+    n = lib().or_clip_prepare(ctypes.byref(o), ctypes.byref(p), _ptr(raw), _ptr(cal[0]), _ptr(cal[1]), _ptr(cal[2]),
+                              _ptr(allzap), _ptr(pv), blk, nblk, _ptr(pad), _ptr(clipped))
+    if n < 0:
+        raise ValueError("or_clip_prepare rejected its arguments")
+    return Clean(blk, nblk, zap, allzap, pad, clipped, int(n))
+
+
 def stage1(obs, opts, raw, nsub, ds, subdm, t0=0, count=None, calib=(None, None, None),
-           mask=None, ptsperint=0, padvals=None, omp=False):
+           mask=None, ptsperint=0, padvals=None, omp=False, clean=None, dtint=0.0, zapint=None):
     """Subbands [nsub][count] for output samples [t0, t0+count)."""
     nds = obs.N // ds
     if count is None:
         count = nds - t0
+    if clean is None:
+        clean = prepare(obs, opts, raw, calib, mask, ptsperint, padvals, dtint, zapint)
     idd = chan_delays(obs, nsub, subdm)
     dt = np.int16 if opts.sub_dtype == 0 else np.float32
     out = np.zeros((nsub, count), dt)
     raw = np.ascontiguousarray(raw, np.uint8)
     cal = [None if c is None else np.ascontiguousarray(c, np.float32) for c in calib]
-    m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
-    pv = None if padvals is None else np.ascontiguousarray(padvals, np.float32)
     o, p = _obs(obs), _opts(opts)
     rc = lib(omp).or_stage1(ctypes.byref(o), ctypes.byref(p), _ptr(raw), _ptr(cal[0]), _ptr(cal[1]), _ptr(cal[2]),
-                            _ptr(m), 0 if m is None else m.shape[0], int(ptsperint), _ptr(pv), nsub, ds,
-                            _ptr(idd), int(t0), int(count), _ptr(out), int(count))
+                            _ptr(clean.zap), _ptr(clean.pad), _ptr(clean.clipped), clean.blk, clean.nblk,
+                            nsub, ds, _ptr(idd), int(t0), int(count), _ptr(out), int(count))
     if rc:
         raise ValueError("or_stage1 rejected its arguments")
     return out
@@ -141,18 +200,34 @@ def stage2(sub, off, t0=0, count=None, omp=False):
     return out
 
 
-def run_pass(obs, opts, raw, pp, calib=(None, None, None), mask=None, ptsperint=0, padvals=None, omp=False):
+def pad_series(out, nds, pad_mode):
+    """Pad [numdms][numout] series in place past nds (or_pad)."""
+    out = np.ascontiguousarray(out, np.float32)
+    lib().or_pad(_ptr(out), out.shape[0], int(nds), out.shape[1], int(pad_mode))
+    return out
+
+
+def run_pass(obs, opts, raw, pp, calib=(None, None, None), mask=None, ptsperint=0, padvals=None, omp=False,
+             clean=None, dtint=0.0, zapint=None):
     """Full pass -> (subbands [nsub][nds], series [numdms][numout]) exactly as the engine defines it."""
     nds = obs.N // pp.ds
     numout = pp.numout if pp.numout > 0 else nds
     sub = stage1(obs, opts, raw, pp.nsub, pp.ds, pp.subdm, calib=calib, mask=mask, ptsperint=ptsperint,
-                 padvals=padvals, omp=omp)
+                 padvals=padvals, omp=omp, clean=clean, dtint=dtint, zapint=zapint)
     off = dm_offsets(obs, opts, pp.nsub, pp.ds, pp.lodm, pp.dmstep, pp.numdms)
     out = np.zeros((pp.numdms, numout), np.float32)
     n = min(numout, nds)
     out[:, :n] = stage2(sub, off, 0, n, omp=omp)
     lib(omp).or_pad(_ptr(out), pp.numdms, nds, numout, opts.pad_mode)
     return sub, out
+
+
+def stats_padvals(dataavg):
+    """determine_padvals from rfifind .stats interval averages [numint][numchan]."""
+    a = np.ascontiguousarray(dataavg, np.float32)
+    out = np.zeros(a.shape[1], np.float32)
+    lib().or_stats_padvals(_ptr(a), a.shape[0], a.shape[1], _ptr(out))
+    return out
 
 
 def num_threads(omp=True):

@@ -1,5 +1,6 @@
 /*
- * prepsubband_oracle.c — TEST INFRASTRUCTURE ONLY (see oracle.h for the parity status).
+ * prepsubband_oracle.c — TEST INFRASTRUCTURE ONLY (see oracle.h for the parity status and
+ * the per-block model).
  *
  * A plain-C restatement of what PRESTO `prepsubband` computes for the two calls that
  * PALFA2_presto_search.search_job() makes per DDplan pass
@@ -7,15 +8,16 @@
  * HIP engine and, built with OpenMP, the CPU baseline timed by bench.py.  It is never
  * linked into libhipdedisp.so.
  *
- * Data flow (mirrors PRESTO's block pipeline: raw block -> float block -> subbands ->
- * downsample -> .subNN int16; then .subNN -> per-DM float sums):
- *   stage 1  sub[s][t'] = Q( sum_{k<ds} ( sum_{c in s} X(t'*ds + k + idispdt[c], c) ) )
- *            X(t, c)  = ((raw * scl) + offs) * wts   for channel c (ascending freq),
- *                       padvals[c] if (t / ptsperint, c) is zapped in the mask or t >= N
- *            Q        = nearest integer, ties away from zero, saturated to int16
- *                       (HD_SUB_I16), or identity (HD_SUB_F32); /ds first if ds_mode=mean
+ * Data flow (mirrors PRESTO's block pipeline: raw block -> float block -> mask / clip ->
+ * subbands -> downsample -> .subNN int16; then .subNN -> per-DM float sums):
+ *   stage 1  sub[s][t'] = Q( D( sum_{k<ds} ( sum_{c in s} X'(t'*ds + k + idispdt[c], c) ) ) )
+ *            X'(t, c) = pad[b][c] if spectrum t was clipped or (b, c) is zapped, else
+ *                       ((raw * scl) + offs) * wts (channel c ascending); b = t / blk;
+ *                       t >= N reads pad[nblk-1][c]
+ *            D        = / ds (mean, prepsubband get_data) or identity (sum)
+ *            Q        = (short)(x + 0.5) as x86 evaluates it, or nearest-saturated (sub_round)
  *   stage 2  out[d][t] = sum_{s=0}^{nsub-1} sub[s][t + off[d][s]]   (sub past N/ds = 0)
- *            then pad [N/ds, numout) with the series mean (or 0).
+ *            then pad [N/ds, numout) (first-DM running mean, per-DM mean or 0).
  * Every float sum is accumulated in float32 in ascending channel / subband / k order,
  * starting from 0.0f, with FP contraction disabled (Makefile: -ffp-contract=off).
  */
@@ -145,7 +147,7 @@ void or_dm_offsets(const or_obs* obs, const or_opts* opts, int nsub, int ds,
 }
 
 /* ------------------------------------------------------------------------------- */
-/* stage 1                                                                          */
+/* raw decode                                                                       */
 /* ------------------------------------------------------------------------------- */
 
 static inline float raw_sample(const or_obs* o, const or_opts* op, const uint8_t* row, int rc)
@@ -169,7 +171,248 @@ static inline float raw_sample(const or_obs* o, const or_opts* op, const uint8_t
     }
 }
 
-static inline int16_t quant_i16(float x)
+/* decoded, calibrated sample of ascending channel c at spectrum t (t < N) */
+static inline float decoded(const or_obs* o, const or_opts* op, const uint8_t* raw,
+                            const float* scl, const float* offs, const float* wts, int64_t t, int c)
+{
+    const int64_t rowbytes = (int64_t)o->nchan * o->nbits / 8;
+    const int rc = o->flip ? o->nchan - 1 - c : c;
+    float x = raw_sample(o, op, raw + t * rowbytes, rc);
+    if (scl) x = x * scl[rc];
+    if (offs) x = x + offs[rc];
+    if (wts) x = x * wts[rc];
+    return x;
+}
+
+/* ------------------------------------------------------------------------------- */
+/* rfifind mask per read block [PRESTO-ext, mask.c check_mask]                      */
+/* ------------------------------------------------------------------------------- */
+
+void or_check_mask_blocks(const or_obs* obs, const or_mask* m, int blk, int nblk,
+                          uint8_t* zap, uint8_t* allzap)
+{
+    const int nchan = obs->nchan;
+    memset(zap, 0, (size_t)nblk * nchan);
+    memset(allzap, 0, (size_t)nblk);
+    if (!m || !m->chans || m->numint <= 0) return;
+    const double dtint = m->dtint > 0 ? m->dtint : m->ptsperint * obs->dt;
+    const double duration = blk * obs->dt;               /* time_per_subint */
+    for (int b = 0; b < nblk; b++) {
+        const double starttime = (double)((int64_t)b * blk) * obs->dt;
+        const double endtime = starttime + duration;
+        int lo = (int)(starttime / dtint), hi = (int)(endtime / dtint);
+        /* PRESTO indexes the interval tables with these; past the last interval they are
+         * clamped here (rfifind's numint = ceil(N / ptsperint) makes hi == numint only
+         * for the final block) */
+        if (lo > m->numint - 1) lo = m->numint - 1;
+        if (hi > m->numint - 1) hi = m->numint - 1;
+        int all = 0;
+        for (int k = 0; k < 2 && !all; k++) {
+            const int iv = k ? hi : lo;
+            const uint8_t* row = m->chans + (int64_t)iv * nchan;
+            if (m->zapint) {
+                all = m->zapint[iv] != 0;
+            } else {
+                int n = 0;
+                for (int c = 0; c < nchan; c++) n += row[c] != 0;
+                all = n == nchan;
+            }
+        }
+        if (all) {
+            allzap[b] = 1;
+            memset(zap + (int64_t)b * nchan, 1, (size_t)nchan);
+            continue;
+        }
+        for (int c = 0; c < nchan; c++)
+            zap[(int64_t)b * nchan + c] = (m->chans[(int64_t)lo * nchan + c] | m->chans[(int64_t)hi * nchan + c]) != 0;
+    }
+}
+
+/* ------------------------------------------------------------------------------- */
+/* clip_times and its statistics helpers [PRESTO-ext, clipping.c / misc]           */
+/* ------------------------------------------------------------------------------- */
+
+/* Devillard's quick_select (Numerical Recipes 8.5), as PRESTO's median(): the element of
+ * rank (n - 1) / 2 of arr (arr is permuted). */
+static float quick_select(float* arr, int n)
+{
+    int low = 0, high = n - 1, median = (low + high) / 2, middle, ll, hh;
+    float t;
+#define SWAPF(a, b) { t = (a); (a) = (b); (b) = t; }
+    for (;;) {
+        if (high <= low) return arr[median];
+        if (high == low + 1) {
+            if (arr[low] > arr[high]) SWAPF(arr[low], arr[high]);
+            return arr[median];
+        }
+        middle = (low + high) / 2;
+        if (arr[middle] > arr[high]) SWAPF(arr[middle], arr[high]);
+        if (arr[low] > arr[high]) SWAPF(arr[low], arr[high]);
+        if (arr[middle] > arr[low]) SWAPF(arr[middle], arr[low]);
+        SWAPF(arr[middle], arr[low + 1]);
+        ll = low + 1;
+        hh = high;
+        for (;;) {
+            do ll++; while (arr[low] > arr[ll]);
+            do hh--; while (arr[hh] > arr[low]);
+            if (hh < ll) break;
+            SWAPF(arr[ll], arr[hh]);
+        }
+        SWAPF(arr[low], arr[hh]);
+        if (hh <= median) low = ll;
+        if (hh >= median) high = hh - 1;
+    }
+#undef SWAPF
+}
+
+/* avg_var: mean and (n-1)-normalised variance of a float vector, AS 52 one-pass update */
+static void avg_var(const float* x, int n, double* mean, double* var)
+{
+    double an = 0.0, an1 = 0.0, dx;
+    *mean = (double)x[0];
+    *var = 0.0;
+    for (int i = 1; i < n; i++) {
+        an = (double)(i + 1);
+        an1 = (double)i;
+        dx = ((double)x[i] - *mean) / an;
+        *var += an * an1 * dx * dx;
+        *mean += dx;
+    }
+    if (n > 1) *var /= an1;
+}
+
+#define BLOCKSTOAVG 30
+
+typedef struct {
+    float running_avg, running_std;
+    int blocksread;
+    float* chan_running_avg;
+} clipstate;
+
+/* clip_times(rawdata [ptsperblk][numchan], ..., good_chan_levels): returns the number of
+ * spectra replaced; flags[ii] = 1 for each of them. */
+static int clip_times(float* rawdata, int ptsperblk, int numchan, float clip_sigma,
+                      float* good_chan_levels, clipstate* st, uint8_t* flags)
+{
+    float* zero_dm_block = (float*)malloc(sizeof(float) * ptsperblk);
+    float* median_temp = (float*)malloc(sizeof(float) * ptsperblk);
+    double* chan_avg_temp = (double*)malloc(sizeof(double) * numchan);
+    double current_avg = 0.0, current_std = 0.0;
+    int clipit = 0, clipped = 0;
+
+    /* the zero-DM time series */
+    for (int ii = 0; ii < ptsperblk; ii++) {
+        zero_dm_block[ii] = 0.0f;
+        for (int jj = 0; jj < numchan; jj++) zero_dm_block[ii] += rawdata[(int64_t)ii * numchan + jj];
+        median_temp[ii] = zero_dm_block[ii];
+    }
+    const float current_med = quick_select(median_temp, ptsperblk);
+
+    /* mean / std / channel means of the points within 0.7..1.3 x the median */
+    {
+        const float lo_cutoff = 0.7 * current_med;
+        const float hi_cutoff = 1.3 * current_med;
+        int numgoodpts = 0;
+        for (int jj = 0; jj < numchan; jj++) chan_avg_temp[jj] = 0.0;
+        for (int ii = 0; ii < ptsperblk; ii++) {
+            if (zero_dm_block[ii] > lo_cutoff && zero_dm_block[ii] < hi_cutoff) {
+                median_temp[numgoodpts] = zero_dm_block[ii];
+                for (int jj = 0; jj < numchan; jj++) chan_avg_temp[jj] += rawdata[(int64_t)ii * numchan + jj];
+                numgoodpts++;
+            }
+        }
+        if (numgoodpts < 1) {
+            current_avg = st->running_avg;
+            current_std = st->running_std;
+            for (int jj = 0; jj < numchan; jj++) chan_avg_temp[jj] = st->chan_running_avg[jj];
+        } else {
+            avg_var(median_temp, numgoodpts, &current_avg, &current_std);
+            current_std = sqrt(current_std);
+            for (int jj = 0; jj < numchan; jj++) chan_avg_temp[jj] /= numgoodpts;
+        }
+    }
+
+    /* pseudo running averages over BLOCKSTOAVG blocks */
+    if (st->blocksread) {
+        st->running_avg = (st->running_avg * (BLOCKSTOAVG - 1) + current_avg) / BLOCKSTOAVG;
+        st->running_std = (st->running_std * (BLOCKSTOAVG - 1) + current_std) / BLOCKSTOAVG;
+        for (int ii = 0; ii < numchan; ii++)
+            st->chan_running_avg[ii] = (st->chan_running_avg[ii] * (BLOCKSTOAVG - 1) + chan_avg_temp[ii]) / BLOCKSTOAVG;
+    } else {
+        st->running_avg = current_avg;
+        st->running_std = current_std;
+        for (int ii = 0; ii < numchan; ii++) st->chan_running_avg[ii] = chan_avg_temp[ii];
+    }
+    for (int ii = 0; ii < numchan; ii++) good_chan_levels[ii] = st->chan_running_avg[ii];
+
+    /* clip */
+    const float trigger = clip_sigma * st->running_std;
+    for (int ii = 0; ii < ptsperblk; ii++)
+        if (fabs(zero_dm_block[ii] - st->running_avg) > trigger) {
+            clipit = 1;
+            break;
+        }
+    if (clipit) {
+        for (int ii = 0; ii < ptsperblk; ii++) {
+            if (fabs(zero_dm_block[ii] - st->running_avg) > trigger) {
+                for (int jj = 0; jj < numchan; jj++) rawdata[(int64_t)ii * numchan + jj] = st->chan_running_avg[jj];
+                flags[ii] = 1;
+                clipped++;
+            }
+        }
+    }
+    st->blocksread++;
+    free(zero_dm_block);
+    free(median_temp);
+    free(chan_avg_temp);
+    return clipped;
+}
+
+int64_t or_clip_prepare(const or_obs* obs, const or_opts* opts, const uint8_t* raw,
+                        const float* scl, const float* offs, const float* wts,
+                        const uint8_t* allzap, const float* padvals0, int blk, int nblk,
+                        float* pad, uint8_t* clipped)
+{
+    const int nchan = obs->nchan;
+    if (blk <= 0 || nblk != (int)((obs->N + blk - 1) / blk)) return -1;
+    float* padvals = (float*)calloc((size_t)nchan, sizeof(float));
+    if (padvals0) memcpy(padvals, padvals0, sizeof(float) * nchan);
+    clipstate st = {0.0f, 0.0f, 0, (float*)calloc((size_t)nchan, sizeof(float))};
+    float* X = (float*)malloc(sizeof(float) * (size_t)blk * nchan);
+    memset(clipped, 0, (size_t)obs->N);
+    int64_t total = 0;
+    for (int b = 0; b < nblk; b++) {
+        const int64_t t0 = (int64_t)b * blk;
+        const int nb = (int)((t0 + blk <= obs->N) ? blk : obs->N - t0);
+        /* the reference's -sub command leaves prepsubband's default clip on; a block whose
+         * every channel is masked is neither clipped nor counted (read_psrdata) */
+        if (opts->clip_sigma > 0.0f && !(allzap && allzap[b])) {
+            for (int ii = 0; ii < nb; ii++)
+                for (int c = 0; c < nchan; c++) X[(int64_t)ii * nchan + c] = decoded(obs, opts, raw, scl, offs, wts, t0 + ii, c);
+            total += clip_times(X, nb, nchan, opts->clip_sigma, padvals, &st, clipped + t0);
+        }
+        memcpy(pad + (int64_t)b * nchan, padvals, sizeof(float) * nchan);
+    }
+    free(X);
+    free(st.chan_running_avg);
+    free(padvals);
+    return total;
+}
+
+/* ------------------------------------------------------------------------------- */
+/* stage 1                                                                          */
+/* ------------------------------------------------------------------------------- */
+
+/* prepsubband writes subbands as `subsdata[jj][ii] = (short)(infloat + 0.5)` [PRESTO-ext]:
+ * double x + 0.5 truncated to int32 (cvttsd2si; out of range -> 0x80000000), low 16 bits. */
+static inline int16_t presto_short(float x)
+{
+    const double y = (double)x + 0.5;
+    int32_t i = (y > -2147483649.0 && y < 2147483648.0) ? (int32_t)y : INT32_MIN;
+    return (int16_t)(uint16_t)(uint32_t)i;
+}
+
+static inline int16_t nearest_i16(float x)
 {
     int64_t v = or_nearest_long((double)x);
     if (v > 32767) v = 32767;
@@ -179,14 +422,14 @@ static inline int16_t quant_i16(float x)
 
 int or_stage1(const or_obs* obs, const or_opts* opts, const uint8_t* raw,
               const float* scl, const float* offs, const float* wts,
-              const uint8_t* mask, int numint, int ptsperint, const float* padvals,
+              const uint8_t* zap, const float* pad, const uint8_t* clipped, int blk, int nblk,
               int nsub, int ds, const int32_t* idispdt,
               int64_t t0, int64_t count, void* out, int64_t out_stride)
 {
     const int nchan = obs->nchan;
     if (nsub <= 0 || nchan % nsub || ds <= 0 || obs->npol != 1) return -1;
+    if ((zap || pad || clipped) && (blk <= 0 || nblk != (int)((obs->N + blk - 1) / blk))) return -1;
     const int cps = nchan / nsub;
-    const int64_t rowbytes = (int64_t)nchan * obs->nbits / 8;
     int maxd = 0;
     for (int c = 0; c < nchan; c++) if (idispdt[c] > maxd) maxd = idispdt[c];
     const int64_t bo = ds >= 8192 ? 1 : 8192 / ds;            /* output samples per block */
@@ -198,31 +441,22 @@ int or_stage1(const or_obs* obs, const or_opts* opts, const uint8_t* raw,
         const int64_t nb = (tb0 + bo <= t0 + count) ? bo : (t0 + count - tb0);
         const int64_t nr = nb * ds + maxd;
         float* fb = (float*)malloc(sizeof(float) * nr * nchan);
-        /* raw -> float block (ascending-frequency channels), like read_psrdata */
+        /* raw -> cleaned float block (ascending-frequency channels), like read_psrdata */
         for (int64_t r = 0; r < nr; r++) {
             const int64_t t = tb0 * ds + r;
             float* f = fb + r * nchan;
-            if (t >= obs->N) {
-                for (int c = 0; c < nchan; c++) f[c] = padvals ? padvals[c] : 0.0f;
+            int64_t rb = blk > 0 ? t / blk : 0;
+            if (rb > nblk - 1) rb = nblk - 1;
+            const float* prow = pad ? pad + rb * nchan : NULL;
+            if (t >= obs->N || (clipped && clipped[t])) {
+                for (int c = 0; c < nchan; c++) f[c] = prow ? prow[c] : 0.0f;
                 continue;
             }
-            const uint8_t* row = raw + t * rowbytes;
-            const uint8_t* mrow = NULL;
-            if (mask && ptsperint > 0) {
-                int64_t iv = t / ptsperint;
-                if (iv < numint) mrow = mask + iv * nchan;
-            }
-            for (int c = 0; c < nchan; c++) {
-                const int rc = obs->flip ? nchan - 1 - c : c;
-                float x = raw_sample(obs, opts, row, rc);
-                if (scl) x = x * scl[rc];
-                if (offs) x = x + offs[rc];
-                if (wts) x = x * wts[rc];
-                if (mrow && mrow[c]) x = padvals ? padvals[c] : 0.0f;
-                f[c] = x;
-            }
+            const uint8_t* zrow = zap ? zap + rb * nchan : NULL;
+            for (int c = 0; c < nchan; c++)
+                f[c] = (zrow && zrow[c]) ? (prow ? prow[c] : 0.0f) : decoded(obs, opts, raw, scl, offs, wts, t, c);
         }
-        /* channel -> subband delay-and-sum at subdm, then downsample */
+        /* channel -> subband delay-and-sum at subdm (dedisp_subbands), then downsample */
         for (int64_t j = 0; j < nb; j++) {
             for (int s = 0; s < nsub; s++) {
                 float acc = 0.0f;
@@ -237,7 +471,8 @@ int or_stage1(const or_obs* obs, const or_opts* opts, const uint8_t* raw,
                 if (opts->ds_mode == 1) acc = acc / (float)ds;
                 const int64_t col = tb0 + j - t0;
                 if (opts->sub_dtype == 0)
-                    ((int16_t*)out)[(int64_t)s * out_stride + col] = quant_i16(acc);
+                    ((int16_t*)out)[(int64_t)s * out_stride + col] =
+                        opts->sub_round == 0 ? presto_short(acc) : nearest_i16(acc);
                 else
                     ((float*)out)[(int64_t)s * out_stride + col] = acc;
             }
@@ -278,12 +513,25 @@ int or_stage2(const void* sub, int sub_dtype, int64_t nds, int64_t sub_stride, i
     return 0;
 }
 
+/* prepsubband pads [N/ds, numout) with `avg`, the one-pass running mean (update_stats)
+ * of the FIRST DM's written samples, for every DM [PRESTO-ext] (pad_mode 2); pad_mode 0 is
+ * a per-DM mean (double sum), 1 zeros. */
 void or_pad(float* out, int numdms, int64_t nds, int64_t numout, int pad_mode)
 {
     if (numout <= nds) return;
+    float v0 = 0.0f;
+    if (pad_mode == 2 && nds > 0) {
+        double avg = 0.0;
+        for (int64_t n = 0; n < nds; n++) {
+            const double x = out[n];
+            const double dev = x - avg;
+            avg += dev / (n + 1.0);
+        }
+        v0 = (float)avg;
+    }
     for (int d = 0; d < numdms; d++) {
         float* o = out + (int64_t)d * numout;
-        float v = 0.0f;
+        float v = v0;
         if (pad_mode == 0 && nds > 0) {
             double sum = 0.0;
             for (int64_t t = 0; t < nds; t++) sum += (double)o[t];
@@ -293,31 +541,32 @@ void or_pad(float* out, int numdms, int64_t nds, int64_t numout, int pad_mode)
     }
 }
 
-int or_run_pass(const or_obs* obs, const or_opts* opts, const uint8_t* raw,
-                const float* scl, const float* offs, const float* wts,
-                const uint8_t* mask, int numint, int ptsperint, const float* padvals,
-                double subdm, double lodm, double dmstep, int numdms, int nsub, int ds,
-                int64_t numout, void* sub_out, float* dat_out)
+/* ------------------------------------------------------------------------------- */
+/* rfifind .stats -> pad values [PRESTO-ext, mask.c determine_padvals]              */
+/* ------------------------------------------------------------------------------- */
+
+static int cmp_float(const void* a, const void* b)
 {
-    const int64_t nds = obs->N / ds;
-    if (numout <= 0) numout = nds;
-    int32_t* idd = (int32_t*)malloc(sizeof(int32_t) * obs->nchan);
-    int32_t* off = (int32_t*)malloc(sizeof(int32_t) * (size_t)numdms * nsub);
-    const size_t esz = opts->sub_dtype == 0 ? 2 : 4;
-    void* sub = sub_out ? sub_out : malloc(esz * (size_t)nsub * (size_t)(nds > 0 ? nds : 1));
-    or_chan_delays(obs, nsub, subdm, idd);
-    or_dm_offsets(obs, opts, nsub, ds, lodm, dmstep, numdms, off);
-    int rc = or_stage1(obs, opts, raw, scl, offs, wts, mask, numint, ptsperint, padvals,
-                       nsub, ds, idd, 0, nds, sub, nds);
-    if (rc == 0) {
-        const int64_t n = numout < nds ? numout : nds;
-        rc = or_stage2(sub, opts->sub_dtype, nds, nds, nsub, off, numdms, 0, n, dat_out, numout);
-        or_pad(dat_out, numdms, nds, numout, opts->pad_mode);
+    const float x = *(const float*)a, y = *(const float*)b;
+    return x < y ? -1 : (x > y ? 1 : 0);
+}
+
+/* calc_avgmedstd(arr, numarr, 0.8, step): mean of the middle `fraction` of the sorted
+ * strided values (avg_var), returned as float */
+void or_stats_padvals(const float* dataavg, int numint, int numchan, float* padvals)
+{
+    const float fraction = 0.8f;
+    float* tmp = (float*)malloc(sizeof(float) * (numint > 0 ? numint : 1));
+    for (int c = 0; c < numchan; c++) {
+        const int len = (int)(numint * fraction + 0.5);
+        const int start = (numint - len) / 2;
+        for (int ii = 0; ii < numint; ii++) tmp[ii] = dataavg[(int64_t)ii * numchan + c];
+        qsort(tmp, (size_t)numint, sizeof(float), cmp_float);
+        double avg = 0.0, var = 0.0;
+        if (len > 0) avg_var(tmp + start, len, &avg, &var);
+        padvals[c] = (float)avg;
     }
-    if (!sub_out) free(sub);
-    free(idd);
-    free(off);
-    return rc;
+    free(tmp);
 }
 
 int or_num_threads(void)

@@ -13,6 +13,8 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cmath>
+#include <map>
 #include <chrono>
 #include <string>
 #include <thread>
@@ -38,10 +40,28 @@ struct hd_ctx {
     int64_t rawT_stride = 0;
     bool rawT_valid = false;           // false whenever the raw block changes
     float *d_scl = nullptr, *d_offs = nullptr, *d_wts = nullptr;
-    uint8_t* d_mask = nullptr;
+    // rfifind mask as given (hd_set_mask) and the initial pad values
+    std::vector<uint8_t> h_mask, h_zapint;  // [numint][nchan], [numint]
     int32_t numint = 0, ptsperint = 0;
+    double dtint = 0.0;
     float* d_padvals = nullptr;
     std::vector<float> h_padvals;      // host copy (bounds for the integer stage-1 path)
+    // per read block (obs.nsblk spectra): check_mask rows, deduplicated (zidx -> zrows)
+    int32_t blk = 1, nblk = 1;
+    bool blocks_valid = false;
+    int32_t* d_zidx = nullptr;
+    uint8_t* d_zrows = nullptr;
+    uint8_t* d_allzap = nullptr;
+    // clip_times state of the current raw block (hd_clip.hip), rebuilt when the raw block,
+    // mask, pad values or calibration change
+    bool clip_valid = false;
+    struct ClipBufs {
+        float* zdm = nullptr;
+        uint8_t *good = nullptr, *clipped = nullptr;
+        int32_t *numgood = nullptr, *doclip = nullptr, *events = nullptr, *nevents = nullptr;
+        double *bavg = nullptr, *bstd = nullptr, *chansum = nullptr;
+        float *ravg = nullptr, *trig = nullptr, *pad = nullptr;
+    } clip;
     size_t lds_attr_set = 64 * 1024;   // dynamic-LDS limit already granted to the tiled kernels
     size_t lds_attr_q8 = 64 * 1024;    // ... and to the 8-bit integer stage-1 kernels
     struct SpecialList {               // stage-1 special-tile list per tile geometry (device)
@@ -195,12 +215,13 @@ extern "C" void hd_opts_default(hd_opts* o)
     if (!o) return;
     memset(o, 0, sizeof *o);
     o->sub_dtype = HD_SUB_I16;
-    o->ds_mode = HD_DS_SUM;
-    o->pad_mode = HD_PAD_MEAN;
+    o->ds_mode = HD_DS_MEAN;
+    o->pad_mode = HD_PAD_DM0;
     o->nibble_hi_first = 1;
     o->be16 = 1;
     o->inf_roundtrip = 1;
-    o->clip_sigma = 0.0f;
+    o->clip_sigma = 6.0f;
+    o->sub_round = HD_ROUND_PRESTO;
 }
 
 extern "C" int hd_device_count(int* n)
@@ -236,6 +257,26 @@ extern "C" int hd_open(int device, hd_ctx** out)
     return HD_OK;
 }
 
+static void free_blocks(hd_ctx* c)
+{
+    dfree(c->d_zidx); c->d_zidx = nullptr;
+    dfree(c->d_zrows); c->d_zrows = nullptr;
+    dfree(c->d_allzap); c->d_allzap = nullptr;
+    c->blocks_valid = false;
+    c->clip_valid = false;
+}
+
+static void free_clip(hd_ctx* c)
+{
+    hd_ctx::ClipBufs& b = c->clip;
+    for (void* p : {(void*)b.zdm, (void*)b.good, (void*)b.clipped, (void*)b.numgood, (void*)b.doclip,
+                    (void*)b.events, (void*)b.nevents, (void*)b.bavg, (void*)b.bstd, (void*)b.chansum,
+                    (void*)b.ravg, (void*)b.trig, (void*)b.pad})
+        dfree(p);
+    b = hd_ctx::ClipBufs{};
+    c->clip_valid = false;
+}
+
 static void free_obs_buffers(hd_ctx* c)
 {
     dfree(c->d_raw); c->d_raw = nullptr;
@@ -244,12 +285,16 @@ static void free_obs_buffers(hd_ctx* c)
     dfree(c->d_scl); c->d_scl = nullptr;
     dfree(c->d_offs); c->d_offs = nullptr;
     dfree(c->d_wts); c->d_wts = nullptr;
-    dfree(c->d_mask); c->d_mask = nullptr;
     dfree(c->d_padvals); c->d_padvals = nullptr;
     c->h_padvals.clear();
+    c->h_mask.clear();
+    c->h_zapint.clear();
+    free_blocks(c);
+    free_clip(c);
     clear_special_cache(c);
     c->raw_ready = false;
     c->numint = c->ptsperint = 0;
+    c->dtint = 0.0;
 }
 
 extern "C" int hd_close(hd_ctx* c)
@@ -288,6 +333,7 @@ extern "C" int hd_touch_raw(hd_ctx* c)
 {
     if (!c) return fail(nullptr, HD_E_INVAL, "hd_touch_raw: NULL context");
     c->rawT_valid = false;
+    c->clip_valid = false;
     return HD_OK;
 }
 
@@ -355,15 +401,21 @@ extern "C" int hd_set_obs(hd_ctx* c, const hd_obs* o, const hd_opts* opts)
     if (opts) op = *opts; else hd_opts_default(&op);
     if (op.sub_dtype != HD_SUB_I16 && op.sub_dtype != HD_SUB_F32) return fail(c, HD_E_INVAL, "bad sub_dtype");
     if (op.ds_mode != HD_DS_SUM && op.ds_mode != HD_DS_MEAN) return fail(c, HD_E_INVAL, "bad ds_mode");
-    if (op.pad_mode != HD_PAD_MEAN && op.pad_mode != HD_PAD_ZERO) return fail(c, HD_E_INVAL, "bad pad_mode");
-    if (op.clip_sigma != 0.0f)
-        return fail(c, HD_E_INVAL, "clip_sigma != 0 is not implemented yet (see DESIGN.md, clipping row)");
+    if (op.pad_mode != HD_PAD_MEAN && op.pad_mode != HD_PAD_ZERO && op.pad_mode != HD_PAD_DM0)
+        return fail(c, HD_E_INVAL, "bad pad_mode");
+    if (op.sub_round != HD_ROUND_PRESTO && op.sub_round != HD_ROUND_NEAREST) return fail(c, HD_E_INVAL, "bad sub_round");
+    if (!(op.clip_sigma >= 0.0f) || !std::isfinite(op.clip_sigma))
+        return fail(c, HD_E_INVAL, "clip_sigma must be finite and >= 0 (0 = -noclip)");
+    if (op.clip_sigma > 0.0f && o->nsblk > hd::clip_max_block())
+        return fail(c, HD_E_INVAL, "clipping needs nsblk <= %d (got %d)", hd::clip_max_block(), o->nsblk);
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, sync_all(c));
     free_obs_buffers(c);
     c->obs = *o;
     c->opts = op;
     c->rowbytes = (int32_t)((int64_t)o->nchan * o->nbits / 8);
+    c->blk = (int32_t)std::min<int64_t>(o->nsblk > 0 ? o->nsblk : o->N, o->N);
+    c->nblk = (int32_t)((o->N + c->blk - 1) / c->blk);
     c->have_obs = true;
     return HD_OK;
 }
@@ -399,32 +451,68 @@ extern "C" int hd_set_chan_calib(hd_ctx* c, const float* scl, const float* offs,
     if ((rc = upload(c, &c->d_scl, scl, c->obs.nchan))) return rc;
     if ((rc = upload(c, &c->d_offs, offs, c->obs.nchan))) return rc;
     if ((rc = upload(c, &c->d_wts, wts, c->obs.nchan))) return rc;
+    c->clip_valid = false;
     return HD_OK;
 }
 
-extern "C" int hd_set_mask(hd_ctx* c, const uint8_t* mask, int32_t numint, int32_t ptsperint, const float* padvals)
+extern "C" int hd_set_mask(hd_ctx* c, const uint8_t* mask, int32_t numint, int32_t ptsperint, double dtint,
+                           const uint8_t* zapint, const float* padvals)
 {
     if (!c) return fail(nullptr, HD_E_INVAL, "hd_set_mask: NULL context");
     if (!c->have_obs) return fail(c, HD_E_STATE, "hd_set_mask before hd_set_obs");
     if (mask && (numint <= 0 || ptsperint <= 0))
         return fail(c, HD_E_INVAL, "hd_set_mask: numint and ptsperint must be > 0");
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    dfree(c->d_mask);
-    c->d_mask = nullptr;
-    c->numint = c->ptsperint = 0;
+    HIPCHK(c, sync_all(c));
+    free_blocks(c);
     clear_special_cache(c);
+    c->h_mask.clear();
+    c->h_zapint.clear();
+    c->numint = c->ptsperint = 0;
+    c->dtint = 0.0;
     if (mask) {
         const size_t n = (size_t)numint * c->obs.nchan;
-        HIPCHK(c, hipMalloc(&c->d_mask, n));
-        HIPCHK(c, hipMemcpy(c->d_mask, mask, n, hipMemcpyHostToDevice));
+        c->h_mask.assign(mask, mask + n);
+        if (zapint) {
+            c->h_zapint.assign(zapint, zapint + numint);
+        } else {   // a row listing every channel stands for a zap_int
+            c->h_zapint.assign((size_t)numint, 0);
+            for (int32_t i = 0; i < numint; i++) {
+                int32_t k = 0;
+                for (int32_t ch = 0; ch < c->obs.nchan; ch++) k += mask[(size_t)i * c->obs.nchan + ch] != 0;
+                c->h_zapint[i] = k == c->obs.nchan;
+            }
+        }
         c->numint = numint;
         c->ptsperint = ptsperint;
+        c->dtint = dtint > 0 ? dtint : ptsperint * c->obs.dt;
     }
     if (padvals) c->h_padvals.assign(padvals, padvals + c->obs.nchan);
     else c->h_padvals.clear();
-    int rc = upload(c, &c->d_padvals, padvals, c->obs.nchan);
-    return rc;
+    return upload(c, &c->d_padvals, padvals, c->obs.nchan);
+}
+
+extern "C" int hd_stats_padvals(const float* dataavg, int32_t numint, int32_t numchan, float* padvals)
+{
+    if (!dataavg || !padvals || numint <= 0 || numchan <= 0)
+        return fail(nullptr, HD_E_INVAL, "hd_stats_padvals: bad arguments");
+    // determine_padvals -> calc_avgmedstd(..., 0.8, numchan, ...) per channel [PRESTO-ext]:
+    // the middle `fraction` of the sorted interval averages, their avg_var (AS 52) mean
+    const float fraction = 0.8f;
+    const int len = (int)(numint * fraction + 0.5);
+    const int start = (numint - len) / 2;
+    std::vector<float> v((size_t)numint);
+    for (int32_t ch = 0; ch < numchan; ch++) {
+        for (int32_t i = 0; i < numint; i++) v[i] = dataavg[(size_t)i * numchan + ch];
+        std::sort(v.begin(), v.end());
+        double mean = 0.0;
+        if (len > 0) {
+            mean = (double)v[start];
+            for (int i = 1; i < len; i++) mean += ((double)v[start + i] - mean) / (double)(i + 1);
+        }
+        padvals[ch] = (float)mean;
+    }
+    return HD_OK;
 }
 
 extern "C" int hd_push_raw(hd_ctx* c, const void* spectra, int64_t start, int64_t n)
@@ -442,6 +530,7 @@ extern "C" int hd_push_raw(hd_ctx* c, const void* spectra, int64_t start, int64_
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->raw_ready = true;
     c->rawT_valid = false;
+    c->clip_valid = false;
     return HD_OK;
 }
 
@@ -532,6 +621,7 @@ extern "C" int hd_push_raw_file(hd_ctx* c, const char* path, const hd_rows_src* 
     if (err || se != hipSuccess) return fail(c, HD_E_HIP, "hd_push_raw_file: HIP copy failed");
     c->raw_ready = true;
     c->rawT_valid = false;
+    c->clip_valid = false;
     if (io_seconds) *io_seconds = io;
     if (total_seconds) *total_seconds = std::chrono::duration<double>(clk::now() - t_all).count();
     return HD_OK;
@@ -553,6 +643,7 @@ extern "C" int hd_push_raw_device(hd_ctx* c, const void* dev_spectra, int64_t st
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->raw_ready = true;
     c->rawT_valid = false;
+    c->clip_valid = false;
     return HD_OK;
 }
 
@@ -728,6 +819,7 @@ extern "C" int hd_synth_device(hd_ctx* c, const hd_synth* s)
         return fail(c, HD_E_HIP, "synth kernel failed: %s", hipGetErrorString(e != hipSuccess ? e : e2));
     c->raw_ready = true;
     c->rawT_valid = false;
+    c->clip_valid = false;
     return HD_OK;
 }
 
@@ -842,8 +934,7 @@ static void wide_tables(hd_plan* p, int nwmax, bool dbuf, bool i16, hd_plan::Wid
     const int per = (numdms + nyb - 1) / nyb;
     const int qneed = (per + nwmax - 1) / nwmax;
     int Q = 2, R = 4;
-    static const int ring_r5 = getenv("HD_RING_R5") ? atoi(getenv("HD_RING_R5")) : 3;   // experiment
-    if (qneed > 4) { Q = 5; R = ring ? ring_r5 : 3; }
+    if (qneed > 4) { Q = 5; R = 3; }
     else if (qneed > 3) { Q = 4; R = ring ? 3 : 4; }
     else if (qneed > 2) { Q = 3; R = 4; }
     const int nw = ring ? 16 : (per + Q - 1) / Q;   // the ring needs all 16 waves as DMA loaders
@@ -1185,11 +1276,164 @@ static hd::RawDesc raw_desc(const hd_ctx* c)
     rd.scl = c->d_scl;
     rd.offs = c->d_offs;
     rd.wts = c->d_wts;
-    rd.mask = c->d_mask;
-    rd.numint = c->numint;
-    rd.ptsperint = c->ptsperint;
-    rd.padvals = c->d_padvals;
+    rd.blk = c->blk;
+    rd.nblk = c->nblk;
+    rd.zidx = c->d_zidx;
+    rd.zrows = c->d_zrows;
+    const bool clip = c->opts.clip_sigma > 0.0f && c->clip_valid;
+    rd.pad = clip ? c->clip.pad : c->d_padvals;
+    rd.pad_stride = clip ? c->obs.nchan : 0;
+    rd.clipped = clip ? c->clip.clipped : nullptr;
     return rd;
+}
+
+// check_mask per read block [PRESTO-ext, mask.c]: block b spans [b*blk*dt, b*blk*dt +
+// blk*dt); its zapped channels are the union of the lists of the intervals holding its
+// start and end time (clamped to the last interval), or all channels when either is a
+// zap_int.  Identical rows are uploaded once (zidx -> zrows).
+static int ensure_blocks(hd_ctx* c)
+{
+    if (c->blocks_valid) return HD_OK;
+    free_blocks(c);
+    const int nchan = c->obs.nchan, nblk = c->nblk;
+    std::vector<uint8_t> allzap((size_t)nblk, 0);
+    if (!c->h_mask.empty()) {
+        std::vector<int32_t> zidx((size_t)nblk);
+        std::vector<uint8_t> rows;
+        std::map<int64_t, int32_t> seen;     // (lo, hi) or all -> row
+        const double duration = c->blk * c->obs.dt;
+        for (int32_t b = 0; b < nblk; b++) {
+            const double starttime = (double)((int64_t)b * c->blk) * c->obs.dt;
+            const double endtime = starttime + duration;
+            const int lo = std::min((int)(starttime / c->dtint), c->numint - 1);
+            const int hi = std::min((int)(endtime / c->dtint), c->numint - 1);
+            const bool all = c->h_zapint[lo] || c->h_zapint[hi];
+            allzap[b] = all;
+            const int64_t key = all ? -1 : (int64_t)lo * c->numint + hi;
+            auto it = seen.find(key);
+            if (it != seen.end()) {
+                zidx[b] = it->second;
+                continue;
+            }
+            const int32_t r = (int32_t)seen.size();
+            seen[key] = r;
+            zidx[b] = r;
+            rows.resize((size_t)(r + 1) * nchan);
+            uint8_t* dst = &rows[(size_t)r * nchan];
+            for (int ch = 0; ch < nchan; ch++)
+                dst[ch] = all || c->h_mask[(size_t)lo * nchan + ch] || c->h_mask[(size_t)hi * nchan + ch];
+        }
+        HIPCHK(c, hipMalloc(&c->d_zidx, sizeof(int32_t) * zidx.size()));
+        HIPCHK(c, hipMemcpy(c->d_zidx, zidx.data(), sizeof(int32_t) * zidx.size(), hipMemcpyHostToDevice));
+        HIPCHK(c, hipMalloc(&c->d_zrows, rows.size()));
+        HIPCHK(c, hipMemcpy(c->d_zrows, rows.data(), rows.size(), hipMemcpyHostToDevice));
+    }
+    HIPCHK(c, hipMalloc(&c->d_allzap, allzap.size()));
+    HIPCHK(c, hipMemcpy(c->d_allzap, allzap.data(), allzap.size(), hipMemcpyHostToDevice));
+    c->blocks_valid = true;
+    c->clip_valid = false;
+    return HD_OK;
+}
+
+// clip_times over the raw block (hd_clip.hip), queued on the context stream; its device
+// time is charged to the stage-1 launch that needs it.
+static int ensure_clip(hd_ctx* c)
+{
+    if (!(c->opts.clip_sigma > 0.0f) || c->clip_valid) return HD_OK;
+    int rc = ensure_blocks(c);
+    if (rc) return rc;
+    hd_ctx::ClipBufs& b = c->clip;
+    const size_t N = (size_t)c->obs.N, nb = (size_t)c->nblk, nch = (size_t)c->obs.nchan;
+    if (!b.zdm) {
+        hipError_t e = hipSuccess;
+        auto al = [&](void** p, size_t bytes) {
+            if (e == hipSuccess) e = hipMalloc(p, bytes);
+        };
+        al((void**)&b.zdm, N * 4);
+        al((void**)&b.good, N);
+        al((void**)&b.clipped, N);
+        al((void**)&b.events, N * 4);
+        al((void**)&b.nevents, 4);
+        al((void**)&b.numgood, nb * 4);
+        al((void**)&b.doclip, nb * 4);
+        al((void**)&b.bavg, nb * 8);
+        al((void**)&b.bstd, nb * 8);
+        al((void**)&b.ravg, nb * 4);
+        al((void**)&b.trig, nb * 4);
+        al((void**)&b.chansum, nb * nch * 8);
+        al((void**)&b.pad, nb * nch * 4);
+        if (e != hipSuccess) {
+            free_clip(c);
+            return fail(c, HD_E_NOMEM, "cannot allocate the clip_times state: %s", hipGetErrorString(e));
+        }
+    }
+    hd::ClipArgs a{};
+    a.rd = raw_desc(c);
+    a.clip_sigma = c->opts.clip_sigma;
+    a.allzap = c->d_allzap;
+    a.padvals0 = c->d_padvals;
+    a.zdm = b.zdm;
+    a.good = b.good;
+    a.numgood = b.numgood;
+    a.bavg = b.bavg;
+    a.bstd = b.bstd;
+    a.chansum = b.chansum;
+    a.ravg = b.ravg;
+    a.trig = b.trig;
+    a.doclip = b.doclip;
+    a.clipped = b.clipped;
+    a.pad = b.pad;
+    a.events = b.events;
+    a.nevents = b.nevents;
+    HIPCHK(c, hd::launch_clip(a, c->stream));
+    c->clip_valid = true;
+    return HD_OK;
+}
+
+extern "C" int hd_get_clean(hd_ctx* c, float* pad, uint8_t* clipped, uint8_t* zap, int64_t* nclipped)
+{
+    if (!c) return fail(nullptr, HD_E_INVAL, "hd_get_clean: NULL context");
+    if (!c->have_obs) return fail(c, HD_E_STATE, "hd_get_clean before hd_set_obs");
+    const bool clip = c->opts.clip_sigma > 0.0f;
+    if (clip && !c->raw_ready) return fail(c, HD_E_STATE, "hd_get_clean: no raw data");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, join_stream2(c));
+    int rc = ensure_blocks(c);
+    if (rc) return rc;
+    if ((rc = ensure_clip(c))) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const size_t nb = (size_t)c->nblk, nch = (size_t)c->obs.nchan;
+    if (pad) {
+        if (clip) {
+            HIPCHK(c, hipMemcpy(pad, c->clip.pad, nb * nch * 4, hipMemcpyDeviceToHost));
+        } else {
+            for (size_t b = 0; b < nb; b++)
+                for (size_t ch = 0; ch < nch; ch++) pad[b * nch + ch] = c->h_padvals.empty() ? 0.0f : c->h_padvals[ch];
+        }
+    }
+    if (clipped) {
+        if (clip) HIPCHK(c, hipMemcpy(clipped, c->clip.clipped, (size_t)c->obs.N, hipMemcpyDeviceToHost));
+        else memset(clipped, 0, (size_t)c->obs.N);
+    }
+    if (zap) {
+        if (c->d_zidx) {
+            std::vector<int32_t> zidx(nb);
+            HIPCHK(c, hipMemcpy(zidx.data(), c->d_zidx, nb * 4, hipMemcpyDeviceToHost));
+            int32_t nrow = 0;
+            for (int32_t v : zidx) nrow = std::max(nrow, v + 1);
+            std::vector<uint8_t> rows((size_t)nrow * nch);
+            HIPCHK(c, hipMemcpy(rows.data(), c->d_zrows, rows.size(), hipMemcpyDeviceToHost));
+            for (size_t b = 0; b < nb; b++) memcpy(zap + b * nch, &rows[(size_t)zidx[b] * nch], nch);
+        } else {
+            memset(zap, 0, nb * nch);
+        }
+    }
+    if (nclipped) {
+        int32_t n = 0;
+        if (clip) HIPCHK(c, hipMemcpy(&n, c->clip.nevents, 4, hipMemcpyDeviceToHost));
+        *nclipped = n;
+    }
+    return HD_OK;
 }
 
 // Tiling of the multi-pass stage-1 kernel: sg subbands per workgroup (64*sg threads),
@@ -1300,6 +1544,8 @@ static bool stage1_q8_tiling(const hd_ctx* c, int nsub, int ds, int dmax, hd::St
         const double smax = cps * maxpad, amax = ds * smax;
         auto ulp2 = [](double x) { return ldexp(1.0, (int)floor(log2(x)) - 22); };
         a.tie_eps = ds * cps * 0.5 * ulp2(smax) + ds * 0.5 * ulp2(amax);
+        // mean mode: x = fl(F / ds) errs by half an ulp of F/ds, i.e. ds/2 ulps in C's units
+        if (c->opts.ds_mode == HD_DS_MEAN) a.tie_eps += ds * 0.5 * ulp2(smax);
     }
     a.ngroups = nsub / sg;
     vb = v;
@@ -1352,8 +1598,12 @@ static int run_subband_chunk(hd_ctx* c, hd_plan** plans, int n)
     if (v1 == 3 && !q8)
         return fail(c, HD_E_INVAL, "stage-1 variant 3 (8-bit integer path) does not apply to this pass");
     const bool tiled = !q8 && (v1 == 0 || v1 == 2) && stage1_tiling(c, p0->pass.nsub, p0->pass.ds, dmax, m, vw);
+    int rc0 = ensure_blocks(c);
+    if (rc0) return rc0;
     for (int i = 0; i < n; i++) HIPCHK(c, hipMemsetAsync(plans[i]->d_maxabs, 0, sizeof(int32_t), c->stream));
     HIPCHK(c, hipEventRecord(p0->ev[0], c->stream));
+    if ((rc0 = ensure_clip(c))) return rc0;          // once per raw block, charged to this launch
+    const bool clip = c->opts.clip_sigma > 0.0f;
     if (q8) {
         m.probe = p0->probe;
         m.rd = raw_desc(c);
@@ -1365,6 +1615,7 @@ static int run_subband_chunk(hd_ctx* c, hd_plan** plans, int n)
         m.ds = p0->pass.ds;
         m.ds_mode = c->opts.ds_mode;
         m.sub_dtype = c->opts.sub_dtype;
+        m.sub_round = c->opts.sub_round;
         m.nds = p0->nds;
         m.out_stride = p0->sub_stride;
         m.ntiles = (int)((p0->nds + m.to - 1) / m.to);
@@ -1395,6 +1646,8 @@ static int run_subband_chunk(hd_ctx* c, hd_plan** plans, int n)
             }
             HIPCHK(c, hd::launch_stage1_tiled(f, fvw, d_sp, nsp, true, c->stream));
         }
+        // clipped spectra, and the block-boundary outputs of the per-block pad constants
+        if (clip) HIPCHK(c, hd::launch_stage1_fixup(m, c->clip.events, c->clip.nevents, m.rd.zidx != nullptr, c->stream));
     } else if (tiled) {
         m.rd = raw_desc(c);
         m.npass = n;
@@ -1403,6 +1656,7 @@ static int run_subband_chunk(hd_ctx* c, hd_plan** plans, int n)
         m.ds = p0->pass.ds;
         m.ds_mode = c->opts.ds_mode;
         m.sub_dtype = c->opts.sub_dtype;
+        m.sub_round = c->opts.sub_round;
         m.nds = p0->nds;
         m.out_stride = p0->sub_stride;
         m.ntiles = (int)((p0->nds + m.to - 1) / m.to);
@@ -1421,7 +1675,8 @@ static int run_subband_chunk(hd_ctx* c, hd_plan** plans, int n)
         int rc = special_tiles(c, m, &d_sp, &nsp);
         if (rc) return rc;
         HIPCHK(c, hd::launch_stage1_tiled(m, vw, d_sp, nsp, false, c->stream));
-    } else {
+        if (clip) HIPCHK(c, hd::launch_stage1_fixup(m, c->clip.events, c->clip.nevents, 0, c->stream));
+    } else {   // one thread per subband sample, every cleaning rule per cell (no fixup needed)
         for (int i = 0; i < n; i++) {
             hd_plan* p = plans[i];
             hd::Stage1Args a{};
@@ -1432,6 +1687,7 @@ static int run_subband_chunk(hd_ctx* c, hd_plan** plans, int n)
             a.ds = p->pass.ds;
             a.ds_mode = c->opts.ds_mode;
             a.sub_dtype = c->opts.sub_dtype;
+            a.sub_round = c->opts.sub_round;
             a.maxdelay = p->maxdelay;
             a.nds = p->nds;
             a.out_stride = p->sub_stride;
@@ -1492,6 +1748,40 @@ extern "C" int hd_get_subbands(hd_plan* p, void* host)
     HIPCHK(c, hipMemcpy2DAsync(host, es * p->nds, p->d_sub, es * p->sub_stride, es * p->nds, p->pass.nsub,
                                hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    return HD_OK;
+}
+
+extern "C" int hd_get_subbands_window(hd_plan* p, int64_t t0, int64_t count, void* host)
+{
+    if (!p || !host) return fail(p ? p->ctx : nullptr, HD_E_INVAL, "hd_get_subbands_window: NULL argument");
+    hd_ctx* c = p->ctx;
+    if (!p->sub_valid) return fail(c, HD_E_STATE, "hd_get_subbands_window: no subbands formed for this plan yet");
+    if (t0 < 0 || count < 0 || t0 + count > p->nds)
+        return fail(c, HD_E_INVAL, "hd_get_subbands_window: [%lld, %lld) outside [0, %lld)", (long long)t0,
+                    (long long)(t0 + count), (long long)p->nds);
+    if (count == 0) return HD_OK;
+    const size_t es = sub_elem(c);
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpy2DAsync(host, es * count, (const char*)p->d_sub + es * t0, es * p->sub_stride, es * count,
+                               p->pass.nsub, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return HD_OK;
+}
+
+extern "C" int hd_get_series(hd_plan* p, int32_t dm0, int32_t ndm, int64_t t0, int64_t count, float* host)
+{
+    if (!p || !host) return fail(p ? p->ctx : nullptr, HD_E_INVAL, "hd_get_series: NULL argument");
+    hd_ctx* c = p->ctx;
+    if (!p->ran_dd || !p->d_out) return fail(c, HD_E_STATE, "hd_get_series: run hd_run_dedisp first");
+    if (dm0 < 0 || ndm < 0 || dm0 + ndm > p->pass.numdms || t0 < 0 || count < 0 || t0 + count > p->numout)
+        return fail(c, HD_E_INVAL, "hd_get_series: window outside [%d DMs] x [0, %lld)", p->pass.numdms,
+                    (long long)p->numout);
+    if (count == 0 || ndm == 0) return HD_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpy2DAsync(host, sizeof(float) * count, p->d_out + (size_t)dm0 * p->out_stride + t0,
+                               sizeof(float) * p->out_stride, sizeof(float) * count, ndm, hipMemcpyDeviceToHost,
+                               p->dd_stream));
+    HIPCHK(c, hipStreamSynchronize(p->dd_stream));
     return HD_OK;
 }
 
@@ -1563,7 +1853,7 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
     const int tile = use_wide ? 256 * p->wide[wk].r : kTT;
     const int ntiles = (int)((p->nvalid + tile - 1) / tile);
     double* partial = nullptr;
-    if (pad && c->opts.pad_mode == HD_PAD_MEAN) {
+    if (pad && c->opts.pad_mode != HD_PAD_ZERO) {
         const size_t need = sizeof(double) * (size_t)p->pass.numdms * std::max(ntiles, 1);
         double*& buf = alt ? c->d_partial2 : c->d_partial;
         size_t& have = alt ? c->partial_bytes2 : c->partial_bytes;

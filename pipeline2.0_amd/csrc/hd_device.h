@@ -1,0 +1,108 @@
+// hd_device.h — device helpers shared by the stage-1 kernels (hd_kernels.hip) and the
+// clip/fixup kernels (hd_clip.hip): raw decode, the per-block cleaning lookups, the
+// subband rounding rules and small wave utilities.
+#pragma once
+#include "hd_internal.h"
+
+namespace hd {
+
+__device__ __forceinline__ float raw_value(const RawDesc& rd, int64_t t, int c)
+{
+    const int rc = rd.flip ? rd.nchan - 1 - c : c;
+    const uint8_t* row = rd.raw + t * rd.rowbytes;
+    float x;
+    if (rd.nbits == 8) {
+        x = (float)row[rc];
+    } else if (rd.nbits == 4) {
+        const uint8_t b = row[rc >> 1];
+        const bool first = (rc & 1) == 0;
+        const bool hi = rd.nibble_hi_first ? first : !first;
+        x = (float)(hi ? (b >> 4) : (b & 15));
+    } else {
+        const uint8_t* p = row + 2 * rc;
+        const uint16_t u = rd.be16 ? (uint16_t)((p[0] << 8) | p[1]) : (uint16_t)((p[1] << 8) | p[0]);
+        x = (float)(int16_t)u;
+    }
+    if (rd.scl) x = x * rd.scl[rc];
+    if (rd.offs) x = x + rd.offs[rc];
+    if (rd.wts) x = x * rd.wts[rc];
+    return x;
+}
+
+// read block of spectrum t (spectra past N belong to the last block)
+__device__ __host__ __forceinline__ int64_t blk_of(const RawDesc& rd, int64_t t)
+{
+    const int64_t b = t / rd.blk;
+    return b < rd.nblk ? b : rd.nblk - 1;
+}
+
+__device__ __forceinline__ float pad_at(const RawDesc& rd, int64_t b, int c)
+{
+    return rd.pad ? rd.pad[b * rd.pad_stride + c] : 0.0f;
+}
+
+__device__ __forceinline__ bool zap_at(const RawDesc& rd, int64_t b, int c)
+{
+    return rd.zidx && rd.zrows[(int64_t)rd.zidx[b] * rd.nchan + c];
+}
+
+// The cleaned sample X'(t, c) of the per-block model (oracle/oracle.h), exactly.
+__device__ __forceinline__ float chan_value(const RawDesc& rd, int64_t t, int c)
+{
+    const int64_t b = blk_of(rd, t);
+    if (t >= rd.N || (rd.clipped && rd.clipped[t]) || zap_at(rd, b, c)) return pad_at(rd, b, c);
+    return raw_value(rd, t, c);
+}
+
+// PRESTO NEAREST_LONG, saturated to int16 (sub_round = 1).
+// Evaluated in float, exactly: for a float x, (double)x +- 0.5 is exact, so floor/ceil of
+// it is trunc(x) stepped by one when the (exact) fraction x - trunc(x) reaches +-0.5.
+__device__ __forceinline__ int16_t quant_i16(float x)
+{
+    const float t = truncf(x);
+    const float f = x - t;
+    float r = x >= 0.0f ? (f >= 0.5f ? t + 1.0f : t) : (f <= -0.5f ? t - 1.0f : t);
+    r = fminf(fmaxf(r, -32768.0f), 32767.0f);
+    return (int16_t)(int)r;
+}
+
+// prepsubband's `(short)(infloat + 0.5)` as x86-64 evaluates it (sub_round = 0): the double
+// x + 0.5 truncated to int32 (cvttsd2si; out of range -> 0x80000000), low 16 bits kept.
+__device__ __forceinline__ int16_t presto_short(float x)
+{
+    const double y = (double)x + 0.5;
+    const int32_t i = (y > -2147483649.0 && y < 2147483648.0) ? (int32_t)y : (int32_t)0x80000000u;
+    return (int16_t)(uint16_t)(uint32_t)i;
+}
+
+__device__ __forceinline__ int16_t to_i16(float x, int sub_round)
+{
+    return sub_round == 0 ? presto_short(x) : quant_i16(x);
+}
+
+// Blocks b, b+8, b+16, ... share an XCD (round-robin dispatch; speed only, never
+// correctness): give each XCD a contiguous range of logical block ids (bijective).
+__device__ __forceinline__ int xcd_remap(int b, int nb)
+{
+    const int xcd = b & 7, q = nb >> 3, r = nb & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
+__device__ __forceinline__ int wave_max_i32(int v)
+{
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v = max(v, __shfl_xor(v, m, 64));
+    return v;
+}
+
+// Raise *addr to v.  Every wave of a pass targets the same word, and same-address atomics
+// serialise at the memory side, so read first (a stale value only costs an extra atomic;
+// atomicMax is monotone, so the result is exact) and publish only a new maximum.
+__device__ __forceinline__ void publish_max(int32_t* addr, int v)
+{
+    if (v <= 0) return;
+    const int cur = __hip_atomic_load(addr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v > cur) atomicMax(addr, v);
+}
+
+}  // namespace hd

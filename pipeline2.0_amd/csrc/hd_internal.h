@@ -8,7 +8,11 @@
 
 namespace hd {
 
-// Raw-sample decode parameters for stage 1 (all device pointers).
+// Raw-sample decode parameters for stage 1 (all device pointers).  The raw block is read
+// in blocks of `blk` spectra (PRESTO's read unit, one PSRFITS subint): per block, an rfifind
+// zap row (mask.c check_mask of the block) and the pad values in force (clip_times' running
+// channel levels when clipping, else the initial pad values); spectra clip_times replaced
+// read as the block's pad values, and spectra past N as the last block's.
 struct RawDesc {
     const uint8_t* raw;       // [N][rowbytes], file layout
     int64_t N;
@@ -16,15 +20,18 @@ struct RawDesc {
     const float* scl;         // per raw channel or nullptr
     const float* offs;
     const float* wts;
-    const uint8_t* mask;      // [numint][nchan] ascending channels or nullptr
-    int32_t numint, ptsperint;
-    const float* padvals;     // per ascending channel or nullptr
+    int32_t blk, nblk;        // read blocks: nblk = ceil(N / blk)
+    const int32_t* zidx;      // [nblk] row of zrows zapped in the block, or nullptr (no mask)
+    const uint8_t* zrows;     // [rows][nchan] ascending channels, 1 = zapped
+    const float* pad;         // [nblk][nchan] (pad_stride = nchan) or [1][nchan] (stride 0), or nullptr (0)
+    int32_t pad_stride;
+    const uint8_t* clipped;   // [N] 1 = spectrum replaced by clip_times, or nullptr
 };
 
 struct Stage1Args {
     RawDesc rd;
     const int32_t* idispdt;   // [nchan]
-    int32_t nsub, cps, ds, ds_mode, sub_dtype, maxdelay;
+    int32_t nsub, cps, ds, ds_mode, sub_dtype, sub_round, maxdelay;
     int64_t nds;              // output samples per subband
     int64_t out_stride;       // elements
     void* out;                // [nsub][out_stride]
@@ -38,7 +45,7 @@ constexpr int kMaxPass = 32;
 struct Stage1Multi {
     RawDesc rd;
     int32_t npass;
-    int32_t nsub, cps, ds, ds_mode, sub_dtype;
+    int32_t nsub, cps, ds, ds_mode, sub_dtype, sub_round;
     int64_t nds, out_stride;
     int32_t sg;               // subbands per workgroup (block = 64*sg threads)
     int32_t to;               // output samples per tile
@@ -47,7 +54,8 @@ struct Stage1Multi {
     int32_t W;                // 8-bit integer path: LDS dwords per channel row (>= S + dmax)
     int32_t two_ok;           // tiles straddling one mask-interval boundary are not special
     int32_t probe;            // profiling only: bit0 skip subband formation, bit1 skip fill
-    double tie_eps;           // 8-bit integer path: bound on |float fold - exact sum| (masked channels)
+    double tie_eps;           // 8-bit integer path: margin the rounding of a masked subband's pad
+                              // constant needs (float-fold error, plus the /ds rounding in mean mode)
     int32_t ntiles, ngroups;
     const int32_t* dly[kMaxPass];   // per-pass idispdt [nchan]
     void* out[kMaxPass];            // per-pass subbands [nsub][out_stride]
@@ -118,6 +126,34 @@ hipError_t launch_stage2_direct(const Stage2Args& a, hipStream_t st);
 hipError_t launch_stage2_lds(const Stage2Args& a, int q, hipStream_t st);
 hipError_t launch_pad(float* out, int64_t out_stride, int numdms, int64_t nds, int64_t numout,
                       const double* partial, int ntiles, int pad_mode, hipStream_t st);
+
+// ---- PRESTO clip_times on the device (hd_clip.hip) ----
+// Scratch of one raw block's clip statistics; device pointers, sized by the host.
+struct ClipArgs {
+    RawDesc rd;               // rd.clipped / rd.pad are outputs here
+    float clip_sigma;
+    const uint8_t* allzap;    // [nblk] block fully masked (clip_times skipped), or nullptr
+    const float* padvals0;    // [nchan] initial pad values (determine_padvals) or nullptr (0)
+    float* zdm;               // [N] zero-DM series (channel-order float fold)
+    uint8_t* good;            // [N] within 0.7..1.3 x the block median
+    int32_t* numgood;         // [nblk]
+    double* bavg;             // [nblk] avg_var mean of the good points
+    double* bstd;             // [nblk] sqrt(avg_var variance)
+    double* chansum;          // [nblk][nchan] sum of the good spectra per channel
+    float* ravg;              // [nblk] running_avg after the block
+    float* trig;              // [nblk] clip_sigma * running_std after the block
+    int32_t* doclip;          // [nblk] clip_times ran on the block
+    uint8_t* clipped;         // [N] out
+    float* pad;               // [nblk][nchan] out: pad values in force for the block
+    int32_t* events;          // [N] out: clipped spectra (any order)
+    int32_t* nevents;         // device counter
+};
+int clip_max_block();
+hipError_t launch_clip(const ClipArgs& a, hipStream_t st);
+// Exact recomputation of the stage-1 outputs a clipped spectrum (events) or a read-block
+// boundary with changing pad values (the 8-bit integer path's straddling outputs) touches.
+hipError_t launch_stage1_fixup(const Stage1Multi& a, const int32_t* events, const int32_t* nevents,
+                               int boundaries, hipStream_t st);
 constexpr int64_t kRawTPad = 65536;   // zero rows after N in each channel-major raw row
 hipError_t launch_raw_transpose8(const uint8_t* raw, int64_t N, int32_t nchan, uint8_t* rawT, int64_t tstride,
                                  hipStream_t st);

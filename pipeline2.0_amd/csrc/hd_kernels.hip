@@ -8,91 +8,41 @@
 //                    packed int16 accumulation (v_pk_add_u16) widened to int32 every G
 //                    subbands (G from the pass's max |subband|, so no wrap is possible)
 //                    (prepsubband -lodm/-dmstep/-numdms; PALFA2_presto_search.py:514-520)
-//   k_pad            per-DM mean (fixed-order reduction of per-tile partials) fill of
-//                    samples [N/ds, numout)
+//   k_pad            first-DM (prepsubband) or per-DM mean (reduction of per-tile partials,
+//                    exact for int16 subbands) fill of samples [N/ds, numout)
 //   k_synth          synthetic beam, bit-identical to the host generator
 //
 // Arithmetic contract with the oracle (oracle/prepsubband_oracle.c): float sums in the
 // same order from 0.0f, no FP contraction (built with -ffp-contract=off), correctly
 // rounded division; int16 subbands make every stage-2 sum an exact integer, so any
 // summation order (including the packed int16 one) is bit-identical.
-#include "hd_internal.h"
+#include "hd_device.h"
+
+#include <map>
+#include <mutex>
 
 namespace hd {
+
+// The dynamic-LDS limit is a per-device property of a kernel: remember per (kernel,
+// device) what was granted, so contexts on several GPUs in one process each get it.
+hipError_t set_max_lds(const void* fn, int bytes)
+{
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    static std::mutex mu;
+    static std::map<std::pair<const void*, int>, int> granted;
+    std::lock_guard<std::mutex> lock(mu);
+    int& have = granted[{fn, dev}];
+    if (have >= bytes) return hipSuccess;
+    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess) have = bytes;
+    return e;
+}
 
 // ------------------------------------------------------------------------------------
 // stage 1
 // ------------------------------------------------------------------------------------
-
-__device__ __forceinline__ float raw_value(const RawDesc& rd, int64_t t, int c)
-{
-    const int rc = rd.flip ? rd.nchan - 1 - c : c;
-    const uint8_t* row = rd.raw + t * rd.rowbytes;
-    float x;
-    if (rd.nbits == 8) {
-        x = (float)row[rc];
-    } else if (rd.nbits == 4) {
-        const uint8_t b = row[rc >> 1];
-        const bool first = (rc & 1) == 0;
-        const bool hi = rd.nibble_hi_first ? first : !first;
-        x = (float)(hi ? (b >> 4) : (b & 15));
-    } else {
-        const uint8_t* p = row + 2 * rc;
-        const uint16_t u = rd.be16 ? (uint16_t)((p[0] << 8) | p[1]) : (uint16_t)((p[1] << 8) | p[0]);
-        x = (float)(int16_t)u;
-    }
-    if (rd.scl) x = x * rd.scl[rc];
-    if (rd.offs) x = x + rd.offs[rc];
-    if (rd.wts) x = x * rd.wts[rc];
-    return x;
-}
-
-__device__ __forceinline__ float chan_value(const RawDesc& rd, int64_t t, int c)
-{
-    if (t >= rd.N) return rd.padvals ? rd.padvals[c] : 0.0f;
-    if (rd.mask && rd.ptsperint > 0) {
-        const int64_t iv = t / rd.ptsperint;
-        if (iv < rd.numint && rd.mask[iv * rd.nchan + c]) return rd.padvals ? rd.padvals[c] : 0.0f;
-    }
-    return raw_value(rd, t, c);
-}
-
-// PRESTO NEAREST_LONG, saturated to int16.
-// Evaluated in float, exactly: for a float x, (double)x +- 0.5 is exact, so floor/ceil of
-// it is trunc(x) stepped by one when the (exact) fraction x - trunc(x) reaches +-0.5.
-__device__ __forceinline__ int16_t quant_i16(float x)
-{
-    const float t = truncf(x);
-    const float f = x - t;
-    float r = x >= 0.0f ? (f >= 0.5f ? t + 1.0f : t) : (f <= -0.5f ? t - 1.0f : t);
-    r = fminf(fmaxf(r, -32768.0f), 32767.0f);
-    return (int16_t)(int)r;
-}
-
-// Blocks b, b+8, b+16, ... share an XCD (round-robin dispatch; speed only, never
-// correctness): give each XCD a contiguous range of logical block ids (bijective).
-__device__ __forceinline__ int xcd_remap(int b, int nb)
-{
-    const int xcd = b & 7, q = nb >> 3, r = nb & 7;
-    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
-}
-
-__device__ __forceinline__ int wave_max_i32(int v)
-{
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v = max(v, __shfl_xor(v, m, 64));
-    return v;
-}
-
-// Raise *addr to v.  Every wave of a pass targets the same word, and same-address atomics
-// serialise at the memory side, so read first (a stale value only costs an extra atomic;
-// atomicMax is monotone, so the result is exact) and publish only a new maximum.
-__device__ __forceinline__ void publish_max(int32_t* addr, int v)
-{
-    if (v <= 0) return;
-    const int cur = __hip_atomic_load(addr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (v > cur) atomicMax(addr, v);
-}
 
 __global__ __launch_bounds__(256) void k_stage1_direct(Stage1Args a)
 {
@@ -113,7 +63,7 @@ __global__ __launch_bounds__(256) void k_stage1_direct(Stage1Args a)
         }
         if (a.ds_mode == 1) acc = acc / (float)a.ds;
         if (a.sub_dtype == 0) {
-            const int16_t q = quant_i16(acc);
+            const int16_t q = to_i16(acc, a.sub_round);
             ((int16_t*)a.out)[(int64_t)s * a.out_stride + tp] = q;
             amax = q < 0 ? -(int)q : (int)q;
         } else {
@@ -147,12 +97,13 @@ hipError_t launch_stage1_direct(const Stage1Args& a, hipStream_t st)
 //         are wave-uniform registers; lane l owns outputs l, l+64, ...  For every pass the
 //         decoded samples are summed in the oracle's order (k outer, channel inner, from
 //         0.0f), quantised and stored coalesced.
-// Mask: on real data a tile (<= ~1.5k spectra) lies inside one rfifind interval
-// (ptsperint ~ 32k), so each channel is either zapped for the whole tile (its samples are
-// the constant pad value: one add, no LDS read) or not: mode FAST.  Tiles that straddle an
-// interval boundary (mode TWO: per-row select between two flags), tiny test intervals
-// (mode GEN: per-row interval table) and the last tile (reads past the end = pad) take
-// per-sample paths.
+// Mask: zap sets and pad values are per read block (blk spectra, PRESTO's subint).  A tile
+// inside one block has, per channel, either zapped samples for the whole tile (the block's
+// constant pad value: one add) or none: mode FAST.  Tiles that straddle one block boundary
+// (mode TWO: per-row select between the two blocks' flags and pads), tiles over >= 3 blocks
+// (mode GEN: per-row block table) and the last tile (reads past the end = the last block's
+// pad) take per-sample paths.  Clipped spectra are not handled here: the fixup kernel
+// (hd_clip.hip) recomputes every output they touch.
 
 constexpr int kModeFast = 0, kModeTwo = 1, kModeGen = 2, kModeClean = 3;
 
@@ -178,8 +129,10 @@ template <int CPS>
 struct SubState {
     int off[CPS];      // LDS byte offset of (row 0 + delay, channel) for this channel
     int dly[CPS];      // channel delay (rows)
-    float scl[CPS], offs[CPS], wts[CPS], pad[CPS];
-    int zap[CPS];      // FAST: 1 = whole tile zapped;  TWO: bit0 first interval, bit1 second
+    float scl[CPS], offs[CPS], wts[CPS];
+    float pad0[CPS], pad1[CPS];   // pad values of the tile's first / second block
+    int zap[CPS];      // FAST: 1 = whole tile zapped;  TWO: bit0 first block, bit1 second;
+                       // GEN: the channel index (per-row lookups)
 };
 
 // One decoded, calibrated, masked sample of channel cc at tile row jrow + k (+ delay).
@@ -198,20 +151,17 @@ __device__ __forceinline__ float s1_sample(const Stage1Multi& a, const uint8_t* 
         x = x * st.wts[cc];
     }
     if (MODE == kModeFast) {
-        x = st.zap[cc] ? st.pad[cc] : x;
+        x = st.zap[cc] ? st.pad0[cc] : x;
     } else if (MODE == kModeTwo) {
         const int row = jk + st.dly[cc];
-        const int bit = row < brow ? 1 : 2;
-        x = (st.zap[cc] & bit) ? st.pad[cc] : x;
+        const bool second = row >= brow;
+        x = (st.zap[cc] & (second ? 2 : 1)) ? (second ? st.pad1[cc] : st.pad0[cc]) : x;
     } else if (MODE == kModeGen) {
         const int row = jk + st.dly[cc];
-        const int iv = livr[row];
-        if (a.rd.mask && iv < a.rd.numint && a.rd.mask[(int64_t)iv * a.rd.nchan + st.zap[cc]]) x = st.pad[cc];
+        const int b = livr[row];
+        const int c = st.zap[cc];
+        if ((TAIL && row >= rows_valid) || zap_at(a.rd, b, c)) x = pad_at(a.rd, b, c);
     }   // kModeClean: no mask logic at all
-    if (TAIL) {
-        const int row = jk + st.dly[cc];
-        x = row >= rows_valid ? st.pad[cc] : x;
-    }
     return x;
 }
 
@@ -246,7 +196,7 @@ __device__ __forceinline__ void form_outputs(const Stage1Multi& a, const uint8_t
         }
         const int64_t tp0 = tO0 + j0, tp1 = tO0 + j1;
         if (a.sub_dtype == 0) {
-            const int16_t q0 = quant_i16(acc0), q1 = quant_i16(acc1);
+            const int16_t q0 = to_i16(acc0, a.sub_round), q1 = to_i16(acc1, a.sub_round);
             int16_t* o = (int16_t*)a.out[p] + (int64_t)s * a.ostride[p];
             o[tp0] = q0;
             amax = max(amax, q0 < 0 ? -(int)q0 : (int)q0);
@@ -263,15 +213,15 @@ __device__ __forceinline__ void form_outputs(const Stage1Multi& a, const uint8_t
 }
 
 // A tile is "special" when it is the last one (reads past the end of the data) or its
-// rows straddle an rfifind interval boundary.  The hot kernel (SPECIAL = false) skips those
+// rows straddle a masked read-block boundary.  The hot kernel (SPECIAL = false) skips those
 // tiles and runs only the CLEAN / FAST paths, which keeps its register footprint at two
 // 8-wave workgroups per CU; the few special tiles (host-built list) get a second launch.
 __device__ __host__ __forceinline__ bool s1_special(const Stage1Multi& a, int64_t tR0, int rows)
 {
     if (tR0 + rows > a.rd.N) return true;
-    if (a.rd.mask) {
-        const int64_t iv0 = tR0 / a.rd.ptsperint, iv1 = (tR0 + rows - 1) / a.rd.ptsperint;
-        if (iv1 > iv0 + (a.two_ok ? 1 : 0)) return true;   // the integer path takes two-interval tiles
+    if (a.rd.zidx) {
+        const int64_t b0 = tR0 / a.rd.blk, b1 = (tR0 + rows - 1) / a.rd.blk;
+        if (b1 > b0 + (a.two_ok ? 1 : 0)) return true;   // the integer path takes two-block tiles
     }
     return false;
 }
@@ -298,19 +248,19 @@ void k_stage1_tiled(Stage1Multi a, const int* __restrict__ special_tiles)
     int* livr = (int*)(smem + ((rows * a.rs + 15) & ~15));
 
     // ---- tile mode (uniform)
-    int mode = kModeFast;
-    int64_t iv0 = 0;
-    int brow = 0;
-    if (a.rd.mask) {
-        iv0 = tR0 / a.rd.ptsperint;
-        const int64_t iv_last = (tR0 + rows - 1) / a.rd.ptsperint;
-        brow = (int)min((iv0 + 1) * a.rd.ptsperint - tR0, (int64_t)rows);
-        mode = iv_last == iv0 ? kModeFast : (iv_last == iv0 + 1 ? kModeTwo : kModeGen);
-        if (SPECIAL && mode == kModeGen)
-            for (int r = threadIdx.x; r < rows; r += blockDim.x) livr[r] = (int)((tR0 + r) / a.rd.ptsperint);
-    }
     const int rows_valid = (int)min(a.rd.N - tR0, (int64_t)rows);
     const bool tail = rows_valid < rows;
+    int mode = kModeFast;
+    const int64_t b0 = blk_of(a.rd, tR0);
+    int brow = rows;
+    if (a.rd.zidx) {
+        const int64_t b_last = (tR0 + rows - 1) / a.rd.blk;
+        brow = (int)min((b0 + 1) * a.rd.blk - tR0, (int64_t)rows);
+        mode = b_last == b0 ? kModeFast : (b_last == b0 + 1 ? kModeTwo : kModeGen);
+    }
+    if (SPECIAL && tail) mode = kModeGen;          // rows past N read the last block's pads
+    if (SPECIAL && mode == kModeGen)
+        for (int r = threadIdx.x; r < rows; r += blockDim.x) livr[r] = (int)blk_of(a.rd, tR0 + r);
 
     // ---- fill: VW-byte global loads, dword LDS stores
     {
@@ -356,19 +306,19 @@ void k_stage1_tiled(Stage1Multi a, const int* __restrict__ special_tiles)
             st.offs[cc] = a.rd.offs ? a.rd.offs[rc] : 0.0f;
             st.wts[cc] = a.rd.wts ? a.rd.wts[rc] : 1.0f;
         }
-        st.pad[cc] = a.rd.padvals ? a.rd.padvals[c] : 0.0f;
+        st.pad0[cc] = pad_at(a.rd, b0, c);
+        st.pad1[cc] = pad_at(a.rd, min(b0 + 1, (int64_t)a.rd.nblk - 1), c);
         int z = 0;
-        if (a.rd.mask) {
-            if (mode == kModeGen) {
-                z = c;   // GEN mode looks the mask up per row; keep the channel index here
-            } else {
-                const int z0 = iv0 < a.rd.numint ? a.rd.mask[iv0 * a.rd.nchan + c] : 0;
-                const int z1 = iv0 + 1 < a.rd.numint ? a.rd.mask[(iv0 + 1) * a.rd.nchan + c] : 0;
-                z = mode == kModeFast ? z0 : (z0 ? 1 : 0) | (z1 ? 2 : 0);
-            }
+        if (mode == kModeGen) {
+            z = c;   // GEN mode looks the mask up per row; keep the channel index here
+            any_zap = 1;
+        } else if (a.rd.zidx) {
+            const int z0 = zap_at(a.rd, b0, c);
+            const int z1 = mode == kModeTwo && zap_at(a.rd, b0 + 1, c);
+            z = mode == kModeFast ? z0 : (z0 ? 1 : 0) | (z1 ? 2 : 0);
+            any_zap |= z;
         }
         st.zap[cc] = z;
-        any_zap |= z;
     }
     const int lrc0 = a.rd.flip ? G - 1 - cl0 : cl0;   // local raw index of channel cc=0
     int pmax = 0;                                      // lane p: max |subband| of pass p
@@ -393,12 +343,7 @@ void k_stage1_tiled(Stage1Multi a, const int* __restrict__ special_tiles)
             else
                 form_outputs<NBITS, CPS, CALIB, kModeGen, false>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax);
         } else {
-            if (mode == kModeFast)
-                form_outputs<NBITS, CPS, CALIB, kModeFast, true>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax);
-            else if (mode == kModeTwo)
-                form_outputs<NBITS, CPS, CALIB, kModeTwo, true>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax);
-            else
-                form_outputs<NBITS, CPS, CALIB, kModeGen, true>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax);
+            form_outputs<NBITS, CPS, CALIB, kModeGen, true>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax);
         }
         if (a.sub_dtype == 0) {
             amax = wave_max_i32(amax);
@@ -461,7 +406,7 @@ static hipError_t set_lds_cps(int bytes)
                           (const void*)k_stage1_tiled<NBITS, CPS, CALIB, 4, false>,
                           (const void*)k_stage1_tiled<NBITS, CPS, CALIB, 4, true>};
     for (const void* f : fns) {
-        hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+        hipError_t e = set_max_lds(f, bytes);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
@@ -548,14 +493,8 @@ int stage1_q8_quarter_rows(int ds)
     }
 }
 
-__device__ __forceinline__ float q8_finish(const Stage1Multi& a, uint32_t v)
-{
-    float x = (float)v;
-    if (a.ds_mode == 1) x = x / (float)a.ds;
-    return x;
-}
-
-// Store the 4 quarter outputs of quarter-position j (integral: exact sums qv; else qf).
+// Store the 4 quarter outputs of quarter-position j: integral -> the exact packed sums qv
+// (each already holding its pad constant, see k_stage1_q8), else the float folds qf.
 template <int DS>
 __device__ __forceinline__ void q8_store(const Stage1Multi& a, int p, int s, int64_t tO0, int j,
                                          const uint32_t* qv, const float* qf, bool integral, int& amax)
@@ -566,15 +505,19 @@ __device__ __forceinline__ void q8_store(const Stage1Multi& a, int p, int s, int
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             int16_t v;
-            if (integral && a.ds_mode == 0) v = (int16_t)qv[q];     // < 32768 (host check)
-            else v = quant_i16(integral ? q8_finish(a, qv[q]) : qf[q]);
+            if (integral) v = (int16_t)(a.ds_mode == 1 ? qv[q] / (uint32_t)DS : qv[q]);   // < 32768 (host check)
+            else v = to_i16(qf[q], a.sub_round);
             o[q * JQ] = v;
             amax = max(amax, v < 0 ? -(int)v : (int)v);
         }
     } else {
         float* o = (float*)a.out[p] + (int64_t)s * a.ostride[p] + tO0 + j;
 #pragma unroll
-        for (int q = 0; q < 4; q++) o[q * JQ] = integral ? q8_finish(a, qv[q]) : qf[q];
+        for (int q = 0; q < 4; q++) {
+            float x = integral ? (float)qv[q] : qf[q];
+            if (integral && a.ds_mode == 1) x = x / (float)DS;
+            o[q * JQ] = x;
+        }
     }
 }
 
@@ -704,64 +647,75 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
     const int s = g * a.sg + sl;
     const int cl0 = sl * CPS;
     int lrb[CPS];
-    float pad[CPS];
-    // rfifind mask: the tile lies in interval iv0, or straddles iv0 | iv0+1 at row brow
+    float pad0[CPS], pad1[CPS];
+    // read blocks: the tile lies in block b0, or straddles b0 | b0+1 at row brow
     uint32_t z0 = 0, z1 = 0;
     int brow = 1 << 30;
-    int64_t iv0 = 0;
-    if (a.rd.mask) {
-        iv0 = tR0 / a.rd.ptsperint;
-        const int64_t b = (iv0 + 1) * a.rd.ptsperint - tR0;
+    const int64_t b0 = tR0 / a.rd.blk;
+    {
+        const int64_t b = (b0 + 1) * a.rd.blk - tR0;
         if (b < 4 * S + a.dmax) brow = (int)b;
     }
+    const int64_t b1 = brow < (1 << 30) ? b0 + 1 : b0;
 #pragma unroll
     for (int cc = 0; cc < CPS; cc++) {
         const int c = c0 + cl0 + cc;
         const int lr = a.rd.flip ? G - 1 - (cl0 + cc) : cl0 + cc;
         lrb[cc] = lr * W;
-        pad[cc] = a.rd.padvals ? a.rd.padvals[c] : 0.0f;
-        if (a.rd.mask) {
-            if (iv0 < a.rd.numint && a.rd.mask[iv0 * a.rd.nchan + c]) z0 |= 1u << cc;
-            if (brow < (1 << 30) && iv0 + 1 < a.rd.numint && a.rd.mask[(iv0 + 1) * a.rd.nchan + c]) z1 |= 1u << cc;
-        }
+        pad0[cc] = pad_at(a.rd, b0, c);
+        pad1[cc] = pad_at(a.rd, b1, c);
+        if (zap_at(a.rd, b0, c)) z0 |= 1u << cc;
+        if (zap_at(a.rd, b1, c)) z1 |= 1u << cc;
     }
-    if (brow >= (1 << 30)) z1 = z0;
     z0 = __builtin_amdgcn_readfirstlane(z0);
     z1 = __builtin_amdgcn_readfirstlane(z1);
     const uint32_t zany = z0 | z1, zall = z0 & z1, zsplit = z0 ^ z1;
     const int fz = zany ? __builtin_ctz(zany) : CPS;      // first channel off the integer path
     const uint32_t* lbase = lds + lane * DS;
-    const bool fast_out = a.sub_dtype == 0 && a.ds_mode == 0;
-    // Masked channels without a float fold.  With int16 sums (sum mode), a subband whose
-    // masked channels are masked for the whole tile outputs NEAREST(F), F = the oracle's float
-    // fold of integers and pad values.  The exact sum is R = I + DS*P (I: integer sum of the
-    // unmasked channels, P: sum of the masked channels' pads, exact in double) and
-    // |F - R| <= a.tie_eps (host bound on the fold's rounding), so while frac(DS*P) stays
-    // further than tie_eps from 1/2, NEAREST(F) = I + floor(DS*P + 1/2) (R >= 0): the integer
-    // path plus a per-tile constant.  Near-ties, split (two-interval) channels, negative pads
-    // and the other output modes take the exact float fold below.
-    int cadd = 0;
+    const bool mean = a.ds_mode == 1;
+    // Masked channels without a float fold.  With int16 output, a subband whose masked
+    // channels are the same in both blocks of the tile outputs Q(D(F)), F = the oracle's float
+    // fold of integers and pad values, D = /DS (mean) or identity (sum), Q = floor(x + 1/2)
+    // (F >= 0).  The exact sum is R = I + DS*P (I: integer sum of the unmasked channels, P:
+    // sum of the masked channels' pads of the block, exact in double) and |F - R| <= the
+    // host bound a.tie_eps (which also covers the rounding of /DS), so while frac(C),
+    // C = DS*P + D/2 with D = DS (mean) or 1 (sum), stays further than tie_eps from 0 and 1,
+    // Q(D(F)) = floor((I + floor(C)) / D): the integer sum plus a per-block constant, then an
+    // integer division (floor((n + f)/D) = floor(n/D) for integer n, 0 <= f < 1).  Integer
+    // pads make F exact (no margin needed).  Outputs whose rows straddle the block boundary
+    // mix both blocks' pads: when those differ (clipping on) the fixup kernel recomputes
+    // them.  Near-ties, split channels (masked in one block only), negative pads and f32
+    // output with masked channels take the exact float fold below.
+    const int Dh = mean ? DS / 2 : 0;                     // floor(D/2) for D = DS or 1
+    int cadd0 = a.sub_dtype == 0 ? Dh : 0, cadd1 = cadd0;
     bool intpath = zany == 0;
-    if (zany && zsplit == 0 && fast_out) {
-        double P = 0.0;
-        bool neg = false;
+    if (zany && zsplit == 0 && a.sub_dtype == 0) {
+        double P0 = 0.0, P1 = 0.0;
+        bool neg = false, integral = true;
 #pragma unroll
         for (int cc = 0; cc < CPS; cc++)
             if (zall & (1u << cc)) {
-                P += (double)pad[cc];
-                neg |= pad[cc] < 0.0f;
+                P0 += (double)pad0[cc];
+                P1 += (double)pad1[cc];
+                neg |= pad0[cc] < 0.0f || pad1[cc] < 0.0f;
+                integral &= pad0[cc] == floorf(pad0[cc]) && pad1[cc] == floorf(pad1[cc]);
             }
-        const double Rp = (double)DS * P;
-        const double fr = Rp - floor(Rp);
-        const double cd = floor(Rp + 0.5);
-        if (!neg && fabs(fr - 0.5) > a.tie_eps && cd + (double)(CPS * DS * 255) <= 32767.0) {
+        const double half = mean ? 0.5 * DS : 0.5;
+        const double C0 = (double)DS * P0 + half, C1 = (double)DS * P1 + half;
+        const double f0 = C0 - floor(C0), f1 = C1 - floor(C1);
+        const double m0 = fmin(f0, 1.0 - f0), m1 = fmin(f1, 1.0 - f1);
+        const double cap = mean ? 65535.0 : 32767.0;
+        if (!neg && (integral || (m0 > a.tie_eps && m1 > a.tie_eps)) &&
+            fmax(C0, C1) + (double)(CPS * DS * 255) <= cap) {
             intpath = true;
-            cadd = (int)cd;
+            cadd0 = (int)floor(C0);
+            cadd1 = (int)floor(C1);
         }
     }
     intpath = __builtin_amdgcn_readfirstlane((int)intpath) != 0;
-    cadd = __builtin_amdgcn_readfirstlane(cadd);
-    const uint32_t cpack = (uint32_t)cadd * 0x00010001u;
+    cadd0 = __builtin_amdgcn_readfirstlane(cadd0);
+    cadd1 = __builtin_amdgcn_readfirstlane(cadd1);
+    const bool fast_out = a.sub_dtype == 0 && !mean;      // int16 sums stored as they are
     // channel delays of pass p live in lanes 0..CPS-1 of vd; pass p+1's are loaded while
     // pass p is formed, so no global-load latency sits at the head of a pass
     // (unconditional, clamped loads: a branch around them would cost a vmcnt(0) drain)
@@ -773,16 +727,29 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
     for (int p = 0; p < npass; p++) {
         const int vd_next = a.dly[min(p + 1, a.npass - 1)][dlane];
         int dl[CPS];
+        int dmx = 0;
 #pragma unroll
-        for (int cc = 0; cc < CPS; cc++) dl[cc] = __builtin_amdgcn_readlane(vd, cc);
+        for (int cc = 0; cc < CPS; cc++) {
+            dl[cc] = __builtin_amdgcn_readlane(vd, cc);
+            dmx = max(dmx, dl[cc]);
+        }
         int amax = 0;
         if (intpath) {
             uint32_t ae[M], ao[M];
 #pragma unroll
-            for (int m = 0; m < M; m++) ae[m] = ao[m] = cpack;
+            for (int m = 0; m < M; m++) {
+                // quarter q of output j: block b1's constant once its last row reaches brow
+                const int lastrow = (lane + 64 * m) * DS + DS - 1 + dmx;
+                const uint32_t k0 = (uint32_t)(lastrow < brow ? cadd0 : cadd1);
+                const uint32_t k1 = (uint32_t)(lastrow + S < brow ? cadd0 : cadd1);
+                const uint32_t k2 = (uint32_t)(lastrow + 2 * S < brow ? cadd0 : cadd1);
+                const uint32_t k3 = (uint32_t)(lastrow + 3 * S < brow ? cadd0 : cadd1);
+                ae[m] = k0 | (k2 << 16);
+                ao[m] = k1 | (k3 << 16);
+            }
 #pragma unroll
             for (int cc = 0; cc < CPS; cc++) {
-                if (zall & (1u << cc)) continue;       // masked channel: its pads are in cpack
+                if (zall & (1u << cc)) continue;       // masked channel: its pads are in the constants
                 const uint32_t* b = lbase + lrb[cc] + dl[cc];
 #pragma unroll
                 for (int m = 0; m < M; m++)
@@ -826,8 +793,8 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
                     f32x2 sk01 = {0.0f, 0.0f}, sk23 = {0.0f, 0.0f};   // quarters (0,1), (2,3): v_pk_add_f32
 #pragma unroll
                     for (int cc = 0; cc < CPS; cc++) {
+                        const uint32_t x = lbase[lrb[cc] + dl[cc] + m * 64 * DS + k];
                         if (cc < fz) {
-                            const uint32_t x = lbase[lrb[cc] + dl[cc] + m * 64 * DS + k];
                             pe += x & 0x00FF00FFu;
                             po += __builtin_amdgcn_perm(0u, x, 0x0c030c01u);
                         } else {
@@ -835,25 +802,20 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
                                 sk01 = f32x2{(float)(pe & 0xFFFFu), (float)(po & 0xFFFFu)};
                                 sk23 = f32x2{(float)(pe >> 16), (float)(po >> 16)};
                             }
-                            if (zall & (1u << cc)) {
-                                const f32x2 pp = {pad[cc], pad[cc]};
-                                sk01 += pp;
-                                sk23 += pp;
-                            } else {
-                                const uint32_t x = lbase[lrb[cc] + dl[cc] + m * 64 * DS + k];
-                                f32x2 v01 = {(float)(x & 0xFFu), (float)((x >> 8) & 0xFFu)};
-                                f32x2 v23 = {(float)((x >> 16) & 0xFFu), (float)(x >> 24)};
-                                if (zsplit & (1u << cc)) {   // zapped on one side of the interval boundary
-                                    const bool zlo = (z0 >> cc) & 1;
-                                    const int rr = t + dl[cc];
-                                    if ((rr < brow) == zlo) v01.x = pad[cc];
-                                    if ((rr + S < brow) == zlo) v01.y = pad[cc];
-                                    if ((rr + 2 * S < brow) == zlo) v23.x = pad[cc];
-                                    if ((rr + 3 * S < brow) == zlo) v23.y = pad[cc];
-                                }
-                                sk01 += v01;
-                                sk23 += v23;
+                            f32x2 v01 = {(float)(x & 0xFFu), (float)((x >> 8) & 0xFFu)};
+                            f32x2 v23 = {(float)((x >> 16) & 0xFFu), (float)(x >> 24)};
+                            if (zany & (1u << cc)) {   // masked in one or both blocks: per-row block
+                                const int rr = t + dl[cc];
+                                const bool h0 = rr >= brow, h1 = rr + S >= brow, h2 = rr + 2 * S >= brow,
+                                           h3 = rr + 3 * S >= brow;
+                                const bool za = (z0 >> cc) & 1, zb = (z1 >> cc) & 1;
+                                if (h0 ? zb : za) v01.x = h0 ? pad1[cc] : pad0[cc];
+                                if (h1 ? zb : za) v01.y = h1 ? pad1[cc] : pad0[cc];
+                                if (h2 ? zb : za) v23.x = h2 ? pad1[cc] : pad0[cc];
+                                if (h3 ? zb : za) v23.y = h3 ? pad1[cc] : pad0[cc];
                             }
+                            sk01 += v01;
+                            sk23 += v23;
                         }
                     }
                     acc[0] += sk01.x;
@@ -861,7 +823,7 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
                     acc[2] += sk23.x;
                     acc[3] += sk23.y;
                 }
-                if (a.ds_mode == 1)
+                if (mean)
 #pragma unroll
                     for (int q = 0; q < 4; q++) acc[q] = acc[q] / (float)DS;
                 q8_store<DS>(a, p, s, tO0, lane + 64 * m, nullptr, acc, false, amax);
@@ -891,11 +853,8 @@ static hipError_t launch_q8_ds(const Stage1Multi& a, int vb, size_t lds, hipStre
 template <int CPS, int DS>
 static hipError_t set_lds_q8_ds(int bytes)
 {
-    hipError_t e = hipFuncSetAttribute((const void*)k_stage1_q8<CPS, DS, 8>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-    if (e == hipSuccess)
-        e = hipFuncSetAttribute((const void*)k_stage1_q8<CPS, DS, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                bytes);
+    hipError_t e = set_max_lds((const void*)k_stage1_q8<CPS, DS, 8>, bytes);
+    if (e == hipSuccess) e = set_max_lds((const void*)k_stage1_q8<CPS, DS, 4>, bytes);
     return e;
 }
 
@@ -1730,12 +1689,9 @@ size_t stage2_ring_lds_bytes(int wstride, int npw, int nbp, int nsub)
 template <int Q, int R>
 static hipError_t launch_ring_qr(const Stage2Args& a, int nyblk, hipStream_t st)
 {
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_stage2_ring<Q, R>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           160 * 1024);
+    {
+        const hipError_t e = set_max_lds((const void*)k_stage2_ring<Q, R>, 160 * 1024);
         if (e != hipSuccess) return e;
-        attr = true;
     }
     const unsigned ntiles = (unsigned)((a.nvalid + 256 * R - 1) / (256 * R));
     hipLaunchKernelGGL((k_stage2_ring<Q, R>), dim3(ntiles, (unsigned)nyblk), dim3(1024),
@@ -2010,12 +1966,9 @@ size_t stage2_pair_lds_bytes(int wstride, int npw, int nbp, int nsub, int umax)
 template <int Q, int R>
 static hipError_t launch_pair_qr(const Stage2Args& a, int nyblk, hipStream_t st)
 {
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_stage2_pair<Q, R>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           160 * 1024);
+    {
+        const hipError_t e = set_max_lds((const void*)k_stage2_pair<Q, R>, 160 * 1024);
         if (e != hipSuccess) return e;
-        attr = true;
     }
     const unsigned ntiles = (unsigned)((a.nvalid + 256 * R - 1) / (256 * R));
     const unsigned nx = a.nwg > 0 && (unsigned)a.nwg < ntiles ? (unsigned)a.nwg : ntiles;
@@ -2222,12 +2175,9 @@ size_t stage2_wide2_lds_bytes(int wstride, int sc, int nsub) { return (size_t)sc
 template <int Q, int R, int SC>
 static hipError_t launch_wide2_qrs(const Stage2Args& a, int nw, int nyblk, hipStream_t st)
 {
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_stage2_wide2<Q, R, SC>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    {
+        const hipError_t e = set_max_lds((const void*)k_stage2_wide2<Q, R, SC>, 160 * 1024);
         if (e != hipSuccess) return e;
-        attr = true;
     }
     const unsigned ntiles = (unsigned)((a.nvalid + 256 * R - 1) / (256 * R));
     hipLaunchKernelGGL((k_stage2_wide2<Q, R, SC>), dim3(ntiles, (unsigned)nyblk), dim3((unsigned)(64 * nw)),
@@ -2285,12 +2235,9 @@ size_t stage2_wide_lds_bytes(int wstride, int sc) { return (size_t)2 * sc * 4 * 
 template <int Q, int R, int SC>
 static hipError_t launch_wide_qrs(const Stage2Args& a, int nw, int nyblk, hipStream_t st)
 {
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_stage2_wide<Q, R, SC>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    {
+        const hipError_t e = set_max_lds((const void*)k_stage2_wide<Q, R, SC>, 160 * 1024);
         if (e != hipSuccess) return e;
-        attr = true;
     }
     const unsigned ntiles = (unsigned)((a.nvalid + 256 * R - 1) / (256 * R));
     hipLaunchKernelGGL((k_stage2_wide<Q, R, SC>), dim3(ntiles, (unsigned)nyblk), dim3((unsigned)(64 * nw)),
@@ -2402,16 +2349,18 @@ __global__ __launch_bounds__(256) void k_pad(float* out, int64_t out_stride, int
     __shared__ double red[256];
     __shared__ float padv;
     const int d = blockIdx.x;
+    // HD_PAD_DM0: every DM takes the first DM's mean (prepsubband's one `avg`)
+    const int dsrc = pad_mode == 2 ? 0 : d;
     double s = 0.0;
-    if (pad_mode == 0 && partial)
-        for (int i = threadIdx.x; i < ntiles; i += 256) s += partial[(int64_t)d * ntiles + i];
+    if (pad_mode != 1 && partial)
+        for (int i = threadIdx.x; i < ntiles; i += 256) s += partial[(int64_t)dsrc * ntiles + i];
     red[threadIdx.x] = s;
     __syncthreads();
     for (int w = 128; w >= 1; w >>= 1) {
         if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
         __syncthreads();
     }
-    if (threadIdx.x == 0) padv = (pad_mode == 0 && nds > 0) ? (float)(red[0] / (double)nds) : 0.0f;
+    if (threadIdx.x == 0) padv = (pad_mode != 1 && nds > 0) ? (float)(red[0] / (double)nds) : 0.0f;
     __syncthreads();
     const float v = padv;
     for (int64_t t = nds + threadIdx.x; t < numout; t += 256) out[(int64_t)d * out_stride + t] = v;

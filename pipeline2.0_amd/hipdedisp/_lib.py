@@ -21,7 +21,8 @@ HD_E_IO = -6
 
 HD_SUB_I16, HD_SUB_F32 = 0, 1
 HD_DS_SUM, HD_DS_MEAN = 0, 1
-HD_PAD_MEAN, HD_PAD_ZERO = 0, 1
+HD_PAD_MEAN, HD_PAD_ZERO, HD_PAD_DM0 = 0, 1, 2
+HD_ROUND_PRESTO, HD_ROUND_NEAREST = 0, 1
 HD_PASS_SUB_INPUT = 1
 
 ERROR_NAMES = {HD_E_INVAL: "HD_E_INVAL", HD_E_NODEV: "HD_E_NODEV", HD_E_HIP: "HD_E_HIP",
@@ -35,7 +36,8 @@ EXPORTED = [
     "hd_plan_get_delays", "hd_plan_sub_params", "hd_run_subband", "hd_get_subbands",
     "hd_set_subbands", "hd_run_dedisp", "hd_plan_last_ms", "hd_plan_set_variant",
     "hd_get_raw", "hd_plan_tables", "hd_run_subband_multi", "hd_push_raw_device", "hd_get_raw_device",
-    "hd_push_raw_file", "hd_set_streams", "hd_touch_raw",
+    "hd_push_raw_file", "hd_set_streams", "hd_touch_raw", "hd_stats_padvals", "hd_get_clean",
+    "hd_get_subbands_window", "hd_get_series",
 ]
 
 
@@ -54,7 +56,7 @@ class hd_opts(ctypes.Structure):
     _fields_ = [("sub_dtype", ctypes.c_int32), ("ds_mode", ctypes.c_int32),
                 ("pad_mode", ctypes.c_int32), ("nibble_hi_first", ctypes.c_int32),
                 ("be16", ctypes.c_int32), ("inf_roundtrip", ctypes.c_int32),
-                ("clip_sigma", ctypes.c_float), ("_pad0", ctypes.c_int32)]
+                ("clip_sigma", ctypes.c_float), ("sub_round", ctypes.c_int32)]
 
 
 class hd_pass(ctypes.Structure):
@@ -117,7 +119,9 @@ def load():
         "hd_touch_raw": (ctypes.c_int, [vp]),
         "hd_set_obs": (ctypes.c_int, [vp, P(hd_obs), P(hd_opts)]),
         "hd_set_chan_calib": (ctypes.c_int, [vp, f32p, f32p, f32p]),
-        "hd_set_mask": (ctypes.c_int, [vp, P(ctypes.c_uint8), i32, i32, f32p]),
+        "hd_set_mask": (ctypes.c_int, [vp, P(ctypes.c_uint8), i32, i32, ctypes.c_double, P(ctypes.c_uint8), f32p]),
+        "hd_stats_padvals": (ctypes.c_int, [f32p, i32, i32, f32p]),
+        "hd_get_clean": (ctypes.c_int, [vp, f32p, P(ctypes.c_uint8), P(ctypes.c_uint8), P(i64)]),
         "hd_push_raw": (ctypes.c_int, [vp, vp, i64, i64]),
         "hd_synth_device": (ctypes.c_int, [vp, P(hd_synth)]),
         "hd_synth_host": (ctypes.c_int, [P(hd_obs), P(hd_synth), i64, i64, vp]),
@@ -128,6 +132,8 @@ def load():
                                               P(ctypes.c_double), P(ctypes.c_int64)]),
         "hd_run_subband": (ctypes.c_int, [vp]),
         "hd_get_subbands": (ctypes.c_int, [vp, vp]),
+        "hd_get_subbands_window": (ctypes.c_int, [vp, i64, i64, vp]),
+        "hd_get_series": (ctypes.c_int, [vp, i32, i32, i64, i64, f32p]),
         "hd_set_subbands": (ctypes.c_int, [vp, vp]),
         "hd_run_dedisp": (ctypes.c_int, [vp, f32p]),
         "hd_plan_last_ms": (ctypes.c_int, [vp, f32p, f32p]),

@@ -51,19 +51,24 @@ class ObsParams:
 
 @dataclass
 class Opts:
-    """PRESTO-semantics switches; defaults mirror the reference's use."""
+    """PRESTO-semantics switches; defaults mirror the reference's use:
+    the stage-1 command (PALFA2_presto_search.py:506-511) passes no -noclip, so
+    prepsubband's default -clip 6 applies; downsampling averages, int16 subbands are
+    (short)(x + 0.5), padding is the first DM's running mean."""
     sub_dtype: int = _lib.HD_SUB_I16
-    ds_mode: int = _lib.HD_DS_SUM
-    pad_mode: int = _lib.HD_PAD_MEAN
+    ds_mode: int = _lib.HD_DS_MEAN
+    pad_mode: int = _lib.HD_PAD_DM0
     nibble_hi_first: bool = True
     be16: bool = True
     inf_roundtrip: bool = True
-    clip_sigma: float = 0.0
+    clip_sigma: float = 6.0
+    sub_round: int = _lib.HD_ROUND_PRESTO
 
     def to_c(self):
         return hd_opts(sub_dtype=self.sub_dtype, ds_mode=self.ds_mode, pad_mode=self.pad_mode,
                        nibble_hi_first=int(self.nibble_hi_first), be16=int(self.be16),
-                       inf_roundtrip=int(self.inf_roundtrip), clip_sigma=self.clip_sigma)
+                       inf_roundtrip=int(self.inf_roundtrip), clip_sigma=self.clip_sigma,
+                       sub_round=self.sub_round)
 
 
 @dataclass
@@ -103,6 +108,15 @@ def plan_tables(obs: "ObsParams", opts: "Opts", pp: "PassParams"):
                             off.ctypes.data_as(I32), ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)),
            "hd_plan_tables")
     return idd, off, (a.value, b.value, c.value)
+
+
+def stats_padvals(dataavg):
+    """determine_padvals [PRESTO-ext] from rfifind .stats interval averages [numint][numchan]
+    (hd_stats_padvals; host only)."""
+    a = np.ascontiguousarray(dataavg, dtype=np.float32)
+    out = np.zeros(a.shape[1], np.float32)
+    _check(_lib.load().hd_stats_padvals(_f32p(a), a.shape[0], a.shape[1], _f32p(out)), "hd_stats_padvals")
+    return out
 
 
 def _f32p(a):
@@ -160,15 +174,43 @@ class Engine:
         arrs = [None if a is None else np.ascontiguousarray(a, dtype=np.float32) for a in (scl, offs, wts)]
         self._chk(self._L.hd_set_chan_calib(self._ctx, *[_f32p(a) for a in arrs]), "hd_set_chan_calib")
 
-    def set_mask(self, mask=None, ptsperint=0, padvals=None):
-        m = None
+    def set_mask(self, mask=None, ptsperint=0, padvals=None, dtint=0.0, zapint=None):
+        """rfifind mask [numint][nchan] (the per-interval channel lists), applied per read
+        block with check_mask's rule; zapint [numint] marks zap_ints (None: full rows);
+        dtint = seconds per interval as stored (0: ptsperint * dt); padvals = initial pad
+        values (e.g. stats_padvals of the rfifind .stats)."""
+        m = zi = None
         numint = 0
+        u8p = ctypes.POINTER(ctypes.c_uint8)
         if mask is not None:
             mask = np.ascontiguousarray(mask, dtype=np.uint8)
             numint = mask.shape[0]
-            m = mask.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+            m = mask.ctypes.data_as(u8p)
+            if zapint is not None:
+                zapint = np.ascontiguousarray(zapint, dtype=np.uint8)
+                zi = zapint.ctypes.data_as(u8p)
         pv = None if padvals is None else np.ascontiguousarray(padvals, dtype=np.float32)
-        self._chk(self._L.hd_set_mask(self._ctx, m, numint, int(ptsperint), _f32p(pv)), "hd_set_mask")
+        self._chk(self._L.hd_set_mask(self._ctx, m, numint, int(ptsperint), float(dtint), zi, _f32p(pv)),
+                  "hd_set_mask")
+
+    def set_rfimask(self, rfimask, padvals=None):
+        """An RfiMask (formats.mask.read_mask) as prepsubband -mask applies it."""
+        self.set_mask(rfimask.bitmap, rfimask.ptsperint, padvals, rfimask.dtint, rfimask.zapint)
+
+    def get_clean(self):
+        """Per-block cleaning state of the current raw block: (pad [nblk][nchan] f32,
+        clipped [N] u8, zap [nblk][nchan] u8, nclipped) -- computes it if needed."""
+        o = self.obs
+        blk = min(o.nsblk if o.nsblk > 0 else o.N, o.N)
+        nblk = (o.N + blk - 1) // blk
+        pad = np.zeros((nblk, o.nchan), np.float32)
+        clipped = np.zeros(o.N, np.uint8)
+        zap = np.zeros((nblk, o.nchan), np.uint8)
+        n = ctypes.c_int64()
+        u8p = ctypes.POINTER(ctypes.c_uint8)
+        self._chk(self._L.hd_get_clean(self._ctx, _f32p(pad), clipped.ctypes.data_as(u8p), zap.ctypes.data_as(u8p),
+                                       ctypes.byref(n)), "hd_get_clean")
+        return pad, clipped, zap, n.value
 
     def push_raw(self, spectra, start=0):
         a = np.ascontiguousarray(spectra, dtype=np.uint8)
@@ -270,6 +312,21 @@ class Plan:
         out = np.empty((self.pp.nsub, self.nds), dtype=self._sub_dtype())
         self.eng._chk(self.eng._L.hd_get_subbands(self._p, out.ctypes.data_as(ctypes.c_void_p)),
                       "hd_get_subbands")
+        return out
+
+    def get_subbands_window(self, t0, count):
+        out = np.empty((self.pp.nsub, int(count)), dtype=self._sub_dtype())
+        self.eng._chk(self.eng._L.hd_get_subbands_window(self._p, int(t0), int(count),
+                                                         out.ctypes.data_as(ctypes.c_void_p)), "hd_get_subbands_window")
+        return out
+
+    def get_series(self, dm0=0, ndm=None, t0=0, count=None):
+        """Window of the device-resident series of the last run_dedisp: [ndm][count] f32."""
+        ndm = self.pp.numdms - dm0 if ndm is None else ndm
+        count = self.numout - t0 if count is None else count
+        out = np.empty((int(ndm), int(count)), dtype=np.float32)
+        self.eng._chk(self.eng._L.hd_get_series(self._p, int(dm0), int(ndm), int(t0), int(count), _f32p(out)),
+                      "hd_get_series")
         return out
 
     def set_subbands(self, sub):

@@ -9,7 +9,13 @@
 
 Exit status is 0 on success and 1 on failure, so timed_execute() (PALFA2_presto_search.py:
 95-139) raises PrestoError exactly as it does for a failing PRESTO binary.  Flags the
-reference never passes are rejected rather than ignored.
+reference never passes are rejected rather than ignored, except prepsubband's own
+-clip/-noclip (default -clip 6, as the reference's commands leave it) and -nobary.
+
+Barycentring: without -nobary PRESTO resamples the series to the barycentre with TEMPO,
+which is not available here.  The shim computes the delay tables at v/c = -baryv (a
+hipdedisp option; 0 by default, or $HIPDEDISP_BARYV) and writes topocentric series, and
+says so on stderr unless -nobary is given.
 """
 import argparse
 import glob
@@ -21,7 +27,7 @@ import numpy as np
 from .engine import Engine, ObsParams, Opts, PassParams, PrestoError
 from .formats import psrfits
 from .formats.inf import InfoData, read_inf
-from .formats.mask import read_mask
+from .formats.mask import mask_padvals, read_mask
 from .formats.series import read_subbands, write_dats, write_subbands
 
 
@@ -38,6 +44,9 @@ def parse(argv):
     ap.add_argument("-numout", type=int, default=0)
     ap.add_argument("-mask", type=str, default=None)
     ap.add_argument("-nobary", action="store_true")
+    ap.add_argument("-clip", type=float, default=6.0)
+    ap.add_argument("-noclip", action="store_true")
+    ap.add_argument("-baryv", type=float, default=float(os.environ.get("HIPDEDISP_BARYV", "0")))
     ap.add_argument("-o", dest="outfile", required=True)
     ap.add_argument("-device", type=int, default=int(os.environ.get("HIPDEDISP_DEVICE", "0")))
     ap.add_argument("infiles", nargs="+")
@@ -57,30 +66,39 @@ def _dm_strings(lodm, dmstep, numdms):
 
 
 def _mask_state(eng, maskfn, nchan):
+    """-mask M: the rfifind mask plus determine_padvals' pad values from <root>.stats."""
     if not maskfn:
         return
+    if not os.path.exists(maskfn):
+        raise PrestoError("rfifind mask %s does not exist" % maskfn)
     m = read_mask(maskfn)
     if m.numchan != nchan:
         raise PrestoError("mask has %d channels, data has %d" % (m.numchan, nchan))
-    side = maskfn + ".padvals"
-    pad = np.loadtxt(side, dtype=np.float32) if os.path.exists(side) else None
-    eng.set_mask(m.bitmap, m.ptsperint, pad)
+    eng.set_rfimask(m, mask_padvals(maskfn, nchan))
+
+
+def _opts(a, **kw):
+    return Opts(clip_sigma=0.0 if a.noclip else a.clip, **kw)
 
 
 def run(argv):
     a = parse(argv)
     files = _expand(a.infiles)
-    opts = Opts()
+    opts = _opts(a)
+    voverc = 0.0 if a.nobary else a.baryv
+    if not a.nobary:
+        sys.stderr.write("prepsubband (hipdedisp): no barycentric resampling (TEMPO unavailable); "
+                         "topocentric series, delays at v/c = %g\n" % voverc)
     if files[0].endswith(".fits") or a.psrfits:
         si = psrfits.SpectraInfo(files)
-        obs = si.obs_params(0.0)
+        obs = si.obs_params(voverc)
         nsub = a.nsub or obs.nchan
         base_info = InfoData(name="", telescope=si.telescope or "Arecibo", instrument=si.backend,
                              object=si.source or "Unknown", ra=si.ra_str, dec=si.dec_str,
                              observer=si.observer or "Unknown", mjd=float(si.start_MJD[0]))
         with Engine(a.device) as eng:
             if not a.sub and nsub == obs.nchan:
-                opts = Opts(sub_dtype=1)    # no .sub int16 round trip without -sub (:522-529)
+                opts = _opts(a, sub_dtype=1)    # no .sub int16 round trip without -sub (:522-529)
             eng.set_obs(obs, opts)
             scl, offs, wts = si.read_calib()
             if scl is not None or offs is not None or wts is not None:
@@ -121,7 +139,7 @@ def run(argv):
         if a.downsamp != 1:
             raise PrestoError("stage-2 -downsamp > 1 is not used by the reference (dd_downsamp = 1)")
         sobs = ObsParams(nchan=nsub, nbits=16, dt=sinfo.dt, lofreq=sinfo.freq, df=sinfo.chan_wid,
-                         N=sub.shape[1], nsblk=1, flip=False)
+                         N=sub.shape[1], nsblk=sub.shape[1], flip=False, voverc=voverc)
         with Engine(a.device) as eng:
             eng.set_obs(sobs, opts)
             p = eng.plan(PassParams(subdm=sinfo.dm, lodm=a.lodm, dmstep=a.dmstep, numdms=a.numdms, nsub=nsub,

@@ -8,8 +8,11 @@ Reference (pipeline2.0, lib/python/PALFA2_presto_search.py):
   :352-358  the two timers go to the .report
 
 `run_pass(job, ddplan, passnum, maskfilenm, tempdir)` replaces the body of :500-529 one for
-one: it leaves the same .dat/.inf files (and, with keep_subbands, the same .subNN/.sub.inf
-files) and returns (t_sub, t_dd) wall seconds, which it also adds to the job's timers.
+one: it creates <tempdir>/subbands as :500-503 does (the reference's own :608-611 removes or
+empties it after every pass), leaves the same .dat/.inf files (and, with keep_subbands, the
+same .subNN/.sub.inf files, which the reference moves to the workdir when it folds from
+subbands, fold_rawdata=False) and returns (t_sub, t_dd) wall seconds, which it also adds to
+the job's timers.
 Failures raise PrestoError, the reference's exception for a failed prepsubband.
 `dedisperse_job(job, per_dm=None)` is the whole loop of :494-537, calling `per_dm(job,
 dmstr, basenm)` where the reference runs single_pulse_search/realfft/accelsearch.
@@ -25,7 +28,7 @@ from . import plan as P
 from .engine import Engine, Opts, PassParams, PrestoError
 from .formats import psrfits
 from .formats.inf import InfoData
-from .formats.mask import read_mask
+from .formats.mask import mask_padvals, read_mask
 from .formats.series import write_dats, write_subbands
 
 
@@ -52,7 +55,10 @@ class DedispJob:
         self.nchan = si.num_channels
         self.samp_per_row = si.spectra_per_subint
         self.fctr = si.fctr
-        self.baryv = voverc                     # TEMPO barycentring is out of scope: -nobary equivalent
+        # average barycentric v/c (the reference's obs_info.baryv, :269-270, from TEMPO): it
+        # enters PRESTO's delay tables; the barycentric resampling of the output series needs
+        # TEMPO and is not performed -- 0 is prepsubband -nobary
+        self.baryv = voverc
         self.hostname = socket.gethostname()
         self.use_subbands = use_subbands
         self.keep_subbands = keep_subbands
@@ -82,27 +88,26 @@ class DedispJob:
         return self.engine
 
     def load_mask(self, maskfilenm):
+        """`-mask M` of the reference's commands: the rfifind mask (prepsubband fails when it
+        is missing, so this raises PrestoError) and the pad values determine_padvals derives
+        from the `.stats` next to it (zeros without one)."""
         if maskfilenm == self._mask_loaded:
             return
         eng = self.open_engine()
-        if maskfilenm and os.path.exists(maskfilenm):
+        if maskfilenm:
+            if not os.path.exists(maskfilenm):
+                raise PrestoError("rfifind mask %s does not exist" % maskfilenm)
             m = read_mask(maskfilenm)
             if m.numchan != self.nchan:
                 raise PrestoError("mask %s has %d channels, data %d" % (maskfilenm, m.numchan, self.nchan))
-            padvals = self._padvals(maskfilenm)
-            eng.set_mask(m.bitmap, m.ptsperint, padvals)
+            try:
+                padvals = mask_padvals(maskfilenm, self.nchan)
+            except ValueError as e:
+                raise PrestoError(str(e))
+            eng.set_rfimask(m, padvals)
         else:
             eng.set_mask(None, 0, None)
         self._mask_loaded = maskfilenm
-
-    def _padvals(self, maskfilenm):
-        """rfifind pad values [PRESTO-ext]: per-channel levels from <base>_rfifind.stats when
-        present; this build reads a plain-text side file `<mask>.padvals` (one float per
-        channel) if it exists, else uses 0 (mask row)."""
-        side = maskfilenm + ".padvals"
-        if os.path.exists(side):
-            return np.loadtxt(side, dtype=np.float32)
-        return None
 
     def close(self):
         if self.engine is not None:
@@ -144,12 +149,12 @@ def run_pass(job, ddplan, passnum, maskfilenm, tempdir):
     job.load_mask(maskfilenm)
     pp = pass_params(job, ddplan, passnum)
     plan = eng.plan(pp)
+    os.makedirs(os.path.join(tempdir, "subbands"), exist_ok=True)     # :500-503
     try:
         t0 = time.time()
         plan.run_subband()
         eng.sync()
         if job.keep_subbands:
-            os.makedirs(os.path.join(tempdir, "subbands"), exist_ok=True)
             info = job.info_template(pp.nsub, plan.sub_lofreq, plan.sub_chanwid, plan.sub_dt)
             info.name, info.dm, info.N = subbasenm, pp.subdm, plan.nds
             write_subbands(os.path.join(tempdir, "subbands", subbasenm), plan.get_subbands(), info)

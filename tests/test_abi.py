@@ -43,7 +43,13 @@ def test_version_and_defaults():
     assert L.hd_version().decode().startswith("hipdedisp")
     o = _lib.hd_opts()
     L.hd_opts_default(ctypes.byref(o))
-    assert (o.sub_dtype, o.ds_mode, o.pad_mode, o.nibble_hi_first, o.be16, o.inf_roundtrip) == (0, 0, 0, 1, 1, 1)
+    # the reference's commands: int16 .sub files, mean downsampling, first-DM padding, default
+    # -clip 6 (no -noclip at PALFA2_presto_search.py:506-511), (short)(x + 0.5) rounding
+    assert (o.sub_dtype, o.ds_mode, o.pad_mode, o.nibble_hi_first, o.be16, o.inf_roundtrip, o.sub_round) == \
+        (0, 1, 2, 1, 1, 1, 0)
+    assert o.clip_sigma == 6.0
+    d = Opts()
+    assert (d.ds_mode, d.pad_mode, d.clip_sigma, d.sub_round) == (o.ds_mode, o.pad_mode, o.clip_sigma, o.sub_round)
 
 
 def test_errors_are_return_codes():
