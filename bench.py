@@ -32,7 +32,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--nspec", type=int, default=1 << 22, help="spectra per beam (2^22 = config 2)")
     ap.add_argument("--nbits", type=int, default=8)
-    ap.add_argument("--variant", type=int, default=0, help="stage-2 kernel: 0 auto, 1 direct, 2 LDS")
+    ap.add_argument("--variant", type=int, default=0,
+                    help="hd_plan_set_variant value for every plan (0 auto; probe bits are for profiling only)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU-baseline leg")
     ap.add_argument("--streams", type=int, default=1, choices=(1, 2),
                     help="stage-2 HIP streams (hd_set_streams): 2 overlaps consecutive passes (no launch tails; "
@@ -133,16 +134,22 @@ def broadcast_beam(eng, obs, rank, dist, torch):
     del t
 
 
-def cpu_baseline(obs, synth, ddplans, target_s):
-    """Oracle (restatement of prepsubband's two stages) on the host cores, on a bounded
-    sample: the first W output samples of one pass per DDplan stage, extrapolated to the
-    whole plan by passes x (N/ds)/W.  W is sized so the sample costs ~target_s seconds."""
-    import numpy as np
+def cpu_baseline(obs, synth, ddplans, target_s, mask, pts, pad, omp):
+    """Oracle (restatement of prepsubband's two stages, clip_times and mask included) on the
+    host cores, on a bounded sample: per DDplan stage, pass 0 over the first W output
+    samples -- read-block cleaning (check_mask + clip_times) of the raw window, stage 1,
+    stage 2 -- extrapolated to the whole plan by passes x (N/ds)/W.  As in the reference,
+    every pass pays its own raw read and clip (each -sub prepsubband call redoes them).
+    omp=False is the reference's one core per beam (ppn=1, pbs.py:67); omp=True spreads the
+    sums over the host threads (the clip recurrence stays serial).  W is sized so the
+    sample costs ~target_s seconds."""
+    import copy
+
     import oracle as OR
     from hipdedisp import Opts
     from hipdedisp.synth import host_spectra
     opts = Opts()
-    threads = OR.num_threads(True)
+    threads = OR.num_threads(True) if omp else 1
 
     def one(d, W):
         subdm = float(d.subdmlist[0])
@@ -150,10 +157,14 @@ def cpu_baseline(obs, synth, ddplans, target_s):
         idd = OR.chan_delays(obs, d.numsub, subdm)
         ws = W + int(off.max())
         nraw = min(obs.N, ws * d.sub_downsamp + int(idd.max()) + d.sub_downsamp)
+        wobs = copy.copy(obs)
+        wobs.N = nraw
         raw = host_spectra(obs, synth, 0, nraw)
+        numint = -(-nraw // pts)
         t0 = time.perf_counter()
-        sub = OR.stage1(obs, opts, raw, d.numsub, d.sub_downsamp, subdm, t0=0, count=ws, omp=True)
-        OR.stage2(sub, off, 0, W, omp=True)
+        cl = OR.prepare(wobs, opts, raw, mask=mask[:numint], ptsperint=pts, padvals=pad, omp=omp)
+        sub = OR.stage1(wobs, opts, raw, d.numsub, d.sub_downsamp, subdm, t0=0, count=ws, omp=omp, clean=cl)
+        OR.stage2(sub, off, 0, W, omp=omp)
         return time.perf_counter() - t0
 
     # per stage: probe a small window, then size the measured window to ~target_s/6 seconds
@@ -161,7 +172,8 @@ def cpu_baseline(obs, synth, ddplans, target_s):
     est_full, done_out, done_t = 0.0, 0, 0.0
     for d in ddplans:
         nds = obs.N // d.sub_downsamp
-        probe_w = 16384
+        probe_w = 32768 if omp else 2048      # OpenMP: enough 8192-sample blocks to spread
+        one(d, probe_w)                       # warm-up (thread pool, first touch)
         tp = one(d, probe_w)
         W = int(min(nds - 8192, max(probe_w, probe_w * budget / max(tp, 1e-3))))
         t = one(d, W)
@@ -170,9 +182,11 @@ def cpu_baseline(obs, synth, ddplans, target_s):
         done_t += t
     total_out = sum(d.numpasses * d.dmsperpass * (obs.N // d.sub_downsamp) for d in ddplans)
     return {"value": total_out / est_full, "unit": "samples/s", "cores": threads, "kind": "port",
-            "sample": "oracle/prepsubband_oracle.c (OpenMP, %d threads): first W output samples of pass 0 of "
-                      "each of the 6 DDplan stages (%d DM-samples, %.1f s), extrapolated by passes x (N/ds)/W "
-                      "to the full 57-pass beam (est. %.0f s)" % (threads, done_out, done_t, est_full),
+            "sample": "oracle/prepsubband_oracle.c (%s): per DDplan stage, pass 0 over its first W output samples "
+                      "(clip_times + mask + stage 1 + stage 2; %d DM-samples, %.1f s), extrapolated by passes x "
+                      "(N/ds)/W to the full 57-pass beam (est. %.0f s per beam)"
+                      % ("OpenMP, %d threads" % threads if omp else "1 thread, the reference's ppn=1",
+                         done_out, done_t, est_full),
             "est_full_beam_s": est_full}
 
 
@@ -285,7 +299,8 @@ def main():
     if shard:
         line["broadcast_ms_per_step"] = 1e3 * bcast_s / args.steps
     if rank == 0 and world == 1 and not args.no_cpu:
-        line["cpu_baseline"] = cpu_baseline(obs, synth, ddplans, args.cpu_seconds)
+        line["cpu_baseline"] = cpu_baseline(obs, synth, ddplans, args.cpu_seconds, mask, pts, pad, omp=False)
+        line["cpu_baseline_openmp"] = cpu_baseline(obs, synth, ddplans, args.cpu_seconds, mask, pts, pad, omp=True)
     if rank == 0:
         print(json.dumps(line), flush=True)
     for p in plans:

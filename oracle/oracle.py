@@ -146,7 +146,7 @@ def block_masks(obs, mask, ptsperint, dtint=0.0, zapint=None, blk=None):
 
 
 def prepare(obs, opts, raw, calib=(None, None, None), mask=None, ptsperint=0, padvals=None, dtint=0.0,
-            zapint=None, blk=None):
+            zapint=None, blk=None, omp=False):
     """Block masks + clip_times over the whole raw block -> Clean."""
     blk = int(blk or obs.nsblk)
     nblk = (obs.N + blk - 1) // blk
@@ -157,7 +157,7 @@ def prepare(obs, opts, raw, calib=(None, None, None), mask=None, ptsperint=0, pa
     cal = [None if c is None else np.ascontiguousarray(c, np.float32) for c in calib]
     pv = None if padvals is None else np.ascontiguousarray(padvals, np.float32)
     o, p = _obs(obs), _opts(opts)
-    n = lib().or_clip_prepare(ctypes.byref(o), ctypes.byref(p), _ptr(raw), _ptr(cal[0]), _ptr(cal[1]), _ptr(cal[2]),
+    n = lib(omp).or_clip_prepare(ctypes.byref(o), ctypes.byref(p), _ptr(raw), _ptr(cal[0]), _ptr(cal[1]), _ptr(cal[2]),
                               _ptr(allzap), _ptr(pv), blk, nblk, _ptr(pad), _ptr(clipped))
     if n < 0:
         raise ValueError("or_clip_prepare rejected its arguments")
@@ -171,7 +171,7 @@ def stage1(obs, opts, raw, nsub, ds, subdm, t0=0, count=None, calib=(None, None,
     if count is None:
         count = nds - t0
     if clean is None:
-        clean = prepare(obs, opts, raw, calib, mask, ptsperint, padvals, dtint, zapint)
+        clean = prepare(obs, opts, raw, calib, mask, ptsperint, padvals, dtint, zapint, omp=omp)
     idd = chan_delays(obs, nsub, subdm)
     dt = np.int16 if opts.sub_dtype == 0 else np.float32
     out = np.zeros((nsub, count), dt)

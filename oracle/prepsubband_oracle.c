@@ -171,17 +171,26 @@ static inline float raw_sample(const or_obs* o, const or_opts* op, const uint8_t
     }
 }
 
-/* decoded, calibrated sample of ascending channel c at spectrum t (t < N) */
-static inline float decoded(const or_obs* o, const or_opts* op, const uint8_t* raw,
-                            const float* scl, const float* offs, const float* wts, int64_t t, int c)
+/* one raw spectrum -> decoded, calibrated f[nchan] in ascending-frequency order */
+static void decode_row(const or_obs* o, const or_opts* op, const uint8_t* row,
+                       const float* scl, const float* offs, const float* wts, float* f)
 {
-    const int64_t rowbytes = (int64_t)o->nchan * o->nbits / 8;
-    const int rc = o->flip ? o->nchan - 1 - c : c;
-    float x = raw_sample(o, op, raw + t * rowbytes, rc);
-    if (scl) x = x * scl[rc];
-    if (offs) x = x + offs[rc];
-    if (wts) x = x * wts[rc];
-    return x;
+    const int n = o->nchan;
+    if (o->nbits == 8) {
+        if (o->flip) for (int c = 0; c < n; c++) f[c] = (float)row[n - 1 - c];
+        else for (int c = 0; c < n; c++) f[c] = (float)row[c];
+    } else {
+        for (int c = 0; c < n; c++) f[c] = raw_sample(o, op, row, o->flip ? n - 1 - c : c);
+    }
+    if (scl || offs || wts)
+        for (int c = 0; c < n; c++) {
+            const int rc = o->flip ? n - 1 - c : c;
+            float x = f[c];
+            if (scl) x = x * scl[rc];
+            if (offs) x = x + offs[rc];
+            if (wts) x = x * wts[rc];
+            f[c] = x;
+        }
 }
 
 /* ------------------------------------------------------------------------------- */
@@ -289,50 +298,68 @@ typedef struct {
     float* chan_running_avg;
 } clipstate;
 
-/* clip_times(rawdata [ptsperblk][numchan], ..., good_chan_levels): returns the number of
- * spectra replaced; flags[ii] = 1 for each of them. */
-static int clip_times(float* rawdata, int ptsperblk, int numchan, float clip_sigma,
-                      float* good_chan_levels, clipstate* st, uint8_t* flags)
-{
-    float* zero_dm_block = (float*)malloc(sizeof(float) * ptsperblk);
-    float* median_temp = (float*)malloc(sizeof(float) * ptsperblk);
-    double* chan_avg_temp = (double*)malloc(sizeof(double) * numchan);
-    double current_avg = 0.0, current_std = 0.0;
-    int clipit = 0, clipped = 0;
+/* clip_times(rawdata [ptsperblk][numchan], ..., good_chan_levels), split in two so the
+ * oracle can run the per-block statistics of many blocks in parallel (OpenMP) and only the
+ * running-average recurrence in block order; the arithmetic is PRESTO's, step for step.
+ *
+ * Part 1 (no state): the zero-DM series, its median, the "good" points within 0.7..1.3 x
+ * the median, their avg_var mean and std and the per-channel sums of the good spectra. */
+typedef struct {
+    int numgood;
+    double avg, std;
+} blockstat;
 
-    /* the zero-DM time series */
+static void clip_block_stats(const float* rawdata, int ptsperblk, int numchan, float* zero_dm_block,
+                             blockstat* bs, double* chan_avg_temp)
+{
+    float* median_temp = (float*)malloc(sizeof(float) * ptsperblk);
     for (int ii = 0; ii < ptsperblk; ii++) {
         zero_dm_block[ii] = 0.0f;
         for (int jj = 0; jj < numchan; jj++) zero_dm_block[ii] += rawdata[(int64_t)ii * numchan + jj];
         median_temp[ii] = zero_dm_block[ii];
     }
     const float current_med = quick_select(median_temp, ptsperblk);
-
-    /* mean / std / channel means of the points within 0.7..1.3 x the median */
-    {
-        const float lo_cutoff = 0.7 * current_med;
-        const float hi_cutoff = 1.3 * current_med;
-        int numgoodpts = 0;
-        for (int jj = 0; jj < numchan; jj++) chan_avg_temp[jj] = 0.0;
-        for (int ii = 0; ii < ptsperblk; ii++) {
-            if (zero_dm_block[ii] > lo_cutoff && zero_dm_block[ii] < hi_cutoff) {
-                median_temp[numgoodpts] = zero_dm_block[ii];
-                for (int jj = 0; jj < numchan; jj++) chan_avg_temp[jj] += rawdata[(int64_t)ii * numchan + jj];
-                numgoodpts++;
-            }
-        }
-        if (numgoodpts < 1) {
-            current_avg = st->running_avg;
-            current_std = st->running_std;
-            for (int jj = 0; jj < numchan; jj++) chan_avg_temp[jj] = st->chan_running_avg[jj];
-        } else {
-            avg_var(median_temp, numgoodpts, &current_avg, &current_std);
-            current_std = sqrt(current_std);
-            for (int jj = 0; jj < numchan; jj++) chan_avg_temp[jj] /= numgoodpts;
+    const float lo_cutoff = 0.7 * current_med;
+    const float hi_cutoff = 1.3 * current_med;
+    int numgoodpts = 0;
+    for (int jj = 0; jj < numchan; jj++) chan_avg_temp[jj] = 0.0;
+    for (int ii = 0; ii < ptsperblk; ii++) {
+        if (zero_dm_block[ii] > lo_cutoff && zero_dm_block[ii] < hi_cutoff) {
+            median_temp[numgoodpts] = zero_dm_block[ii];
+            for (int jj = 0; jj < numchan; jj++) chan_avg_temp[jj] += rawdata[(int64_t)ii * numchan + jj];
+            numgoodpts++;
         }
     }
+    bs->numgood = numgoodpts;
+    bs->avg = bs->std = 0.0;
+    if (numgoodpts >= 1) {
+        double var;
+        avg_var(median_temp, numgoodpts, &bs->avg, &var);
+        bs->std = sqrt(var);
+        for (int jj = 0; jj < numchan; jj++) chan_avg_temp[jj] /= numgoodpts;
+    }
+    free(median_temp);
+}
 
-    /* pseudo running averages over BLOCKSTOAVG blocks */
+/* Part 2 (block order): the BLOCKSTOAVG-block running averages, good_chan_levels, and the
+ * spectra beyond clip_sigma * running_std flagged for replacement by the channel levels. */
+static int clip_update(const float* zero_dm_block, int ptsperblk, int numchan, float clip_sigma,
+                       const blockstat* bs, const double* chan_avg_block, float* good_chan_levels,
+                       clipstate* st, uint8_t* flags)
+{
+    double current_avg, current_std;
+    const double* chan_avg_temp = chan_avg_block;
+    double* fallback = NULL;
+    if (bs->numgood < 1) {
+        current_avg = st->running_avg;
+        current_std = st->running_std;
+        fallback = (double*)malloc(sizeof(double) * numchan);
+        for (int jj = 0; jj < numchan; jj++) fallback[jj] = st->chan_running_avg[jj];
+        chan_avg_temp = fallback;
+    } else {
+        current_avg = bs->avg;
+        current_std = bs->std;
+    }
     if (st->blocksread) {
         st->running_avg = (st->running_avg * (BLOCKSTOAVG - 1) + current_avg) / BLOCKSTOAVG;
         st->running_std = (st->running_std * (BLOCKSTOAVG - 1) + current_std) / BLOCKSTOAVG;
@@ -344,27 +371,15 @@ static int clip_times(float* rawdata, int ptsperblk, int numchan, float clip_sig
         for (int ii = 0; ii < numchan; ii++) st->chan_running_avg[ii] = chan_avg_temp[ii];
     }
     for (int ii = 0; ii < numchan; ii++) good_chan_levels[ii] = st->chan_running_avg[ii];
-
-    /* clip */
     const float trigger = clip_sigma * st->running_std;
+    int clipped = 0;
     for (int ii = 0; ii < ptsperblk; ii++)
         if (fabs(zero_dm_block[ii] - st->running_avg) > trigger) {
-            clipit = 1;
-            break;
+            flags[ii] = 1;      /* clip_times replaces the spectrum by chan_running_avg */
+            clipped++;
         }
-    if (clipit) {
-        for (int ii = 0; ii < ptsperblk; ii++) {
-            if (fabs(zero_dm_block[ii] - st->running_avg) > trigger) {
-                for (int jj = 0; jj < numchan; jj++) rawdata[(int64_t)ii * numchan + jj] = st->chan_running_avg[jj];
-                flags[ii] = 1;
-                clipped++;
-            }
-        }
-    }
     st->blocksread++;
-    free(zero_dm_block);
-    free(median_temp);
-    free(chan_avg_temp);
+    free(fallback);
     return clipped;
 }
 
@@ -375,27 +390,47 @@ int64_t or_clip_prepare(const or_obs* obs, const or_opts* opts, const uint8_t* r
 {
     const int nchan = obs->nchan;
     if (blk <= 0 || nblk != (int)((obs->N + blk - 1) / blk)) return -1;
+    memset(clipped, 0, (size_t)obs->N);
     float* padvals = (float*)calloc((size_t)nchan, sizeof(float));
     if (padvals0) memcpy(padvals, padvals0, sizeof(float) * nchan);
+    /* the reference's -sub command leaves prepsubband's default clip on; a block whose
+     * every channel is masked is neither clipped nor counted (read_psrdata) */
+    const int clip = opts->clip_sigma > 0.0f;
+    float* zdm = clip ? (float*)malloc(sizeof(float) * (size_t)obs->N) : NULL;
+    blockstat* bs = clip ? (blockstat*)calloc((size_t)nblk, sizeof(blockstat)) : NULL;
+    double* cat = clip ? (double*)malloc(sizeof(double) * (size_t)nblk * nchan) : NULL;
+    if (clip) {
+        const int64_t rowbytes = (int64_t)nchan * obs->nbits / 8;
+#pragma omp parallel
+        {
+            float* X = (float*)malloc(sizeof(float) * (size_t)blk * nchan);
+#pragma omp for schedule(dynamic, 1)
+            for (int b = 0; b < nblk; b++) {
+                if (allzap && allzap[b]) continue;
+                const int64_t t0 = (int64_t)b * blk;
+                const int nb = (int)((t0 + blk <= obs->N) ? blk : obs->N - t0);
+                for (int ii = 0; ii < nb; ii++)
+                    decode_row(obs, opts, raw + (t0 + ii) * rowbytes, scl, offs, wts, X + (int64_t)ii * nchan);
+                clip_block_stats(X, nb, nchan, zdm + t0, bs + b, cat + (int64_t)b * nchan);
+            }
+            free(X);
+        }
+    }
     clipstate st = {0.0f, 0.0f, 0, (float*)calloc((size_t)nchan, sizeof(float))};
-    float* X = (float*)malloc(sizeof(float) * (size_t)blk * nchan);
-    memset(clipped, 0, (size_t)obs->N);
     int64_t total = 0;
     for (int b = 0; b < nblk; b++) {
         const int64_t t0 = (int64_t)b * blk;
         const int nb = (int)((t0 + blk <= obs->N) ? blk : obs->N - t0);
-        /* the reference's -sub command leaves prepsubband's default clip on; a block whose
-         * every channel is masked is neither clipped nor counted (read_psrdata) */
-        if (opts->clip_sigma > 0.0f && !(allzap && allzap[b])) {
-            for (int ii = 0; ii < nb; ii++)
-                for (int c = 0; c < nchan; c++) X[(int64_t)ii * nchan + c] = decoded(obs, opts, raw, scl, offs, wts, t0 + ii, c);
-            total += clip_times(X, nb, nchan, opts->clip_sigma, padvals, &st, clipped + t0);
-        }
+        if (clip && !(allzap && allzap[b]))
+            total += clip_update(zdm + t0, nb, nchan, opts->clip_sigma, bs + b, cat + (int64_t)b * nchan,
+                                 padvals, &st, clipped + t0);
         memcpy(pad + (int64_t)b * nchan, padvals, sizeof(float) * nchan);
     }
-    free(X);
     free(st.chan_running_avg);
     free(padvals);
+    free(zdm);
+    free(bs);
+    free(cat);
     return total;
 }
 
@@ -453,8 +488,10 @@ int or_stage1(const or_obs* obs, const or_opts* opts, const uint8_t* raw,
                 continue;
             }
             const uint8_t* zrow = zap ? zap + rb * nchan : NULL;
-            for (int c = 0; c < nchan; c++)
-                f[c] = (zrow && zrow[c]) ? (prow ? prow[c] : 0.0f) : decoded(obs, opts, raw, scl, offs, wts, t, c);
+            decode_row(obs, opts, raw + t * ((int64_t)nchan * obs->nbits / 8), scl, offs, wts, f);
+            if (zrow)
+                for (int c = 0; c < nchan; c++)
+                    if (zrow[c]) f[c] = prow ? prow[c] : 0.0f;
         }
         /* channel -> subband delay-and-sum at subdm (dedisp_subbands), then downsample */
         for (int64_t j = 0; j < nb; j++) {

@@ -59,6 +59,7 @@ struct hd_ctx {
         float* zdm = nullptr;
         uint8_t *good = nullptr, *clipped = nullptr;
         int32_t *numgood = nullptr, *doclip = nullptr, *events = nullptr, *nevents = nullptr;
+        int32_t* nzero = nullptr;           // a device 0 (profiling: a fixup over no clipped spectra)
         double *bavg = nullptr, *bstd = nullptr, *chansum = nullptr;
         float *ravg = nullptr, *trig = nullptr, *pad = nullptr;
     } clip;
@@ -270,7 +271,7 @@ static void free_clip(hd_ctx* c)
 {
     hd_ctx::ClipBufs& b = c->clip;
     for (void* p : {(void*)b.zdm, (void*)b.good, (void*)b.clipped, (void*)b.numgood, (void*)b.doclip,
-                    (void*)b.events, (void*)b.nevents, (void*)b.bavg, (void*)b.bstd, (void*)b.chansum,
+                    (void*)b.events, (void*)b.nevents, (void*)b.nzero, (void*)b.bavg, (void*)b.bstd, (void*)b.chansum,
                     (void*)b.ravg, (void*)b.trig, (void*)b.pad})
         dfree(p);
     b = hd_ctx::ClipBufs{};
@@ -1278,6 +1279,7 @@ static hd::RawDesc raw_desc(const hd_ctx* c)
     rd.wts = c->d_wts;
     rd.blk = c->blk;
     rd.nblk = c->nblk;
+    rd.blk_shift = (c->blk & (c->blk - 1)) ? -1 : __builtin_ctz((unsigned)c->blk);
     rd.zidx = c->d_zidx;
     rd.zrows = c->d_zrows;
     const bool clip = c->opts.clip_sigma > 0.0f && c->clip_valid;
@@ -1354,6 +1356,7 @@ static int ensure_clip(hd_ctx* c)
         al((void**)&b.clipped, N);
         al((void**)&b.events, N * 4);
         al((void**)&b.nevents, 4);
+        al((void**)&b.nzero, 4);
         al((void**)&b.numgood, nb * 4);
         al((void**)&b.doclip, nb * 4);
         al((void**)&b.bavg, nb * 8);
@@ -1366,6 +1369,7 @@ static int ensure_clip(hd_ctx* c)
             free_clip(c);
             return fail(c, HD_E_NOMEM, "cannot allocate the clip_times state: %s", hipGetErrorString(e));
         }
+        HIPCHK(c, hipMemset(b.nzero, 0, 4));
     }
     hd::ClipArgs a{};
     a.rd = raw_desc(c);
@@ -1647,7 +1651,12 @@ static int run_subband_chunk(hd_ctx* c, hd_plan** plans, int n)
             HIPCHK(c, hd::launch_stage1_tiled(f, fvw, d_sp, nsp, true, c->stream));
         }
         // clipped spectra, and the block-boundary outputs of the per-block pad constants
-        if (clip) HIPCHK(c, hd::launch_stage1_fixup(m, c->clip.events, c->clip.nevents, m.rd.zidx != nullptr, c->stream));
+        // (probe bits 5/6 skip the boundary / clipped-spectrum items: profiling only)
+        if (clip && !(p0->probe & 64))
+            HIPCHK(c, hd::launch_stage1_fixup(m, c->clip.events, c->clip.nevents,
+                                              m.rd.zidx != nullptr && !(p0->probe & 32), c->stream));
+        else if (clip && !(p0->probe & 32) && m.rd.zidx)
+            HIPCHK(c, hd::launch_stage1_fixup(m, c->clip.events, c->clip.nzero, 1, c->stream));
     } else if (tiled) {
         m.rd = raw_desc(c);
         m.npass = n;

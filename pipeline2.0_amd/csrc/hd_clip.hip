@@ -149,22 +149,81 @@ __global__ __launch_bounds__(256) void k_clip_chan(ClipArgs a)
     a.chansum[(int64_t)b * nch + c] = acc;
 }
 
+// 8-bit data without calibration: the sums are of integers (exact in any order), so a lane
+// keeps four channels' byte sums in integers over dword loads, 8 spectra in flight, with the
+// block's good flags staged in LDS; the exact integer is the double the fold would give.
+__global__ __launch_bounds__(256) void k_clip_chan_u8(ClipArgs a)
+{
+    __shared__ uint8_t g[kClipMaxBlock];
+    const int nch = a.rd.nchan;
+    const int b = blockIdx.x;
+    const int64_t t0 = (int64_t)b * a.rd.blk;
+    const int nb = (int)min((int64_t)a.rd.blk, a.rd.N - t0);
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) g[i] = a.good[t0 + i];
+    __syncthreads();
+    const int nq = a.rd.rowbytes >> 2;                  // channel quads per spectrum
+    for (int q = threadIdx.x; q < nq; q += blockDim.x) {
+        uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+        const uint8_t* base = a.rd.raw + t0 * a.rd.rowbytes + 4 * q;
+        int k = 0;
+        for (; k + 8 <= nb; k += 8) {
+            uint32_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) v[u] = g[k + u] ? *(const uint32_t*)(base + (int64_t)(k + u) * a.rd.rowbytes) : 0u;
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                s0 += v[u] & 0xFFu;
+                s1 += (v[u] >> 8) & 0xFFu;
+                s2 += (v[u] >> 16) & 0xFFu;
+                s3 += v[u] >> 24;
+            }
+        }
+        for (; k < nb; k++) {
+            const uint32_t v = g[k] ? *(const uint32_t*)(base + (int64_t)k * a.rd.rowbytes) : 0u;
+            s0 += v & 0xFFu;
+            s1 += (v >> 8) & 0xFFu;
+            s2 += (v >> 16) & 0xFFu;
+            s3 += v >> 24;
+        }
+        const uint32_t sv[4] = {s0, s1, s2, s3};
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int rc = 4 * q + i;                   // raw channel -> ascending channel
+            const int c = a.rd.flip ? nch - 1 - rc : rc;
+            a.chansum[(int64_t)b * nch + c] = (double)sv[i];
+        }
+    }
+}
+
 // ---- the serial recurrence over blocks (one workgroup, thread = channel) -------------
 __global__ __launch_bounds__(1024) void k_clip_recur(ClipArgs a)
 {
     const int nch = a.rd.nchan;
     const float clip_sigma = a.clip_sigma;
     const int nloop = nch > 0 ? nch : 1;
+    constexpr int U = 8;                                // chansum loads in flight per thread
     for (int c0 = 0; c0 < nloop; c0 += blockDim.x) {
         const int c = c0 + threadIdx.x;
         const bool own = c < nch;
         float ravg = 0.0f, rstd = 0.0f, cra = 0.0f;
         float lev = own && a.padvals0 ? a.padvals0[c] : 0.0f;
         int nread = 0;
-        for (int b = 0; b < a.rd.nblk; b++) {
+        for (int b8 = 0; b8 < a.rd.nblk; b8 += U) {
+          double csv[U];
+          int ngv[U];
+#pragma unroll
+          for (int u = 0; u < U; u++) {                 // independent of the recurrence: issue first
+              const int b = min(b8 + u, a.rd.nblk - 1);
+              csv[u] = own ? a.chansum[(int64_t)b * nch + c] : 0.0;
+              ngv[u] = a.numgood[b];
+          }
+#pragma unroll
+          for (int u = 0; u < U; u++) {
+            const int b = b8 + u;
+            if (b >= a.rd.nblk) break;
             const bool run = clip_sigma > 0.0f && !(a.allzap && a.allzap[b]);
             if (run) {
-                const int ng = a.numgood[b];
+                const int ng = ngv[u];
                 double cur_avg, cur_std, cat;
                 if (ng < 1) {
                     cur_avg = (double)ravg;
@@ -173,7 +232,7 @@ __global__ __launch_bounds__(1024) void k_clip_recur(ClipArgs a)
                 } else {
                     cur_avg = a.bavg[b];
                     cur_std = a.bstd[b];
-                    cat = own ? a.chansum[(int64_t)b * nch + c] / (double)ng : 0.0;
+                    cat = csv[u] / (double)ng;
                 }
                 if (nread) {
                     const float r29 = ravg * (float)(kBlocksToAvg - 1);
@@ -196,6 +255,7 @@ __global__ __launch_bounds__(1024) void k_clip_recur(ClipArgs a)
                 a.trig[b] = clip_sigma * rstd;
             }
             if (own) a.pad[(int64_t)b * nch + c] = lev;
+          }
         }
     }
 }
@@ -206,7 +266,7 @@ __global__ __launch_bounds__(256) void k_clip_flag(ClipArgs a)
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     bool clip = false;
     if (t < a.rd.N) {
-        const int64_t b = t / a.rd.blk;
+        const int64_t b = blk_of(a.rd, t);
         clip = a.doclip[b] && fabsf(a.zdm[t] - a.ravg[b]) > a.trig[b];
         a.clipped[t] = clip;
     }
@@ -235,7 +295,10 @@ hipError_t launch_clip(const ClipArgs& a, hipStream_t st)
         hipLaunchKernelGGL(k_clip_zdm, dim3((unsigned)((rd.N + 255) / 256)), dim3(256), 0, st, rd, a.zdm);
     hipLaunchKernelGGL(k_clip_block, dim3((unsigned)rd.nblk), dim3(1024), 0, st, a);
     hipLaunchKernelGGL(k_clip_as52, dim3((unsigned)((rd.nblk + 63) / 64)), dim3(64), 0, st, a);
-    hipLaunchKernelGGL(k_clip_chan, dim3((unsigned)(rd.nblk * ((rd.nchan + 255) / 256))), dim3(256), 0, st, a);
+    if (rd.nbits == 8 && !calib && rd.rowbytes % 4 == 0)
+        hipLaunchKernelGGL(k_clip_chan_u8, dim3((unsigned)rd.nblk), dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL(k_clip_chan, dim3((unsigned)(rd.nblk * ((rd.nchan + 255) / 256))), dim3(256), 0, st, a);
     hipLaunchKernelGGL(k_clip_recur, dim3(1), dim3(1024), 0, st, a);
     hipLaunchKernelGGL(k_clip_flag, dim3((unsigned)((rd.N + 255) / 256)), dim3(256), 0, st, a);
     return hipGetLastError();
@@ -244,71 +307,217 @@ hipError_t launch_clip(const ClipArgs& a, hipStream_t st)
 // ------------------------------------------------------------------------------------
 // stage-1 fixup
 // ------------------------------------------------------------------------------------
-// Work item = (event e, pass p, subband s), lanes over consecutive subbands.  Event e <
-// nev is the clipped spectrum r = events[e]: every output whose rows
-// [j*ds + mind_s, j*ds + ds - 1 + maxd_s] contain r is recomputed.  Events past nev are the
-// read-block boundaries r = (e - nev + 1) * blk (only when `boundaries`): outputs whose rows
-// contain both r - 1 and r, in subbands with a channel masked in either block (the integer
-// path's per-block pad constants do not cover them).  Recomputation is the exact per-cell
-// fold of k_stage1_direct; overlapping items write identical values.
+// One workgroup per (event e, pass p); the pass's channel delays, and the zap rows and pad
+// rows of the (at most two) read blocks the item's rows fall in, are staged in LDS.
+//  * e < nev: the clipped spectrum r = events[e].  Channel c of subband s reads spectrum r
+//    for exactly one output, j = floor((r - d_c) / ds); those outputs (one per distinct j
+//    in the subband) are recomputed: at most cps per subband, usually far fewer.
+//  * e >= nev (only when `boundaries`): the read-block boundary r = (e - nev + 1) * blk.
+//    In subbands with a channel masked in both blocks whose pad values differ, the outputs
+//    whose rows contain both r - 1 and r mix the two blocks' pads, which the integer path's
+//    per-block constants do not cover; they are recomputed (every other subband was exact).
+// Recomputation is the exact per-cell fold of k_stage1_direct; overlapping events write
+// identical values.  Index arithmetic is 32-bit (the host checks N < 2^31).
+constexpr int kFixMaxSub = 1024, kFixMaxChan = 4096;
+
+struct FixCtx {
+    const int* dly;          // LDS: delays of the pass
+    const uint8_t* zap2;     // LDS: [2][nchan] zap rows of blocks b0, b0 + 1
+    const float* pad2;       // LDS: [2][nchan] pad rows of blocks b0, b0 + 1
+    int b0;                  // first block staged
+    int bnd;                 // first spectrum of block b0 + 1
+    int lo, hi;              // spectra [lo, hi) are inside the staged blocks
+};
+
+__device__ __forceinline__ float fix_cell(const RawDesc& rd, const FixCtx& f, int t, int c)
+{
+    if (t < f.lo || t >= f.hi) return chan_value(rd, t, c);      // outside the staged blocks
+    const int part = t >= f.bnd;
+    const bool repl = (rd.clipped && rd.clipped[t]) || f.zap2[part * rd.nchan + c];
+    return repl ? f.pad2[part * rd.nchan + c] : raw_value(rd, t, c);
+}
+
+// One output (s, j), exactly.  The cells of a k-step are gathered with their loads issued
+// together (16 channels at a time, no data-dependent branch between them): a dependent
+// chain of one latency per cell would dominate the fixup.
+__device__ __forceinline__ int fix_one(const Stage1Multi& a, const FixCtx& f, int p, int s, int j)
+{
+    const RawDesc& rd = a.rd;
+    const int ds = a.ds, cps = a.cps, nch = rd.nchan;
+    const bool fast = rd.nbits == 8 && !rd.scl && !rd.offs && !rd.wts;
+    float acc = 0.0f;
+    for (int k = 0; k < ds; k++) {
+        float sk = 0.0f;
+        const int tb = j * ds + k;
+        for (int c0 = 0; c0 < cps; c0 += 16) {
+            float x[16];
+            if (fast) {
+                uint32_t b[16], cf[16];
+#pragma unroll
+                for (int i = 0; i < 16; i++) {
+                    const int cc = min(c0 + i, cps - 1);
+                    const int c = s * cps + cc;
+                    const int t = tb + f.dly[c];
+                    const int tt = min(t, (int)rd.N - 1);
+                    b[i] = rd.raw[(int64_t)tt * rd.rowbytes + (rd.flip ? nch - 1 - c : c)];
+                    cf[i] = rd.clipped ? rd.clipped[tt] : 0u;
+                }
+#pragma unroll
+                for (int i = 0; i < 16; i++) {
+                    const int cc = min(c0 + i, cps - 1);
+                    const int c = s * cps + cc;
+                    const int t = tb + f.dly[c];
+                    if (t < f.lo || t >= f.hi) {
+                        x[i] = chan_value(rd, t, c);
+                    } else {
+                        const int part = t >= f.bnd;
+                        const bool repl = t >= rd.N || cf[i] || f.zap2[part * nch + c];
+                        x[i] = repl ? f.pad2[part * nch + c] : (float)b[i];
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 16; i++) {
+                    const int cc = min(c0 + i, cps - 1);
+                    x[i] = fix_cell(rd, f, tb + f.dly[s * cps + cc], s * cps + cc);
+                }
+            }
+            const int n = min(16, cps - c0);
+#pragma unroll
+            for (int i = 0; i < 16; i++)
+                if (i < n) sk += x[i];
+        }
+        acc += sk;
+    }
+    if (a.ds_mode == 1) acc = acc / (float)ds;
+    if (a.sub_dtype == 0) {
+        const int16_t q = to_i16(acc, a.sub_round);
+        ((int16_t*)a.out[p])[(int64_t)s * a.ostride[p] + j] = q;
+        return q < 0 ? -(int)q : (int)q;
+    }
+    ((float*)a.out[p])[(int64_t)s * a.ostride[p] + j] = acc;
+    return 0;
+}
+
 __global__ __launch_bounds__(256) void k_stage1_fixup(Stage1Multi a, const int32_t* __restrict__ events,
                                                      const int32_t* __restrict__ nevents, int boundaries)
 {
+    __shared__ int dly_s[kFixMaxChan];
+    __shared__ uint8_t zap_s[2 * kFixMaxChan];
+    __shared__ float pad_s[2 * kFixMaxChan];
+    __shared__ int jlo_s[kFixMaxSub], cnt_s[kFixMaxSub + 1];
+    __shared__ int amax_s, dmax_s;
     const int nev = *nevents;
     const int nbound = boundaries ? a.rd.nblk - 1 : 0;
-    const int64_t per_ev = (int64_t)a.npass * a.nsub;
-    const int64_t total = (int64_t)(nev + nbound) * per_ev;
-    const int ds = a.ds, cps = a.cps;
-    for (int64_t it = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; it < total;
-         it += (int64_t)gridDim.x * blockDim.x) {
-        const int e = (int)(it / per_ev);
-        const int rem = (int)(it - (int64_t)e * per_ev);
-        const int p = rem / a.nsub, s = rem - p * a.nsub;
-        const int32_t* dly = a.dly[p] + s * cps;
-        int mind = 1 << 30, maxd = 0;
-        for (int cc = 0; cc < cps; cc++) {
-            mind = min(mind, dly[cc]);
-            maxd = max(maxd, dly[cc]);
+    const int nitems = (nev + nbound) * a.npass;
+    const int ds = a.ds, cps = a.cps, nsub = a.nsub, nchan = a.rd.nchan;
+    const int nds = (int)a.nds;
+    for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
+        const int e = it / a.npass, p = it - e * a.npass;
+        const bool clip_ev = e < nev;
+        const int r = clip_ev ? events[e] : (e - nev + 1) * a.rd.blk;
+        __syncthreads();                                  // the previous item is done with LDS
+        if (threadIdx.x == 0) {
+            amax_s = 0;
+            dmax_s = 0;
         }
-        int64_t jlo, jhi;
-        if (e < nev) {
-            const int64_t r = events[e];
-            jlo = r - (ds - 1) - maxd;
-            jhi = r - mind;
-        } else {
-            const int64_t bb = e - nev + 1;
-            const int64_t r = bb * a.rd.blk;
-            bool masked = false;
-            for (int cc = 0; cc < cps; cc++) {
-                const int c = s * cps + cc;
-                masked |= zap_at(a.rd, bb - 1, c) || zap_at(a.rd, bb, c);
+        __syncthreads();
+        int dmx = 0;
+        for (int c = threadIdx.x; c < nchan; c += blockDim.x) {
+            const int d = a.dly[p][c];
+            dly_s[c] = d;
+            dmx = max(dmx, d);
+        }
+        dmx = wave_max_i32(dmx);
+        if ((threadIdx.x & 63) == 0) atomicMax(&dmax_s, dmx);
+        __syncthreads();
+        // the item's rows: within [r - dmax - ds, r + dmax + ds]; stage the blocks they start in
+        FixCtx f;
+        f.dly = dly_s;
+        f.zap2 = zap_s;
+        f.pad2 = pad_s;
+        {
+            const int w = dmax_s + ds;
+            const int b0 = (int)blk_of(a.rd, max(r - w, 0));
+            f.b0 = b0;
+            f.bnd = (b0 + 1) * a.rd.blk;
+            f.lo = b0 * a.rd.blk;
+            f.hi = b0 + 1 < a.rd.nblk ? min((int64_t)(b0 + 2) * a.rd.blk, a.rd.N) : a.rd.N;
+            const int b1 = min(b0 + 1, a.rd.nblk - 1);
+            for (int c = threadIdx.x; c < nchan; c += blockDim.x) {
+                zap_s[c] = zap_at(a.rd, b0, c);
+                zap_s[nchan + c] = zap_at(a.rd, b1, c);
+                pad_s[c] = pad_at(a.rd, b0, c);
+                pad_s[nchan + c] = pad_at(a.rd, b1, c);
             }
-            if (!masked) continue;
-            jlo = r - (ds - 1) - maxd;
-            jhi = r - 1 - mind;
         }
-        jlo = jlo <= 0 ? 0 : (jlo + ds - 1) / ds;       // ceil for jlo > 0
-        jhi = jhi < 0 ? -1 : jhi / ds;
-        if (jhi > a.nds - 1) jhi = a.nds - 1;
+        __syncthreads();
         int amax = 0;
-        for (int64_t j = jlo; j <= jhi; j++) {
-            float acc = 0.0f;
-            for (int k = 0; k < ds; k++) {
-                float sk = 0.0f;
-                const int64_t tb = j * ds + k;
-                for (int cc = 0; cc < cps; cc++) sk += chan_value(a.rd, tb + dly[cc], s * cps + cc);
-                acc += sk;
+        if (clip_ev) {
+            for (int c = threadIdx.x; c < nchan; c += blockDim.x) {
+                const int s = c / cps;
+                const int jn = r - dly_s[c];
+                if (jn < 0) continue;
+                const int j = jn / ds;
+                if (j >= nds) continue;
+                bool dup = false;                         // an earlier channel already names j
+                for (int c2 = s * cps; c2 < c; c2++) {
+                    const int jn2 = r - dly_s[c2];
+                    dup |= jn2 >= 0 && jn2 / ds == j;
+                }
+                if (!dup) amax = max(amax, fix_one(a, f, p, s, j));
             }
-            if (a.ds_mode == 1) acc = acc / (float)ds;
-            if (a.sub_dtype == 0) {
-                const int16_t q = to_i16(acc, a.sub_round);
-                ((int16_t*)a.out[p])[(int64_t)s * a.ostride[p] + j] = q;
-                amax = max(amax, q < 0 ? -(int)q : (int)q);
-            } else {
-                ((float*)a.out[p])[(int64_t)s * a.ostride[p] + j] = acc;
+        } else {
+            const int bb = e - nev + 1;                   // boundary between blocks bb-1 and bb
+            const int hb = bb - f.b0;                     // their parts in the staged rows
+            for (int s = threadIdx.x; s < nsub; s += blockDim.x) {
+                int mind = 1 << 30, maxd = 0;
+                bool need = false;
+                for (int cc = 0; cc < cps; cc++) {
+                    const int c = s * cps + cc;
+                    mind = min(mind, dly_s[c]);
+                    maxd = max(maxd, dly_s[c]);
+                    if (hb == 1)
+                        need |= zap_s[c] && zap_s[nchan + c] && pad_s[c] != pad_s[nchan + c];
+                    else
+                        need |= zap_at(a.rd, bb - 1, c) && zap_at(a.rd, bb, c) &&
+                                pad_at(a.rd, bb - 1, c) != pad_at(a.rd, bb, c);
+                }
+                int lo = r - (ds - 1) - maxd, hi = r - 1 - mind;
+                lo = lo <= 0 ? 0 : (lo + ds - 1) / ds;   // ceil for lo > 0
+                hi = hi < 0 ? -1 : hi / ds;
+                hi = min(hi, nds - 1);
+                jlo_s[s] = lo;
+                cnt_s[s] = need && hi >= lo ? hi - lo + 1 : 0;
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {                       // exclusive prefix sum (nsub is small)
+                int acc = 0;
+                for (int s = 0; s < nsub; s++) {
+                    const int n = cnt_s[s];
+                    cnt_s[s] = acc;
+                    acc += n;
+                }
+                cnt_s[nsub] = acc;
+            }
+            __syncthreads();
+            const int ntask = cnt_s[nsub];
+            for (int t = threadIdx.x; t < ntask; t += blockDim.x) {
+                int lo = 0, hi = nsub - 1;                // subband of task t: last s with cnt_s[s] <= t
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (cnt_s[mid] <= t) lo = mid;
+                    else hi = mid - 1;
+                }
+                amax = max(amax, fix_one(a, f, p, lo, jlo_s[lo] + (t - cnt_s[lo])));
             }
         }
-        if (a.sub_dtype == 0) publish_max(a.maxabs[p], amax);
+        if (a.sub_dtype == 0) {
+            amax = wave_max_i32(amax);
+            if ((threadIdx.x & 63) == 0 && amax > 0) atomicMax(&amax_s, amax);
+            __syncthreads();
+            if (threadIdx.x == 0) publish_max(a.maxabs[p], amax_s);
+        }
     }
 }
 
@@ -316,8 +525,10 @@ hipError_t launch_stage1_fixup(const Stage1Multi& a, const int32_t* events, cons
                                hipStream_t st)
 {
     if (a.nds <= 0 || a.npass <= 0) return hipSuccess;
+    if (a.nsub > kFixMaxSub || a.rd.nchan > kFixMaxChan || a.rd.N >= ((int64_t)1 << 31) - (1 << 24))
+        return hipErrorInvalidValue;
     // grid-stride over a device-side item count: no host round trip for the event count
-    hipLaunchKernelGGL(k_stage1_fixup, dim3(2048), dim3(256), 0, st, a, events, nevents, boundaries);
+    hipLaunchKernelGGL(k_stage1_fixup, dim3(4096), dim3(256), 0, st, a, events, nevents, boundaries);
     return hipGetLastError();
 }
 

@@ -32,7 +32,8 @@ __device__ __forceinline__ float raw_value(const RawDesc& rd, int64_t t, int c)
 // read block of spectrum t (spectra past N belong to the last block)
 __device__ __host__ __forceinline__ int64_t blk_of(const RawDesc& rd, int64_t t)
 {
-    const int64_t b = t / rd.blk;
+    const int64_t b = rd.blk_shift >= 0 ? (t >> rd.blk_shift)
+                                        : (t < 0x7fffffff ? (int64_t)((int32_t)t / rd.blk) : t / rd.blk);
     return b < rd.nblk ? b : rd.nblk - 1;
 }
 

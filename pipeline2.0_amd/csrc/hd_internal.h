@@ -21,6 +21,7 @@ struct RawDesc {
     const float* offs;
     const float* wts;
     int32_t blk, nblk;        // read blocks: nblk = ceil(N / blk)
+    int32_t blk_shift;        // log2(blk) when blk is a power of two, else -1
     const int32_t* zidx;      // [nblk] row of zrows zapped in the block, or nullptr (no mask)
     const uint8_t* zrows;     // [rows][nchan] ascending channels, 1 = zapped
     const float* pad;         // [nblk][nchan] (pad_stride = nchan) or [1][nchan] (stride 0), or nullptr (0)

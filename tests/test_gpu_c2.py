@@ -46,7 +46,7 @@ def c2(engine):
     pts = rfifind_ptsperint(obs.dt)
     mask, pad = synth_mask(obs, s, pts)
     engine.set_mask(mask, pts, pad)
-    cl = OR.prepare(obs, Opts(), raw, mask=mask, ptsperint=pts, padvals=pad)
+    cl = OR.prepare(obs, Opts(), raw, mask=mask, ptsperint=pts, padvals=pad, omp=True)
     yield obs, s, raw, cl
     engine.set_mask()
 
