@@ -39,6 +39,8 @@ def parse():
                     help="stage-2 HIP streams (hd_set_streams): 2 overlaps consecutive passes (no launch tails; "
                          "per-kernel event times then include the shared time, so the roofline is taken at 1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU work for the baseline sample")
+    ap.add_argument("--e2e-beams", type=int, default=1,
+                    help="beams run end to end (.dat/.inf files written) after the timed steps; 0 = skip")
     ap.add_argument("--mode", choices=["beam", "shard"], default="beam",
                     help="beam: one beam per rank (weak scaling, configs[4]); shard: ONE beam's 57 passes "
                          "LPT-sharded over the ranks after an RCCL broadcast of the raw block (strong, configs[2])")
@@ -86,6 +88,7 @@ def build_plans(eng, obs, ddplans, variant):
                             dmstep=float(d.dmstep_arg()), numdms=d.dmsperpass, nsub=d.numsub,
                             ds=d.sub_downsamp, numout=P.choose_N(obs.N / d.downsamp))
             p = eng.plan(pp)
+            p.dmstrs = list(d.dmlist[i])
             if variant:
                 p.set_variant(variant)
             plans.append(p)
@@ -104,6 +107,55 @@ def run_step(eng, stages):
         for p in plans:
             p.run_dedisp(to_host=False)
     eng.sync()
+
+
+def e2e_dir(need_bytes):
+    """tmpfs when it has room (the reference's base_tmp_dir is /dev/shm), else the temp dir."""
+    import shutil
+    import tempfile
+    for base in ("/dev/shm", tempfile.gettempdir()):
+        try:
+            if os.path.isdir(base) and shutil.disk_usage(base).free > need_bytes:
+                return tempfile.mkdtemp(prefix="hd_e2e_", dir=base)
+        except OSError:
+            pass
+    return None
+
+
+def end_to_end(eng, stages, obs, outdir):
+    """One beam as the reference's search loop produces it (PALFA2_presto_search.py:494-537):
+    per DDplan stage, stage 1 of its passes, then per pass stage 2 and the pass's
+    <base>_DM<dm>.dat/.inf files in outdir (device series -> pinned buffers -> writer
+    threads, hd_write_series; .inf text from Python), the clock running until every file
+    of the stage is complete.  The files of each stage are then deleted with the clock
+    stopped (the reference removes each .dat after its per-DM tools, :598-606)."""
+    from hipdedisp.formats.inf import InfoData
+    from hipdedisp.formats.series import write_dats_device
+    info = InfoData(name="", telescope="Arecibo", instrument="Mock", object="synthetic", ra="00:00:00.0000",
+                    dec="00:00:00.0000", observer="hipdedisp bench", mjd=56000.0, bary=0, dt=obs.dt,
+                    freq=obs.lofreq, freqband=obs.nchan * obs.df, num_chan=obs.nchan, chan_wid=obs.df)
+    base = os.path.join(outdir, "beam")
+    w0, b0 = eng.wait_writes()
+    elapsed = 0.0
+    eng.sync()
+    t = time.perf_counter()
+    eng.touch_raw()
+    for plans in stages:
+        if not plans:
+            continue
+        eng.run_subband_multi(plans)
+        for p in plans:
+            p.run_dedisp(to_host=False)
+            info.dt, info.freq, info.chan_wid, info.num_chan = p.sub_dt, p.sub_lofreq, p.sub_chanwid, p.pp.nsub
+            info.freqband = p.pp.nsub * p.sub_chanwid
+            write_dats_device(p, base, p.dmstrs, info, p.nds, wait=False)
+        eng.wait_writes()
+        elapsed += time.perf_counter() - t
+        for f in os.listdir(outdir):
+            os.remove(os.path.join(outdir, f))
+        t = time.perf_counter()
+    w1, b1 = eng.wait_writes()
+    return elapsed, b1 - b0, w1 - w0
 
 
 def shard_stages(eng, obs, ddplans, rank, world, variant):
@@ -298,6 +350,23 @@ def main():
     }
     if shard:
         line["broadcast_ms_per_step"] = 1e3 * bcast_s / args.steps
+    if not shard and args.e2e_beams > 0:
+        out_bytes = 4 * sum(p.pp.numdms * p.numout for p in plans)
+        outdir = e2e_dir(1.1 * max(4 * p.pp.numdms * p.numout for p in plans) * 30)
+        if outdir:
+            tot = nb = wsec = 0.0
+            for _ in range(args.e2e_beams):
+                el, b, w = end_to_end(eng, stages, obs, outdir)
+                tot, nb, wsec = tot + el, nb + b, wsec + w
+            os.rmdir(outdir)
+            beams = args.e2e_beams
+            line["end_to_end"] = {
+                "samples_per_s": out_per_step * beams / tot, "s_per_beam": tot / beams,
+                "dat_bytes_per_beam": out_bytes, "write_GBps": nb / tot / 1e9,
+                "writer_busy_s_per_beam": wsec / beams, "dir": os.path.dirname(outdir),
+                "note": "stage 1 + stage 2 + every .dat/.inf file of the 57 passes complete in the directory; "
+                        "per-rank (this rank's beam)"}
+            line["end_to_end_samples_per_s"] = line["end_to_end"]["samples_per_s"]
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(obs, synth, ddplans, args.cpu_seconds, mask, pts, pad, omp=False)
         line["cpu_baseline_openmp"] = cpu_baseline(obs, synth, ddplans, args.cpu_seconds, mask, pts, pad, omp=True)

@@ -252,6 +252,18 @@ HD_API int hd_run_dedisp(hd_plan* plan, float* host_out);
 /* Samples [t0, t0+count) of DMs [dm0, dm0+ndm) of the device-resident series of the last
  * hd_run_dedisp, host layout [ndm][count] (t0+count <= numout).                        */
 HD_API int hd_get_series(hd_plan* plan, int32_t dm0, int32_t ndm, int64_t t0, int64_t count, float* host);
+/* The .dat output path (replaces the files prepsubband leaves in the tempdir,
+ * PALFA2_presto_search.py:514-520, 532-537): queue the device-resident series of the last
+ * hd_run_dedisp of this plan to paths[numdms] -- raw little-endian float32, numout samples,
+ * no header.  Chunks are copied device->host into pinned buffers on a copy stream ordered
+ * after the plan's stage 2 (so later kernels keep running) and written by a pool of writer
+ * threads.  wait = 0 returns once everything is queued; wait = 1 also waits for the files.
+ * A later hd_run_dedisp of the plan is ordered after its queued copies.                */
+HD_API int hd_write_series(hd_plan* plan, const char* const* paths, int32_t wait);
+/* Wait for every queued write of the context; *write_seconds / *bytes (may be NULL): the
+ * writer threads' cumulative busy seconds and bytes written since hd_open.  Returns the
+ * first I/O error of the writes (HD_E_IO) if any.                                       */
+HD_API int hd_wait_writes(hd_ctx* ctx, double* write_seconds, int64_t* bytes);
 /* Device-time of the last hd_run_subband / hd_run_dedisp of this plan, ms.           */
 HD_API int hd_plan_last_ms(const hd_plan* plan, float* ms_subband, float* ms_dedisp);
 /* Kernel variants: (s1 << 8) | s2.  s2: 0 auto, 1 direct, 2 LDS-tiled (4 waves x 256 samples),

@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "hd_internal.h"
+#include "hd_io.h"
 #include "../../include/hipdedisp.h"
 
 #define HD_VERSION_STR "hipdedisp 0.1.0 (gfx950)"
@@ -88,6 +89,7 @@ struct hd_ctx {
     uint32_t dd_count = 0;
     double* d_partial2 = nullptr;
     size_t partial_bytes2 = 0;
+    hd::Writer* writer = nullptr;   // .dat output path (hd_io.hip), opened on first use
 };
 
 // main-stream work from here on runs after every stage-2 pass queued on stream2
@@ -146,6 +148,8 @@ struct hd_plan {
     int32_t probe = 0;              // profiling switches (hd_plan_set_variant bits 16-23)
     int32_t pair_persist = 0;       // hd_plan_set_variant bits 24-25 (pair kernel tile scheduling)
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t ev_copy = nullptr;   // after the writer's copies of this plan's series
+    bool copy_pending = false;
     bool ran_sub = false, ran_dd = false;
     hipStream_t dd_stream = nullptr;  // stream of the last hd_run_dedisp (its ev[3] marks the end)
 };
@@ -303,6 +307,12 @@ extern "C" int hd_close(hd_ctx* c)
     if (!c) return HD_OK;
     (void)hipSetDevice(c->device);
     (void)sync_all(c);
+    if (c->writer) {
+        std::string e;
+        (void)hd::writer_wait(c->writer, e, nullptr, nullptr);
+        hd::writer_close(c->writer);
+        c->writer = nullptr;
+    }
     free_obs_buffers(c);
     dfree(c->d_partial);
     dfree(c->d_partial2);
@@ -844,6 +854,7 @@ static void plan_free(hd_plan* p)
     dfree(p->d_sub);
     for (auto& e : p->ev)
         if (e) (void)hipEventDestroy(e);
+    if (p->ev_copy) (void)hipEventDestroy(p->ev_copy);
 }
 
 struct Tables {
@@ -1201,6 +1212,7 @@ extern "C" int hd_plan_destroy(hd_plan* p)
     hd_ctx* c = p->ctx;
     (void)hipSetDevice(c->device);
     (void)sync_all(c);
+    if (p->copy_pending && c->writer) (void)hipEventSynchronize(p->ev_copy);   // copies read p->d_out
     plan_free(p);
     delete p;
     return HD_OK;
@@ -1843,6 +1855,10 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
     }
     if (p->ran_dd && p->dd_stream != st) HIPCHK(c, hipStreamWaitEvent(st, p->ev[3], 0));
+    if (p->copy_pending) {            // the writer may still be copying the previous series
+        HIPCHK(c, hipStreamWaitEvent(st, p->ev_copy, 0));
+        p->copy_pending = false;
+    }
     // pair partials need |sub[s0] + sub[s1]| <= 32767 (packed int16), known on the host
     const bool pair_ok = p->wide[3].ok && p->sub_bound >= 0 && 2 * p->sub_bound <= 32767;
     if (p->variant == 6 && !pair_ok)
@@ -1933,6 +1949,38 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
                                    sizeof(float) * p->numout, p->pass.numdms, hipMemcpyDeviceToHost, st));
         HIPCHK(c, hipStreamSynchronize(st));
     }
+    return HD_OK;
+}
+
+extern "C" int hd_write_series(hd_plan* p, const char* const* paths, int32_t wait)
+{
+    if (!p || !paths) return fail(p ? p->ctx : nullptr, HD_E_INVAL, "hd_write_series: NULL argument");
+    hd_ctx* c = p->ctx;
+    if (!p->ran_dd || !p->d_out) return fail(c, HD_E_STATE, "hd_write_series: run hd_run_dedisp first");
+    for (int d = 0; d < p->pass.numdms; d++)
+        if (!paths[d]) return fail(c, HD_E_INVAL, "hd_write_series: path %d is NULL", d);
+    HIPCHK(c, hipSetDevice(c->device));
+    if (!c->writer) HIPCHK(c, hd::writer_open(&c->writer, c->device));
+    if (!p->ev_copy) HIPCHK(c, hipEventCreateWithFlags(&p->ev_copy, hipEventDisableTiming));
+    std::string err;
+    int rc = hd::writer_series(c->writer, p->ev[3], p->d_out, p->out_stride, p->pass.numdms, p->numout, paths, err);
+    if (rc == 0) {
+        HIPCHK(c, hipEventRecord(p->ev_copy, hd::writer_stream(c->writer)));
+        p->copy_pending = true;
+    }
+    if (rc) return fail(c, rc, "hd_write_series: %s", err.c_str());
+    if (wait) return hd_wait_writes(c, nullptr, nullptr);
+    return HD_OK;
+}
+
+extern "C" int hd_wait_writes(hd_ctx* c, double* write_seconds, int64_t* bytes)
+{
+    if (!c) return fail(nullptr, HD_E_INVAL, "hd_wait_writes: NULL context");
+    if (write_seconds) *write_seconds = 0.0;
+    if (bytes) *bytes = 0;
+    if (!c->writer) return HD_OK;
+    std::string err;
+    if (hd::writer_wait(c->writer, err, write_seconds, bytes)) return fail(c, HD_E_IO, "hd_wait_writes: %s", err.c_str());
     return HD_OK;
 }
 

@@ -37,7 +37,7 @@ EXPORTED = [
     "hd_set_subbands", "hd_run_dedisp", "hd_plan_last_ms", "hd_plan_set_variant",
     "hd_get_raw", "hd_plan_tables", "hd_run_subband_multi", "hd_push_raw_device", "hd_get_raw_device",
     "hd_push_raw_file", "hd_set_streams", "hd_touch_raw", "hd_stats_padvals", "hd_get_clean",
-    "hd_get_subbands_window", "hd_get_series",
+    "hd_get_subbands_window", "hd_get_series", "hd_write_series", "hd_wait_writes",
 ]
 
 
@@ -134,6 +134,8 @@ def load():
         "hd_get_subbands": (ctypes.c_int, [vp, vp]),
         "hd_get_subbands_window": (ctypes.c_int, [vp, i64, i64, vp]),
         "hd_get_series": (ctypes.c_int, [vp, i32, i32, i64, i64, f32p]),
+        "hd_write_series": (ctypes.c_int, [vp, P(ctypes.c_char_p), i32]),
+        "hd_wait_writes": (ctypes.c_int, [vp, P(ctypes.c_double), P(i64)]),
         "hd_set_subbands": (ctypes.c_int, [vp, vp]),
         "hd_run_dedisp": (ctypes.c_int, [vp, f32p]),
         "hd_plan_last_ms": (ctypes.c_int, [vp, f32p, f32p]),

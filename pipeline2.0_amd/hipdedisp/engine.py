@@ -253,6 +253,12 @@ class Engine:
     def synth_device(self, synth: hd_synth):
         self._chk(self._L.hd_synth_device(self._ctx, ctypes.byref(synth)), "hd_synth_device")
 
+    def wait_writes(self):
+        """hd_wait_writes: every queued .dat write done; (writer busy seconds, bytes) so far."""
+        sec, nb = ctypes.c_double(), ctypes.c_int64()
+        self._chk(self._L.hd_wait_writes(self._ctx, ctypes.byref(sec), ctypes.byref(nb)), "hd_wait_writes")
+        return sec.value, nb.value
+
     def plan(self, pp: PassParams):
         return Plan(self, pp)
 
@@ -346,6 +352,13 @@ class Plan:
                       "prepsubband -lodm %.2f -dmstep %.2f -numdms %d"
                       % (self.pp.lodm, self.pp.dmstep, self.pp.numdms))
         return out
+
+    def write_series(self, paths, wait=True):
+        """hd_write_series: the device series of the last run_dedisp to paths[numdms] (.dat)."""
+        if len(paths) != self.pp.numdms:
+            raise PrestoError("write_series needs %d paths, got %d" % (self.pp.numdms, len(paths)))
+        arr = (ctypes.c_char_p * len(paths))(*[os.fsencode(p) for p in paths])
+        self.eng._chk(self.eng._L.hd_write_series(self._p, arr, int(bool(wait))), "hd_write_series")
 
     def last_ms(self):
         a, b = ctypes.c_float(), ctypes.c_float()

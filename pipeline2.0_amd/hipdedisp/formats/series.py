@@ -46,15 +46,30 @@ def dat_basename(outbase, dmstr):
     return "%s_DM%s" % (outbase, dmstr)
 
 
-def write_dats(outbase, dmstrs, series, info_template: InfoData, nds):
-    """series: [numdms][numout] float32.  Writes <outbase>_DM<dm>.dat/.inf per DM."""
-    numout = series.shape[1]
-    for dmstr, row in zip(dmstrs, series):
+def write_infs(outbase, dmstrs, info_template: InfoData, nds, numout):
+    """<outbase>_DM<dm>.inf per DM (the padded tail recorded as an on/off break)."""
+    for dmstr in dmstrs:
         base = dat_basename(outbase, dmstr)
-        row.astype(np.float32, copy=False).tofile(base + ".dat")
         d = InfoData(**{**info_template.__dict__})
         d.name = os.path.basename(base)
         d.dm = float(dmstr)
         d.N = numout
         d.onoff = [0.0, float(nds - 1), float(numout - 1), float(numout - 1)] if numout > nds else []
         write_inf(base + ".inf", d)
+
+
+def write_dats(outbase, dmstrs, series, info_template: InfoData, nds):
+    """series: [numdms][numout] float32 on the host.  Writes <outbase>_DM<dm>.dat/.inf per DM."""
+    for dmstr, row in zip(dmstrs, series):
+        row.astype(np.float32, copy=False).tofile(dat_basename(outbase, dmstr) + ".dat")
+    write_infs(outbase, dmstrs, info_template, nds, series.shape[1])
+
+
+def write_dats_device(plan, outbase, dmstrs, info_template: InfoData, nds, wait=True):
+    """The device-resident series of plan (after run_dedisp(to_host=False)) straight to
+    <outbase>_DM<dm>.dat through the library's pinned-buffer writer threads
+    (hd_write_series), the .inf files meanwhile from here."""
+    plan.write_series([dat_basename(outbase, d) + ".dat" for d in dmstrs], wait=False)
+    write_infs(outbase, dmstrs, info_template, nds, plan.numout)
+    if wait:
+        plan.eng.wait_writes()

@@ -29,7 +29,7 @@ from .engine import Engine, Opts, PassParams, PrestoError
 from .formats import psrfits
 from .formats.inf import InfoData
 from .formats.mask import mask_padvals, read_mask
-from .formats.series import write_dats, write_subbands
+from .formats.series import write_dats_device, write_subbands
 
 
 class DedispJob:
@@ -160,9 +160,9 @@ def run_pass(job, ddplan, passnum, maskfilenm, tempdir):
             write_subbands(os.path.join(tempdir, "subbands", subbasenm), plan.get_subbands(), info)
         t_sub = time.time() - t0
         t0 = time.time()
-        series = plan.run_dedisp(to_host=True)
+        plan.run_dedisp(to_host=False)
         info = job.info_template(pp.nsub, plan.sub_lofreq, plan.sub_chanwid, plan.sub_dt)
-        write_dats(os.path.join(tempdir, job.basefilenm), ddplan.dmlist[passnum], series, info, plan.nds)
+        write_dats_device(plan, os.path.join(tempdir, job.basefilenm), ddplan.dmlist[passnum], info, plan.nds)
         t_dd = time.time() - t0
     finally:
         plan.destroy()
@@ -182,9 +182,9 @@ def _run_pass_nosub(job, ddplan, passnum, maskfilenm, tempdir):
     try:
         t0 = time.time()
         plan.run_subband()
-        series = plan.run_dedisp(to_host=True)
+        plan.run_dedisp(to_host=False)
         info = job.info_template(pp.nsub, plan.sub_lofreq, plan.sub_chanwid, plan.sub_dt)
-        write_dats(os.path.join(tempdir, job.basefilenm), ddplan.dmlist[passnum], series, info, plan.nds)
+        write_dats_device(plan, os.path.join(tempdir, job.basefilenm), ddplan.dmlist[passnum], info, plan.nds)
         t_dd = time.time() - t0
     finally:
         plan.destroy()

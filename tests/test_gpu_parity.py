@@ -642,3 +642,37 @@ def test_prepsubband_cli_shim_commands(engine, tmp_path):
     for k in (0, 7):
         got = np.fromfile(str(tmp_path / ("nosub_DM%.2f.dat" % (100.0 + k))), np.float32)
         assert np.array_equal(got, want[k]), k
+
+
+def test_write_series_async_files(engine, tmp_path):
+    """hd_write_series: the device series of a pass land in .dat files (pinned buffers, copy
+    stream, writer threads) equal to the host copy, while the next pass runs; re-running a
+    plan with copies still queued is ordered after them; a bad path fails with HD_E_IO."""
+    obs = palfa_obs(N=3 * 8192 + 5, nbits=8)
+    load_beam(engine, obs)
+    d = plan.ddplans_for("pdev")[2]
+    plans = [engine.plan(PassParams(subdm=float(d.subdmlist[i]), lodm=float(d.lodm_arg(i)),
+                                    dmstep=float(d.dmstep_arg()), numdms=d.dmsperpass, nsub=96, ds=d.sub_downsamp,
+                                    numout=obs.N // 3 + 100)) for i in range(3)]
+    try:
+        engine.run_subband_multi(plans)
+        paths = []
+        for i, p in enumerate(plans):
+            p.run_dedisp(to_host=False)
+            paths.append([str(tmp_path / ("p%d_DM%s.dat" % (i, s))) for s in d.dmlist[i]])
+            p.write_series(paths[-1], wait=False)
+        want0 = plans[0].get_series()
+        plans[0].run_dedisp(to_host=False)            # ordered after its queued copies
+        sec, nbytes = engine.wait_writes()
+        assert nbytes >= 3 * 76 * 4 * plans[0].numout and sec > 0
+        for i, p in enumerate(plans):
+            want = p.get_series()
+            for k in (0, 40, 75):
+                got = np.fromfile(paths[i][k], np.float32)
+                assert np.array_equal(got, want[k]), (i, k)
+        assert np.array_equal(plans[0].get_series(), want0)
+        with pytest.raises(PrestoError, match="cannot create"):
+            plans[1].write_series([str(tmp_path / "missing_dir" / "x.dat")] * 76)
+    finally:
+        for p in plans:
+            p.destroy()
