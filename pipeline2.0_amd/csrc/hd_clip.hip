@@ -307,8 +307,9 @@ hipError_t launch_clip(const ClipArgs& a, hipStream_t st)
 // ------------------------------------------------------------------------------------
 // stage-1 fixup
 // ------------------------------------------------------------------------------------
-// One workgroup per (event e, pass p); the pass's channel delays, and the zap rows and pad
-// rows of the (at most two) read blocks the item's rows fall in, are staged in LDS.
+// One workgroup per event e, over the launch's passes: the zap rows and pad rows of the (at
+// most two) read blocks the event's rows fall in, and each pass's channel delays in turn,
+// are staged in LDS.
 //  * e < nev: the clipped spectrum r = events[e].  Channel c of subband s reads spectrum r
 //    for exactly one output, j = floor((r - d_c) / ds); those outputs (one per distinct j
 //    in the subband) are recomputed: at most cps per subband, usually far fewer.
@@ -318,7 +319,6 @@ hipError_t launch_clip(const ClipArgs& a, hipStream_t st)
 //    per-block constants do not cover; they are recomputed (every other subband was exact).
 // Recomputation is the exact per-cell fold of k_stage1_direct; overlapping events write
 // identical values.  Index arithmetic is 32-bit (the host checks N < 2^31).
-constexpr int kFixMaxSub = 1024, kFixMaxChan = 4096;
 
 struct FixCtx {
     const int* dly;          // LDS: delays of the pass
@@ -349,12 +349,12 @@ __device__ __forceinline__ int fix_one(const Stage1Multi& a, const FixCtx& f, in
     for (int k = 0; k < ds; k++) {
         float sk = 0.0f;
         const int tb = j * ds + k;
-        for (int c0 = 0; c0 < cps; c0 += 16) {
-            float x[16];
+        for (int c0 = 0; c0 < cps; c0 += 8) {
+            float x[8];
             if (fast) {
-                uint32_t b[16], cf[16];
+                uint32_t b[8], cf[8];
 #pragma unroll
-                for (int i = 0; i < 16; i++) {
+                for (int i = 0; i < 8; i++) {
                     const int cc = min(c0 + i, cps - 1);
                     const int c = s * cps + cc;
                     const int t = tb + f.dly[c];
@@ -363,7 +363,7 @@ __device__ __forceinline__ int fix_one(const Stage1Multi& a, const FixCtx& f, in
                     cf[i] = rd.clipped ? rd.clipped[tt] : 0u;
                 }
 #pragma unroll
-                for (int i = 0; i < 16; i++) {
+                for (int i = 0; i < 8; i++) {
                     const int cc = min(c0 + i, cps - 1);
                     const int c = s * cps + cc;
                     const int t = tb + f.dly[c];
@@ -377,14 +377,14 @@ __device__ __forceinline__ int fix_one(const Stage1Multi& a, const FixCtx& f, in
                 }
             } else {
 #pragma unroll
-                for (int i = 0; i < 16; i++) {
+                for (int i = 0; i < 8; i++) {
                     const int cc = min(c0 + i, cps - 1);
                     x[i] = fix_cell(rd, f, tb + f.dly[s * cps + cc], s * cps + cc);
                 }
             }
-            const int n = min(16, cps - c0);
+            const int n = min(8, cps - c0);
 #pragma unroll
-            for (int i = 0; i < 16; i++)
+            for (int i = 0; i < 8; i++)
                 if (i < n) sk += x[i];
         }
         acc += sk;
@@ -402,133 +402,147 @@ __device__ __forceinline__ int fix_one(const Stage1Multi& a, const FixCtx& f, in
 __global__ __launch_bounds__(256) void k_stage1_fixup(Stage1Multi a, const int32_t* __restrict__ events,
                                                      const int32_t* __restrict__ nevents, int boundaries)
 {
-    __shared__ int dly_s[kFixMaxChan];
-    __shared__ uint8_t zap_s[2 * kFixMaxChan];
-    __shared__ float pad_s[2 * kFixMaxChan];
-    __shared__ int jlo_s[kFixMaxSub], cnt_s[kFixMaxSub + 1];
-    __shared__ int amax_s, dmax_s;
+    // dynamic LDS: delays [nchan] | zap rows [2][nchan] | pad rows [2][nchan] | jlo, cnt [nsub+1]
+    extern __shared__ __attribute__((aligned(16))) char fsm[];
+    const int nchan = a.rd.nchan, nsub = a.nsub;
+    int* dly_s = (int*)fsm;
+    float* pad_s = (float*)(dly_s + nchan);
+    int* jlo_s = (int*)(pad_s + 2 * nchan);
+    int* cnt_s = jlo_s + nsub + 1;
+    uint8_t* zap_s = (uint8_t*)(cnt_s + nsub + 1);
+    __shared__ int amax_s[kMaxPass];
+    __shared__ int dmax_s, wsum[8];
     const int nev = *nevents;
     const int nbound = boundaries ? a.rd.nblk - 1 : 0;
-    const int nitems = (nev + nbound) * a.npass;
-    const int ds = a.ds, cps = a.cps, nsub = a.nsub, nchan = a.rd.nchan;
+    const int nitems = nev + nbound;
+    const int ds = a.ds, cps = a.cps;
     const int nds = (int)a.nds;
-    for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
-        const int e = it / a.npass, p = it - e * a.npass;
+    // the delays of every pass reach at most dmax rows: stage the blocks of [r - dmax - ds, ...]
+    if (threadIdx.x == 0) dmax_s = 0;
+    __syncthreads();
+    {
+        int m = 0;
+        for (int p = 0; p < a.npass; p++)
+            for (int c = threadIdx.x; c < nchan; c += blockDim.x) m = max(m, a.dly[p][c]);
+        m = wave_max_i32(m);
+        if ((threadIdx.x & 63) == 0) atomicMax(&dmax_s, m);
+    }
+    __syncthreads();
+    const int dmax = dmax_s;
+    for (int e = blockIdx.x; e < nitems; e += gridDim.x) {
         const bool clip_ev = e < nev;
         const int r = clip_ev ? events[e] : (e - nev + 1) * a.rd.blk;
-        __syncthreads();                                  // the previous item is done with LDS
-        if (threadIdx.x == 0) {
-            amax_s = 0;
-            dmax_s = 0;
-        }
-        __syncthreads();
-        int dmx = 0;
-        for (int c = threadIdx.x; c < nchan; c += blockDim.x) {
-            const int d = a.dly[p][c];
-            dly_s[c] = d;
-            dmx = max(dmx, d);
-        }
-        dmx = wave_max_i32(dmx);
-        if ((threadIdx.x & 63) == 0) atomicMax(&dmax_s, dmx);
-        __syncthreads();
-        // the item's rows: within [r - dmax - ds, r + dmax + ds]; stage the blocks they start in
         FixCtx f;
         f.dly = dly_s;
         f.zap2 = zap_s;
         f.pad2 = pad_s;
-        {
-            const int w = dmax_s + ds;
-            const int b0 = (int)blk_of(a.rd, max(r - w, 0));
-            f.b0 = b0;
-            f.bnd = (b0 + 1) * a.rd.blk;
-            f.lo = b0 * a.rd.blk;
-            f.hi = b0 + 1 < a.rd.nblk ? min((int64_t)(b0 + 2) * a.rd.blk, a.rd.N) : a.rd.N;
-            const int b1 = min(b0 + 1, a.rd.nblk - 1);
-            for (int c = threadIdx.x; c < nchan; c += blockDim.x) {
-                zap_s[c] = zap_at(a.rd, b0, c);
-                zap_s[nchan + c] = zap_at(a.rd, b1, c);
-                pad_s[c] = pad_at(a.rd, b0, c);
-                pad_s[nchan + c] = pad_at(a.rd, b1, c);
+        const int b0 = (int)blk_of(a.rd, max(r - dmax - ds, 0));
+        f.b0 = b0;
+        f.bnd = (b0 + 1) * a.rd.blk;
+        f.lo = b0 * a.rd.blk;
+        f.hi = b0 + 1 < a.rd.nblk ? (int)min((int64_t)(b0 + 2) * a.rd.blk, a.rd.N) : (int)a.rd.N;
+        const int b1 = min(b0 + 1, a.rd.nblk - 1);
+        __syncthreads();                                  // the previous event is done with LDS
+        for (int c = threadIdx.x; c < nchan; c += blockDim.x) {
+            zap_s[c] = zap_at(a.rd, b0, c);
+            zap_s[nchan + c] = zap_at(a.rd, b1, c);
+            pad_s[c] = pad_at(a.rd, b0, c);
+            pad_s[nchan + c] = pad_at(a.rd, b1, c);
+        }
+        if (threadIdx.x < kMaxPass) amax_s[threadIdx.x] = 0;
+        for (int p = 0; p < a.npass; p++) {
+            __syncthreads();                              // zap/pad staged; previous pass done with dly_s
+            for (int c = threadIdx.x; c < nchan; c += blockDim.x) dly_s[c] = a.dly[p][c];
+            __syncthreads();
+            int amax = 0;
+            if (clip_ev) {
+                for (int c = threadIdx.x; c < nchan; c += blockDim.x) {
+                    const int s = c / cps;
+                    const int jn = r - dly_s[c];
+                    if (jn < 0) continue;
+                    const int j = jn / ds;
+                    if (j >= nds) continue;
+                    bool dup = false;                     // an earlier channel already names j
+                    for (int c2 = s * cps; c2 < c; c2++) {
+                        const int jn2 = r - dly_s[c2];
+                        dup |= jn2 >= 0 && jn2 / ds == j;
+                    }
+                    if (!dup) amax = max(amax, fix_one(a, f, p, s, j));
+                }
+            } else {
+                const int bb = e - nev + 1;               // boundary between blocks bb-1 and bb
+                const bool staged = bb - b0 == 1;
+                int n = 0;
+                const int s = threadIdx.x;                // nsub <= blockDim.x (host check)
+                if (s < nsub) {
+                    int mind = 1 << 30, maxd = 0;
+                    bool need = false;
+                    for (int cc = 0; cc < cps; cc++) {
+                        const int c = s * cps + cc;
+                        mind = min(mind, dly_s[c]);
+                        maxd = max(maxd, dly_s[c]);
+                        if (staged)
+                            need |= zap_s[c] && zap_s[nchan + c] && pad_s[c] != pad_s[nchan + c];
+                        else
+                            need |= zap_at(a.rd, bb - 1, c) && zap_at(a.rd, bb, c) &&
+                                    pad_at(a.rd, bb - 1, c) != pad_at(a.rd, bb, c);
+                    }
+                    int lo = r - (ds - 1) - maxd, hi = r - 1 - mind;
+                    lo = lo <= 0 ? 0 : (lo + ds - 1) / ds;   // ceil for lo > 0
+                    hi = hi < 0 ? -1 : min(hi / ds, nds - 1);
+                    jlo_s[s] = lo;
+                    n = need && hi >= lo ? hi - lo + 1 : 0;
+                }
+                // exclusive scan of the task counts over the workgroup (wave scans + wave sums)
+                const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+                int incl = n;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const int v = __shfl_up(incl, d, 64);
+                    if (lane >= d) incl += v;
+                }
+                if (lane == 63) wsum[w] = incl;
+                __syncthreads();
+                int base = 0;
+                for (int k = 0; k < w; k++) base += wsum[k];
+                int total = 0;
+                for (int k = 0; k < (int)(blockDim.x >> 6); k++) total += wsum[k];
+                if (s < nsub) cnt_s[s] = base + incl - n;
+                __syncthreads();
+                for (int t = threadIdx.x; t < total; t += blockDim.x) {
+                    int lo = 0, hi = nsub - 1;            // subband of task t: last s with cnt_s[s] <= t
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (cnt_s[mid] <= t) lo = mid;
+                        else hi = mid - 1;
+                    }
+                    amax = max(amax, fix_one(a, f, p, lo, jlo_s[lo] + (t - cnt_s[lo])));
+                }
+            }
+            if (a.sub_dtype == 0) {
+                amax = wave_max_i32(amax);
+                if ((threadIdx.x & 63) == 0 && amax > 0) atomicMax(&amax_s[p], amax);
             }
         }
         __syncthreads();
-        int amax = 0;
-        if (clip_ev) {
-            for (int c = threadIdx.x; c < nchan; c += blockDim.x) {
-                const int s = c / cps;
-                const int jn = r - dly_s[c];
-                if (jn < 0) continue;
-                const int j = jn / ds;
-                if (j >= nds) continue;
-                bool dup = false;                         // an earlier channel already names j
-                for (int c2 = s * cps; c2 < c; c2++) {
-                    const int jn2 = r - dly_s[c2];
-                    dup |= jn2 >= 0 && jn2 / ds == j;
-                }
-                if (!dup) amax = max(amax, fix_one(a, f, p, s, j));
-            }
-        } else {
-            const int bb = e - nev + 1;                   // boundary between blocks bb-1 and bb
-            const int hb = bb - f.b0;                     // their parts in the staged rows
-            for (int s = threadIdx.x; s < nsub; s += blockDim.x) {
-                int mind = 1 << 30, maxd = 0;
-                bool need = false;
-                for (int cc = 0; cc < cps; cc++) {
-                    const int c = s * cps + cc;
-                    mind = min(mind, dly_s[c]);
-                    maxd = max(maxd, dly_s[c]);
-                    if (hb == 1)
-                        need |= zap_s[c] && zap_s[nchan + c] && pad_s[c] != pad_s[nchan + c];
-                    else
-                        need |= zap_at(a.rd, bb - 1, c) && zap_at(a.rd, bb, c) &&
-                                pad_at(a.rd, bb - 1, c) != pad_at(a.rd, bb, c);
-                }
-                int lo = r - (ds - 1) - maxd, hi = r - 1 - mind;
-                lo = lo <= 0 ? 0 : (lo + ds - 1) / ds;   // ceil for lo > 0
-                hi = hi < 0 ? -1 : hi / ds;
-                hi = min(hi, nds - 1);
-                jlo_s[s] = lo;
-                cnt_s[s] = need && hi >= lo ? hi - lo + 1 : 0;
-            }
-            __syncthreads();
-            if (threadIdx.x == 0) {                       // exclusive prefix sum (nsub is small)
-                int acc = 0;
-                for (int s = 0; s < nsub; s++) {
-                    const int n = cnt_s[s];
-                    cnt_s[s] = acc;
-                    acc += n;
-                }
-                cnt_s[nsub] = acc;
-            }
-            __syncthreads();
-            const int ntask = cnt_s[nsub];
-            for (int t = threadIdx.x; t < ntask; t += blockDim.x) {
-                int lo = 0, hi = nsub - 1;                // subband of task t: last s with cnt_s[s] <= t
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (cnt_s[mid] <= t) lo = mid;
-                    else hi = mid - 1;
-                }
-                amax = max(amax, fix_one(a, f, p, lo, jlo_s[lo] + (t - cnt_s[lo])));
-            }
-        }
-        if (a.sub_dtype == 0) {
-            amax = wave_max_i32(amax);
-            if ((threadIdx.x & 63) == 0 && amax > 0) atomicMax(&amax_s, amax);
-            __syncthreads();
-            if (threadIdx.x == 0) publish_max(a.maxabs[p], amax_s);
-        }
+        if (a.sub_dtype == 0 && threadIdx.x < a.npass) publish_max(a.maxabs[threadIdx.x], amax_s[threadIdx.x]);
     }
+}
+
+size_t fixup_lds_bytes(const Stage1Multi& a)
+{
+    return (size_t)a.rd.nchan * 4 + (size_t)2 * a.rd.nchan * 4 + (size_t)2 * (a.nsub + 1) * 4 + (size_t)2 * a.rd.nchan;
 }
 
 hipError_t launch_stage1_fixup(const Stage1Multi& a, const int32_t* events, const int32_t* nevents, int boundaries,
                                hipStream_t st)
 {
     if (a.nds <= 0 || a.npass <= 0) return hipSuccess;
-    if (a.nsub > kFixMaxSub || a.rd.nchan > kFixMaxChan || a.rd.N >= ((int64_t)1 << 31) - (1 << 24))
-        return hipErrorInvalidValue;
-    // grid-stride over a device-side item count: no host round trip for the event count
-    hipLaunchKernelGGL(k_stage1_fixup, dim3(4096), dim3(256), 0, st, a, events, nevents, boundaries);
+    if (a.nsub > 256 || a.rd.N >= ((int64_t)1 << 31) - (1 << 24)) return hipErrorInvalidValue;
+    const size_t lds = fixup_lds_bytes(a);
+    if (lds > 64 * 1024) return hipErrorInvalidValue;
+    // grid-stride over a device-side event count: no host round trip for the count
+    hipLaunchKernelGGL(k_stage1_fixup, dim3(4096), dim3(256), lds, st, a, events, nevents, boundaries);
     return hipGetLastError();
 }
 
