@@ -82,12 +82,17 @@ def by_stage(passes: Sequence[PassRef]) -> List[Tuple[int, List[int]]]:
 def broadcast_raw(tensor, src=0, group=None, chunk_bytes=256 << 20):
     """Broadcast a flat uint8 tensor (the raw block) from `src` in chunks of `chunk_bytes`
     (RCCL on GPU tensors, gloo on CPU tensors).  Chunking bounds the staging each collective
-    needs and lets a receiver start copying early."""
+    needs.  Returns when the data is in `tensor` on this rank (GPU: stream synchronised)."""
     import torch.distributed as dist
     flat = tensor.view(-1)
     n = flat.numel()
     for off in range(0, n, chunk_bytes):
         dist.broadcast(flat[off:off + chunk_bytes], src=src, group=group)
+    # RCCL queues the broadcast on torch's current stream; hd_push_raw_device copies on the
+    # engine's own stream, which has no ordering with it: return only once the data landed
+    if flat.is_cuda:
+        import torch
+        torch.cuda.current_stream(flat.device).synchronize()
 
 
 class ShardedBeam:

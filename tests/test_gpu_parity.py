@@ -676,3 +676,47 @@ def test_write_series_async_files(engine, tmp_path):
     finally:
         for p in plans:
             p.destroy()
+
+
+@pytest.mark.parametrize("fold_rawdata", [True, False])
+def test_reference_pass_loop_control_flow(engine, tmp_path, fold_rawdata):
+    """The reference's own loop around the drop-in (PALFA2_presto_search.py:494-615 with the
+    INTEGRATION.md patch): run_pass, then the per-DM .dat/.inf handling, then :608-614 --
+    shutil.rmtree(tempdir/subbands) when folding raw data, else moving the .subNN files to
+    workdir/subbands.  Neither branch may raise, and without fold_rawdata the subband files
+    the folds need (one per subband plus .sub.inf) must be there to move."""
+    import copy
+    import glob
+    import os
+    import shutil
+    from hipdedisp.formats import psrfits
+    from hipdedisp.search_stage import DedispJob, run_pass
+    obs = palfa_obs(N=4096, nbits=8, nsblk=512)
+    fn = str(tmp_path / "beam.fits")
+    psrfits.write_psrfits(fn, host_spectra(obs, palfa_synth()), obs)
+    workdir = tmp_path / "work"
+    (workdir / "subbands").mkdir(parents=True)
+    job = DedispJob([fn], resultsdir=str(workdir), tmpdir_base=str(tmp_path), device=0,
+                    backend="pdev", keep_subbands=not fold_rawdata)
+    try:
+        d = copy.copy(job.ddplans[0])
+        d.numpasses = 2
+        for passnum in range(d.numpasses):
+            run_pass(job, d, passnum, None, job.tempdir)
+            for dmstr in d.dmlist[passnum]:                                    # :531-606
+                basenm = os.path.join(job.tempdir, job.basefilenm + "_DM" + dmstr)
+                assert os.path.getsize(basenm + ".dat") > 0
+                shutil.move(basenm + ".inf", str(workdir))
+                os.remove(basenm + ".dat")
+            if fold_rawdata:                                                    # :608-611
+                shutil.rmtree(os.path.join(job.tempdir, "subbands"))
+            else:                                                               # :612-614
+                subs = glob.glob(os.path.join(job.tempdir, "subbands", "*"))
+                assert len(subs) == d.numsub + 1, len(subs)
+                for sub in subs:
+                    shutil.move(sub, os.path.join(str(workdir), "subbands"))
+        moved = os.listdir(workdir / "subbands")
+        assert len(moved) == (0 if fold_rawdata else d.numpasses * (d.numsub + 1))
+        assert len(glob.glob(str(workdir / "*.inf"))) == d.numpasses * d.dmsperpass
+    finally:
+        job.close()
