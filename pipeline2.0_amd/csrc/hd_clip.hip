@@ -534,10 +534,226 @@ size_t fixup_lds_bytes(const Stage1Multi& a)
     return (size_t)a.rd.nchan * 4 + (size_t)2 * a.rd.nchan * 4 + (size_t)2 * (a.nsub + 1) * 4 + (size_t)2 * a.rd.nchan;
 }
 
+// ------------------------------------------------------------------------------------
+// stage-1 fixup, 8-bit data without calibration: LDS windows from the channel-major copy
+// ------------------------------------------------------------------------------------
+// The items are those of k_stage1_fixup (clipped spectra, then read-block boundaries), but
+// a workgroup takes one (item r, chunk of SG subbands) and first copies the raw window every
+// output it may recompute reads -- rows [r - dmax - ds + 1, r + dmax + ds) of the chunk's G
+// channels, coalesced 16-byte runs of rawT -- into LDS, with the window's replaced-row flags
+// (clipped, or past N), the zap/pad rows of its two read blocks and the chunk's delays of
+// every pass.  The exact folds then read only LDS: per output cps*ds LDS bytes instead of as
+// many scattered global byte loads (plus a clip-flag load each).
+// Window bound: an output j that channel c maps r to (j = floor((r - d_c)/ds)) reads rows
+// j*ds + k + d_c' >= r - d_c - ds + 1 >= r - dmax - ds + 1 and <= r - d_c + ds - 1 + dmax;
+// a boundary output (rows containing r - 1 and r) stays inside the same bounds.  The host
+// only takes this kernel when the window is shorter than a read block (<= 2 blocks staged).
+struct Fix8Geom {
+    int SG, G, Wp;            // subbands per chunk, channels per chunk, LDS bytes per channel row
+    int nchunk, jmax;         // chunks per item; boundary outputs per (pass, subband) at most
+};
+
+__device__ __forceinline__ float fix8_fold(const Stage1Multi& a, const uint8_t* lraw, const uint8_t* flg,
+                                           const uint8_t* zap, const float* pad, const int16_t* dl, int Wp, int G,
+                                           int lc0, int64_t trel, int bndrel)
+{
+    // trel = j*ds - wlo: window row of (k = 0, delay 0); dl: this pass's delays of the chunk
+    const int ds = a.ds, cps = a.cps;
+    float acc = 0.0f;
+    for (int k = 0; k < ds; k++) {
+        float sk = 0.0f;
+        for (int cc = 0; cc < cps; cc++) {
+            const int lc = lc0 + cc;
+            const int lr = (int)trel + k + dl[lc];
+            const int part = lr >= bndrel;
+            const bool rep = flg[lr] | zap[part * G + lc];
+            const float x = rep ? pad[part * G + lc] : (float)lraw[lc * Wp + lr];
+            sk += x;
+        }
+        acc += sk;
+    }
+    if (a.ds_mode == 1) acc = acc / (float)ds;
+    return acc;
+}
+
+__global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm, const int32_t* __restrict__ events,
+                                                    const int32_t* __restrict__ nevents, int boundaries)
+{
+    // dynamic LDS: raw [G][Wp] | flags [Wp] | zap [2][G] | pad [2][G] f32 | dly [npass][G] i16
+    //              | lo, cnt [npass][SG] (boundary items)
+    extern __shared__ __attribute__((aligned(16))) char fsm[];
+    const int G = gm.G, Wp = gm.Wp, SG = gm.SG, npass = a.npass, cps = a.cps, ds = a.ds;
+    uint8_t* lraw = (uint8_t*)fsm;
+    uint8_t* flg = lraw + G * Wp;
+    float* pad = (float*)(flg + Wp);                      // Wp is a multiple of 16
+    uint8_t* zap = (uint8_t*)(pad + 2 * G);
+    int16_t* dly = (int16_t*)(zap + ((2 * G + 15) & ~15));
+    int* lo_s = (int*)(dly + ((npass * G + 7) & ~7));
+    int* cnt_s = lo_s + npass * SG;
+    __shared__ int amax_s[kMaxPass];
+    __shared__ int needany;
+    const int nev = *nevents;
+    const int nbound = boundaries ? a.rd.nblk - 1 : 0;
+    const int nwork = (nev + nbound) * gm.nchunk;
+    const int N = (int)a.rd.N, nds = (int)a.nds, nchan = a.rd.nchan;
+    for (int w = blockIdx.x; w < nwork; w += gridDim.x) {
+        const int e = w / gm.nchunk, chunk = w - e * gm.nchunk;
+        const bool clip_ev = e < nev;
+        const int r = clip_ev ? events[e] : (e - nev + 1) * a.rd.blk;
+        const int c0 = chunk * G;
+        const int wlo = max(r - a.dmax - ds + 1, 0) & ~15;
+        const int b0 = (int)blk_of(a.rd, wlo);
+        const int b1 = min(b0 + 1, a.rd.nblk - 1);
+        const int bndrel = (b0 + 1) * a.rd.blk - wlo;
+        __syncthreads();                                  // the previous item is done with LDS
+        if (threadIdx.x < kMaxPass) amax_s[threadIdx.x] = 0;
+        if (threadIdx.x == 0) needany = clip_ev;
+        for (int i = threadIdx.x; i < G; i += blockDim.x) {
+            zap[i] = zap_at(a.rd, b0, c0 + i);
+            zap[G + i] = zap_at(a.rd, b1, c0 + i);
+            pad[i] = pad_at(a.rd, b0, c0 + i);
+            pad[G + i] = pad_at(a.rd, b1, c0 + i);
+        }
+        for (int i = threadIdx.x; i < npass * G; i += blockDim.x) {
+            const int p = i / G;
+            dly[i] = (int16_t)a.dly[p][c0 + i - p * G];
+        }
+        __syncthreads();
+        if (!clip_ev) {
+            // boundary r between blocks b0 and b1: subbands with a channel masked in both whose
+            // pads differ; per pass their outputs whose rows contain r - 1 and r
+            for (int i = threadIdx.x; i < npass * SG; i += blockDim.x) {
+                const int p = i / SG, sl = i - p * SG;
+                int mind = 1 << 30, maxd = 0;
+                bool need = false;
+                for (int cc = 0; cc < cps; cc++) {
+                    const int lc = sl * cps + cc;
+                    const int d = dly[p * G + lc];
+                    mind = min(mind, d);
+                    maxd = max(maxd, d);
+                    need |= zap[lc] && zap[G + lc] && pad[lc] != pad[G + lc];
+                }
+                int lo = r - (ds - 1) - maxd, hi = r - 1 - mind;
+                lo = lo <= 0 ? 0 : (lo + ds - 1) / ds;
+                hi = hi < 0 ? -1 : min(hi / ds, nds - 1);
+                lo_s[i] = lo;
+                cnt_s[i] = need && hi >= lo ? hi - lo + 1 : 0;
+                if (cnt_s[i]) needany = 1;
+            }
+            __syncthreads();
+            if (!needany) continue;                       // uniform
+        }
+        // the window: raw bytes of the chunk's channels (16-byte runs), replaced-row flags
+        {
+            const int nq = Wp >> 4;
+            for (int i = threadIdx.x; i < G * nq; i += blockDim.x) {
+                const int lc = i / nq, q = i - lc * nq;
+                const int c = c0 + lc;
+                const int rc = a.rd.flip ? nchan - 1 - c : c;
+                const uint4 v = *(const uint4*)(a.rawT + (int64_t)rc * a.tstride + wlo + 16 * q);
+                *(uint4*)(lraw + lc * Wp + 16 * q) = v;
+            }
+            for (int i = threadIdx.x; i < Wp; i += blockDim.x) {
+                const int t = wlo + i;
+                flg[i] = t >= N ? 1 : (a.rd.clipped ? a.rd.clipped[t] : 0);
+            }
+        }
+        __syncthreads();
+        if (clip_ev) {
+            // task (p, lc): the output channel lc maps r to, unless an earlier channel of its
+            // subband maps r to the same output
+            for (int i = threadIdx.x; i < npass * G; i += blockDim.x) {
+                const int p = i / G, lc = i - p * G;
+                const int16_t* dl = dly + p * G;
+                const int jn = r - dl[lc];
+                if (jn < 0) continue;
+                const int j = jn / ds;
+                if (j >= nds) continue;
+                const int lc0 = lc - lc % cps;
+                bool dup = false;
+                for (int l2 = lc0; l2 < lc; l2++) {
+                    const int jn2 = r - dl[l2];
+                    dup |= jn2 >= 0 && jn2 / ds == j;
+                }
+                if (dup) continue;
+                const float acc = fix8_fold(a, lraw, flg, zap, pad, dl, Wp, G, lc0, (int64_t)j * ds - wlo, bndrel);
+                const int s = (c0 + lc0) / cps;
+                if (a.sub_dtype == 0) {
+                    const int16_t q = to_i16(acc, a.sub_round);
+                    ((int16_t*)a.out[p])[(int64_t)s * a.ostride[p] + j] = q;
+                    const int aq = q < 0 ? -(int)q : (int)q;
+                    if (aq > 0) atomicMax(&amax_s[p], aq);
+                } else {
+                    ((float*)a.out[p])[(int64_t)s * a.ostride[p] + j] = acc;
+                }
+            }
+        } else {
+            for (int i = threadIdx.x; i < npass * SG * gm.jmax; i += blockDim.x) {
+                const int ps = i / gm.jmax, jj = i - ps * gm.jmax;
+                if (jj >= cnt_s[ps]) continue;
+                const int p = ps / SG, sl = ps - p * SG;
+                const int j = lo_s[ps] + jj;
+                const int16_t* dl = dly + p * G;
+                const float acc = fix8_fold(a, lraw, flg, zap, pad, dl, Wp, G, sl * cps, (int64_t)j * ds - wlo, bndrel);
+                const int s = chunk * SG + sl;
+                if (a.sub_dtype == 0) {
+                    const int16_t q = to_i16(acc, a.sub_round);
+                    ((int16_t*)a.out[p])[(int64_t)s * a.ostride[p] + j] = q;
+                    const int aq = q < 0 ? -(int)q : (int)q;
+                    if (aq > 0) atomicMax(&amax_s[p], aq);
+                } else {
+                    ((float*)a.out[p])[(int64_t)s * a.ostride[p] + j] = acc;
+                }
+            }
+        }
+        __syncthreads();
+        if (a.sub_dtype == 0 && threadIdx.x < npass) publish_max(a.maxabs[threadIdx.x], amax_s[threadIdx.x]);
+    }
+}
+
+static size_t fix8_lds_bytes(const Stage1Multi& a, const Fix8Geom& g)
+{
+    return (size_t)g.G * g.Wp + g.Wp + (size_t)2 * g.G * 4 + (size_t)((2 * g.G + 15) & ~15) +
+           (size_t)2 * ((a.npass * g.G + 7) & ~7) + (size_t)2 * a.npass * g.SG * 4;
+}
+
+// Geometry for k_stage1_fix8, or false when it does not apply (the generic kernel then runs).
+static bool fix8_geom(const Stage1Multi& a, Fix8Geom& g)
+{
+    if (!a.rawT || a.rd.nbits != 8 || a.rd.scl || a.rd.offs || a.rd.wts) return false;
+    if (a.dmax > 32767 || a.rd.N >= ((int64_t)1 << 31) - (1 << 24)) return false;
+    g.Wp = (2 * a.dmax + 2 * a.ds + 15 + 15) & ~15;       // + alignment of the window start
+    if (g.Wp + 16 > a.rd.blk || a.dmax + a.ds + 16 > kRawTPad) return false;
+    g.SG = 0;
+    for (int sg = a.nsub; sg >= 1; sg--) {
+        if (a.nsub % sg) continue;
+        const int G = sg * a.cps;
+        if (G > 1024) continue;
+        Fix8Geom t = g;
+        t.SG = sg;
+        t.G = G;
+        if (fix8_lds_bytes(a, t) <= 40 * 1024) {
+            g.SG = sg;
+            break;
+        }
+    }
+    if (!g.SG) return false;
+    g.G = g.SG * a.cps;
+    g.nchunk = a.nsub / g.SG;
+    g.jmax = (a.dmax + a.ds - 1) / a.ds + 1;
+    return true;
+}
+
 hipError_t launch_stage1_fixup(const Stage1Multi& a, const int32_t* events, const int32_t* nevents, int boundaries,
                                hipStream_t st)
 {
     if (a.nds <= 0 || a.npass <= 0) return hipSuccess;
+    Fix8Geom g;
+    if (!(a.probe & 128) && fix8_geom(a, g)) {           // probe bit 7: the generic kernel
+        hipLaunchKernelGGL(k_stage1_fix8, dim3(4096), dim3(256), fix8_lds_bytes(a, g), st, a, g, events, nevents,
+                           boundaries);
+        return hipGetLastError();
+    }
     if (a.nsub > 256 || a.rd.N >= ((int64_t)1 << 31) - (1 << 24)) return hipErrorInvalidValue;
     const size_t lds = fixup_lds_bytes(a);
     if (lds > 64 * 1024) return hipErrorInvalidValue;

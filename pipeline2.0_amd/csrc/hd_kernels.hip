@@ -322,7 +322,11 @@ void k_stage1_tiled(Stage1Multi a, const int* __restrict__ special_tiles)
     }
     const int lrc0 = a.rd.flip ? G - 1 - cl0 : cl0;   // local raw index of channel cc=0
     int pmax = 0;                                      // lane p: max |subband| of pass p
-    for (int p = 0; p < a.npass; p++) {
+    // a SPECIAL grid with y > 1 gives every pass its own workgroup (few special tiles: the
+    // passes would otherwise run back to back in a handful of workgroups)
+    const int p_lo = SPECIAL && gridDim.y > 1 ? (int)blockIdx.y : 0;
+    const int p_hi = SPECIAL && gridDim.y > 1 ? (int)blockIdx.y + 1 : a.npass;
+    for (int p = p_lo; p < p_hi; p++) {
 #pragma unroll
         for (int cc = 0; cc < CPS; cc++) {
             const int lrc = a.rd.flip ? lrc0 - cc : lrc0 + cc;
@@ -383,7 +387,10 @@ static hipError_t launch_s1(const Stage1Multi& a, int vw, size_t lds, const int*
                             bool special_only, hipStream_t st)
 {
     const dim3 block((unsigned)(64 * a.sg));
-    const dim3 grid((unsigned)(a.ntiles * a.ngroups)), grid_sp((unsigned)(nspecial * a.ngroups));
+    // special tiles are few (the last tile; tiles over >= 3 read blocks): split them by pass
+    // unless they already fill the chip
+    const unsigned split = nspecial * a.ngroups < 2048 ? (unsigned)a.npass : 1u;
+    const dim3 grid((unsigned)(a.ntiles * a.ngroups)), grid_sp((unsigned)(nspecial * a.ngroups), split);
     if (vw == 16) {
         if (!special_only)
             hipLaunchKernelGGL((k_stage1_tiled<NBITS, CPS, CALIB, 16, false>), grid, block, lds, st, a, special);

@@ -63,13 +63,16 @@ def test_clean_state_matches_oracle(engine, nbits, calib, masked, nsblk):
 
 
 @pytest.mark.parametrize("ds", [1, 2, 3, 5, 6, 10])
-@pytest.mark.parametrize("s1,masked", [(3, True), (3, False), (2, True), (1, True)])
-def test_stage1_clip_bitexact(engine, ds, s1, masked):
+@pytest.mark.parametrize("s1,masked,N", [(3, True, 65536 + 777), (3, True, 98304 + 388), (3, False, 65536 + 777),
+                                         (2, True, 65536 + 777), (1, True, 65536 + 777)])
+def test_stage1_clip_bitexact(engine, ds, s1, masked, N):
     """Stage 1 with clipping over 3 passes of one launch, every kernel path: the 8-bit
     integer kernel (3) + its float special tiles + the fixup (clipped spectra and block
-    boundaries with changing pad constants), the float tiled kernel (2) + fixup, and the
-    direct kernel (1, clipping per cell).  Equal to the oracle."""
-    obs = palfa_obs(N=65536 + 777, nbits=8, nsblk=2048)
+    boundaries with changing pad constants; N % 4 == 0 gives the integer kernel its
+    channel-major raw copy and the fixup its LDS-window kernel, else the row-major fill and
+    the generic fixup), the float tiled kernel (2) + fixup, and the direct kernel (1,
+    clipping per cell).  Equal to the oracle."""
+    obs = palfa_obs(N=N, nbits=8, nsblk=2048)
     raw, s = beam(engine, obs, Opts(), spiky_synth())
     mask = pad = None
     pts = 8192
@@ -153,4 +156,36 @@ def test_rfimask_file_and_stats_pads(engine, tmp_path):
         assert np.array_equal(p.get_subbands(), want)
     finally:
         p.destroy()
+        engine.set_mask()
+
+
+@pytest.mark.parametrize("stage", [0, 1, 3, 5])
+def test_fixup_kernels_agree_full_stage(engine, stage):
+    """All passes of a Mock DDplan stage in one launch (28 at stage 0: the LDS-window fixup's
+    largest delay table), masked, with spikes: the 8-bit LDS-window fixup and the generic
+    per-cell fixup (probe bit 128) give identical subbands, and pass 0 equals the oracle."""
+    obs = palfa_obs(N=1 << 17, nbits=8, nsblk=2048)
+    raw, s = beam(engine, obs, Opts(), spiky_synth())
+    pts = 16384
+    mask, pad = synth_mask(obs, s, pts, frac=0.05)
+    engine.set_mask(mask, pts, pad)
+    d = plan.ddplans_for("pdev")[stage]
+    pps = [PassParams(subdm=float(d.subdmlist[i]), lodm=float(d.lodm_arg(i)), dmstep=float(d.dmstep_arg()),
+                      numdms=d.dmsperpass, nsub=d.numsub, ds=d.sub_downsamp) for i in range(d.numpasses)]
+    plans = [engine.plan(pp) for pp in pps]
+    try:
+        engine.run_subband_multi(plans)
+        fast = [p.get_subbands() for p in plans]
+        for p in plans:
+            p.set_variant(128 << 16)
+        engine.run_subband_multi(plans)
+        for i, p in enumerate(plans):
+            assert np.array_equal(p.get_subbands(), fast[i]), i
+        cl = OR.prepare(obs, Opts(), raw, mask=mask, ptsperint=pts, padvals=pad)
+        assert cl.nclipped > 50
+        want = OR.stage1(obs, Opts(), raw, d.numsub, d.sub_downsamp, pps[0].subdm, clean=cl, omp=True)
+        assert np.array_equal(fast[0], want)
+    finally:
+        for p in plans:
+            p.destroy()
         engine.set_mask()
