@@ -41,9 +41,11 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU work for the baseline sample")
     ap.add_argument("--e2e-beams", type=int, default=1,
                     help="beams run end to end (.dat/.inf files written) after the timed steps; 0 = skip")
-    ap.add_argument("--mode", choices=["beam", "shard"], default="beam",
-                    help="beam: one beam per rank (weak scaling, configs[4]); shard: ONE beam's 57 passes "
-                         "LPT-sharded over the ranks after an RCCL broadcast of the raw block (strong, configs[2])")
+    ap.add_argument("--mode", choices=["beam", "slices", "shard"], default="beam",
+                    help="beam: one beam per rank (weak scaling, configs[4]); slices: ONE beam cut into per-rank "
+                         "time slices, every rank runs all 57 passes on its slice (strong, configs[2]; RCCL carries "
+                         "only the clip statistics and padding sums); shard: ONE beam's passes LPT-sharded after "
+                         "an RCCL broadcast of the raw block (strong, the round-1 design, kept for comparison)")
     return ap.parse_args()
 
 
@@ -172,6 +174,63 @@ def shard_stages(eng, obs, ddplans, rank, world, variant):
     return stages
 
 
+def slice_stages(eng, ts, rank, variant):
+    """This rank's time slice of the beam: every pass, -numout local (the last rank pads)."""
+    from hipdedisp import PassParams, plan as P
+    stages = []
+    for d in ts.ddplans:
+        plans = []
+        stages.append(plans)
+        for i in range(d.numpasses):
+            pp = PassParams(subdm=float(d.subdmlist[i]), lodm=float(d.lodm_arg(i)), dmstep=float(d.dmstep_arg()),
+                            numdms=d.dmsperpass, nsub=d.numsub, ds=d.sub_downsamp,
+                            numout=ts.numout_local(rank, P.choose_N(ts.obs.N / d.downsamp), d.sub_downsamp))
+            p = eng.plan(pp)
+            if variant:
+                p.set_variant(variant)
+            plans.append(p)
+    return stages
+
+
+def run_slice_step(eng, ts, rank, stages, dist, torch):
+    """One beam as time slices: clip statistics of the owned read blocks -> all-reduce ->
+    clip_times finished on each slice; every pass; padding sums -> all-reduce -> last rank pads."""
+    import numpy as np
+    eng.touch_raw()
+    on_gpu = dist is not None and dist.get_backend() == "nccl"
+    if eng.opts.clip_sigma > 0:
+        if on_gpu:
+            table = torch.zeros((ts.nblk_total, ts.obs.nchan + 3), dtype=torch.float64, device="cuda")
+            ts.contribute_clip_stats(eng, rank, table.data_ptr())
+            dist.all_reduce(table)
+            torch.cuda.current_stream().synchronize()
+            eng.clip_set_stats(table.data_ptr())
+        else:
+            table = ts.stats_table()
+            ts.contribute_clip_stats(eng, rank, table)
+            if dist is not None:
+                t = torch.from_numpy(table)
+                dist.all_reduce(t)
+            eng.clip_set_stats(table)
+    plans = []
+    for st in stages:
+        if not st:
+            continue
+        eng.run_subband_multi(st)
+        for p in st:
+            p.run_dedisp(to_host=False)
+        plans += st
+    sums = ts.pass_sums(rank, plans)
+    if dist is not None:
+        t = torch.from_numpy(sums)
+        if on_gpu:
+            t = t.cuda()
+        dist.all_reduce(t)
+        sums = t.cpu().numpy().astype(np.float64)
+    ts.pad_passes(rank, plans, sums)
+    eng.sync()
+
+
 def broadcast_beam(eng, obs, rank, dist, torch):
     """Rank 0's raw block to every rank over RCCL (xGMI), then into each engine."""
     from hipdedisp import sharding as S
@@ -252,10 +311,18 @@ def main():
     synth = palfa_synth(beam=rank, nbits=args.nbits)
     ddplans = P.ddplans_for("pdev")
     shard = args.mode == "shard"
-    if shard:
+    slices = args.mode == "slices"
+    if shard or slices:
         synth = palfa_synth(beam=0, nbits=args.nbits)       # one beam for the whole node
     eng = Engine(local)
-    eng.set_obs(obs, Opts())
+    ts = None
+    if slices:
+        from hipdedisp.sharding import TimeSlices
+        ts = TimeSlices(obs, ddplans, world)
+        eng.set_obs(ts.local_obs(rank), Opts())
+        eng.set_slice(ts.slice(rank)[0], obs.N)
+    else:
+        eng.set_obs(obs, Opts())
     eng.set_streams(args.streams)
     if not shard or rank == 0:
         eng.synth_device(synth)
@@ -264,16 +331,28 @@ def main():
     eng.set_mask(mask, pts, pad)
     if shard:
         stages = shard_stages(eng, obs, ddplans, rank, world, args.variant)
+    elif slices:
+        stages = slice_stages(eng, ts, rank, args.variant)
     else:
         stages = build_plans(eng, obs, ddplans, args.variant)
     plans = [p for st in stages for p in st]
-    out_per_step = sum(p.pp.numdms * p.nds for p in plans)          # this rank's samples
+    if slices:                                                      # this rank's owned samples
+        out_per_step = sum(p.pp.numdms * ts.out_range(rank, p.pp.ds)[1] for p in plans)
+    else:
+        out_per_step = sum(p.pp.numdms * p.nds for p in plans)
     if shard and world > 1:
         broadcast_beam(eng, obs, rank, dist, torch)                 # untimed: makes warmup valid
 
     bcast_s = 0.0
+
+    def step():
+        if slices:
+            run_slice_step(eng, ts, rank, stages, dist, torch)
+        else:
+            run_step(eng, stages)
+
     for _ in range(args.warmup):
-        run_step(eng, stages)
+        step()
     barrier(dist, torch)
     eng.sync()
     t0 = time.perf_counter()
@@ -282,7 +361,7 @@ def main():
             tb = time.perf_counter()
             broadcast_beam(eng, obs, rank, dist, torch)
             bcast_s += time.perf_counter() - tb
-        run_step(eng, stages)
+        step()
     eng.sync()
     barrier(dist, torch)
     dt = time.perf_counter() - t0
@@ -299,7 +378,7 @@ def main():
         a, b = p.last_ms()
         ms1 += a
         ms2 += b
-    raw_bytes = obs.N * obs.rowbytes
+    raw_bytes = (ts.slice(rank)[1] if slices else obs.N) * obs.rowbytes
     sub_bytes = sum(p.pp.nsub * p.nds * 2 for p in plans)
     adds2 = sum(p.pp.numdms * p.nds * p.pp.nsub for p in plans)
     # algorithmic bytes per output sample (SURVEY §8d compulsory model): raw once + 4 B out
@@ -330,7 +409,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": step_s * 1e3,
         "higher_is_better": True,
-        "scaling": "strong" if shard else "weak",
+        "scaling": "strong" if (shard or slices) else "weak",
         "vs_baseline": None,
         "dtype": "u8->f32 subbanding, i16 subbands, i16x2/i32 exact sums, f32 out",
         "data": "synthetic",
@@ -339,6 +418,8 @@ def main():
                    "nchan": obs.nchan, "nspec": obs.N, "nbits": obs.nbits, "dm_trials": 4188, "passes": len(plans),
                    "out_samples_per_beam": sum(d.numpasses * d.dmsperpass * (obs.N // d.sub_downsamp) for d in ddplans),
                    "parallelism": ("1 beam, passes LPT-sharded x%d, RCCL raw broadcast" % world) if shard
+                   else ("1 beam, time slices x%d (halo %d spectra), RCCL clip-stats + padding all-reduce"
+                         % (world, ts.halo)) if slices
                    else "beam-per-GPU x%d" % world},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -350,7 +431,7 @@ def main():
     }
     if shard:
         line["broadcast_ms_per_step"] = 1e3 * bcast_s / args.steps
-    if not shard and args.e2e_beams > 0:
+    if not (shard or slices) and args.e2e_beams > 0:
         out_bytes = 4 * sum(p.pp.numdms * p.numout for p in plans)
         outdir = e2e_dir(1.1 * max(4 * p.pp.numdms * p.numout for p in plans) * 30)
         if outdir:

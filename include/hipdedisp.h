@@ -220,6 +220,23 @@ HD_API int hd_get_raw(hd_ctx* ctx, void* out, int64_t start, int64_t count);
  * GPU -- e.g. a block another rank broadcast over RCCL -- in / out, device-to-device.      */
 HD_API int hd_push_raw_device(hd_ctx* ctx, const void* dev_spectra, int64_t start, int64_t nspectra);
 HD_API int hd_get_raw_device(hd_ctx* ctx, void* dev_out, int64_t start, int64_t count);
+/* Multi-GPU time slices (hipdedisp.sharding.TimeSlices): the context (after hd_set_obs with
+ * obs.N = the slice's spectra) holds spectra [t0, t0 + N) of an observation of n_total
+ * spectra; t0 is a multiple of nsblk.  Read blocks and mask intervals count from the
+ * observation's start and hd_synth_device generates the observation's spectra t0.. .
+ * (0, 0) returns to a whole observation.  Clears the mask-block and clip state.           */
+HD_API int hd_set_slice(hd_ctx* ctx, int64_t t0, int64_t n_total);
+/* clip_times across slices: its running statistics carry from block to block over the
+ * whole observation, so every slice contributes the per-block statistics of the read
+ * blocks it owns and every slice then runs the recurrence over all blocks before its end.
+ * Layout of `stats` (host or device memory of this context's GPU; the observation's
+ * ceil(n_total / nsblk) rows of nchan + 3 doubles: bavg, bstd, numgood, chansum[nchan]):
+ * hd_clip_stats writes the rows of this slice's first nown blocks (global rows t0/nsblk ..)
+ * and leaves the others alone, so a zero-filled buffer summed over the slices (an all-reduce)
+ * is complete; hd_clip_set_stats reads rows [0, t0/nsblk + nblk) and finishes clip_times
+ * for this slice (no-ops when clipping is off).                                            */
+HD_API int hd_clip_stats(hd_ctx* ctx, int64_t nown, double* stats);
+HD_API int hd_clip_set_stats(hd_ctx* ctx, const double* stats);
 
 /* ---- passes --------------------------------------------------------------------- */
 /* Host-only: the integer tables and subband-level parameters a plan would use, without
@@ -252,6 +269,12 @@ HD_API int hd_run_dedisp(hd_plan* plan, float* host_out);
 /* Samples [t0, t0+count) of DMs [dm0, dm0+ndm) of the device-resident series of the last
  * hd_run_dedisp, host layout [ndm][count] (t0+count <= numout).                        */
 HD_API int hd_get_series(hd_plan* plan, int32_t dm0, int32_t ndm, int64_t t0, int64_t count, float* host);
+/* Exact (double) sum of the device series samples [t0, t0+count) of DM dm (int16 subbands:
+ * integer-valued samples, so the order of the sum does not matter), and a fill of samples
+ * [t0, numout) of every DM with value -- the padding of a time-sliced pass, whose value
+ * (prepsubband's first-DM mean) is the observation's, not the slice's.                 */
+HD_API int hd_series_sum(hd_plan* plan, int32_t dm, int64_t t0, int64_t count, double* sum);
+HD_API int hd_series_fill(hd_plan* plan, int64_t t0, float value);
 /* The .dat output path (replaces the files prepsubband leaves in the tempdir,
  * PALFA2_presto_search.py:514-520, 532-537): queue the device-resident series of the last
  * hd_run_dedisp of this plan to paths[numdms] -- raw little-endian float32, numout samples,

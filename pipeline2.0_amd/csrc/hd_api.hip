@@ -63,7 +63,17 @@ struct hd_ctx {
         int32_t* nzero = nullptr;           // a device 0 (profiling: a fixup over no clipped spectra)
         double *bavg = nullptr, *bstd = nullptr, *chansum = nullptr;
         float *ravg = nullptr, *trig = nullptr, *pad = nullptr;
+        // time-sliced context: the recurrence runs over the observation's blocks [0, g0 + nblk)
+        // from exchanged statistics (hd_clip_set_stats) into these global arrays
+        bool stats_valid = false;           // this slice's per-block statistics are computed
+        int32_t *numgood_g = nullptr, *doclip_g = nullptr;
+        double *bavg_g = nullptr, *bstd_g = nullptr, *chansum_g = nullptr, *xbuf = nullptr;
+        float *ravg_g = nullptr, *trig_g = nullptr, *pad_g = nullptr;
+        uint8_t* allzap_g = nullptr;
     } clip;
+    // time slice (hd_set_slice): the context holds spectra [slice_t0, slice_t0 + obs.N) of an
+    // observation of slice_total spectra (0: the whole observation)
+    int64_t slice_t0 = 0, slice_total = 0;
     size_t lds_attr_set = 64 * 1024;   // dynamic-LDS limit already granted to the tiled kernels
     size_t lds_attr_q8 = 64 * 1024;    // ... and to the 8-bit integer stage-1 kernels
     struct SpecialList {               // stage-1 special-tile list per tile geometry (device)
@@ -269,6 +279,7 @@ static void free_blocks(hd_ctx* c)
     dfree(c->d_allzap); c->d_allzap = nullptr;
     c->blocks_valid = false;
     c->clip_valid = false;
+    c->clip.stats_valid = false;
 }
 
 static void free_clip(hd_ctx* c)
@@ -276,10 +287,13 @@ static void free_clip(hd_ctx* c)
     hd_ctx::ClipBufs& b = c->clip;
     for (void* p : {(void*)b.zdm, (void*)b.good, (void*)b.clipped, (void*)b.numgood, (void*)b.doclip,
                     (void*)b.events, (void*)b.nevents, (void*)b.nzero, (void*)b.bavg, (void*)b.bstd, (void*)b.chansum,
-                    (void*)b.ravg, (void*)b.trig, (void*)b.pad})
+                    (void*)b.ravg, (void*)b.trig, (void*)b.pad, (void*)b.numgood_g, (void*)b.doclip_g,
+                    (void*)b.bavg_g, (void*)b.bstd_g, (void*)b.chansum_g, (void*)b.xbuf, (void*)b.ravg_g,
+                    (void*)b.trig_g, (void*)b.pad_g, (void*)b.allzap_g})
         dfree(p);
     b = hd_ctx::ClipBufs{};
     c->clip_valid = false;
+    c->clip.stats_valid = false;
 }
 
 static void free_obs_buffers(hd_ctx* c)
@@ -345,6 +359,7 @@ extern "C" int hd_touch_raw(hd_ctx* c)
     if (!c) return fail(nullptr, HD_E_INVAL, "hd_touch_raw: NULL context");
     c->rawT_valid = false;
     c->clip_valid = false;
+    c->clip.stats_valid = false;
     return HD_OK;
 }
 
@@ -427,7 +442,32 @@ extern "C" int hd_set_obs(hd_ctx* c, const hd_obs* o, const hd_opts* opts)
     c->rowbytes = (int32_t)((int64_t)o->nchan * o->nbits / 8);
     c->blk = (int32_t)std::min<int64_t>(o->nsblk > 0 ? o->nsblk : o->N, o->N);
     c->nblk = (int32_t)((o->N + c->blk - 1) / c->blk);
+    c->slice_t0 = c->slice_total = 0;
     c->have_obs = true;
+    return HD_OK;
+}
+
+extern "C" int hd_set_slice(hd_ctx* c, int64_t t0, int64_t n_total)
+{
+    if (!c) return fail(nullptr, HD_E_INVAL, "hd_set_slice: NULL context");
+    if (!c->have_obs) return fail(c, HD_E_STATE, "hd_set_slice before hd_set_obs");
+    if (n_total == 0 && t0 == 0) {
+        c->slice_t0 = c->slice_total = 0;
+    } else {
+        const int64_t blk = c->obs.nsblk > 0 ? c->obs.nsblk : 0;
+        if (blk <= 0 || t0 < 0 || t0 % blk || t0 + c->obs.N > n_total)
+            return fail(c, HD_E_INVAL, "hd_set_slice: need 0 <= t0, t0 %% nsblk == 0 and t0 + N <= n_total "
+                        "(t0 %lld, N %lld, n_total %lld, nsblk %lld)", (long long)t0, (long long)c->obs.N,
+                        (long long)n_total, (long long)blk);
+        if (c->blk != blk) return fail(c, HD_E_INVAL, "hd_set_slice: the slice is shorter than one read block");
+        c->slice_t0 = t0;
+        c->slice_total = n_total;
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, sync_all(c));
+    free_blocks(c);
+    free_clip(c);
+    clear_special_cache(c);
     return HD_OK;
 }
 
@@ -463,6 +503,7 @@ extern "C" int hd_set_chan_calib(hd_ctx* c, const float* scl, const float* offs,
     if ((rc = upload(c, &c->d_offs, offs, c->obs.nchan))) return rc;
     if ((rc = upload(c, &c->d_wts, wts, c->obs.nchan))) return rc;
     c->clip_valid = false;
+    c->clip.stats_valid = false;
     return HD_OK;
 }
 
@@ -542,6 +583,7 @@ extern "C" int hd_push_raw(hd_ctx* c, const void* spectra, int64_t start, int64_
     c->raw_ready = true;
     c->rawT_valid = false;
     c->clip_valid = false;
+    c->clip.stats_valid = false;
     return HD_OK;
 }
 
@@ -633,6 +675,7 @@ extern "C" int hd_push_raw_file(hd_ctx* c, const char* path, const hd_rows_src* 
     c->raw_ready = true;
     c->rawT_valid = false;
     c->clip_valid = false;
+    c->clip.stats_valid = false;
     if (io_seconds) *io_seconds = io;
     if (total_seconds) *total_seconds = std::chrono::duration<double>(clk::now() - t_all).count();
     return HD_OK;
@@ -655,6 +698,7 @@ extern "C" int hd_push_raw_device(hd_ctx* c, const void* dev_spectra, int64_t st
     c->raw_ready = true;
     c->rawT_valid = false;
     c->clip_valid = false;
+    c->clip.stats_valid = false;
     return HD_OK;
 }
 
@@ -816,14 +860,17 @@ extern "C" int hd_synth_device(hd_ctx* c, const hd_synth* s)
     if (!s) return fail(c, HD_E_INVAL, "hd_synth_device: synth is NULL");
     std::vector<uint8_t> buf;
     std::string err;
-    int rc = build_synth_table(&c->obs, s, buf, err);
+    hd_obs whole = c->obs;                     // a time slice holds spectra [t0, t0 + N) of the beam
+    if (c->slice_total) whole.N = c->slice_total;
+    int rc = build_synth_table(&whole, s, buf, err);
     if (rc) return fail(c, rc, "%s", err.c_str());
     HIPCHK(c, hipSetDevice(c->device));
     if ((rc = ensure_raw(c))) return rc;
     void* d_tab = nullptr;
     HIPCHK(c, hipMalloc(&d_tab, buf.size()));
     HIPCHK(c, hipMemcpy(d_tab, buf.data(), buf.size(), hipMemcpyHostToDevice));
-    hipError_t e = hd::launch_synth(c->d_raw, c->obs.N, c->rowbytes, (const hd_synth_tab*)d_tab, c->stream);
+    hipError_t e = hd::launch_synth(c->d_raw, c->obs.N, c->rowbytes, (const hd_synth_tab*)d_tab, c->slice_t0,
+                                    c->stream);
     hipError_t e2 = hipStreamSynchronize(c->stream);
     (void)hipFree(d_tab);
     if (e != hipSuccess || e2 != hipSuccess)
@@ -831,6 +878,7 @@ extern "C" int hd_synth_device(hd_ctx* c, const hd_synth* s)
     c->raw_ready = true;
     c->rawT_valid = false;
     c->clip_valid = false;
+    c->clip.stats_valid = false;
     return HD_OK;
 }
 
@@ -1295,7 +1343,8 @@ static hd::RawDesc raw_desc(const hd_ctx* c)
     rd.zidx = c->d_zidx;
     rd.zrows = c->d_zrows;
     const bool clip = c->opts.clip_sigma > 0.0f && c->clip_valid;
-    rd.pad = clip ? c->clip.pad : c->d_padvals;
+    const float* cpad = c->slice_total ? c->clip.pad_g + (c->slice_t0 / c->blk) * (int64_t)c->obs.nchan : c->clip.pad;
+    rd.pad = clip ? cpad : c->d_padvals;
     rd.pad_stride = clip ? c->obs.nchan : 0;
     rd.clipped = clip ? c->clip.clipped : nullptr;
     return rd;
@@ -1310,14 +1359,29 @@ static int ensure_blocks(hd_ctx* c)
     if (c->blocks_valid) return HD_OK;
     free_blocks(c);
     const int nchan = c->obs.nchan, nblk = c->nblk;
+    const int64_t g0 = c->slice_t0 / c->blk;          // global index of local block 0 (time slices)
     std::vector<uint8_t> allzap((size_t)nblk, 0);
+    if (c->slice_total && !c->h_mask.empty()) {
+        // the clip recurrence of a slice walks every block of the observation before it
+        std::vector<uint8_t> ag((size_t)(g0 + nblk), 0);
+        for (int64_t b = 0; b < g0 + nblk; b++) {
+            const double st = (double)(b * c->blk) * c->obs.dt, en = st + c->blk * c->obs.dt;
+            const int lo = std::min((int)(st / c->dtint), c->numint - 1);
+            const int hi = std::min((int)(en / c->dtint), c->numint - 1);
+            ag[(size_t)b] = c->h_zapint[lo] || c->h_zapint[hi];
+        }
+        dfree(c->clip.allzap_g);
+        c->clip.allzap_g = nullptr;
+        HIPCHK(c, hipMalloc(&c->clip.allzap_g, ag.size()));
+        HIPCHK(c, hipMemcpy(c->clip.allzap_g, ag.data(), ag.size(), hipMemcpyHostToDevice));
+    }
     if (!c->h_mask.empty()) {
         std::vector<int32_t> zidx((size_t)nblk);
         std::vector<uint8_t> rows;
         std::map<int64_t, int32_t> seen;     // (lo, hi) or all -> row
         const double duration = c->blk * c->obs.dt;
         for (int32_t b = 0; b < nblk; b++) {
-            const double starttime = (double)((int64_t)b * c->blk) * c->obs.dt;
+            const double starttime = (double)((g0 + b) * c->blk) * c->obs.dt;
             const double endtime = starttime + duration;
             const int lo = std::min((int)(starttime / c->dtint), c->numint - 1);
             const int hi = std::min((int)(endtime / c->dtint), c->numint - 1);
@@ -1346,14 +1410,30 @@ static int ensure_blocks(hd_ctx* c)
     HIPCHK(c, hipMemcpy(c->d_allzap, allzap.data(), allzap.size(), hipMemcpyHostToDevice));
     c->blocks_valid = true;
     c->clip_valid = false;
+    c->clip.stats_valid = false;
     return HD_OK;
 }
 
 // clip_times over the raw block (hd_clip.hip), queued on the context stream; its device
 // time is charged to the stage-1 launch that needs it.
+static int alloc_clip(hd_ctx* c);
+static hd::ClipArgs clip_args(hd_ctx* c);
+
 static int ensure_clip(hd_ctx* c)
 {
     if (!(c->opts.clip_sigma > 0.0f) || c->clip_valid) return HD_OK;
+    if (c->slice_total)
+        return fail(c, HD_E_STATE, "time-sliced context: clip_times needs the observation's per-block statistics "
+                    "(hd_clip_stats on every slice, then hd_clip_set_stats) before stage 1");
+    int rc = alloc_clip(c);
+    if (rc) return rc;
+    HIPCHK(c, hd::launch_clip(clip_args(c), c->stream));
+    c->clip_valid = true;
+    return HD_OK;
+}
+
+static int alloc_clip(hd_ctx* c)
+{
     int rc = ensure_blocks(c);
     if (rc) return rc;
     hd_ctx::ClipBufs& b = c->clip;
@@ -1383,6 +1463,33 @@ static int ensure_clip(hd_ctx* c)
         }
         HIPCHK(c, hipMemset(b.nzero, 0, 4));
     }
+    if (c->slice_total && !b.numgood_g) {
+        const size_t ng = (size_t)(c->slice_t0 / c->blk + c->nblk);
+        hipError_t e = hipSuccess;
+        auto al = [&](void** p, size_t bytes) {
+            if (e == hipSuccess) e = hipMalloc(p, bytes);
+        };
+        al((void**)&b.numgood_g, ng * 4);
+        al((void**)&b.doclip_g, ng * 4);
+        al((void**)&b.bavg_g, ng * 8);
+        al((void**)&b.bstd_g, ng * 8);
+        al((void**)&b.ravg_g, ng * 4);
+        al((void**)&b.trig_g, ng * 4);
+        al((void**)&b.chansum_g, ng * nch * 8);
+        al((void**)&b.pad_g, ng * nch * 4);
+        al((void**)&b.xbuf, ng * (nch + 3) * 8);
+        if (e != hipSuccess) {
+            free_clip(c);
+            return fail(c, HD_E_NOMEM, "cannot allocate the sliced clip_times state: %s", hipGetErrorString(e));
+        }
+    }
+    return HD_OK;
+}
+
+// the context's own (local) clip arguments
+static hd::ClipArgs clip_args(hd_ctx* c)
+{
+    hd_ctx::ClipBufs& b = c->clip;
     hd::ClipArgs a{};
     a.rd = raw_desc(c);
     a.clip_sigma = c->opts.clip_sigma;
@@ -1401,7 +1508,72 @@ static int ensure_clip(hd_ctx* c)
     a.pad = b.pad;
     a.events = b.events;
     a.nevents = b.nevents;
-    HIPCHK(c, hd::launch_clip(a, c->stream));
+    return a;
+}
+
+// ---- time-sliced contexts: clip_times across slices ----------------------------------
+extern "C" int hd_clip_stats(hd_ctx* c, int64_t nown, double* stats)
+{
+    if (!c) return fail(nullptr, HD_E_INVAL, "hd_clip_stats: NULL context");
+    if (!c->slice_total) return fail(c, HD_E_STATE, "hd_clip_stats: the context is not a time slice (hd_set_slice)");
+    if (!(c->opts.clip_sigma > 0.0f)) return HD_OK;
+    if (!c->raw_ready) return fail(c, HD_E_STATE, "hd_clip_stats: no raw data");
+    if (nown < 0 || nown > c->nblk || !stats) return fail(c, HD_E_INVAL, "hd_clip_stats: nown must be in [0, %d]", c->nblk);
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, join_stream2(c));
+    int rc = alloc_clip(c);
+    if (rc) return rc;
+    hd::ClipArgs a = clip_args(c);
+    if (!c->clip.stats_valid) {
+        HIPCHK(c, hd::launch_clip_stats(a, c->stream));
+        c->clip.stats_valid = true;
+    }
+    const size_t w = (size_t)c->obs.nchan + 3;
+    HIPCHK(c, hd::launch_clip_pack(a, c->clip.xbuf, (int)nown, c->stream));
+    HIPCHK(c, hipMemcpyAsync(stats + (size_t)(c->slice_t0 / c->blk) * w, c->clip.xbuf, (size_t)nown * w * 8,
+                             hipMemcpyDefault, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return HD_OK;
+}
+
+extern "C" int hd_clip_set_stats(hd_ctx* c, const double* stats)
+{
+    if (!c) return fail(nullptr, HD_E_INVAL, "hd_clip_set_stats: NULL context");
+    if (!c->slice_total) return fail(c, HD_E_STATE, "hd_clip_set_stats: the context is not a time slice");
+    if (!(c->opts.clip_sigma > 0.0f)) return HD_OK;
+    if (!c->raw_ready) return fail(c, HD_E_STATE, "hd_clip_set_stats: no raw data");
+    if (!stats) return fail(c, HD_E_INVAL, "hd_clip_set_stats: stats is NULL");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, join_stream2(c));
+    int rc = alloc_clip(c);
+    if (rc) return rc;
+    hd_ctx::ClipBufs& b = c->clip;
+    const int64_t g0 = c->slice_t0 / c->blk, ng = g0 + c->nblk, nch = c->obs.nchan;
+    const size_t w = (size_t)nch + 3;
+    hd::ClipArgs a = clip_args(c);
+    if (!b.stats_valid) {                       // this slice's own zero-DM series and good flags
+        HIPCHK(c, hd::launch_clip_stats(a, c->stream));
+        b.stats_valid = true;
+    }
+    HIPCHK(c, hipMemcpyAsync(b.xbuf, stats, (size_t)ng * w * 8, hipMemcpyDefault, c->stream));
+    hd::ClipArgs g = a;                         // the observation's blocks [0, ng)
+    g.rd.nblk = (int32_t)ng;
+    g.numgood = b.numgood_g;
+    g.bavg = b.bavg_g;
+    g.bstd = b.bstd_g;
+    g.chansum = b.chansum_g;
+    g.allzap = c->h_mask.empty() ? nullptr : b.allzap_g;
+    g.doclip = b.doclip_g;
+    g.ravg = b.ravg_g;
+    g.trig = b.trig_g;
+    g.pad = b.pad_g;
+    HIPCHK(c, hd::launch_clip_unpack(g, b.xbuf, c->stream));
+    HIPCHK(c, hd::launch_clip_recur(g, c->stream));
+    a.doclip = b.doclip_g + g0;                 // this slice's spectra against its blocks' state
+    a.ravg = b.ravg_g + g0;
+    a.trig = b.trig_g + g0;
+    HIPCHK(c, hd::launch_clip_flag(a, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     c->clip_valid = true;
     return HD_OK;
 }
@@ -1421,7 +1593,8 @@ extern "C" int hd_get_clean(hd_ctx* c, float* pad, uint8_t* clipped, uint8_t* za
     const size_t nb = (size_t)c->nblk, nch = (size_t)c->obs.nchan;
     if (pad) {
         if (clip) {
-            HIPCHK(c, hipMemcpy(pad, c->clip.pad, nb * nch * 4, hipMemcpyDeviceToHost));
+            const float* src = c->slice_total ? c->clip.pad_g + (c->slice_t0 / c->blk) * nch : c->clip.pad;
+            HIPCHK(c, hipMemcpy(pad, src, nb * nch * 4, hipMemcpyDeviceToHost));
         } else {
             for (size_t b = 0; b < nb; b++)
                 for (size_t ch = 0; ch < nch; ch++) pad[b * nch + ch] = c->h_padvals.empty() ? 0.0f : c->h_padvals[ch];
@@ -1523,7 +1696,7 @@ static bool stage1_q8_tiling(const hd_ctx* c, int nsub, int ds, int dmax, hd::St
     if (c->obs.nbits != 8 || c->d_scl || c->d_offs || c->d_wts) return false;
     if (!hd::stage1_q8_supports(cps, ds)) return false;
     const int S = hd::stage1_q8_quarter_rows(ds);
-    const int W = S + dmax;
+    const int W = S + ((dmax + 15) & ~15);            // whole 16-row fill units (16-byte LDS stores)
     int sg = 0, v = 0;
     size_t best = 0;
     for (int cand : {4, 2, 1}) {
@@ -1550,7 +1723,7 @@ static bool stage1_q8_tiling(const hd_ctx* c, int nsub, int ds, int dmax, hd::St
     a.dmax = dmax;
     a.W = W;
     a.rs = 0;
-    a.two_ok = 1;
+    a.two_ok = ds >= 10 ? 2 : 1;                      // read blocks past the first a tile may span
     // bound on the rounding of the oracle's float fold (CPS channel adds per ds step, then
     // ds adds of the steps) for sums of 8-bit samples and pad values: each add errs by at most
     // half an ulp of its result; ulps are over-estimated 2x by taking 2^(floor(log2 x) - 22)
@@ -1803,6 +1976,43 @@ extern "C" int hd_get_series(hd_plan* p, int32_t dm0, int32_t ndm, int64_t t0, i
                                sizeof(float) * p->out_stride, sizeof(float) * count, ndm, hipMemcpyDeviceToHost,
                                p->dd_stream));
     HIPCHK(c, hipStreamSynchronize(p->dd_stream));
+    return HD_OK;
+}
+
+extern "C" int hd_series_sum(hd_plan* p, int32_t dm, int64_t t0, int64_t count, double* sum)
+{
+    if (!p || !sum) return fail(p ? p->ctx : nullptr, HD_E_INVAL, "hd_series_sum: NULL argument");
+    hd_ctx* c = p->ctx;
+    if (!p->ran_dd || !p->d_out) return fail(c, HD_E_STATE, "hd_series_sum: run hd_run_dedisp first");
+    if (dm < 0 || dm >= p->pass.numdms || t0 < 0 || count < 0 || t0 + count > p->numout)
+        return fail(c, HD_E_INVAL, "hd_series_sum: window outside [%d DMs] x [0, %lld)", p->pass.numdms,
+                    (long long)p->numout);
+    *sum = 0.0;
+    if (count == 0) return HD_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    constexpr int kParts = 512;
+    double* d = nullptr;
+    HIPCHK(c, hipMallocAsync((void**)&d, kParts * sizeof(double), p->dd_stream));
+    HIPCHK(c, hd::launch_series_sum(p->d_out + (size_t)dm * p->out_stride + t0, count, d, kParts, p->dd_stream));
+    std::vector<double> h(kParts);
+    HIPCHK(c, hipMemcpyAsync(h.data(), d, kParts * sizeof(double), hipMemcpyDeviceToHost, p->dd_stream));
+    HIPCHK(c, hipFreeAsync(d, p->dd_stream));
+    HIPCHK(c, hipStreamSynchronize(p->dd_stream));
+    double acc = 0.0;
+    for (double v : h) acc += v;
+    *sum = acc;
+    return HD_OK;
+}
+
+extern "C" int hd_series_fill(hd_plan* p, int64_t t0, float value)
+{
+    if (!p) return fail(nullptr, HD_E_INVAL, "hd_series_fill: NULL plan");
+    hd_ctx* c = p->ctx;
+    if (!p->ran_dd || !p->d_out) return fail(c, HD_E_STATE, "hd_series_fill: run hd_run_dedisp first");
+    if (t0 < 0 || t0 > p->numout) return fail(c, HD_E_INVAL, "hd_series_fill: t0 outside [0, %lld]", (long long)p->numout);
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hd::launch_series_fill(p->d_out, p->out_stride, p->pass.numdms, t0, p->numout, value, p->dd_stream));
+    HIPCHK(c, hipEventRecord(p->ev[3], p->dd_stream));   // the series' end: hd_write_series copies after it
     return HD_OK;
 }
 

@@ -20,6 +20,8 @@
 // are bit-identical to the oracle's restatement.
 #include "hd_device.h"
 
+#include <algorithm>
+
 namespace hd {
 
 constexpr int kClipMaxBlock = 8192;           // LDS sort capacity (32 KiB of floats)
@@ -281,13 +283,76 @@ __global__ __launch_bounds__(256) void k_clip_flag(ClipArgs a)
     }
 }
 
-hipError_t launch_clip(const ClipArgs& a, hipStream_t st)
+// ---- time-sliced contexts: per-block statistics in and out ----------------------------
+// Row b of the exchange layout: [bavg, bstd, numgood, chansum[nchan]] (doubles; numgood and
+// the 8-bit channel sums are exact integers).
+__global__ __launch_bounds__(256) void k_clip_pack(ClipArgs a, double* __restrict__ out, int nown)
+{
+    const int nch = a.rd.nchan, w = nch + 3;
+    const int64_t n = (int64_t)nown * w;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const int b = (int)(i / w), k = (int)(i - (int64_t)b * w);
+        out[i] = k == 0 ? a.bavg[b] : k == 1 ? a.bstd[b] : k == 2 ? (double)a.numgood[b]
+                                                                  : a.chansum[(int64_t)b * nch + k - 3];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_clip_unpack(ClipArgs g, const double* __restrict__ in)
+{
+    const int nch = g.rd.nchan, w = nch + 3;
+    const int64_t n = (int64_t)g.rd.nblk * w;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const int b = (int)(i / w), k = (int)(i - (int64_t)b * w);
+        const double v = in[i];
+        if (k == 0) g.bavg[b] = v;
+        else if (k == 1) g.bstd[b] = v;
+        else if (k == 2) g.numgood[b] = (int32_t)v;
+        else g.chansum[(int64_t)b * nch + k - 3] = v;
+    }
+}
+
+static unsigned grid_for(int64_t n)
+{
+    int64_t nb = (n + 255) / 256;
+    return (unsigned)(nb < 1 ? 1 : nb > 4096 ? 4096 : nb);
+}
+
+hipError_t launch_clip_pack(const ClipArgs& a, double* out, int nown, hipStream_t st)
+{
+    if (nown <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_clip_pack, dim3(grid_for((int64_t)nown * (a.rd.nchan + 3))), dim3(256), 0, st, a, out, nown);
+    return hipGetLastError();
+}
+
+hipError_t launch_clip_unpack(const ClipArgs& g, const double* in, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_clip_unpack, dim3(grid_for((int64_t)g.rd.nblk * (g.rd.nchan + 3))), dim3(256), 0, st, g, in);
+    return hipGetLastError();
+}
+
+// the serial recurrence over a.rd.nblk blocks (a's arrays), one workgroup
+hipError_t launch_clip_recur(const ClipArgs& a, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_clip_recur, dim3(1), dim3(1024), 0, st, a);
+    return hipGetLastError();
+}
+
+// clip flags + event list of a's spectra (doclip/ravg/trig indexed by a's blocks)
+hipError_t launch_clip_flag(const ClipArgs& a, hipStream_t st)
+{
+    hipError_t e = hipMemsetAsync(a.nevents, 0, sizeof(int32_t), st);
+    if (e != hipSuccess) return e;
+    if (a.rd.N <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_clip_flag, dim3((unsigned)((a.rd.N + 255) / 256)), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+// per-block statistics of a's spectra (everything before the recurrence)
+hipError_t launch_clip_stats(const ClipArgs& a, hipStream_t st)
 {
     const RawDesc& rd = a.rd;
     if (rd.N <= 0) return hipSuccess;
     if (rd.blk > kClipMaxBlock) return hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync(a.nevents, 0, sizeof(int32_t), st);
-    if (e != hipSuccess) return e;
     const bool calib = rd.scl || rd.offs || rd.wts;
     if (rd.nbits == 8 && !calib && rd.rowbytes % 16 == 0)
         hipLaunchKernelGGL(k_clip_zdm_u8, dim3((unsigned)((rd.N + 3) / 4)), dim3(256), 0, st, rd, a.zdm);
@@ -299,9 +364,16 @@ hipError_t launch_clip(const ClipArgs& a, hipStream_t st)
         hipLaunchKernelGGL(k_clip_chan_u8, dim3((unsigned)rd.nblk), dim3(256), 0, st, a);
     else
         hipLaunchKernelGGL(k_clip_chan, dim3((unsigned)(rd.nblk * ((rd.nchan + 255) / 256))), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(k_clip_recur, dim3(1), dim3(1024), 0, st, a);
-    hipLaunchKernelGGL(k_clip_flag, dim3((unsigned)((rd.N + 255) / 256)), dim3(256), 0, st, a);
     return hipGetLastError();
+}
+
+hipError_t launch_clip(const ClipArgs& a, hipStream_t st)
+{
+    if (a.rd.N <= 0) return hipMemsetAsync(a.nevents, 0, sizeof(int32_t), st);
+    hipError_t e = launch_clip_stats(a, st);
+    if (e == hipSuccess) e = launch_clip_recur(a, st);
+    if (e == hipSuccess) e = launch_clip_flag(a, st);
+    return e;
 }
 
 // ------------------------------------------------------------------------------------
@@ -594,13 +666,19 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
     __shared__ int needany;
     const int nev = *nevents;
     const int nbound = boundaries ? a.rd.nblk - 1 : 0;
-    const int nwork = (nev + nbound) * gm.nchunk;
+    const int nitems = nev + nbound;
     const int N = (int)a.rd.N, nds = (int)a.nds, nchan = a.rd.nchan;
-    for (int w = blockIdx.x; w < nwork; w += gridDim.x) {
-        const int e = w / gm.nchunk, chunk = w - e * gm.nchunk;
+    // the grid is a multiple of nchunk: a workgroup keeps one chunk, so its delays of every
+    // pass are staged once for all its items
+    const int chunk = blockIdx.x % gm.nchunk;
+    const int c0 = chunk * G;
+    for (int i = threadIdx.x; i < npass * G; i += blockDim.x) {
+        const int p = i / G;
+        dly[i] = (int16_t)a.dly[p][c0 + i - p * G];
+    }
+    for (int e = blockIdx.x / gm.nchunk; e < nitems; e += gridDim.x / gm.nchunk) {
         const bool clip_ev = e < nev;
         const int r = clip_ev ? events[e] : (e - nev + 1) * a.rd.blk;
-        const int c0 = chunk * G;
         const int wlo = max(r - a.dmax - ds + 1, 0) & ~15;
         const int b0 = (int)blk_of(a.rd, wlo);
         const int b1 = min(b0 + 1, a.rd.nblk - 1);
@@ -613,10 +691,6 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
             zap[G + i] = zap_at(a.rd, b1, c0 + i);
             pad[i] = pad_at(a.rd, b0, c0 + i);
             pad[G + i] = pad_at(a.rd, b1, c0 + i);
-        }
-        for (int i = threadIdx.x; i < npass * G; i += blockDim.x) {
-            const int p = i / G;
-            dly[i] = (int16_t)a.dly[p][c0 + i - p * G];
         }
         __syncthreads();
         if (!clip_ev) {
@@ -750,7 +824,8 @@ hipError_t launch_stage1_fixup(const Stage1Multi& a, const int32_t* events, cons
     if (a.nds <= 0 || a.npass <= 0) return hipSuccess;
     Fix8Geom g;
     if (!(a.probe & 128) && fix8_geom(a, g)) {           // probe bit 7: the generic kernel
-        hipLaunchKernelGGL(k_stage1_fix8, dim3(4096), dim3(256), fix8_lds_bytes(a, g), st, a, g, events, nevents,
+        const unsigned grid = (unsigned)(std::max(1, 4096 / g.nchunk) * g.nchunk);
+        hipLaunchKernelGGL(k_stage1_fix8, dim3(grid), dim3(256), fix8_lds_bytes(a, g), st, a, g, events, nevents,
                            boundaries);
         return hipGetLastError();
     }

@@ -53,7 +53,7 @@ struct Stage1Multi {
     int32_t dmax;             // max channel delay over the passes
     int32_t rs;               // LDS bytes per raw row (multiple of 4, odd dword count)
     int32_t W;                // 8-bit integer path: LDS dwords per channel row (>= S + dmax)
-    int32_t two_ok;           // tiles straddling one mask-interval boundary are not special
+    int32_t two_ok;           // read-block boundaries a non-special tile may straddle (0, 1; q8 ds >= 10: 2)
     int32_t probe;            // profiling only: bit0 skip subband formation, bit1 skip fill
     double tie_eps;           // 8-bit integer path: margin the rounding of a masked subband's pad
                               // constant needs (float-fold error, plus the /ds rounding in mean mode)
@@ -127,6 +127,9 @@ hipError_t launch_stage2_direct(const Stage2Args& a, hipStream_t st);
 hipError_t launch_stage2_lds(const Stage2Args& a, int q, hipStream_t st);
 hipError_t launch_pad(float* out, int64_t out_stride, int numdms, int64_t nds, int64_t numout,
                       const double* partial, int ntiles, int pad_mode, hipStream_t st);
+hipError_t launch_series_sum(const float* x, int64_t n, double* part, int nparts, hipStream_t st);
+hipError_t launch_series_fill(float* out, int64_t out_stride, int numdms, int64_t t0, int64_t t1, float v,
+                              hipStream_t st);
 
 // ---- PRESTO clip_times on the device (hd_clip.hip) ----
 // Scratch of one raw block's clip statistics; device pointers, sized by the host.
@@ -150,7 +153,14 @@ struct ClipArgs {
     int32_t* nevents;         // device counter
 };
 int clip_max_block();
-hipError_t launch_clip(const ClipArgs& a, hipStream_t st);
+hipError_t launch_clip(const ClipArgs& a, hipStream_t st);       // = stats + recur + flag
+hipError_t launch_clip_stats(const ClipArgs& a, hipStream_t st);
+hipError_t launch_clip_recur(const ClipArgs& a, hipStream_t st);
+hipError_t launch_clip_flag(const ClipArgs& a, hipStream_t st);
+// time-sliced contexts: rows [bavg, bstd, numgood, chansum[nchan]] of the first nown blocks
+// out; a global block range in (g.rd.nblk rows into g's arrays)
+hipError_t launch_clip_pack(const ClipArgs& a, double* out, int nown, hipStream_t st);
+hipError_t launch_clip_unpack(const ClipArgs& g, const double* in, hipStream_t st);
 // Exact recomputation of the stage-1 outputs a clipped spectrum (events) or a read-block
 // boundary with changing pad values (the 8-bit integer path's straddling outputs) touches.
 hipError_t launch_stage1_fixup(const Stage1Multi& a, const int32_t* events, const int32_t* nevents,
@@ -158,7 +168,7 @@ hipError_t launch_stage1_fixup(const Stage1Multi& a, const int32_t* events, cons
 constexpr int64_t kRawTPad = 65536;   // zero rows after N in each channel-major raw row
 hipError_t launch_raw_transpose8(const uint8_t* raw, int64_t N, int32_t nchan, uint8_t* rawT, int64_t tstride,
                                  hipStream_t st);
-hipError_t launch_synth(uint8_t* raw, int64_t N, int32_t rowbytes, const hd_synth_tab* tab_dev,
+hipError_t launch_synth(uint8_t* raw, int64_t N, int32_t rowbytes, const hd_synth_tab* tab_dev, int64_t t0,
                         hipStream_t st);
 
 }  // namespace hd

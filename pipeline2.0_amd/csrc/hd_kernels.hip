@@ -18,6 +18,7 @@
 // summation order (including the packed int16 one) is bit-identical.
 #include "hd_device.h"
 
+#include <algorithm>
 #include <map>
 #include <mutex>
 
@@ -221,7 +222,7 @@ __device__ __host__ __forceinline__ bool s1_special(const Stage1Multi& a, int64_
     if (tR0 + rows > a.rd.N) return true;
     if (a.rd.zidx) {
         const int64_t b0 = tR0 / a.rd.blk, b1 = (tR0 + rows - 1) / a.rd.blk;
-        if (b1 > b0 + (a.two_ok ? 1 : 0)) return true;   // the integer path takes two-block tiles
+        if (b1 > b0 + a.two_ok) return true;   // the integer path takes two- (ds >= 10: three-) block tiles
     }
     return false;
 }
@@ -485,6 +486,7 @@ struct Q8Geom {
     static constexpr int M = DS == 1 ? 4 : DS == 2 ? 2 : 1;   // outputs per lane per quarter
     static constexpr int JQ = 64 * M;                          // outputs per quarter
     static constexpr int S = JQ * DS;                          // dwords (raw rows) per quarter
+    static constexpr bool THREE = DS >= 10;                    // 4S + dmax may exceed a 2048-row block
 };
 
 int stage1_q8_quarter_rows(int ds)
@@ -534,6 +536,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 template <int CPS, int DS, int VB>
 __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
 {
+    constexpr bool THREE = Q8Geom<DS>::THREE;
     using Gm = Q8Geom<DS>;
     constexpr int M = Gm::M, JQ = Gm::JQ, S = Gm::S;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -579,7 +582,7 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
             }
 #pragma unroll
             for (int h = 0; h < U; h++) {
-                uint32_t* d = lds + lcs[h] * W + 16 * kbs[h];
+                uint32_t o[16];
 #pragma unroll
                 for (int w = 0; w < 4; w++) {
                     const uint32_t x0 = w == 0 ? r[h][0].x : w == 1 ? r[h][0].y : w == 2 ? r[h][0].z : r[h][0].w;
@@ -591,13 +594,25 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
                     const uint32_t ab_hi = __builtin_amdgcn_perm(x1, x0, 0x07030602u);
                     const uint32_t cd_lo = __builtin_amdgcn_perm(x3, x2, 0x05010400u);
                     const uint32_t cd_hi = __builtin_amdgcn_perm(x3, x2, 0x07030602u);
-                    const uint32_t o4[4] = {__builtin_amdgcn_perm(cd_lo, ab_lo, 0x05040100u),
-                                            __builtin_amdgcn_perm(cd_lo, ab_lo, 0x07060302u),
-                                            __builtin_amdgcn_perm(cd_hi, ab_hi, 0x05040100u),
-                                            __builtin_amdgcn_perm(cd_hi, ab_hi, 0x07060302u)};
+                    o[4 * w + 0] = __builtin_amdgcn_perm(cd_lo, ab_lo, 0x05040100u);
+                    o[4 * w + 1] = __builtin_amdgcn_perm(cd_lo, ab_lo, 0x07060302u);
+                    o[4 * w + 2] = __builtin_amdgcn_perm(cd_hi, ab_hi, 0x05040100u);
+                    o[4 * w + 3] = __builtin_amdgcn_perm(cd_hi, ab_hi, 0x07060302u);
+                }
+                // the unit's 16 dwords are contiguous (W is a multiple of 16): four 16-byte
+                // stores, the lanes of an 8-lane store group staggered over the four chunks
+                // (lanes are 64 B apart, so chunk w of every lane would share 2 of the 8
+                // bank quads: 4-way conflicts; staggered, the 8 lanes hit 8 distinct quads)
+                uint4* d = (uint4*)(lds + lcs[h] * W + 16 * kbs[h]);
+                const int rot = (threadIdx.x >> 1) & 3;
 #pragma unroll
-                    for (int j = 0; j < 4; j++)
-                        if (16 * kbs[h] + 4 * w + j < K) d[4 * w + j] = o4[j];
+                for (int st = 0; st < 4; st++) {
+                    const int w = (st + rot) & 3;
+                    const uint4 v = w == 0 ? make_uint4(o[0], o[1], o[2], o[3])
+                                  : w == 1 ? make_uint4(o[4], o[5], o[6], o[7])
+                                  : w == 2 ? make_uint4(o[8], o[9], o[10], o[11])
+                                           : make_uint4(o[12], o[13], o[14], o[15]);
+                    d[w] = v;
                 }
             }
         }
@@ -654,16 +669,19 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
     const int s = g * a.sg + sl;
     const int cl0 = sl * CPS;
     int lrb[CPS];
-    float pad0[CPS], pad1[CPS];
-    // read blocks: the tile lies in block b0, or straddles b0 | b0+1 at row brow
-    uint32_t z0 = 0, z1 = 0;
-    int brow = 1 << 30;
+    float pad0[CPS], pad1[CPS], pad2[THREE ? CPS : 1];
+    // read blocks: the tile lies in block b0, or straddles b0 | b0+1 at row brow (and, for
+    // THREE, b0+1 | b0+2 at row brow2: the 2560-row tiles of ds >= 6 outgrow a 2048-row block)
+    uint32_t z0 = 0, z1 = 0, z2 = 0;
+    int brow = 1 << 30, brow2 = 1 << 30;
     const int64_t b0 = tR0 / a.rd.blk;
     {
         const int64_t b = (b0 + 1) * a.rd.blk - tR0;
         if (b < 4 * S + a.dmax) brow = (int)b;
+        if (THREE && b + a.rd.blk < 4 * S + a.dmax) brow2 = (int)(b + a.rd.blk);
     }
     const int64_t b1 = brow < (1 << 30) ? b0 + 1 : b0;
+    const int64_t b2 = brow2 < (1 << 30) ? b0 + 2 : b1;
 #pragma unroll
     for (int cc = 0; cc < CPS; cc++) {
         const int c = c0 + cl0 + cc;
@@ -671,12 +689,16 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
         lrb[cc] = lr * W;
         pad0[cc] = pad_at(a.rd, b0, c);
         pad1[cc] = pad_at(a.rd, b1, c);
+        if (THREE) pad2[cc] = pad_at(a.rd, b2, c);
         if (zap_at(a.rd, b0, c)) z0 |= 1u << cc;
         if (zap_at(a.rd, b1, c)) z1 |= 1u << cc;
+        if (THREE && zap_at(a.rd, b2, c)) z2 |= 1u << cc;
     }
     z0 = __builtin_amdgcn_readfirstlane(z0);
     z1 = __builtin_amdgcn_readfirstlane(z1);
-    const uint32_t zany = z0 | z1, zall = z0 & z1, zsplit = z0 ^ z1;
+    if (!THREE) z2 = z1;
+    z2 = __builtin_amdgcn_readfirstlane(z2);
+    const uint32_t zany = z0 | z1 | z2, zall = z0 & z1 & z2, zsplit = (z0 ^ z1) | (z1 ^ z2);
     const int fz = zany ? __builtin_ctz(zany) : CPS;      // first channel off the integer path
     const uint32_t* lbase = lds + lane * DS;
     const bool mean = a.ds_mode == 1;
@@ -694,34 +716,38 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
     // them.  Near-ties, split channels (masked in one block only), negative pads and f32
     // output with masked channels take the exact float fold below.
     const int Dh = mean ? DS / 2 : 0;                     // floor(D/2) for D = DS or 1
-    int cadd0 = a.sub_dtype == 0 ? Dh : 0, cadd1 = cadd0;
+    int cadd0 = a.sub_dtype == 0 ? Dh : 0, cadd1 = cadd0, cadd2 = cadd0;
     bool intpath = zany == 0;
     if (zany && zsplit == 0 && a.sub_dtype == 0) {
-        double P0 = 0.0, P1 = 0.0;
+        double P0 = 0.0, P1 = 0.0, P2 = 0.0;
         bool neg = false, integral = true;
 #pragma unroll
         for (int cc = 0; cc < CPS; cc++)
             if (zall & (1u << cc)) {
+                const float p2 = THREE ? pad2[cc] : pad1[cc];
                 P0 += (double)pad0[cc];
                 P1 += (double)pad1[cc];
-                neg |= pad0[cc] < 0.0f || pad1[cc] < 0.0f;
-                integral &= pad0[cc] == floorf(pad0[cc]) && pad1[cc] == floorf(pad1[cc]);
+                P2 += (double)p2;
+                neg |= pad0[cc] < 0.0f || pad1[cc] < 0.0f || p2 < 0.0f;
+                integral &= pad0[cc] == floorf(pad0[cc]) && pad1[cc] == floorf(pad1[cc]) && p2 == floorf(p2);
             }
         const double half = mean ? 0.5 * DS : 0.5;
-        const double C0 = (double)DS * P0 + half, C1 = (double)DS * P1 + half;
-        const double f0 = C0 - floor(C0), f1 = C1 - floor(C1);
-        const double m0 = fmin(f0, 1.0 - f0), m1 = fmin(f1, 1.0 - f1);
+        const double C0 = (double)DS * P0 + half, C1 = (double)DS * P1 + half, C2 = (double)DS * P2 + half;
+        const double f0 = C0 - floor(C0), f1 = C1 - floor(C1), f2 = C2 - floor(C2);
+        const double m0 = fmin(f0, 1.0 - f0), m1 = fmin(f1, 1.0 - f1), m2 = fmin(f2, 1.0 - f2);
         const double cap = mean ? 65535.0 : 32767.0;
-        if (!neg && (integral || (m0 > a.tie_eps && m1 > a.tie_eps)) &&
-            fmax(C0, C1) + (double)(CPS * DS * 255) <= cap) {
+        if (!neg && (integral || (m0 > a.tie_eps && m1 > a.tie_eps && m2 > a.tie_eps)) &&
+            fmax(fmax(C0, C1), C2) + (double)(CPS * DS * 255) <= cap) {
             intpath = true;
             cadd0 = (int)floor(C0);
             cadd1 = (int)floor(C1);
+            cadd2 = (int)floor(C2);
         }
     }
     intpath = __builtin_amdgcn_readfirstlane((int)intpath) != 0;
     cadd0 = __builtin_amdgcn_readfirstlane(cadd0);
     cadd1 = __builtin_amdgcn_readfirstlane(cadd1);
+    cadd2 = __builtin_amdgcn_readfirstlane(cadd2);
     const bool fast_out = a.sub_dtype == 0 && !mean;      // int16 sums stored as they are
     // channel delays of pass p live in lanes 0..CPS-1 of vd; pass p+1's are loaded while
     // pass p is formed, so no global-load latency sits at the head of a pass
@@ -745,12 +771,13 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
             uint32_t ae[M], ao[M];
 #pragma unroll
             for (int m = 0; m < M; m++) {
-                // quarter q of output j: block b1's constant once its last row reaches brow
+                // quarter q of output j: the constant of the block its last row lies in
                 const int lastrow = (lane + 64 * m) * DS + DS - 1 + dmx;
-                const uint32_t k0 = (uint32_t)(lastrow < brow ? cadd0 : cadd1);
-                const uint32_t k1 = (uint32_t)(lastrow + S < brow ? cadd0 : cadd1);
-                const uint32_t k2 = (uint32_t)(lastrow + 2 * S < brow ? cadd0 : cadd1);
-                const uint32_t k3 = (uint32_t)(lastrow + 3 * S < brow ? cadd0 : cadd1);
+                auto kof = [&](int row) {
+                    return (uint32_t)(row < brow ? cadd0 : (!THREE || row < brow2) ? cadd1 : cadd2);
+                };
+                const uint32_t k0 = kof(lastrow), k1 = kof(lastrow + S), k2 = kof(lastrow + 2 * S),
+                               k3 = kof(lastrow + 3 * S);
                 ae[m] = k0 | (k2 << 16);
                 ao[m] = k1 | (k3 << 16);
             }
@@ -811,15 +838,22 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
                             }
                             f32x2 v01 = {(float)(x & 0xFFu), (float)((x >> 8) & 0xFFu)};
                             f32x2 v23 = {(float)((x >> 16) & 0xFFu), (float)(x >> 24)};
-                            if (zany & (1u << cc)) {   // masked in one or both blocks: per-row block
+                            if (zany & (1u << cc)) {   // masked in some block: per-row block
                                 const int rr = t + dl[cc];
-                                const bool h0 = rr >= brow, h1 = rr + S >= brow, h2 = rr + 2 * S >= brow,
-                                           h3 = rr + 3 * S >= brow;
-                                const bool za = (z0 >> cc) & 1, zb = (z1 >> cc) & 1;
-                                if (h0 ? zb : za) v01.x = h0 ? pad1[cc] : pad0[cc];
-                                if (h1 ? zb : za) v01.y = h1 ? pad1[cc] : pad0[cc];
-                                if (h2 ? zb : za) v23.x = h2 ? pad1[cc] : pad0[cc];
-                                if (h3 ? zb : za) v23.y = h3 ? pad1[cc] : pad0[cc];
+                                const bool za = (z0 >> cc) & 1, zb = (z1 >> cc) & 1, zc = (z2 >> cc) & 1;
+                                auto cl = [&](int row, float x) {
+                                    if (!THREE || row < brow2) {
+                                        const bool h = row >= brow;
+                                        if (h ? zb : za) x = h ? pad1[cc] : pad0[cc];
+                                    } else if (zc) {
+                                        x = pad2[THREE ? cc : 0];
+                                    }
+                                    return x;
+                                };
+                                v01.x = cl(rr, v01.x);
+                                v01.y = cl(rr + S, v01.y);
+                                v23.x = cl(rr + 2 * S, v23.x);
+                                v23.y = cl(rr + 3 * S, v23.y);
                             }
                             sk01 += v01;
                             sk23 += v23;
@@ -2382,12 +2416,47 @@ hipError_t launch_pad(float* out, int64_t out_stride, int numdms, int64_t nds, i
     return hipGetLastError();
 }
 
+// ---- series sums and fills (time-sliced passes: the padding value is the observation's) --
+__global__ __launch_bounds__(256) void k_series_sum(const float* __restrict__ x, int64_t n, double* __restrict__ part)
+{
+    __shared__ double red[256];
+    double acc = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) acc += (double)x[i];
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = 128; w >= 1; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+hipError_t launch_series_sum(const float* x, int64_t n, double* part, int nparts, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_series_sum, dim3((unsigned)nparts), dim3(256), 0, st, x, n, part);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_series_fill(float* out, int64_t out_stride, int64_t t0, int64_t t1, float v)
+{
+    float* o = out + (int64_t)blockIdx.y * out_stride;
+    for (int64_t t = t0 + (int64_t)blockIdx.x * 256 + threadIdx.x; t < t1; t += (int64_t)gridDim.x * 256) o[t] = v;
+}
+
+hipError_t launch_series_fill(float* out, int64_t out_stride, int numdms, int64_t t0, int64_t t1, float v, hipStream_t st)
+{
+    if (t1 <= t0 || numdms <= 0) return hipSuccess;
+    const int64_t nb = std::min<int64_t>((t1 - t0 + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_series_fill, dim3((unsigned)nb, (unsigned)numdms), dim3(256), 0, st, out, out_stride, t0, t1, v);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------------------------
 // synthetic beam
 // ------------------------------------------------------------------------------------
 
 __global__ __launch_bounds__(256) void k_synth(uint8_t* raw, int64_t N, int32_t rowbytes,
-                                              const hd_synth_tab* __restrict__ tb)
+                                              const hd_synth_tab* __restrict__ tb, int64_t t0)
 {
     const int32_t *base_q4, *noise_mul, *rfi_flag;
     const int64_t *psr_delay, *sp_delay;
@@ -2396,17 +2465,18 @@ __global__ __launch_bounds__(256) void k_synth(uint8_t* raw, int64_t N, int32_t 
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
         const int64_t t = i / rowbytes;
         const int32_t b = (int32_t)(i - t * rowbytes);
-        raw[i] = hd_synth_byte(tb, base_q4, noise_mul, rfi_flag, psr_delay, sp_delay, t, b);
+        raw[i] = hd_synth_byte(tb, base_q4, noise_mul, rfi_flag, psr_delay, sp_delay, t0 + t, b);
     }
 }
 
-hipError_t launch_synth(uint8_t* raw, int64_t N, int32_t rowbytes, const hd_synth_tab* tab_dev, hipStream_t st)
+hipError_t launch_synth(uint8_t* raw, int64_t N, int32_t rowbytes, const hd_synth_tab* tab_dev, int64_t t0,
+                        hipStream_t st)
 {
     const int64_t total = N * rowbytes;
     int64_t nb = (total + 255) / 256;
     if (nb > 256 * 64) nb = 256 * 64;
     if (nb < 1) nb = 1;
-    hipLaunchKernelGGL(k_synth, dim3((unsigned)nb), dim3(256), 0, st, raw, N, rowbytes, tab_dev);
+    hipLaunchKernelGGL(k_synth, dim3((unsigned)nb), dim3(256), 0, st, raw, N, rowbytes, tab_dev, t0);
     return hipGetLastError();
 }
 

@@ -38,6 +38,7 @@ EXPORTED = [
     "hd_get_raw", "hd_plan_tables", "hd_run_subband_multi", "hd_push_raw_device", "hd_get_raw_device",
     "hd_push_raw_file", "hd_set_streams", "hd_touch_raw", "hd_stats_padvals", "hd_get_clean",
     "hd_get_subbands_window", "hd_get_series", "hd_write_series", "hd_wait_writes",
+    "hd_set_slice", "hd_clip_stats", "hd_clip_set_stats", "hd_series_sum", "hd_series_fill",
 ]
 
 
@@ -146,6 +147,11 @@ def load():
         "hd_get_raw_device": (ctypes.c_int, [vp, vp, i64, i64]),
         "hd_push_raw_file": (ctypes.c_int, [vp, ctypes.c_char_p, P(hd_rows_src), i64, P(ctypes.c_double),
                                             P(ctypes.c_double)]),
+        "hd_set_slice": (ctypes.c_int, [vp, i64, i64]),
+        "hd_clip_stats": (ctypes.c_int, [vp, i64, vp]),
+        "hd_clip_set_stats": (ctypes.c_int, [vp, vp]),
+        "hd_series_sum": (ctypes.c_int, [vp, i32, i64, i64, P(ctypes.c_double)]),
+        "hd_series_fill": (ctypes.c_int, [vp, i64, ctypes.c_float]),
         "hd_plan_tables": (ctypes.c_int, [P(hd_obs), P(hd_opts), P(hd_pass), P(ctypes.c_int32),
                                           P(ctypes.c_int32), P(ctypes.c_double), P(ctypes.c_double),
                                           P(ctypes.c_double)]),

@@ -250,6 +250,23 @@ class Engine:
                   "hd_get_raw")
         return out
 
+    # -- time slices (multi-GPU, hipdedisp.sharding.TimeSlices) --
+    def set_slice(self, t0, n_total):
+        """This context holds spectra [t0, t0 + obs.N) of an observation of n_total spectra
+        (hd_set_slice; (0, 0) = the whole observation)."""
+        self._chk(self._L.hd_set_slice(self._ctx, int(t0), int(n_total)), "hd_set_slice")
+
+    def clip_stats(self, nown, stats):
+        """Rows of this slice's first `nown` read blocks into `stats` (hd_clip_stats): a
+        float64 numpy array [nblk_total][nchan + 3] or an int device address of one."""
+        ptr = stats if isinstance(stats, int) else stats.ctypes.data
+        self._chk(self._L.hd_clip_stats(self._ctx, int(nown), ctypes.c_void_p(ptr)), "hd_clip_stats")
+
+    def clip_set_stats(self, stats):
+        """Finish clip_times for this slice from the observation's per-block statistics."""
+        ptr = stats if isinstance(stats, int) else stats.ctypes.data
+        self._chk(self._L.hd_clip_set_stats(self._ctx, ctypes.c_void_p(ptr)), "hd_clip_set_stats")
+
     def synth_device(self, synth: hd_synth):
         self._chk(self._L.hd_synth_device(self._ctx, ctypes.byref(synth)), "hd_synth_device")
 
@@ -334,6 +351,17 @@ class Plan:
         self.eng._chk(self.eng._L.hd_get_series(self._p, int(dm0), int(ndm), int(t0), int(count), _f32p(out)),
                       "hd_get_series")
         return out
+
+    def series_sum(self, dm, t0, count):
+        """Exact double sum of series samples [t0, t0+count) of DM dm (hd_series_sum)."""
+        v = ctypes.c_double()
+        self.eng._chk(self.eng._L.hd_series_sum(self._p, int(dm), int(t0), int(count), ctypes.byref(v)),
+                      "hd_series_sum")
+        return v.value
+
+    def series_fill(self, t0, value):
+        """Samples [t0, numout) of every DM := value (hd_series_fill)."""
+        self.eng._chk(self.eng._L.hd_series_fill(self._p, int(t0), float(value)), "hd_series_fill")
 
     def set_subbands(self, sub):
         a = np.ascontiguousarray(sub, dtype=self._sub_dtype())

@@ -1,5 +1,17 @@
 """Multi-GPU partitioning of a beam's DDplan (north_star (d)).
 
+Two ways to spread ONE beam over the G GPUs of a node, plus the trivial beam-per-GPU mode:
+
+* **time slices** (`TimeSlices`, the default for one beam): rank r dedisperses spectra
+  [t0_r, t0_r + own_r) through ALL 57 passes; it holds those spectra plus a halo of the next
+  rank's first spectra (the longest delay of any pass), so its output samples are exact and
+  each output sample is computed once.  No raw-block exchange: each rank ingests only its
+  own rows.  The one true exchange is PRESTO's clip_times, whose running statistics carry
+  across read blocks: every rank contributes the per-block statistics of its own blocks
+  (an all-reduce of a [nblk][nchan + 3] double table, ~16 MB for a PALFA beam) and runs the
+  serial recurrence up to its end.  The padding value of each pass (the first DM's mean) is
+  the observation's: one all-reduce of a [passes] vector of series sums at the end.
+
 The reference runs one beam per batch job on one core (`nodes=X:ppn=1`,
 lib/python/queue_managers/pbs.py:67) and its passes strictly in sequence
 (lib/python/PALFA2_presto_search.py:494-529).  The passes are independent: each has its own
@@ -154,3 +166,110 @@ def dm_strings_of(ddplans, assignment: List[List[PassRef]]):
 
 def sample_counts(ddplans, N):
     return np.array([d.dmsperpass * (N // d.sub_downsamp) for d in ddplans for _ in range(d.numpasses)])
+
+
+# ---------------------------------------------------------------------------------------
+# time slices
+# ---------------------------------------------------------------------------------------
+
+def _lcm(a, b):
+    from math import gcd
+    return a * b // gcd(a, b)
+
+
+class TimeSlices:
+    """One beam's spectra cut into `world` contiguous slices (one per rank) for the DDplan
+    `ddplans`.  Slice boundaries are multiples of lcm(nsblk, every downsampling factor), so
+    every read block and every downsampled output sample belongs to exactly one rank.
+
+        ts = TimeSlices(obs, ddplans, world)
+        t0, own, n_local = ts.slice(rank)      # spectra [t0, t0 + n_local) held, own computed
+        j0, nj = ts.out_range(rank, ds)        # output samples [j0, j0 + nj) this rank owns
+    """
+
+    def __init__(self, obs, ddplans, world, opts=None):
+        from .engine import Opts, PassParams, plan_tables
+        if world < 1:
+            raise ValueError("world must be >= 1")
+        self.obs, self.ddplans, self.world = obs, list(ddplans), world
+        self.opts = opts or Opts()
+        if world > 1 and self.opts.pad_mode == 0:        # HD_PAD_MEAN: one value per DM
+            raise ValueError("time slices support pad_mode HD_PAD_DM0 / HD_PAD_ZERO")
+        blk = obs.nsblk if 0 < obs.nsblk < obs.N else obs.N
+        unit = blk
+        reach = 0
+        for d in self.ddplans:
+            unit = _lcm(unit, d.sub_downsamp)
+            for i in range(d.numpasses):
+                pp = PassParams(subdm=float(d.subdmlist[i]), lodm=float(d.lodm_arg(i)),
+                                dmstep=float(d.dmstep_arg()), numdms=d.dmsperpass, nsub=d.numsub,
+                                ds=d.sub_downsamp)
+                idd, off, _ = plan_tables(obs, self.opts, pp)
+                # last raw row output j uses: (j + max offset) * ds + ds - 1 + max channel delay
+                reach = max(reach, int(off.max()) * d.sub_downsamp + int(idd.max()) + d.sub_downsamp)
+        self.blk, self.unit = blk, unit
+        self.halo = -(-reach // blk) * blk
+        N = obs.N
+        cuts = [0] + [min(N, round(k * N / world / unit) * unit) for k in range(1, world)] + [N]
+        for k in range(1, len(cuts)):
+            cuts[k] = max(cuts[k], cuts[k - 1])
+        self.cuts = cuts
+        self.nblk_total = -(-N // blk)
+
+    def slice(self, rank):
+        """(t0, own, n_local): first spectrum, spectra owned, spectra held (own + halo)."""
+        t0, t1 = self.cuts[rank], self.cuts[rank + 1]
+        n_local = min(self.obs.N, t1 + self.halo) - t0
+        return t0, t1 - t0, n_local
+
+    def local_obs(self, rank):
+        import copy
+        o = copy.copy(self.obs)
+        o.N = self.slice(rank)[2]
+        return o
+
+    def nown_blocks(self, rank):
+        t0, own, _ = self.slice(rank)
+        return -(-own // self.blk) if rank == self.world - 1 else own // self.blk
+
+    def out_range(self, rank, ds):
+        """(first global output sample, count) this rank owns at downsampling ds."""
+        t0, own, _ = self.slice(rank)
+        nds = self.obs.N // ds
+        j0 = t0 // ds
+        nj = nds - j0 if rank == self.world - 1 else own // ds
+        return j0, max(nj, 0)
+
+    def numout_local(self, rank, numout_global, ds):
+        """-numout of a rank's local pass: the last rank pads to the global length."""
+        if rank == self.world - 1:
+            return max(numout_global - self.slice(rank)[0] // ds, 0)
+        return 0
+
+    def stats_table(self):
+        """A zeroed [nblk_total][nchan + 3] float64 table for the clip statistics."""
+        return np.zeros((self.nblk_total, self.obs.nchan + 3), np.float64)
+
+    # -- the two exchanges of a sliced beam (callers all-reduce between the phases) --
+    def contribute_clip_stats(self, engine, rank, table):
+        """Phase A: this rank's own read blocks' clip statistics into `table` (a zeroed
+        stats_table(), or the device address of one); sum the tables over the ranks, then
+        engine.clip_set_stats(table) (phase B) before stage 1."""
+        engine.clip_stats(self.nown_blocks(rank), table)
+
+    def pass_sums(self, rank, plans):
+        """Phase C: per plan, the exact sum of the first DM's owned output samples (the
+        padding value of prepsubband is the observation's first-DM mean)."""
+        return np.array([p.series_sum(0, 0, self.out_range(rank, p.pp.ds)[1]) for p in plans], np.float64)
+
+    def pad_passes(self, rank, plans, sums):
+        """Phase D (after summing pass_sums over the ranks): the last rank pads its series
+        from N/ds to -numout with the observation's value (HD_PAD_DM0) or 0 (HD_PAD_ZERO)."""
+        if rank != self.world - 1:
+            return
+        for p, s in zip(plans, sums):
+            nj = self.out_range(rank, p.pp.ds)[1]
+            if p.numout > nj:
+                nds = self.obs.N // p.pp.ds
+                v = np.float32(s / nds) if self.opts.pad_mode == 2 and nds > 0 else np.float32(0.0)
+                p.series_fill(nj, float(v))

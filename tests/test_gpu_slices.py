@@ -1,0 +1,112 @@
+"""Multi-GPU time slices (hipdedisp.sharding.TimeSlices) on one GPU: the ranks of a world-3
+node run one after another on their own contexts, their two exchanges (clip statistics,
+padding sums) summed in numpy where the node all-reduces over RCCL.  The union of the
+ranks' owned series must equal a whole-beam run bit for bit -- clipping, mask and padding
+included -- and so must the per-block cleaning state."""
+import copy
+
+import numpy as np
+import pytest
+
+from hipdedisp import Engine, Opts, PassParams, plan as P
+from hipdedisp import sharding as S
+from hipdedisp.synth import palfa_obs, palfa_synth, synth_mask
+
+pytestmark = pytest.mark.gpu
+
+
+def spiky():
+    s = palfa_synth()
+    s.spike_frac, s.spike_amp = 0.002, 40.0
+    return s
+
+
+def small_plan():
+    out = []
+    for st, n in ((0, 2), (3, 1), (5, 1)):
+        d = copy.copy(P.ddplans_for("pdev")[st])
+        d.numpasses = n
+        out.append(d)
+    return out
+
+
+def pass_params(obs, d, i, numout=None):
+    return PassParams(subdm=float(d.subdmlist[i]), lodm=float(d.lodm_arg(i)), dmstep=float(d.dmstep_arg()),
+                      numdms=d.dmsperpass, nsub=d.numsub, ds=d.sub_downsamp,
+                      numout=P.choose_N(obs.N / d.downsamp) if numout is None else numout)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_time_slices_union_equals_whole_beam(engine, world):
+    obs = palfa_obs(N=(1 << 18) + 4 * 30720 + 777, nbits=8, nsblk=2048)
+    synth = spiky()
+    pts = 16384
+    mask, pad = synth_mask(obs, synth, pts, frac=0.03)
+    ddplans = small_plan()
+    # the whole beam on the test engine
+    engine.set_obs(obs, Opts())
+    engine.synth_device(synth)
+    engine.set_mask(mask, pts, pad)
+    want = {}
+    gpad, gclip, _, _ = engine.get_clean()
+    for d in ddplans:
+        plans = [engine.plan(pass_params(obs, d, i)) for i in range(d.numpasses)]
+        engine.run_subband_multi(plans)
+        for i, p in enumerate(plans):
+            want[(d.sub_downsamp, i)] = p.run_dedisp()
+            p.destroy()
+    engine.set_mask()
+
+    ts = S.TimeSlices(obs, ddplans, world)
+    assert ts.cuts[0] == 0 and ts.cuts[-1] == obs.N and all(c % ts.unit == 0 for c in ts.cuts[1:-1])
+    engs, plans = [], []
+    try:
+        table = ts.stats_table()
+        for r in range(world):                          # phase A on every rank
+            e = Engine(0)
+            engs.append(e)
+            t0, own, nloc = ts.slice(r)
+            e.set_obs(ts.local_obs(r), Opts())
+            e.set_slice(t0, obs.N)
+            e.synth_device(synth)
+            e.set_mask(mask, pts, pad)
+            mine = ts.stats_table()
+            ts.contribute_clip_stats(e, r, mine)
+            table += mine                               # the all-reduce
+        for r, e in enumerate(engs):                    # phase B: clip state, then every pass
+            e.clip_set_stats(table)
+            t0, own, nloc = ts.slice(r)
+            lpad, lclip, _, _ = e.get_clean()
+            assert np.array_equal(lclip[:own], gclip[t0:t0 + own]), r
+            nb = ts.nown_blocks(r)
+            assert np.array_equal(lpad[:nb], gpad[t0 // ts.blk:t0 // ts.blk + nb]), r
+            mine = []
+            for d in ddplans:
+                ps = [e.plan(pass_params(ts.local_obs(r), d, i,
+                                         ts.numout_local(r, P.choose_N(obs.N / d.downsamp), d.sub_downsamp)))
+                      for i in range(d.numpasses)]
+                e.run_subband_multi(ps)
+                for p in ps:
+                    p.run_dedisp(to_host=False)
+                mine += ps
+            plans.append(mine)
+        sums = sum(ts.pass_sums(r, plans[r]) for r in range(world))      # phase C + all-reduce
+        for r in range(world):
+            ts.pad_passes(r, plans[r], sums)                               # phase D
+        for r in range(world):
+            k = 0
+            for d in ddplans:
+                for i in range(d.numpasses):
+                    p = plans[r][k]
+                    k += 1
+                    j0, nj = ts.out_range(r, d.sub_downsamp)
+                    full = want[(d.sub_downsamp, i)]
+                    n = p.numout if r == world - 1 else nj
+                    got = p.get_series(0, None, 0, n)
+                    assert np.array_equal(got, full[:, j0:j0 + n]), (r, d.sub_downsamp, i)
+    finally:
+        for lst in plans:
+            for p in lst:
+                p.destroy()
+        for e in engs:
+            e.close()

@@ -157,3 +157,103 @@ def test_sharded_union_equals_single_rank(engine):
     assert sorted(got) == sorted(want)
     for k in want:
         assert np.array_equal(got[k], want[k]), k
+
+
+# ---- time slices ----------------------------------------------------------------------
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 7, 8])
+def test_time_slices_partition(world):
+    """Slices cover the beam once, start on lcm(nsblk, every ds) boundaries, carry a halo of
+    whole read blocks past the longest delay of any pass, and every downsampled output
+    sample of every DDplan stage is owned by exactly one rank."""
+    plans = P.ddplans_for("pdev")
+    obs = palfa_obs(N=1 << 22)
+    ts = S.TimeSlices(obs, plans, world)
+    assert ts.unit == 30720 and ts.halo % obs.nsblk == 0 and ts.halo > 0
+    owned = 0
+    for r in range(world):
+        t0, own, nloc = ts.slice(r)
+        assert t0 == owned and t0 % ts.unit == 0
+        assert nloc == min(obs.N, t0 + own + ts.halo) - t0
+        owned += own
+        assert abs(own - obs.N / world) <= ts.unit
+    assert owned == obs.N
+    assert sum(ts.nown_blocks(r) for r in range(world)) == ts.nblk_total
+    for d in plans:
+        ds = d.sub_downsamp
+        cover = np.zeros(obs.N // ds, np.int32)
+        for r in range(world):
+            j0, nj = ts.out_range(r, ds)
+            cover[j0:j0 + nj] += 1
+        assert (cover == 1).all(), ds
+
+
+def test_time_slices_halo_covers_every_pass():
+    """The halo reaches the last raw row any owned output sample reads, for every pass."""
+    from hipdedisp import Opts, PassParams
+    from hipdedisp.engine import plan_tables
+    plans = P.ddplans_for("pdev")
+    obs = palfa_obs(N=1 << 22)
+    ts = S.TimeSlices(obs, plans, 4)
+    for d in plans:
+        for i in (0, d.numpasses - 1):
+            pp = PassParams(subdm=float(d.subdmlist[i]), lodm=float(d.lodm_arg(i)), dmstep=float(d.dmstep_arg()),
+                            numdms=d.dmsperpass, nsub=d.numsub, ds=d.sub_downsamp)
+            idd, off, _ = plan_tables(obs, Opts(), pp)
+            t0, own, nloc = ts.slice(1)
+            last_out = own // d.sub_downsamp - 1
+            last_row = (last_out + int(off.max())) * d.sub_downsamp + d.sub_downsamp - 1 + int(idd.max())
+            assert last_row < nloc
+
+
+class _FakeSliceEngine:
+    """Stands in for a sliced Engine in the exchange test: per-block statistics are a known
+    function of the global block index."""
+
+    def __init__(self, t0, blk, nchan):
+        self.t0, self.blk, self.nchan = t0, blk, nchan
+
+    def clip_stats(self, nown, table):
+        g0 = self.t0 // self.blk
+        for b in range(nown):
+            table[g0 + b] = (g0 + b) * 1000.0 + np.arange(self.nchan + 3)
+
+
+def _slice_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        obs = palfa_obs(N=(1 << 20) + 777, nchan=96)
+        ts = S.TimeSlices(obs, P.ddplans_for("pdev"), world)
+        t = torch.zeros((ts.nblk_total, obs.nchan + 3), dtype=torch.float64)
+        ts.contribute_clip_stats(_FakeSliceEngine(ts.slice(rank)[0], ts.blk, obs.nchan), rank, t.numpy())
+        dist.all_reduce(t)                                   # phase A exchange
+        sums = torch.tensor([float(rank + 1), 2.0 * (rank + 1)], dtype=torch.float64)
+        dist.all_reduce(sums)                                # phase C exchange
+        q.put((rank, t.numpy().copy(), sums.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_time_slice_exchanges_gloo_world2():
+    """The two all-reduces of a sliced beam on gloo at world size 2: the summed clip
+    statistics table has every read block's row exactly once, and the padding sums add."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_slice_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    nblk = res[0][1].shape[0]
+    want = np.arange(nblk)[:, None] * 1000.0 + np.arange(res[0][1].shape[1])[None, :]
+    for rank, table, sums in res:
+        assert np.array_equal(table, want)
+        assert sums == [3.0, 6.0]
