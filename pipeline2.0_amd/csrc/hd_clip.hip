@@ -829,7 +829,9 @@ hipError_t launch_stage1_fixup(const Stage1Multi& a, const int32_t* events, cons
                            boundaries);
         return hipGetLastError();
     }
-    if (a.nsub > 256 || a.rd.N >= ((int64_t)1 << 31) - (1 << 24)) return hipErrorInvalidValue;
+    // boundary items scan one subband per thread (nsub <= blockDim); clipped-spectrum items loop
+    // over channels, so any nsub (e.g. the nsub = nchan no-subband pass) takes them
+    if ((boundaries && a.nsub > 256) || a.rd.N >= ((int64_t)1 << 31) - (1 << 24)) return hipErrorInvalidValue;
     const size_t lds = fixup_lds_bytes(a);
     if (lds > 64 * 1024) return hipErrorInvalidValue;
     // grid-stride over a device-side event count: no host round trip for the count
