@@ -363,31 +363,41 @@ extern "C" int hd_touch_raw(hd_ctx* c)
     return HD_OK;
 }
 
-// Channel-major copy of the 8-bit raw block for k_stage1_q8's fill, rebuilt on the stream
-// (and charged to the stage-1 launch that needs it) once per raw block.  nullptr when it
-// does not apply (the kernel then fills from the row-major block).
-static const uint8_t* ensure_rawT(hd_ctx* c, int dmax)
+// Channel-major one-byte-per-sample copy of the 8- or 4-bit raw block for k_stage1_q8's and
+// k_stage1_fix8's fills, rebuilt on the stream (and charged to the stage-1 launch that needs
+// it) once per raw block.  nullptr when it does not apply (8-bit data then fills from the
+// row-major block; 4-bit data takes the float tiled kernel).
+static bool alloc_rawT(hd_ctx* c, int dmax)
 {
-    if (c->obs.nbits != 8 || c->obs.nchan % 4 || c->obs.N % 4 || (int64_t)dmax + 8 > hd::kRawTPad) return nullptr;
+    const int nb = c->obs.nbits;
+    if ((nb != 8 && nb != 4) || c->obs.nchan % (nb == 4 ? 8 : 4) || c->obs.N % 4 || (int64_t)dmax + 8 > hd::kRawTPad)
+        return false;
     if (!c->d_rawT) {
         const int64_t stride = (int64_t)round_up((size_t)(c->obs.N + hd::kRawTPad), 256);
         const size_t bytes = (size_t)stride * c->obs.nchan;
         if (hipMalloc(&c->d_rawT, bytes) != hipSuccess) {
             c->d_rawT = nullptr;
             (void)hipGetLastError();
-            return nullptr;                // no room: row-major fill
+            return false;                // no room: row-major fill
         }
         if (hipMemsetAsync(c->d_rawT, 0, bytes, c->stream) != hipSuccess) {
             dfree(c->d_rawT);
             c->d_rawT = nullptr;
-            return nullptr;
+            return false;
         }
         c->rawT_stride = stride;
         c->rawT_valid = false;
     }
+    return true;
+}
+
+static const uint8_t* ensure_rawT(hd_ctx* c, int dmax)
+{
+    if (!alloc_rawT(c, dmax)) return nullptr;
+    const int nb = c->obs.nbits;
     if (!c->rawT_valid) {
-        if (hd::launch_raw_transpose8(c->d_raw, c->obs.N, c->obs.nchan, c->d_rawT, c->rawT_stride, c->stream) !=
-            hipSuccess)
+        if (hd::launch_raw_transpose(c->d_raw, c->obs.N, c->obs.nchan, nb, c->opts.nibble_hi_first, c->d_rawT,
+                                     c->rawT_stride, c->stream) != hipSuccess)
             return nullptr;
         c->rawT_valid = true;
     }
@@ -1693,7 +1703,9 @@ static bool stage1_tiling_fixed(const hd_ctx* c, int nsub, int ds, int dmax, int
 static bool stage1_q8_tiling(const hd_ctx* c, int nsub, int ds, int dmax, hd::Stage1Multi& a, int& vb)
 {
     const int nchan = c->obs.nchan, cps = nchan / nsub;
-    if (c->obs.nbits != 8 || c->d_scl || c->d_offs || c->d_wts) return false;
+    // 8-bit data, or 4-bit data through its unpacked channel-major copy (the fill then never
+    // reads the packed rows)
+    if ((c->obs.nbits != 8 && c->obs.nbits != 4) || c->d_scl || c->d_offs || c->d_wts) return false;
     if (!hd::stage1_q8_supports(cps, ds)) return false;
     const int S = hd::stage1_q8_quarter_rows(ds);
     const int W = S + ((dmax + 15) & ~15);            // whole 16-row fill units (16-byte LDS stores)
@@ -1783,7 +1795,8 @@ static int run_subband_chunk(hd_ctx* c, hd_plan** plans, int n)
     hd::Stage1Multi m{};
     int vw = 4, vb = 4;
     const int v1 = p0->s1_variant;
-    const bool q8 = (v1 == 0 || v1 == 3) && stage1_q8_tiling(c, p0->pass.nsub, p0->pass.ds, dmax, m, vb);
+    const bool q8 = (v1 == 0 || v1 == 3) && stage1_q8_tiling(c, p0->pass.nsub, p0->pass.ds, dmax, m, vb) &&
+                    (c->obs.nbits == 8 || (!(p0->probe & 4) && alloc_rawT(c, dmax)));
     if (v1 == 3 && !q8)
         return fail(c, HD_E_INVAL, "stage-1 variant 3 (8-bit integer path) does not apply to this pass");
     const bool tiled = !q8 && (v1 == 0 || v1 == 2) && stage1_tiling(c, p0->pass.nsub, p0->pass.ds, dmax, m, vw);
@@ -1797,6 +1810,7 @@ static int run_subband_chunk(hd_ctx* c, hd_plan** plans, int n)
         m.probe = p0->probe;
         m.rd = raw_desc(c);
         m.rawT = (p0->probe & 4) ? nullptr : ensure_rawT(c, dmax);   // probe bit 2: row-major fill
+        if (!m.rawT && c->obs.nbits != 8) return fail(c, HD_E_HIP, "stage 1: 4-bit channel-major copy failed");
         m.tstride = c->rawT_stride;
         m.npass = n;
         m.nsub = p0->pass.nsub;

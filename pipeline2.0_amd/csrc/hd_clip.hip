@@ -51,6 +51,28 @@ __global__ __launch_bounds__(256) void k_clip_zdm_u8(RawDesc rd, float* __restri
     if (lane == 0) zdm[t] = (float)acc;
 }
 
+// 4-bit data without calibration: the same with the low and high nibbles of every byte.
+__global__ __launch_bounds__(256) void k_clip_zdm_u4(RawDesc rd, float* __restrict__ zdm)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (t >= rd.N) return;
+    const uint8_t* row = rd.raw + t * rd.rowbytes;
+    uint32_t acc = 0;
+    for (int o = lane * 16; o < rd.rowbytes; o += 1024) {
+        const uint4 v = *(const uint4*)(row + o);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            acc = __builtin_amdgcn_udot4(w[i] & 0x0F0F0F0Fu, 0x01010101u, acc, false);
+            acc = __builtin_amdgcn_udot4((w[i] >> 4) & 0x0F0F0F0Fu, 0x01010101u, acc, false);
+        }
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 64);
+    if (lane == 0) zdm[t] = (float)acc;
+}
+
 // General data: one thread per spectrum folds its channels in ascending-frequency order.
 __global__ __launch_bounds__(256) void k_clip_zdm(RawDesc rd, float* __restrict__ zdm)
 {
@@ -194,6 +216,55 @@ __global__ __launch_bounds__(256) void k_clip_chan_u8(ClipArgs a)
             const int c = a.rd.flip ? nch - 1 - rc : rc;
             a.chansum[(int64_t)b * nch + c] = (double)sv[i];
         }
+    }
+}
+
+// 4-bit data without calibration: a lane keeps the eight nibble sums of one raw dword
+// (file channels 8q .. 8q+7; channel 2i+j is the first (j = 0) or second nibble of byte i,
+// first = high nibble when nibble_hi_first) over the block's good spectra.
+__global__ __launch_bounds__(256) void k_clip_chan_u4(ClipArgs a)
+{
+    __shared__ uint8_t g[kClipMaxBlock];
+    const int nch = a.rd.nchan;
+    const int b = blockIdx.x;
+    const int64_t t0 = (int64_t)b * a.rd.blk;
+    const int nb = (int)min((int64_t)a.rd.blk, a.rd.N - t0);
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) g[i] = a.good[t0 + i];
+    __syncthreads();
+    const int nq = a.rd.rowbytes >> 2;                  // 8-channel dwords per spectrum
+    for (int q = threadIdx.x; q < nq; q += blockDim.x) {
+        uint32_t sh[4] = {0, 0, 0, 0}, sl[4] = {0, 0, 0, 0};   // high / low nibble sums of byte i
+        const uint8_t* base = a.rd.raw + t0 * a.rd.rowbytes + 4 * q;
+        int k = 0;
+        for (; k + 8 <= nb; k += 8) {
+            uint32_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) v[u] = g[k + u] ? *(const uint32_t*)(base + (int64_t)(k + u) * a.rd.rowbytes) : 0u;
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    sl[i] += (v[u] >> (8 * i)) & 15u;
+                    sh[i] += (v[u] >> (8 * i + 4)) & 15u;
+                }
+        }
+        for (; k < nb; k++) {
+            const uint32_t v = g[k] ? *(const uint32_t*)(base + (int64_t)k * a.rd.rowbytes) : 0u;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                sl[i] += (v >> (8 * i)) & 15u;
+                sh[i] += (v >> (8 * i + 4)) & 15u;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                const int rc = 8 * q + 2 * i + j;       // raw channel -> ascending channel
+                const int c = a.rd.flip ? nch - 1 - rc : rc;
+                const bool hi = a.rd.nibble_hi_first ? j == 0 : j == 1;
+                a.chansum[(int64_t)b * nch + c] = (double)(hi ? sh[i] : sl[i]);
+            }
     }
 }
 
@@ -356,12 +427,16 @@ hipError_t launch_clip_stats(const ClipArgs& a, hipStream_t st)
     const bool calib = rd.scl || rd.offs || rd.wts;
     if (rd.nbits == 8 && !calib && rd.rowbytes % 16 == 0)
         hipLaunchKernelGGL(k_clip_zdm_u8, dim3((unsigned)((rd.N + 3) / 4)), dim3(256), 0, st, rd, a.zdm);
+    else if (rd.nbits == 4 && !calib && rd.rowbytes % 16 == 0)
+        hipLaunchKernelGGL(k_clip_zdm_u4, dim3((unsigned)((rd.N + 3) / 4)), dim3(256), 0, st, rd, a.zdm);
     else
         hipLaunchKernelGGL(k_clip_zdm, dim3((unsigned)((rd.N + 255) / 256)), dim3(256), 0, st, rd, a.zdm);
     hipLaunchKernelGGL(k_clip_block, dim3((unsigned)rd.nblk), dim3(1024), 0, st, a);
     hipLaunchKernelGGL(k_clip_as52, dim3((unsigned)((rd.nblk + 63) / 64)), dim3(64), 0, st, a);
     if (rd.nbits == 8 && !calib && rd.rowbytes % 4 == 0)
         hipLaunchKernelGGL(k_clip_chan_u8, dim3((unsigned)rd.nblk), dim3(256), 0, st, a);
+    else if (rd.nbits == 4 && !calib && rd.rowbytes % 4 == 0)
+        hipLaunchKernelGGL(k_clip_chan_u4, dim3((unsigned)rd.nblk), dim3(256), 0, st, a);
     else
         hipLaunchKernelGGL(k_clip_chan, dim3((unsigned)(rd.nblk * ((rd.nchan + 255) / 256))), dim3(256), 0, st, a);
     return hipGetLastError();
@@ -794,7 +869,7 @@ static size_t fix8_lds_bytes(const Stage1Multi& a, const Fix8Geom& g)
 // Geometry for k_stage1_fix8, or false when it does not apply (the generic kernel then runs).
 static bool fix8_geom(const Stage1Multi& a, Fix8Geom& g)
 {
-    if (!a.rawT || a.rd.nbits != 8 || a.rd.scl || a.rd.offs || a.rd.wts) return false;
+    if (!a.rawT || (a.rd.nbits != 8 && a.rd.nbits != 4) || a.rd.scl || a.rd.offs || a.rd.wts) return false;
     if (a.dmax > 32767 || a.rd.N >= ((int64_t)1 << 31) - (1 << 24)) return false;
     g.Wp = (2 * a.dmax + 2 * a.ds + 15 + 15) & ~15;       // + alignment of the window start
     if (g.Wp + 16 > a.rd.blk || a.dmax + a.ds + 16 > kRawTPad) return false;

@@ -166,8 +166,8 @@ hipError_t launch_clip_unpack(const ClipArgs& g, const double* in, hipStream_t s
 hipError_t launch_stage1_fixup(const Stage1Multi& a, const int32_t* events, const int32_t* nevents,
                                int boundaries, hipStream_t st);
 constexpr int64_t kRawTPad = 65536;   // zero rows after N in each channel-major raw row
-hipError_t launch_raw_transpose8(const uint8_t* raw, int64_t N, int32_t nchan, uint8_t* rawT, int64_t tstride,
-                                 hipStream_t st);
+hipError_t launch_raw_transpose(const uint8_t* raw, int64_t N, int32_t nchan, int nbits, int nibble_hi_first,
+                                uint8_t* rawT, int64_t tstride, hipStream_t st);
 hipError_t launch_synth(uint8_t* raw, int64_t N, int32_t rowbytes, const hd_synth_tab* tab_dev, int64_t t0,
                         hipStream_t st);
 

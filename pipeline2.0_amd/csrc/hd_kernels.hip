@@ -2315,13 +2315,17 @@ hipError_t launch_stage2_wide(const Stage2Args& a, int q, int r, int nw, hipStre
 }
 
 // ------------------------------------------------------------------------------------
-// channel-major copy of an 8-bit raw block (k_stage1_q8's fill source)
+// channel-major copy of an 8- or 4-bit raw block (k_stage1_q8's and k_stage1_fix8's source)
 // ------------------------------------------------------------------------------------
-// Tile = 128 rows x 128 channels: coalesced 128-B row reads into LDS, then per thread 4x4
-// byte transposes of 4 rows x 4 channels and 128-B channel runs out.  rawT[c][t] = raw[t][c];
-// the kRawTPad bytes after N in every channel row are zeroed by the host allocation.
-__global__ __launch_bounds__(256) void k_raw_transpose8(const uint8_t* __restrict__ raw, int64_t N, int32_t nchan,
-                                                       uint8_t* __restrict__ rawT, int64_t tstride)
+// Tile = 128 rows x 128 channels: coalesced row reads into LDS, then per thread 4x4 byte
+// transposes of 4 rows x 4 channels and 128-B channel runs out.  rawT[c][t] = raw[t][c] as one
+// byte per sample: 4-bit data is unpacked on the way into LDS (file channel 2k is the high
+// nibble of byte k when nibble_hi_first, as raw_value decodes it), so the 8-bit integer
+// stage-1 path runs 4-bit beams (PALFA's production format) unchanged.  The kRawTPad bytes
+// after N in every channel row are zeroed by the host allocation.
+template <int NB>
+__global__ __launch_bounds__(256) void k_raw_transpose(const uint8_t* __restrict__ raw, int64_t N, int32_t nchan,
+                                                      int nibble_hi_first, uint8_t* __restrict__ rawT, int64_t tstride)
 {
     __shared__ uint32_t tile[128][33];
     // 1-D grid, XCD-aware: workgroup L runs on XCD L % 8; its s-th workgroup there takes
@@ -2335,15 +2339,32 @@ __global__ __launch_bounds__(256) void k_raw_transpose8(const uint8_t* __restric
     if (tb * 128 >= N) return;
     const int64_t t0 = tb * 128;
     const int c0 = (sl % nct) * 128;
-    const int rb = nchan;                                   // bytes per raw row (8-bit)
-    const int ncw = min(128, nchan - c0) >> 2;              // channel dwords in this tile
+    const int rb = nchan * NB / 8;                          // bytes per raw row
+    const int ncw = min(128, nchan - c0) >> 2;              // 8-bit channel dwords in this tile
+    if constexpr (NB == 8) {
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const int idx = threadIdx.x + 256 * k;
-        const int row = idx >> 5, col = idx & 31;
-        uint32_t v = 0;
-        if (t0 + row < N && col < ncw) v = *(const uint32_t*)(raw + (t0 + row) * rb + c0 + 4 * col);
-        tile[row][col] = v;
+        for (int k = 0; k < 16; k++) {
+            const int idx = threadIdx.x + 256 * k;
+            const int row = idx >> 5, col = idx & 31;
+            uint32_t v = 0;
+            if (t0 + row < N && col < ncw) v = *(const uint32_t*)(raw + (t0 + row) * rb + c0 + 4 * col);
+            tile[row][col] = v;
+        }
+    } else {
+        // one raw dword = 8 channels: H = high nibbles, L = low nibbles of its 4 bytes; the
+        // output bytes interleave them in file-channel order (first nibble first)
+        const uint32_t s0 = 0x05010400u, s1 = 0x07030602u;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const int idx = threadIdx.x + 256 * k;
+            const int row = idx >> 4, col = idx & 15;
+            uint32_t v = 0;
+            if (t0 + row < N && 2 * col < ncw) v = *(const uint32_t*)(raw + (t0 + row) * rb + c0 / 2 + 4 * col);
+            const uint32_t H = (v >> 4) & 0x0F0F0F0Fu, L = v & 0x0F0F0F0Fu;
+            const uint32_t F = nibble_hi_first ? H : L, Sd = nibble_hi_first ? L : H;
+            tile[row][2 * col] = __builtin_amdgcn_perm(Sd, F, s0);
+            tile[row][2 * col + 1] = __builtin_amdgcn_perm(Sd, F, s1);
+        }
     }
     __syncthreads();
 #pragma unroll
@@ -2369,14 +2390,19 @@ __global__ __launch_bounds__(256) void k_raw_transpose8(const uint8_t* __restric
     }
 }
 
-hipError_t launch_raw_transpose8(const uint8_t* raw, int64_t N, int32_t nchan, uint8_t* rawT, int64_t tstride,
-                                 hipStream_t st)
+hipError_t launch_raw_transpose(const uint8_t* raw, int64_t N, int32_t nchan, int nbits, int nibble_hi_first,
+                                uint8_t* rawT, int64_t tstride, hipStream_t st)
 {
-    if (nchan % 4 || N % 4) return hipErrorInvalidValue;
+    if (nchan % (nbits == 4 ? 8 : 4) || N % 4 || (nbits != 8 && nbits != 4)) return hipErrorInvalidValue;
     const int64_t ntb8 = ((N + 127) / 128 + 7) / 8 * 8;          // time blocks, padded to the 8 XCDs
     const int64_t nwg = ntb8 * ((nchan + 127) / 128);
     if (nwg > 0x7fffffffLL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_raw_transpose8, dim3((unsigned)nwg), dim3(256), 0, st, raw, N, nchan, rawT, tstride);
+    if (nbits == 8)
+        hipLaunchKernelGGL(k_raw_transpose<8>, dim3((unsigned)nwg), dim3(256), 0, st, raw, N, nchan, nibble_hi_first,
+                           rawT, tstride);
+    else
+        hipLaunchKernelGGL(k_raw_transpose<4>, dim3((unsigned)nwg), dim3(256), 0, st, raw, N, nchan, nibble_hi_first,
+                           rawT, tstride);
     return hipGetLastError();
 }
 

@@ -240,8 +240,11 @@ def test_stage1_int8_path_bitexact(engine, ds, flip, sub_dtype, ds_mode, masked)
     engine.set_mask()
 
 
-def test_stage1_int8_variant_rejects_other_data(engine):
-    obs = palfa_obs(N=8192, nbits=4)
+@pytest.mark.parametrize("nbits,N", [(16, 8192), (4, 8190)])
+def test_stage1_int8_variant_rejects_other_data(engine, nbits, N):
+    """The integer path takes 8-bit data and 4-bit data through its unpacked channel-major
+    copy (N % 4 == 0); 16-bit data, and 4-bit beams without that copy, are refused."""
+    obs = palfa_obs(N=N, nbits=nbits)
     load_beam(engine, obs)
     p = engine.plan(PassParams(subdm=10.0, lodm=0.0, dmstep=1.0, numdms=4, nsub=96, ds=1))
     p.set_variant(3 << 8)
