@@ -393,7 +393,7 @@ def main():
         achieved = (n1 * raw_bytes + sub_bytes) / (ms1 * 1e-3) / 1e9
         launch_ms = ms1 / n1
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_r01.json")
+    pmc = os.path.join(ROOT, "profiles", "pmc_r02.json")
     if os.path.exists(pmc):
         try:
             traffic = json.load(open(pmc)).get("hbm_bytes_per_launch", {}).get(dom.split()[0])

@@ -145,8 +145,9 @@ struct hd_plan {
         int32_t umax = 0;               // [3] only: largest pattern count of a subband pair
         int32_t* d_omin = nullptr;      // [3]: the pair table (kPairTab ints per y-block and pair)
         int32_t* d_boff = nullptr;
-    } wide[4];                      // [2]: k_stage2_ring (16 waves, LDS-DMA staging ring);
-                                    // [3]: k_stage2_pair (the ring over subband-pair partials)
+    } wide[5];                      // [2]: k_stage2_ring (16 waves, LDS-DMA staging ring);
+                                    // [3]: k_stage2_pair (the ring over subband-pair partials),
+                                    // [4]: the same in 8-wave half y-blocks, two workgroups per CU
     int32_t sub_bound = -1;         // bound on |subband| known on the host (-1: none), set when
                                     // the subbands are formed or uploaded (pair variant gate)
     int32_t variant = 0;
@@ -1072,20 +1073,20 @@ static void wide_tables(hd_plan* p, int nwmax, bool dbuf, bool i16, hd_plan::Wid
 // variant does not apply), base0 = min off[d][2c], b1 = base0 + min r, and the S1 staging
 // index k1[u] = r_u - min r + (b1 & 1) of pattern u.  boff[yb][c][k] = LDS byte offset
 // (from the expanded area) of DM k's 4 samples: buffer (c & 1), pattern u(k), copy o2 & 3.
-static void pair_tables(hd_plan* p, bool i16, hd_plan::Wide& w, std::vector<int32_t>& ptab,
+static void pair_tables(hd_plan* p, bool i16, int nw, hd_plan::Wide& w, std::vector<int32_t>& ptab,
                         std::vector<int32_t>& boff)
 {
     w = hd_plan::Wide{};
     const int nsub = p->pass.nsub, numdms = p->pass.numdms;
     if (!i16 || nsub % 2 || numdms < 1) return;
-    int nyb = (numdms + 80 - 1) / 80;
+    int nyb = (numdms + 5 * nw - 1) / (5 * nw);
     const int per = (numdms + nyb - 1) / nyb;
-    const int qneed = (per + 15) / 16;
+    const int qneed = (per + nw - 1) / nw;
     int Q = 2, R = 4;
     if (qneed > 4) { Q = 5; R = 3; }
     else if (qneed > 3) { Q = 4; R = 3; }
     else if (qneed > 2) { Q = 3; R = 4; }
-    const int dpb = 16 * Q;
+    const int dpb = nw * Q;
     nyb = (numdms + dpb - 1) / dpb;
     const int npair = nsub / 2;
     ptab.assign((size_t)nyb * npair * hd::kPairTab, 0);
@@ -1123,7 +1124,8 @@ static void pair_tables(hd_plan* p, bool i16, hd_plan::Wide& w, std::vector<int3
     const int ws = (int)round_up((size_t)(256 * R + span0 + 4), 4);
     const int npw = (int)((((size_t)ws + 10 + k1max) * 2 + 1023) / 1024);
     const int nbp = (int)(((size_t)dpb * 4 + 1023) / 1024);
-    if (2 * npw + nbp > 16 || hd::stage2_pair_lds_bytes(ws, npw, nbp, nsub, umax) > 160 * 1024 ||
+    // 16 waves: one workgroup per CU; 8 waves: two, so each must fit half the LDS
+    if (2 * npw + nbp > nw || hd::stage2_pair_lds_bytes(ws, npw, nbp, nsub, umax) > (nw == 16 ? 160 : 80) * 1024 ||
         !hd::stage2_pair_supports(Q, R))
         return;
     boff.assign((size_t)nyb * npair * dpb + 256, 0);   // the last DMA piece may over-read
@@ -1142,7 +1144,7 @@ static void pair_tables(hd_plan* p, bool i16, hd_plan::Wide& w, std::vector<int3
     w.ok = true;
     w.q = Q;
     w.r = R;
-    w.nw = 16;
+    w.nw = nw;
     w.dpb = dpb;
     w.ws = ws;
     w.sc = 2;
@@ -1228,14 +1230,15 @@ extern "C" int hd_plan_create(hd_ctx* c, const hd_pass* ps, hd_plan** out)
                 boff[((size_t)yb * nsub + s) * p->dpb + k] = ((sl * 4 + (o2 & 3)) * p->wstride + (o2 & ~3)) * 2;
             }
 
-    std::vector<int32_t> womin[4], wboff[4];
+    std::vector<int32_t> womin[5], wboff[5];
     for (int k = 0; k < 3; k++)
         wide_tables(p, k == 1 ? 8 : 16, k != 1, c->opts.sub_dtype == HD_SUB_I16, p->wide[k], womin[k], wboff[k], k == 2);
-    pair_tables(p, c->opts.sub_dtype == HD_SUB_I16, p->wide[3], womin[3], wboff[3]);
+    pair_tables(p, c->opts.sub_dtype == HD_SUB_I16, 16, p->wide[3], womin[3], wboff[3]);
+    pair_tables(p, c->opts.sub_dtype == HD_SUB_I16, 8, p->wide[4], womin[4], wboff[4]);
 
     int rc = HD_OK;
     hipError_t e = hipSetDevice(c->device);
-    for (int k = 0; k < 4 && e == hipSuccess; k++) {
+    for (int k = 0; k < 5 && e == hipSuccess; k++) {
         hd_plan::Wide& w = p->wide[k];
         if (!w.ok) continue;
         e = hipMalloc(&w.d_omin, sizeof(int32_t) * womin[k].size());
@@ -1303,11 +1306,11 @@ extern "C" int hd_plan_set_variant(hd_plan* p, int32_t v)
     p->probe = (v >> 16) & 0xFF;     // profiling only (results invalid): see hipdedisp.h
     p->pair_persist = (v >> 24) & 0x3;   // pair kernel: 0/1 persistent workgroups (default), 2 one per tile
     v &= 0xFF;
-    if (v < 0 || v > 6 || v1 > 3) return fail(p->ctx, HD_E_INVAL, "variant must be (s1<<8)|s2 with s1 in 0..3, s2 in 0..6");
+    if (v < 0 || v > 7 || v1 > 3) return fail(p->ctx, HD_E_INVAL, "variant must be (s1<<8)|s2 with s1 in 0..3, s2 in 0..7");
     p->s1_variant = v1;
     if (v == 2 && !p->lds_ok) return fail(p->ctx, HD_E_INVAL, "LDS variant unavailable for this plan (needs int16 subbands and a window that fits 64 KiB)");
     if ((v == 3 && !p->wide[0].ok) || (v == 4 && !p->wide[1].ok) || (v == 5 && !p->wide[2].ok) ||
-        (v == 6 && !p->wide[3].ok))
+        (v == 6 && !p->wide[3].ok) || (v == 7 && !p->wide[4].ok))
         return fail(p->ctx, HD_E_INVAL, "wide-tile variant unavailable for this plan (needs int16 subbands and a window that fits LDS)");
     p->variant = v;
     return HD_OK;
@@ -2084,8 +2087,9 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         p->copy_pending = false;
     }
     // pair partials need |sub[s0] + sub[s1]| <= 32767 (packed int16), known on the host
-    const bool pair_ok = p->wide[3].ok && p->sub_bound >= 0 && 2 * p->sub_bound <= 32767;
-    if (p->variant == 6 && !pair_ok)
+    const bool pair_bound = p->sub_bound >= 0 && 2 * p->sub_bound <= 32767;
+    const bool pair_ok = p->wide[3].ok && pair_bound;
+    if ((p->variant == 6 && !pair_ok) || (p->variant == 7 && !(p->wide[4].ok && pair_bound)))
         return fail(c, HD_E_INVAL, "hd_run_dedisp: pair variant needs 2 * max|subband| <= 32767 known on the host "
                     "(bound %d)", (int)p->sub_bound);
     int wk = -1;                       // wide variant in use (index into p->wide), or -1
@@ -2150,7 +2154,7 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         if (wk == 0) HIPCHK(c, hd::launch_stage2_wide(a, w.q, w.r, w.nw, st));
         else if (wk == 1) HIPCHK(c, hd::launch_stage2_wide2(a, w.q, w.r, w.nw, st));
         else if (wk == 2) HIPCHK(c, hd::launch_stage2_ring(a, w.q, w.r, st));
-        else HIPCHK(c, hd::launch_stage2_pair(a, w.q, w.r, st));
+        else HIPCHK(c, hd::launch_stage2_pair(a, w.q, w.r, w.nw, st));
     } else if (use_lds) {
         a.off = p->d_boff;
         HIPCHK(c, hd::launch_stage2_lds(a, p->q, st));

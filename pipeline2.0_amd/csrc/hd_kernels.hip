@@ -2005,7 +2005,7 @@ size_t stage2_pair_lds_bytes(int wstride, int npw, int nbp, int nsub, int umax)
 }
 
 template <int Q, int R>
-static hipError_t launch_pair_qr(const Stage2Args& a, int nyblk, hipStream_t st)
+static hipError_t launch_pair_qr(const Stage2Args& a, int nyblk, int nw, hipStream_t st)
 {
     {
         const hipError_t e = set_max_lds((const void*)k_stage2_pair<Q, R>, 160 * 1024);
@@ -2015,7 +2015,7 @@ static hipError_t launch_pair_qr(const Stage2Args& a, int nyblk, hipStream_t st)
     const unsigned nx = a.nwg > 0 && (unsigned)a.nwg < ntiles ? (unsigned)a.nwg : ntiles;
     Stage2Args b = a;
     if (nx == ntiles) b.nwg = 0;
-    hipLaunchKernelGGL((k_stage2_pair<Q, R>), dim3(nx, (unsigned)nyblk), dim3(1024),
+    hipLaunchKernelGGL((k_stage2_pair<Q, R>), dim3(nx, (unsigned)nyblk), dim3(64 * nw),
                        stage2_pair_lds_bytes(a.wstride, a.ring_npw, a.ring_nbp, a.nsub, a.umax), st, b, a.off);
     return hipGetLastError();
 }
@@ -2251,11 +2251,12 @@ hipError_t launch_stage2_ring(const Stage2Args& a, int q, int r, hipStream_t st)
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_stage2_pair(const Stage2Args& a, int q, int r, hipStream_t st)
+hipError_t launch_stage2_pair(const Stage2Args& a, int q, int r, int nw, hipStream_t st)
 {
     if (a.nvalid <= 0) return hipSuccess;
+    if (nw != 16 && nw != 8) return hipErrorInvalidValue;
     const int nyblk = (a.numdms + a.dms_per_blk - 1) / a.dms_per_blk;
-#define HD_PL(QQ, RR) if (q == QQ && r == RR) return launch_pair_qr<QQ, RR>(a, nyblk, st);
+#define HD_PL(QQ, RR) if (q == QQ && r == RR) return launch_pair_qr<QQ, RR>(a, nyblk, nw, st);
     HD_RING_QR(HD_PL)
 #undef HD_PL
     return hipErrorInvalidValue;

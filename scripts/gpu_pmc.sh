@@ -4,7 +4,7 @@
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out/pmc
-B="python3 bench.py --steps 1 --warmup 0 --no-cpu"
+B="python3 bench.py --steps 1 --warmup 0 --no-cpu --e2e-beams 0"
 run() {  # name counters...
   local n=$1; shift
   timeout -s KILL 240 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pmc/$n -o $n --pmc "$@" -- $B \

@@ -87,7 +87,7 @@ def test_stage1_calib_mask_bitexact(engine, sub_dtype, ds_mode):
 
 @pytest.mark.parametrize("numdms,ds,numout_mode", [(76, 1, "none"), (64, 2, "none"), (76, 3, "pad"),
                                                    (5, 1, "trunc"), (100, 5, "pad"), (76, 10, "pad")])
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7])
 def test_stage2_bitexact(engine, numdms, ds, numout_mode, variant):
     obs = palfa_obs(N=3 * 8192, nbits=8)
     raw = load_beam(engine, obs)
@@ -100,14 +100,14 @@ def test_stage2_bitexact(engine, numdms, ds, numout_mode, variant):
     try:
         p.set_variant(variant)
     except PrestoError:
-        if variant == 6:   # wide DM steps: > kPairUMax patterns per pair or LDS (the DDplan passes apply, below)
+        if variant in (6, 7):   # wide DM steps: > kPairUMax patterns per pair or LDS (the DDplan passes apply, below)
             pytest.skip("pair variant not applicable to this plan")
         raise
     p.run_subband()
     try:
         got = p.run_dedisp()
     except PrestoError:
-        if variant == 6 and ds == 10:
+        if variant in (6, 7) and ds == 10:
             pytest.skip("pair variant not applicable (subband bound)")
         raise
     sub, want = OR.run_pass(obs, Opts(), raw, pp)
@@ -131,11 +131,12 @@ def test_stage2_pair_ddplan_passes(engine, stage, passnum):
     p = engine.plan(pp)
     p.run_subband()
     outs = []
-    for v in (6, 0, 5):
+    vs = (6, 0, 5, 7)
+    for v in vs:
         p.set_variant(v)
         outs.append(p.run_dedisp())
     _, want = OR.run_pass(obs, Opts(), raw, pp, mask=mask, ptsperint=pts, padvals=pad)
-    for v, got in zip((6, 0, 5), outs):
+    for v, got in zip(vs, outs):
         assert_series(got, want, obs.N // pp.ds)
         assert np.array_equal(got, outs[0]), v
     engine.set_mask()
@@ -159,14 +160,15 @@ def test_stage2_pair_persistent_bitexact(engine, stage):
     p = engine.plan(pp)
     p.run_subband()
     outs = []
-    for v in (6 | (1 << 24), 6 | (2 << 24)):
+    for v in (6 | (1 << 24), 6 | (2 << 24), 7 | (1 << 24), 7 | (2 << 24)):
         p.set_variant(v)
         outs.append(p.run_dedisp())
     p.destroy()
     engine.set_mask()
     _, want = OR.run_pass(obs, Opts(), raw, pp, mask=mask, ptsperint=pts, padvals=pad, omp=True)
     assert_series(outs[0], want, obs.N // pp.ds)
-    assert np.array_equal(outs[1], outs[0])
+    for o in outs[1:]:
+        assert np.array_equal(o, outs[0])
 
 
 def test_stage2_pair_rejects_unbounded_subbands(engine):
