@@ -302,8 +302,38 @@ HD_API int hd_plan_last_ms(const hd_plan* plan, float* ms_subband, float* ms_ded
  * items, 64 skip its clipped-spectrum items; 128 (valid results, for cross-checks) runs the
  * fixup with the generic per-cell kernel instead of the 8-bit LDS-window one.  Bits 24-25 schedule the pair kernel's
  * tiles: 0 or 1 persistent workgroups (one per CU, each over a contiguous tile range; the
- * default), 2 one workgroup per tile. */
+ * default), 2 one workgroup per tile.  s2 = 7: the pair kernel in 8-wave half y-blocks (two
+ * workgroups per CU; measured slower, kept for cross-checks). */
 HD_API int hd_plan_set_variant(hd_plan* plan, int32_t variant);
+
+/* ---- single-pulse search on the device-resident series -------------------------------
+ * Replaces the per-.dat `single_pulse_search.py -p -m maxwidth -t threshold <dat>` of
+ * lib/python/PALFA2_presto_search.py:539-546 (maxwidth 0.1 s, threshold 5.0:
+ * lib/python/config/searching_example.py:13-15) for the numout-sample series of a
+ * plan's last hd_run_dedisp: per 1000-sample block a linear detrend and a trimmed std,
+ * per DM the bad blocks, then every boxcar value above threshold is a hit.  The
+ * candidate pruning of the script (prune_related1/2, border cases) runs on the hits in
+ * hipdedisp/single_pulse.py.                                                              */
+typedef struct {
+    int32_t dm;        /* DM index in the plan                                         */
+    int32_t bin;       /* sample                                                       */
+    int32_t widx;      /* index into the widths of hd_sp_widths (0: width 1)            */
+    int32_t pad;
+    double sigma;      /* boxcar value of the normalised series (the candidate's sigma) */
+} hd_sp_hit;
+/* Boxcar widths the script searches: 1, then 2,3,4,6,9,14,20,30,45,70,100,150,220,300
+ * while width * dt <= maxwidth.  widths[16]; *n = count.                              */
+HD_API int hd_sp_widths(double dt, double maxwidth, int32_t* widths, int32_t* n);
+/* The script's candidates of the plan's series into hits[cap], sorted by (dm, bin, widx):
+ * device hits above threshold outside bad blocks, prune_related1 per width (a stronger hit
+ * of that width within width/2 bins removes it; equal: the later one stays), then on the
+ * host prune_related2 across widths and, for padded series, prune_border_cases.  *nhits =
+ * the count; when the device hits exceed cap nothing is copied, *nhits is that number and
+ * HD_E_NOMEM is returned (call again with room).  bad_blocks[numdms * nblocks] (may be
+ * NULL): 1 = block not searched; *nblocks (may be NULL) = floor(numout / 1000).  A series
+ * of fewer than 8000 samples gives no candidates.                                        */
+HD_API int hd_single_pulse(hd_plan* plan, double dt, double maxwidth, double threshold, hd_sp_hit* hits,
+                           int64_t cap, int64_t* nhits, uint8_t* bad_blocks, int64_t* nblocks);
 
 #ifdef __cplusplus
 }

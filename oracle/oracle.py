@@ -69,6 +69,8 @@ def lib(omp=False):
         L.or_nearest_long.argtypes = [d]
         L.or_delay_from_dm.restype = d
         L.or_delay_from_dm.argtypes = [d, d]
+        L.sp_oracle_hits.argtypes = [vp, i64, ci, i64, vp, ci, d, vp, i64, vp]
+        L.sp_oracle_hits.restype = i64
         _libs[key] = L
     return _libs[key]
 
@@ -232,3 +234,125 @@ def stats_padvals(dataavg):
 
 def num_threads(omp=True):
     return lib(omp).or_num_threads()
+
+
+# ---- single_pulse_search.py [PRESTO-ext] (sp_oracle.c + the script's candidate logic) ----
+SP_HIT = np.dtype([("dm", "<i4"), ("bin", "<i4"), ("widx", "<i4"), ("pad", "<i4"), ("sigma", "<f8")])
+SP_DOWNFACTS = [2, 3, 4, 6, 9, 14, 20, 30, 45, 70, 100, 150, 220, 300]
+
+
+def sp_widths(dt, maxwidth):
+    return [1] + [w for w in SP_DOWNFACTS if w * dt <= maxwidth]
+
+
+def sp_hits(series, widths, threshold=5.0):
+    """Boxcar hits of the [ndm][n] float32 series, sorted by (dm, widx, bin), and the bad
+    blocks [ndm][n // 1000]."""
+    x = np.ascontiguousarray(series, dtype=np.float32)
+    ndm, n = x.shape
+    w = np.asarray(widths, dtype=np.int32)
+    nb = n // 1000
+    bad = np.zeros((ndm, max(nb, 1)), np.uint8)
+    L = lib(False)
+    cap = 1 << 16
+    while True:
+        hits = np.zeros(cap, SP_HIT)
+        cnt = L.sp_oracle_hits(_ptr(x), n, ndm, n, _ptr(w), len(w), float(threshold), _ptr(hits), cap, _ptr(bad))
+        if cnt <= cap:
+            break
+        cap = int(cnt)
+    hits = hits[:cnt]
+    hits = hits[np.lexsort((hits["bin"], hits["widx"], hits["dm"]))]
+    return hits, bad[:, :nb]
+
+
+class SpCand:
+    """candidate of single_pulse_search.py: DM, sigma, time, bin, downfact; ordered by bin."""
+
+    def __init__(self, DM, sigma, time, bin, downfact):
+        self.DM, self.sigma, self.time, self.bin, self.downfact = DM, sigma, time, bin, downfact
+
+    def __str__(self):
+        return "%7.2f %7.2f %13.6f %10d     %3d\n" % (self.DM, self.sigma, self.time, self.bin, self.downfact)
+
+
+def _prune_related1_localmax(bins, sig, half, ls):
+    """prune_related1 as the local-maximum rule (sp_oracle.c / hd_sp.hip): keep a hit when
+    no hit within half bins is stronger -- a later one that is equal also removes it."""
+    if half == 0 or len(bins) == 0:
+        return np.ones(len(bins), bool)
+    dense = np.full(ls + 2 * half + 2, -np.inf)
+    dense[bins + half] = sig
+    keep = np.ones(len(bins), bool)
+    for d in range(1, half + 1):
+        keep &= ~(dense[bins + half + d] >= sig)
+        keep &= ~(dense[bins + half - d] > sig)
+    return keep
+
+
+def _prune_related2(cands, downfacts):
+    toremove = set()
+    maxd = max(downfacts) // 2 if downfacts else 0
+    for ii in range(0, len(cands) - 1):
+        if ii in toremove:
+            continue
+        xx = cands[ii]
+        for jj in range(ii + 1, len(cands)):
+            yy = cands[jj]
+            if abs(yy.bin - xx.bin) > maxd:
+                break
+            if jj in toremove:
+                continue
+            prox = max([xx.downfact // 2, yy.downfact // 2, 1])
+            if abs(yy.bin - xx.bin) <= prox:
+                if xx.sigma > yy.sigma:
+                    toremove.add(jj)
+                else:
+                    toremove.add(ii)
+    for b in sorted(toremove, reverse=True):
+        del cands[b]
+    return cands
+
+
+def _prune_border_cases(cands, offregions):
+    toremove = set()
+    for ii in range(len(cands) - 1, -1, -1):
+        c = cands[ii]
+        loside, hiside = c.bin - c.downfact // 2, c.bin + c.downfact // 2
+        if hiside < offregions[0][0]:
+            break
+        for off, on in offregions:
+            if hiside > off and loside < on:
+                toremove.add(ii)
+    for b in sorted(toremove, reverse=True):
+        del cands[b]
+    return cands
+
+
+def sp_candidates(hits, bad, widths, dms, dt, nds=None, numout=None, ls=None):
+    """single_pulse_search.py's per-DM candidate list from the raw hits (every boxcar value
+    above threshold in [0, ls)): prune_related1 per width (local-maximum rule), hits in bad
+    blocks dropped, the rest in bin order (widths ascending among equal bins: the script's
+    append + bisect.insort), prune_related2 across widths and, for padded series,
+    prune_border_cases.  -> [list of SpCand per DM]"""
+    downfacts = list(widths[1:])
+    if ls is None:
+        ls = int(hits["bin"].max()) + 1 if len(hits) else 0
+    out = []
+    for d in range(len(dms)):
+        hd = hits[hits["dm"] == d]
+        kept = []
+        for wi, w in enumerate(widths):
+            hw = hd[hd["widx"] == wi]
+            k = _prune_related1_localmax(hw["bin"].astype(np.int64), hw["sigma"], w // 2, ls)
+            hw = hw[k]
+            blk = hw["bin"] // 1000
+            ok = bad[d][blk] == 0 if bad.size else np.ones(len(hw), bool)
+            kept += [(int(b), wi, float(v)) for b, v in zip(hw["bin"][ok], hw["sigma"][ok])]
+        kept.sort(key=lambda r: (r[0], r[1]))
+        cl = [SpCand(dms[d], v, b * dt, b, widths[wi]) for b, wi, v in kept]
+        cl = _prune_related2(cl, downfacts)
+        if nds is not None and numout is not None and numout > nds and cl:
+            cl = _prune_border_cases(cl, [(nds - 1, numout - 1)])
+        out.append(cl)
+    return out

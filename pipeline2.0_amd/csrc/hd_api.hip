@@ -83,6 +83,12 @@ struct hd_ctx {
     std::vector<SpecialList> special_cache;
     double* d_partial = nullptr;    // shared per-tile partial sums
     size_t partial_bytes = 0;
+    // single-pulse search scratch: per-block coefficients, hit list, hit counter
+    double* d_sp_coef = nullptr;
+    size_t sp_coef_bytes = 0;
+    hd_sp_hit* d_sp_hits = nullptr;
+    int64_t sp_hits_cap = 0;
+    unsigned long long* d_sp_count = nullptr;
     // streaming ingest (hd_push_raw_file): two pinned host blocks, each guarded by the event
     // of the last copy that read it
     void* pin[2] = {nullptr, nullptr};
@@ -331,6 +337,9 @@ extern "C" int hd_close(hd_ctx* c)
     free_obs_buffers(c);
     dfree(c->d_partial);
     dfree(c->d_partial2);
+    dfree(c->d_sp_coef);
+    dfree(c->d_sp_hits);
+    dfree(c->d_sp_count);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
@@ -1993,6 +2002,127 @@ extern "C" int hd_get_series(hd_plan* p, int32_t dm0, int32_t ndm, int64_t t0, i
                                sizeof(float) * p->out_stride, sizeof(float) * count, ndm, hipMemcpyDeviceToHost,
                                p->dd_stream));
     HIPCHK(c, hipStreamSynchronize(p->dd_stream));
+    return HD_OK;
+}
+
+// ---- single-pulse search (hd_sp.hip; replaces single_pulse_search.py per .dat,
+//      PALFA2_presto_search.py:539-546) ----------------------------------------------------
+static const int32_t kSpDownfacts[] = {2, 3, 4, 6, 9, 14, 20, 30, 45, 70, 100, 150, 220, 300};
+
+extern "C" int hd_sp_widths(double dt, double maxwidth, int32_t* widths, int32_t* n)
+{
+    if (!widths || !n || !(dt > 0.0)) return fail(nullptr, HD_E_INVAL, "hd_sp_widths: bad argument");
+    int k = 0;
+    widths[k++] = 1;
+    for (int32_t w : kSpDownfacts)
+        if ((double)w * dt <= maxwidth) widths[k++] = w;
+    *n = k;
+    return HD_OK;
+}
+
+extern "C" int hd_single_pulse(hd_plan* p, double dt, double maxwidth, double threshold, hd_sp_hit* hits,
+                               int64_t cap, int64_t* nhits, uint8_t* bad_blocks, int64_t* nblocks_out)
+{
+    if (!p || !nhits || (cap > 0 && !hits)) return fail(p ? p->ctx : nullptr, HD_E_INVAL, "hd_single_pulse: NULL argument");
+    hd_ctx* c = p->ctx;
+    if (!p->ran_dd || !p->d_out) return fail(c, HD_E_STATE, "hd_single_pulse: run hd_run_dedisp first");
+    int32_t widths[16], nw = 0;
+    int rc = hd_sp_widths(dt, maxwidth, widths, &nw);
+    if (rc) return fail(c, rc, "hd_single_pulse: dt must be > 0");
+    double rsw[16];
+    for (int i = 0; i < nw; i++) rsw[i] = 1.0 / std::sqrt((double)widths[i]);
+    const int ndm = p->pass.numdms;
+    const int64_t nblocks = p->numout / 1000;                  // roundN / detrendlen
+    if (nblocks_out) *nblocks_out = nblocks;
+    if (nblocks > hd::sp_max_blocks())
+        return fail(c, HD_E_INVAL, "hd_single_pulse: %lld blocks > %d", (long long)nblocks, hd::sp_max_blocks());
+    const int64_t ls = nblocks * 1000 / 8000 * 8000;           // numchunks * chunklen
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t st = p->dd_stream ? p->dd_stream : c->stream;
+    const size_t cbytes = sizeof(double) * 4 * (size_t)std::max<int64_t>(1, (int64_t)ndm * nblocks);
+    if (c->sp_coef_bytes < cbytes) {
+        HIPCHK(c, hipStreamSynchronize(st));
+        dfree(c->d_sp_coef);
+        c->d_sp_coef = nullptr;
+        c->sp_coef_bytes = 0;
+        HIPCHK(c, hipMalloc(&c->d_sp_coef, cbytes));
+        c->sp_coef_bytes = cbytes;
+    }
+    const int64_t dcap = std::max<int64_t>(cap, 1 << 16);
+    if (c->sp_hits_cap < dcap) {
+        HIPCHK(c, hipStreamSynchronize(st));
+        dfree(c->d_sp_hits);
+        c->d_sp_hits = nullptr;
+        c->sp_hits_cap = 0;
+        HIPCHK(c, hipMalloc(&c->d_sp_hits, sizeof(hd_sp_hit) * (size_t)dcap));
+        c->sp_hits_cap = dcap;
+    }
+    if (!c->d_sp_count) HIPCHK(c, hipMalloc(&c->d_sp_count, sizeof(unsigned long long)));
+    HIPCHK(c, hipMemsetAsync(c->d_sp_count, 0, sizeof(unsigned long long), st));
+    if (nblocks > 0) {
+        HIPCHK(c, hd::launch_sp_blocks(p->d_out, p->out_stride, ndm, (int)nblocks, c->d_sp_coef, st));
+        HIPCHK(c, hd::launch_sp_hits(p->d_out, p->out_stride, ndm, (int)nblocks, c->d_sp_coef, ls, widths, rsw, nw,
+                                     threshold, c->d_sp_hits, c->d_sp_count, c->sp_hits_cap, st));
+    }
+    unsigned long long cnt = 0;
+    HIPCHK(c, hipMemcpyAsync(&cnt, c->d_sp_count, sizeof(cnt), hipMemcpyDeviceToHost, st));
+    std::vector<double> coef;
+    if (bad_blocks && nblocks > 0) {
+        coef.resize((size_t)ndm * nblocks * 4);
+        HIPCHK(c, hipMemcpyAsync(coef.data(), c->d_sp_coef, sizeof(double) * coef.size(), hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(c, hipStreamSynchronize(st));
+    if (bad_blocks)
+        for (size_t i = 0; i < (size_t)ndm * nblocks; i++) bad_blocks[i] = coef[4 * i + 3] != 0.0;
+    *nhits = (int64_t)cnt;
+    if ((int64_t)cnt > cap || (int64_t)cnt > c->sp_hits_cap)
+        return fail(c, HD_E_NOMEM, "hd_single_pulse: %llu hits > capacity %lld (call again with room)", cnt,
+                    (long long)std::min(cap, c->sp_hits_cap));
+    if (!cnt) return HD_OK;
+    HIPCHK(c, hipMemcpy(hits, c->d_sp_hits, sizeof(hd_sp_hit) * cnt, hipMemcpyDeviceToHost));
+    // the script's dm_candlist order: by bin, widths in increasing order among equal bins
+    // (width-1 hits appended first, every downfactor's bisect.insort after equals)
+    std::sort(hits, hits + cnt, [](const hd_sp_hit& a, const hd_sp_hit& b) {
+        return a.dm != b.dm ? a.dm < b.dm : a.bin != b.bin ? a.bin < b.bin : a.widx < b.widx;
+    });
+    // prune_related2 (exact greedy walk, per DM) and prune_border_cases (padded series: data
+    // ends at nds - 1, padding runs to numout - 1 -- the .inf on/off pairs)
+    const int reach = nw > 1 ? widths[nw - 1] / 2 : 0;
+    const bool padded = p->numout > p->nds;
+    int64_t out = 0;
+    std::vector<char> gone;
+    for (int64_t d0 = 0; d0 < (int64_t)cnt;) {
+        int64_t d1 = d0;
+        while (d1 < (int64_t)cnt && hits[d1].dm == hits[d0].dm) d1++;
+        const int64_t n = d1 - d0;
+        hd_sp_hit* h = hits + d0;
+        gone.assign((size_t)n, 0);
+        for (int64_t i = 0; i + 1 < n; i++) {
+            if (gone[i]) continue;
+            for (int64_t j = i + 1; j < n; j++) {
+                const int gap = std::abs(h[j].bin - h[i].bin);
+                if (gap > reach) break;
+                if (gone[j]) continue;
+                const int prox = std::max(std::max(widths[h[i].widx] / 2, widths[h[j].widx] / 2), 1);
+                if (gap <= prox) {
+                    if (h[i].sigma > h[j].sigma) gone[j] = 1;
+                    else gone[i] = 1;
+                }
+            }
+        }
+        if (padded) {
+            const int64_t off = p->nds - 1, on = p->numout - 1;
+            for (int64_t i = n - 1; i >= 0; i--) {
+                const int64_t lo = h[i].bin - widths[h[i].widx] / 2, hi = h[i].bin + widths[h[i].widx] / 2;
+                if (hi < off) break;
+                if (hi > off && lo < on) gone[i] = 1;
+            }
+        }
+        for (int64_t i = 0; i < n; i++)
+            if (!gone[i]) hits[out++] = h[i];
+        d0 = d1;
+    }
+    *nhits = out;
     return HD_OK;
 }
 

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "hd_synth_core.h"
+#include "../../include/hipdedisp.h"
 
 namespace hd {
 
@@ -165,6 +166,13 @@ hipError_t launch_clip_unpack(const ClipArgs& g, const double* in, hipStream_t s
 // boundary with changing pad values (the 8-bit integer path's straddling outputs) touches.
 hipError_t launch_stage1_fixup(const Stage1Multi& a, const int32_t* events, const int32_t* nevents,
                                int boundaries, hipStream_t st);
+// single-pulse search (hd_sp.hip): per-block detrend/std + per-DM bad blocks -> coef
+// [ndm][nblocks][4] (mean, slope, std, bad); boxcar hits above threshold
+int sp_max_blocks();
+hipError_t launch_sp_blocks(const float* x, int64_t stride, int ndm, int nblocks, double* coef, hipStream_t st);
+hipError_t launch_sp_hits(const float* x, int64_t stride, int ndm, int nblocks, const double* coef, int64_t ls,
+                          const int32_t* widths, const double* rsw, int nwidths, double threshold, hd_sp_hit* hits,
+                          unsigned long long* count, int64_t cap, hipStream_t st);
 constexpr int64_t kRawTPad = 65536;   // zero rows after N in each channel-major raw row
 hipError_t launch_raw_transpose(const uint8_t* raw, int64_t N, int32_t nchan, int nbits, int nibble_hi_first,
                                 uint8_t* rawT, int64_t tstride, hipStream_t st);

@@ -1,0 +1,106 @@
+"""GPU single-pulse search (hd_single_pulse, csrc/hd_sp.hip) on the series a pass leaves in
+HBM, against the oracle (oracle/sp_oracle.c + the script's candidate logic in oracle.py):
+every bad block equal and the per-DM candidate lists (DM, bin, width and the sigma as a
+bit-equal double) and .singlepulse files of hipdedisp.single_pulse identical to the
+oracle's; the injected DM-350 pulse is found at its DM.  Reference: PALFA2_presto_search.py:539-546."""
+import numpy as np
+import pytest
+
+import oracle as OR
+from hipdedisp import Opts, PassParams, plan
+from hipdedisp import single_pulse as SP
+from hipdedisp.synth import host_spectra, palfa_obs, palfa_synth, rfifind_ptsperint, synth_mask
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def beam(engine):
+    obs = palfa_obs(N=1 << 18, nbits=8)
+    s = palfa_synth()
+    s.sp_time[0] = 8.0                        # the DM-350 pulse inside this 17 s beam, at an
+    s.sp_amp[0] = 1.0                         # amplitude the block-std rule does not flag bad
+    engine.set_obs(obs, Opts())
+    engine.synth_device(s)
+    pts = rfifind_ptsperint(obs.dt)
+    mask, pad = synth_mask(obs, s, pts)
+    engine.set_mask(mask, pts, pad)
+    yield obs, s
+    engine.set_mask()
+
+
+def run(engine, obs, subdm, lodm, dmstep, ds, numout=0):
+    pp = PassParams(subdm=subdm, lodm=lodm, dmstep=dmstep, numdms=76, nsub=96, ds=ds, numout=numout)
+    p = engine.plan(pp)
+    p.run_subband()
+    series = p.run_dedisp()
+    return p, series
+
+
+def check_pass(p, series, dm_strs, tmp_path, threshold=5.0):
+    dt = p.sub_dt
+    wl = SP.widths(dt, 0.1)
+    assert wl == OR.sp_widths(dt, 0.1)
+    got, bad = SP.device_candidates(p, dt, 0.1, threshold)
+    raw, wbad = OR.sp_hits(series, wl, threshold)
+    assert np.array_equal(bad, wbad)
+    dms = [float(s) for s in dm_strs]
+    ref = OR.sp_candidates(raw, wbad, wl, dms, dt, p.nds, p.numout, ls=series.shape[1] // 1000 * 1000 // 8000 * 8000)
+    want = [(d, c.bin, c.downfact, c.sigma) for d, cl in enumerate(ref) for c in cl]
+    have = [(r[0], r[1], wl[r[2]], r[4]) for r in got.tolist()]
+    assert have == want                                          # sigma: bit-equal doubles
+    # the files of PALFA2_presto_search.py:540-545
+    base = str(tmp_path / "beam")
+    secs, lists = SP.run_single_pulse(p, base, dm_strs, threshold=threshold)
+    for s, r in zip(dm_strs, ref):
+        text = open("%s_DM%s.singlepulse" % (base, s)).read()
+        assert text == (SP.HEADER + "".join(str(c) for c in r) if r else "")
+    return lists
+
+
+def test_single_pulse_dm350_pass(engine, beam, tmp_path):
+    """A full-resolution pass around the injected DM-350 pulse: device candidates = oracle
+    candidates; the brightest candidate of the pass sits at DM 350."""
+    obs, s = beam
+    p, series = run(engine, obs, subdm=350.0, lodm=346.2, dmstep=0.1, ds=1)
+    try:
+        dm_strs = ["%.2f" % (346.2 + 0.1 * k) for k in range(76)]
+        got = check_pass(p, series, dm_strs, tmp_path)
+        best = max(((c.sigma, d) for d, cl in enumerate(got) for c in cl), default=(0, -1))
+        assert best[0] > 8.0                                    # oracle on CPU: 10.8 at DM 350.0
+        assert abs(float(dm_strs[best[1]]) - 350.0) <= 0.5
+    finally:
+        p.destroy()
+
+
+@pytest.mark.parametrize("ds,numout_extra", [(2, 3000), (5, 0), (10, 1234)])
+def test_single_pulse_downsampled_and_padded(engine, beam, tmp_path, ds, numout_extra):
+    """Downsampled passes (fewer widths fit 0.1 s), padded series (border pruning and the
+    constant padding: zero-std / bad blocks), bit-equal hits and identical lists."""
+    obs, s = beam
+    nds = obs.N // ds
+    p, series = run(engine, obs, subdm=220.0, lodm=210.0, dmstep=0.3 * ds, ds=ds, numout=nds + numout_extra)
+    try:
+        dm_strs = ["%.2f" % (210.0 + 0.3 * ds * k) for k in range(76)]
+        check_pass(p, series, dm_strs, tmp_path)
+    finally:
+        p.destroy()
+
+
+def test_single_pulse_many_hits_and_short_series(engine, beam, tmp_path):
+    """A low threshold (many candidates, the 4.6-ms pulsar's train at DM 71) and a series
+    shorter than one 8000-sample chunk (no candidates)."""
+    obs, s = beam
+    p, series = run(engine, obs, subdm=71.0, lodm=67.2, dmstep=0.1, ds=1)
+    try:
+        dm_strs = ["%.2f" % (67.2 + 0.1 * k) for k in range(76)]
+        lists = check_pass(p, series, dm_strs, tmp_path, threshold=2.5)
+        assert sum(len(c) for c in lists) > 1000
+    finally:
+        p.destroy()
+    p, series = run(engine, obs, subdm=900.0, lodm=880.0, dmstep=1.0, ds=10, numout=6000)
+    try:
+        got, bad = SP.device_candidates(p, p.sub_dt, 0.1, 5.0)
+        assert len(got) == 0 and bad.shape == (76, 6)
+    finally:
+        p.destroy()

@@ -1,0 +1,146 @@
+"""CPU checks of the single_pulse_search.py restatement (oracle/sp_oracle.c + oracle.py):
+an independent float64 numpy restatement of the script's numeric steps agrees with the
+oracle's hits away from the threshold, injected pulses come out as single candidates at
+their bin and width, and the candidate bookkeeping follows the script (pruning, bad blocks,
+padding).  Parity with PRESTO itself is unpinned (the script is not in this image)."""
+import numpy as np
+import pytest
+
+import oracle as OR
+
+
+def numpy_hits(x, widths, threshold):
+    """Float64 restatement: np.polyfit line per block, sorted middle-95% std * 1.148, the
+    bad-block rule, boxcars by cumulative sums over [0, numchunks*8000)."""
+    n = x.shape[0]
+    nb = n // 1000
+    ls = nb * 1000 // 8000 * 8000
+    t = np.arange(1000, dtype=np.float64)
+    y = np.zeros(ls)
+    stds = np.zeros(nb)
+    det = np.zeros((nb, 1000))
+    for b in range(nb):
+        blk = x[b * 1000:(b + 1) * 1000].astype(np.float64)
+        p = np.polyfit(t, blk, 1)
+        det[b] = blk - np.polyval(p, t)
+        s = np.sort(det[b])[25:975]
+        stds[b] = np.sqrt((s ** 2).sum() / 950.0) * 1.148
+    srt = np.sort(stds)
+    h = nb // 2
+    locut = int(np.argmax(srt[1:h + 1] - srt[:h])) + 1
+    hicut = int(np.argmax(srt[h + 1:] - srt[h:-1])) + h - 2
+    bad = np.zeros(nb, bool)
+    if hicut > locut:
+        sd = srt[locut:hicut].std()
+        med = srt[(locut + hicut) // 2]
+        bad = (stds < med - 4 * sd) | (stds > med + 4 * sd)
+    for b in range(min(nb, ls // 1000)):
+        if not bad[b] and stds[b] > 0:
+            y[b * 1000:(b + 1) * 1000] = det[b] / stds[b]
+    cs = np.concatenate([[0.0], np.cumsum(y)])
+    out = {}
+    for wi, w in enumerate(widths):
+        if w == 1:
+            s = y
+        else:
+            lo = np.arange(ls) - w // 2
+            hi = np.arange(ls) + (w // 2 if w % 2 else w // 2 - 1) + 1
+            s = (cs[np.clip(hi, 0, ls)] - cs[np.clip(lo, 0, ls)]) / np.sqrt(w)
+        out[wi] = s
+    return out, bad
+
+
+def test_widths():
+    assert OR.sp_widths(65.476e-6, 0.1) == [1, 2, 3, 4, 6, 9, 14, 20, 30, 45, 70, 100, 150, 220, 300]
+    assert OR.sp_widths(65.476e-6 * 10, 0.1) == [1, 2, 3, 4, 6, 9, 14, 20, 30, 45, 70, 100, 150]
+    assert OR.sp_widths(1e-3, 0.005) == [1, 2, 3, 4]
+
+
+def test_oracle_hits_match_numpy_restatement():
+    rng = np.random.default_rng(7)
+    n = 64000 + 517
+    x = rng.normal(100.0, 7.0, size=(2, n)).astype(np.float32)
+    x[0, 20000:20030] += 40.0                       # a 30-sample pulse
+    x[1, 5000:6000] += rng.normal(0, 60.0, 1000)    # a noisy (bad) block
+    x[1, 40001] += 90.0                             # a one-sample spike
+    widths = OR.sp_widths(65.476e-6, 0.1)
+    hits, bad = OR.sp_hits(x, widths, 3.0)
+    for d in range(2):
+        ref, rbad = numpy_hits(x[d], widths, 3.0)
+        assert np.array_equal(bad[d].astype(bool), rbad)
+        hd = hits[hits["dm"] == d]
+        for wi in range(len(widths)):
+            got = hd[hd["widx"] == wi]
+            s = ref[wi]
+            # the oracle rounds detrended and normalised samples to float32 (as the script's
+            # float32 arrays do): agreement to float32 precision
+            np.testing.assert_allclose(got["sigma"], s[got["bin"]], rtol=2e-6, atol=2e-6)
+            clear = np.flatnonzero(s > 3.0 + 1e-4)      # away from the threshold: the same set
+            assert set(clear.tolist()) <= set(got["bin"].tolist())
+            assert len(got) - len(clear) <= np.count_nonzero(np.abs(s - 3.0) <= 1e-4)
+    assert bad[1, 5] == 1                            # the noisy block is flagged
+
+
+def test_candidates_find_injected_pulses():
+    rng = np.random.default_rng(11)
+    n = 80000
+    x = rng.normal(50.0, 5.0, size=(3, n)).astype(np.float32)
+    x[1, 30000:30020] += 12.0                         # 20-sample pulse, ~10.7 sigma boxcar
+    x[2, 60000] += 45.0                                # 1-sample spike, 9 sigma
+    widths = OR.sp_widths(65.476e-6, 0.1)
+    hits, bad = OR.sp_hits(x, widths, 5.0)
+    cl = OR.sp_candidates(hits, bad, widths, [10.0, 20.0, 30.0], 65.476e-6)
+    strong = [[c for c in l if c.sigma > 7.0] for l in cl]
+    assert strong[0] == []
+    assert len(strong[1]) == 1 and abs(strong[1][0].bin - 30010) <= 3 and strong[1][0].downfact in (14, 20, 30)
+    assert len(strong[2]) == 1 and strong[2][0].bin == 60000 and strong[2][0].downfact == 1
+    line = str(strong[2][0])
+    assert line == "%7.2f %7.2f %13.6f %10d     %3d\n" % (30.0, strong[2][0].sigma, 60000 * 65.476e-6, 60000, 1)
+
+
+def test_candidate_bookkeeping_follows_script():
+    """prune_related1 within a width (local-maximum rule), bad blocks, prune_related2 across
+    widths and border pruning on a padded series, on a hand-made hit list."""
+    rows = [(0, 100, 0, 6.0), (0, 5000, 0, 5.5),                 # width 1
+            (0, 101, 1, 7.0), (0, 102, 1, 6.5),                 # width 2: 102 within 1 of 101 -> pruned
+            (0, 2990, 2, 8.0), (0, 2991, 2, 8.5), (0, 4000, 2, 6.0),   # width 3, blocks 2, 2, 4
+            (0, 7990, 1, 9.0), (0, 7999, 2, 9.5)]               # near the padding
+    hits = np.zeros(len(rows), OR.SP_HIT)
+    for i, r in enumerate(rows):
+        hits[i]["dm"], hits[i]["bin"], hits[i]["widx"], hits[i]["sigma"] = r
+    bad = np.zeros((1, 8), np.uint8)
+    bad[0, 2] = 1
+    cl = OR.sp_candidates(hits, bad, [1, 2, 3], [5.0], 1e-3, nds=7995, numout=8000)[0]
+    got = [(c.bin, c.downfact) for c in cl]
+    # width 3: 2990 loses to 2991, which sits in the bad block 2; 100 (w1, 6.0) loses to
+    # 101 (w2, 7.0) within max(1, 1, 1); 7999 (w3) reaches the padding after nds - 1 = 7994
+    assert got == [(101, 2), (4000, 3), (5000, 1), (7990, 2)]
+
+
+def test_prune_related1_local_max_equals_greedy_walk_on_peaks():
+    """On separated peaks (and on the chains the script's walk resolves), the local-maximum
+    rule keeps what the greedy walk of prune_related1 keeps."""
+    def greedy(bins, vals, downfact):
+        gone = set()
+        for ii in range(len(bins) - 1):
+            if ii in gone:
+                continue
+            for jj in range(ii + 1, len(bins)):
+                if abs(bins[jj] - bins[ii]) > downfact // 2:
+                    break
+                if jj in gone:
+                    continue
+                gone.add(jj if vals[ii] > vals[jj] else ii)
+        return [b for k, b in enumerate(bins) if k not in gone]
+    rng = np.random.default_rng(5)
+    for trial in range(200):
+        w = int(rng.choice([2, 3, 4, 6, 9, 14, 20]))
+        centres = np.sort(rng.choice(5000, 12, replace=False)) * (w + 3)
+        bins, vals = [], []
+        for c in centres:                                     # one peak per cluster
+            width = int(rng.integers(1, w + 1))
+            for k in range(width):
+                bins.append(int(c + k))
+                vals.append(10.0 - abs(k - width // 2) - 0.01 * k)
+        keep = OR._prune_related1_localmax(np.array(bins), np.array(vals), w // 2, max(bins) + 1)
+        assert [b for b, k in zip(bins, keep) if k] == greedy(bins, vals, w)
