@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU work for the baseline sample")
     ap.add_argument("--e2e-beams", type=int, default=1,
                     help="beams run end to end (.dat/.inf files written) after the timed steps; 0 = skip")
+    ap.add_argument("--sp-beams", type=int, default=1,
+                    help="beams of single-pulse search (hd_single_pulse) timed after the steps; 0 = skip")
     ap.add_argument("--mode", choices=["beam", "slices", "shard"], default="beam",
                     help="beam: one beam per rank (weak scaling, configs[4]); slices: ONE beam cut into per-rank "
                          "time slices, every rank runs all 57 passes on its slice (strong, configs[2]; RCCL carries "
@@ -109,6 +111,25 @@ def run_step(eng, stages):
         for p in plans:
             p.run_dedisp(to_host=False)
     eng.sync()
+
+
+def single_pulse_leg(eng, stages, beams):
+    """single_pulse_search.py over every DM of the beam (PALFA2_presto_search.py:539-546):
+    hd_single_pulse on each pass's device-resident series (as left by the timed steps),
+    candidates back on the host; wall seconds per beam and the candidate count."""
+    from hipdedisp import single_pulse as SP
+    eng.sync()
+    t = time.perf_counter()
+    ncand = 0
+    for _ in range(beams):
+        for plans in stages:
+            for p in plans:
+                hits, _ = SP.device_candidates(p, p.sub_dt, 0.1, 5.0)
+                ncand += len(hits)
+    s = (time.perf_counter() - t) / beams
+    return {"s_per_beam": s, "candidates_per_beam": ncand // beams,
+            "note": "hd_single_pulse over the 57 passes' series in HBM (-m 0.1 -t 5.0): detrend, block stds, "
+                    "boxcars, prune_related1 on the GPU; prune_related2 + border cases on the host; wall time"}
 
 
 def e2e_dir(need_bytes):
@@ -448,6 +469,8 @@ def main():
                 "note": "stage 1 + stage 2 + every .dat/.inf file of the 57 passes complete in the directory; "
                         "per-rank (this rank's beam)"}
             line["end_to_end_samples_per_s"] = line["end_to_end"]["samples_per_s"]
+    if not (shard or slices) and args.sp_beams > 0:
+        line["single_pulse"] = single_pulse_leg(eng, stages, args.sp_beams)
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(obs, synth, ddplans, args.cpu_seconds, mask, pts, pad, omp=False)
         line["cpu_baseline_openmp"] = cpu_baseline(obs, synth, ddplans, args.cpu_seconds, mask, pts, pad, omp=True)

@@ -302,8 +302,8 @@ HD_API int hd_plan_last_ms(const hd_plan* plan, float* ms_subband, float* ms_ded
  * items, 64 skip its clipped-spectrum items; 128 (valid results, for cross-checks) runs the
  * fixup with the generic per-cell kernel instead of the 8-bit LDS-window one.  Bits 24-25 schedule the pair kernel's
  * tiles: 0 or 1 persistent workgroups (one per CU, each over a contiguous tile range; the
- * default), 2 one workgroup per tile.  s2 = 7: the pair kernel in 8-wave half y-blocks (two
- * workgroups per CU; measured slower, kept for cross-checks). */
+ * default), 2 one workgroup per tile.  s2 = 7: the pair kernel with two subband pairs per
+ * chunk (half the chunks per tile; HD_E_INVAL when its LDS does not fit). */
 HD_API int hd_plan_set_variant(hd_plan* plan, int32_t variant);
 
 /* ---- single-pulse search on the device-resident series -------------------------------

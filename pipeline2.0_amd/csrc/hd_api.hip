@@ -153,7 +153,7 @@ struct hd_plan {
         int32_t* d_boff = nullptr;
     } wide[5];                      // [2]: k_stage2_ring (16 waves, LDS-DMA staging ring);
                                     // [3]: k_stage2_pair (the ring over subband-pair partials),
-                                    // [4]: the same in 8-wave half y-blocks, two workgroups per CU
+                                    // [4]: the same with two pairs per chunk (half the chunks)
     int32_t sub_bound = -1;         // bound on |subband| known on the host (-1: none), set when
                                     // the subbands are formed or uploaded (pair variant gate)
     int32_t variant = 0;
@@ -1082,12 +1082,15 @@ static void wide_tables(hd_plan* p, int nwmax, bool dbuf, bool i16, hd_plan::Wid
 // variant does not apply), base0 = min off[d][2c], b1 = base0 + min r, and the S1 staging
 // index k1[u] = r_u - min r + (b1 & 1) of pattern u.  boff[yb][c][k] = LDS byte offset
 // (from the expanded area) of DM k's 4 samples: buffer (c & 1), pattern u(k), copy o2 & 3.
-static void pair_tables(hd_plan* p, bool i16, int nw, hd_plan::Wide& w, std::vector<int32_t>& ptab,
+static void pair_tables(hd_plan* p, bool i16, int ppc, hd_plan::Wide& w, std::vector<int32_t>& ptab,
                         std::vector<int32_t>& boff)
 {
     w = hd_plan::Wide{};
     const int nsub = p->pass.nsub, numdms = p->pass.numdms;
-    if (!i16 || nsub % 2 || numdms < 1) return;
+    const int nw = 16;
+    // chunks of ppc pairs; an even chunk count per tile keeps the expanded-buffer parity of a
+    // pair the same in every tile (the tables below fix it per pair)
+    if (!i16 || nsub % (4 * ppc) || numdms < 1) return;
     int nyb = (numdms + 5 * nw - 1) / (5 * nw);
     const int per = (numdms + nyb - 1) / nyb;
     const int qneed = (per + nw - 1) / nw;
@@ -1132,9 +1135,8 @@ static void pair_tables(hd_plan* p, bool i16, int nw, hd_plan::Wide& w, std::vec
         }
     const int ws = (int)round_up((size_t)(256 * R + span0 + 4), 4);
     const int npw = (int)((((size_t)ws + 10 + k1max) * 2 + 1023) / 1024);
-    const int nbp = (int)(((size_t)dpb * 4 + 1023) / 1024);
-    // 16 waves: one workgroup per CU; 8 waves: two, so each must fit half the LDS
-    if (2 * npw + nbp > nw || hd::stage2_pair_lds_bytes(ws, npw, nbp, nsub, umax) > (nw == 16 ? 160 : 80) * 1024 ||
+    const int nbp = (int)(((size_t)ppc * dpb * 4 + 1023) / 1024);
+    if (2 * ppc * npw + nbp > nw || hd::stage2_pair_lds_bytes(ws, npw, nbp, nsub, umax, ppc) > 160 * 1024 ||
         !hd::stage2_pair_supports(Q, R))
         return;
     boff.assign((size_t)nyb * npair * dpb + 256, 0);   // the last DMA piece may over-read
@@ -1147,7 +1149,8 @@ static void pair_tables(hd_plan* p, bool i16, int nw, hd_plan::Wide& w, std::vec
                 const int32_t o0 = p->off[(size_t)dm * nsub + 2 * c], o1 = p->off[(size_t)dm * nsub + 2 * c + 1];
                 const int u = (int)(std::lower_bound(r.begin(), r.end(), o1 - o0) - r.begin());
                 const int32_t o2 = o0 - base0;
-                boff[((size_t)yb * npair + c) * dpb + k] = ((((c & 1) * umax + u) * 4 + (o2 & 3)) * ws + (o2 & ~3)) * 2;
+                const int buf = ((c / ppc) & 1) * ppc + c % ppc;   // expanded buffer of pair c
+                boff[((size_t)yb * npair + c) * dpb + k] = (((buf * umax + u) * 4 + (o2 & 3)) * ws + (o2 & ~3)) * 2;
             }
         }
     w.ok = true;
@@ -1242,8 +1245,8 @@ extern "C" int hd_plan_create(hd_ctx* c, const hd_pass* ps, hd_plan** out)
     std::vector<int32_t> womin[5], wboff[5];
     for (int k = 0; k < 3; k++)
         wide_tables(p, k == 1 ? 8 : 16, k != 1, c->opts.sub_dtype == HD_SUB_I16, p->wide[k], womin[k], wboff[k], k == 2);
-    pair_tables(p, c->opts.sub_dtype == HD_SUB_I16, 16, p->wide[3], womin[3], wboff[3]);
-    pair_tables(p, c->opts.sub_dtype == HD_SUB_I16, 8, p->wide[4], womin[4], wboff[4]);
+    pair_tables(p, c->opts.sub_dtype == HD_SUB_I16, 1, p->wide[3], womin[3], wboff[3]);
+    pair_tables(p, c->opts.sub_dtype == HD_SUB_I16, 2, p->wide[4], womin[4], wboff[4]);
 
     int rc = HD_OK;
     hipError_t e = hipSetDevice(c->device);
@@ -2229,7 +2232,11 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         // of >= 72 DMs: 1.31 vs 1.39 ms per Mock stage-0 pass; at ds >= 2 or 64 DMs the extra
         // expand work outweighs the halved sums, profiles/r01_stage2_variants.txt)
         const bool pair_auto = pair_ok && p->pass.ds == 1 && p->pass.numdms >= 72;
-        wk = pair_auto ? 3 : p->wide[2].ok ? 2 : p->wide[0].ok ? 0 : (p->wide[1].ok ? 1 : -1);
+        // two pairs per chunk beat the ring and the one-pair kernel at every Mock DDplan
+        // stage (profiles/r02_stage2_variants.txt: 1.10 / 0.56 / 0.42 / 0.27 / 0.22 / 0.17 ms
+        // vs the ring's 1.42 / 0.60 / 0.53 / 0.33 / 0.27 / 0.20)
+        const bool pair2_auto = p->wide[4].ok && pair_bound;
+        wk = pair2_auto ? 4 : pair_auto ? 3 : p->wide[2].ok ? 2 : p->wide[0].ok ? 0 : (p->wide[1].ok ? 1 : -1);
     }
     const bool use_wide = wk >= 0;
     const bool use_lds = !use_wide && (p->variant == 2 || (p->variant == 0 && p->lds_ok));
@@ -2284,7 +2291,7 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         if (wk == 0) HIPCHK(c, hd::launch_stage2_wide(a, w.q, w.r, w.nw, st));
         else if (wk == 1) HIPCHK(c, hd::launch_stage2_wide2(a, w.q, w.r, w.nw, st));
         else if (wk == 2) HIPCHK(c, hd::launch_stage2_ring(a, w.q, w.r, st));
-        else HIPCHK(c, hd::launch_stage2_pair(a, w.q, w.r, w.nw, st));
+        else HIPCHK(c, hd::launch_stage2_pair(a, w.q, w.r, wk == 4 ? 2 : 1, st));
     } else if (use_lds) {
         a.off = p->d_boff;
         HIPCHK(c, hd::launch_stage2_lds(a, p->q, st));

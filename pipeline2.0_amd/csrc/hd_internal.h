@@ -120,9 +120,9 @@ constexpr int kRingSC = 4, kRingNS = 5;   // ring variant: subbands per chunk, s
 size_t stage2_ring_lds_bytes(int wstride, int npw, int nbp, int nsub);
 hipError_t launch_stage2_ring(const Stage2Args& a, int q, int r, hipStream_t st);
 constexpr int kPairUMax = 6, kPairTab = 16;   // pair variant: patterns per pair, table ints per pair
-size_t stage2_pair_lds_bytes(int wstride, int npw, int nbp, int nsub, int umax);
+size_t stage2_pair_lds_bytes(int wstride, int npw, int nbp, int nsub, int umax, int ppc);
 bool stage2_pair_supports(int q, int r);
-hipError_t launch_stage2_pair(const Stage2Args& a, int q, int r, int nw, hipStream_t st);
+hipError_t launch_stage2_pair(const Stage2Args& a, int q, int r, int ppc, hipStream_t st);
 hipError_t launch_stage2_wide2(const Stage2Args& a, int q, int r, int nw, hipStream_t st);
 hipError_t launch_stage2_direct(const Stage2Args& a, hipStream_t st);
 hipError_t launch_stage2_lds(const Stage2Args& a, int q, hipStream_t st);

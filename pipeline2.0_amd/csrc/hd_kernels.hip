@@ -1766,11 +1766,13 @@ __device__ __forceinline__ void load8_shift(const uint32_t* w32, int x, uint32_t
     for (int m = 0; m < 4; m++) o[m] = __builtin_amdgcn_alignbit(w[m + 1], w[m], sh);
 }
 
-template <int Q, int R>
+template <int Q, int R, int PPC>
 __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, const int32_t* __restrict__ boff)
 {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
-    constexpr int NS = kRingNS, T = 256 * R;
+    // PPC subband pairs per chunk: two halve the chunks (barriers, DMA/offset bookkeeping) per
+    // tile; their staging ring has one slot less (4) so the doubled expanded buffers fit
+    constexpr int NS = PPC == 2 ? 4 : kRingNS, T = 256 * R;
     // one tile per workgroup (nwg == 0), or a persistent workgroup over a contiguous tile
     // range whose chunks (tile, pair) form one stream through the DMA ring, so the table
     // load, ring prologue and launch of the next tile overlap the current one
@@ -1794,7 +1796,7 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, const int32_
     const int npw = a.ring_npw;                       // 1 KiB DMA pieces per window
     const int nbp = a.ring_nbp;                       // pieces of a chunk's offset block
     const int umax = a.umax;
-    const int slot_bytes = (2 * npw + nbp) * 1024;
+    const int slot_bytes = (2 * PPC * npw + nbp) * 1024;
     const int npair = a.nsub >> 1;
     const int tab_bytes = npair * kPairTab * 4;
     int32_t* ltab = (int32_t*)lds_raw;
@@ -1803,7 +1805,7 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, const int32_
     const uint32_t lane_byte = exp0 + (uint32_t)lane * 8u;   // host offsets are relative to exp0
     const int16_t* sub = (const int16_t*)a.sub;
     const int32_t* bo_g = boff + (int64_t)yb * npair * dpb;
-    const int nchunk = npair;
+    const int nchunk = npair / PPC;
 
     for (int i = threadIdx.x; i < npair * kPairTab; i += nthr) ltab[i] = a.ptab[(int64_t)yb * npair * kPairTab + i];
     __syncthreads();
@@ -1826,60 +1828,65 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, const int32_
             acc16[q][r][1] = short2v{0, 0};
         }
     int gcount = 0;
-    const bool loader = wave < 2 * npw + nbp;
+    const bool loader = wave < 2 * PPC * npw + nbp;
 
     const int ntot = ntl * nchunk;
-    int dpair = 0, dtile = 0, dcount = 0;              // source chunk of the next DMA (clamped at the end)
+    int dchunk = 0, dtile = 0, dcount = 0;             // source chunk of the next DMA (clamped at the end)
     auto dma = [&](int cc) {
-        const int c2 = dpair;
+        const int c2 = dchunk;
         const int64_t t0 = (int64_t)(tb + dtile) * T;
         if (dcount + 1 < ntot) {
             dcount++;
-            if (++dpair == nchunk) { dpair = 0; dtile++; }
+            if (++dchunk == nchunk) { dchunk = 0; dtile++; }
         }
         if (!loader) return;
         const uint32_t slot = ring0 + (uint32_t)((cc % NS) * slot_bytes);
-        if (wave < 2 * npw) {
-            const int sl = wave >= npw ? 1 : 0, pc = wave - sl * npw;
-            const int s = 2 * c2 + sl;
-            const int b = __builtin_amdgcn_readfirstlane(ltab[c2 * kPairTab + sl]);   // base0 | b1
+        if (wave < 2 * PPC * npw) {
+            const int sl = wave / npw, pc = wave - sl * npw;      // window sl: pair sl / 2, side sl % 2
+            const int pr = PPC * c2 + (sl >> 1);
+            const int s = 2 * pr + (sl & 1);
+            const int b = __builtin_amdgcn_readfirstlane(ltab[pr * kPairTab + (sl & 1)]);   // base0 | b1
             const int64_t e0 = t0 + b - (b & 1);
             const char* src = (const char*)(sub + (int64_t)s * a.sub_stride + e0) + pc * 1024;
             dma16s(src, (uint32_t)lane * 16u, slot + (uint32_t)((sl * npw + pc) * 1024));
         } else {
-            const int bp = wave - 2 * npw;
-            const char* src = (const char*)(bo_g + (int64_t)c2 * dpb) + bp * 1024;
-            dma16s(src, (uint32_t)lane * 16u, slot + (uint32_t)((2 * npw + bp) * 1024));
+            const int bp = wave - 2 * PPC * npw;
+            const char* src = (const char*)(bo_g + (int64_t)PPC * c2 * dpb) + bp * 1024;
+            dma16s(src, (uint32_t)lane * 16u, slot + (uint32_t)((2 * PPC * npw + bp) * 1024));
         }
     };
-    // staging slot of chunk cc -> the 4 shifted copies of each pattern partial, buffer cc & 1
-    auto expand = [&](int cc, int pr) {
+    // staging slot of chunk cc -> the 4 shifted copies of each pattern partial of its pairs,
+    // expanded buffers (cc & 1) * PPC + k
+    auto expand = [&](int cc, int chk) {
         const char* slot = lds_raw + ring0 + (cc % NS) * slot_bytes;
-        const uint32_t* S0 = (const uint32_t*)slot;
-        const uint32_t* S1 = (const uint32_t*)(slot + npw * 1024);
-        const int32_t* pt = ltab + pr * kPairTab;
-        const int k0 = pt[0] & 1;
-        const int U = pt[2];
-        int16_t* buf = (int16_t*)(lds_raw + exp0) + (cc & 1) * (umax * 4 * ws);
-        for (int idx = threadIdx.x; idx < U * upw; idx += nthr) {
-            int u = 0, uu = idx;
 #pragma unroll
-            for (int k = 1; k < kPairUMax; k++)
-                if (uu >= upw) { uu -= upw; u++; }
-            uint32_t A[4], B[4], P[4];
-            load8_shift(S0, k0 + 4 * uu, A);
-            load8_shift(S1, pt[3 + u] + 4 * uu, B);
+        for (int k = 0; k < PPC; k++) {
+            const uint32_t* S0 = (const uint32_t*)(slot + (2 * k) * npw * 1024);
+            const uint32_t* S1 = (const uint32_t*)(slot + (2 * k + 1) * npw * 1024);
+            const int32_t* pt = ltab + (PPC * chk + k) * kPairTab;
+            const int k0 = pt[0] & 1;
+            const int U = pt[2];
+            int16_t* buf = (int16_t*)(lds_raw + exp0) + ((cc & 1) * PPC + k) * (umax * 4 * ws);
+            for (int idx = threadIdx.x; idx < U * upw; idx += nthr) {
+                int u = 0, uu = idx;
 #pragma unroll
-            for (int m = 0; m < 4; m++)
-                P[m] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(short2v, A[m]) + __builtin_bit_cast(short2v, B[m]));
-            uint2* dst0 = (uint2*)(buf + (u * 4) * ws);
-            const uint32_t h1 = __builtin_amdgcn_alignbit(P[1], P[0], 16);
-            const uint32_t h3 = __builtin_amdgcn_alignbit(P[2], P[1], 16);
-            const uint32_t h5 = __builtin_amdgcn_alignbit(P[3], P[2], 16);
-            dst0[uu] = make_uint2(P[0], P[1]);
-            dst0[upw + uu] = make_uint2(h1, h3);
-            dst0[2 * upw + uu] = make_uint2(P[1], P[2]);
-            dst0[3 * upw + uu] = make_uint2(h3, h5);
+                for (int m = 1; m < kPairUMax; m++)
+                    if (uu >= upw) { uu -= upw; u++; }
+                uint32_t A[4], B[4], P[4];
+                load8_shift(S0, k0 + 4 * uu, A);
+                load8_shift(S1, pt[3 + u] + 4 * uu, B);
+#pragma unroll
+                for (int m = 0; m < 4; m++)
+                    P[m] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(short2v, A[m]) + __builtin_bit_cast(short2v, B[m]));
+                uint2* dst0 = (uint2*)(buf + (u * 4) * ws);
+                const uint32_t h1 = __builtin_amdgcn_alignbit(P[1], P[0], 16);
+                const uint32_t h3 = __builtin_amdgcn_alignbit(P[2], P[1], 16);
+                const uint32_t h5 = __builtin_amdgcn_alignbit(P[3], P[2], 16);
+                dst0[uu] = make_uint2(P[0], P[1]);
+                dst0[upw + uu] = make_uint2(h1, h3);
+                dst0[2 * upw + uu] = make_uint2(P[1], P[2]);
+                dst0[3 * upw + uu] = make_uint2(h3, h5);
+            }
         }
     };
 
@@ -1934,31 +1941,33 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, const int32_
 
 #pragma unroll
     for (int cc = 0; cc < NS - 1; cc++) dma(cc);
-    ring_wait_vm<R>();
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NS - 3) : "memory");
     ring_barrier();
     expand(0, 0);
     ring_barrier();
 
-    int pr = 0, ktile = 0;                             // pair and tile of chunk c
+    int chk = 0, ktile = 0;                            // chunk (within the tile) and tile of chunk c
     for (int c = 0; c < ntot; c++) {
         if (!(a.probe & 2)) dma(c + NS - 1);   // probe 2: no window DMA after the prologue
-        const int prn = pr + 1 == nchunk ? 0 : pr + 1;
-        if (c + 1 < ntot && !(a.probe & 8)) expand(c + 1, prn);
-        // this chunk's per-DM byte offsets: entry q in lane q
-        const int32_t* sboff = (const int32_t*)(lds_raw + ring0 + (c % NS) * slot_bytes + 2 * npw * 1024);
-        const int voff = lane < Q ? sboff[wave * Q + lane] : 0;
+        const int chn = chk + 1 == nchunk ? 0 : chk + 1;
+        if (c + 1 < ntot && !(a.probe & 8)) expand(c + 1, chn);
+        // this chunk's per-DM byte offsets: pair k, DM entry q in lane q of voff[k]
+        const int32_t* sboff = (const int32_t*)(lds_raw + ring0 + (c % NS) * slot_bytes + 2 * PPC * npw * 1024);
+        int voff[PPC];
+#pragma unroll
+        for (int k = 0; k < PPC; k++) voff[k] = lane < Q ? sboff[k * dpb + wave * Q + lane] : 0;
         if (!(a.probe & 1)) {
-            constexpr int nsteps = Q, LA = ring_la<Q, R>() < Q - 1 ? ring_la<Q, R>() : Q - 1;
+            constexpr int nsteps = PPC * Q, LA0 = ring_la<Q, R>() < Q - 1 ? ring_la<Q, R>() : Q - 1, LA = LA0;
             uint64_t bb[LA + 1][R];
 #pragma unroll
             for (int e = 0; e < LA; e++)
-                lds_read_r<R>(bb[e], (uint32_t)__builtin_amdgcn_readlane(voff, e) + lane_byte);
+                lds_read_r<R>(bb[e], (uint32_t)__builtin_amdgcn_readlane(voff[e / Q], e % Q) + lane_byte);
 #pragma unroll
             for (int e = 0; e < nsteps; e++) {
                 uint64_t (&cur)[R] = bb[e % (LA + 1)];
                 if (e + LA < nsteps) {
                     lds_read_r<R>(bb[(e + LA) % (LA + 1)],
-                                  (uint32_t)__builtin_amdgcn_readlane(voff, e + LA) + lane_byte);
+                                  (uint32_t)__builtin_amdgcn_readlane(voff[(e + LA) / Q], (e + LA) % Q) + lane_byte);
                     lds_wait_n<LA * R>(cur);
                 } else if (e + 3 == nsteps && LA >= 2) {
                     lds_wait_n<2 * R>(cur);
@@ -1967,56 +1976,58 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, const int32_
                 } else {
                     lds_wait_n<0>(cur);
                 }
+                const int q = e % Q;
 #pragma unroll
                 for (int r = 0; r < R; r++) {
-                    acc16[e][r][0] += __builtin_bit_cast(short2v, (uint32_t)cur[r]);
-                    acc16[e][r][1] += __builtin_bit_cast(short2v, (uint32_t)(cur[r] >> 32));
+                    acc16[q][r][0] += __builtin_bit_cast(short2v, (uint32_t)cur[r]);
+                    acc16[q][r][1] += __builtin_bit_cast(short2v, (uint32_t)(cur[r] >> 32));
+                }
+                if (q == Q - 1 && ++gcount == G) {                // one pair done: widen every G pairs
+                    gcount = 0;
+#pragma unroll
+                    for (int qq = 0; qq < Q; qq++)
+#pragma unroll
+                        for (int r = 0; r < R; r++) {
+                            acc32[qq][r][0] += acc16[qq][r][0].x;
+                            acc32[qq][r][1] += acc16[qq][r][0].y;
+                            acc32[qq][r][2] += acc16[qq][r][1].x;
+                            acc32[qq][r][3] += acc16[qq][r][1].y;
+                            acc16[qq][r][0] = short2v{0, 0};
+                            acc16[qq][r][1] = short2v{0, 0};
+                        }
                 }
             }
-            if (++gcount == G) {
-                gcount = 0;
-#pragma unroll
-                for (int qq = 0; qq < Q; qq++)
-#pragma unroll
-                    for (int r = 0; r < R; r++) {
-                        acc32[qq][r][0] += acc16[qq][r][0].x;
-                        acc32[qq][r][1] += acc16[qq][r][0].y;
-                        acc32[qq][r][2] += acc16[qq][r][1].x;
-                        acc32[qq][r][3] += acc16[qq][r][1].y;
-                        acc16[qq][r][0] = short2v{0, 0};
-                        acc16[qq][r][1] = short2v{0, 0};
-                    }
-            }
         }
-        ring_wait_vm<R>();
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NS - 3) : "memory");
         ring_barrier();
         // tile done: its stores go out after this chunk's DMA wait, so they do not hold it up
-        if (pr == nchunk - 1) flush(tb + ktile++);
-        pr = prn;
+        if (chk == nchunk - 1) flush(tb + ktile++);
+        chk = chn;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may land after the workgroup ends
 
 }
 
-size_t stage2_pair_lds_bytes(int wstride, int npw, int nbp, int nsub, int umax)
+size_t stage2_pair_lds_bytes(int wstride, int npw, int nbp, int nsub, int umax, int ppc)
 {
-    return (size_t)(nsub / 2) * kPairTab * 4 + (size_t)kRingNS * (2 * npw + nbp) * 1024 +
-           (size_t)2 * umax * 4 * wstride * 2;
+    const int ns = ppc == 2 ? 4 : kRingNS;
+    return (size_t)(nsub / 2) * kPairTab * 4 + (size_t)ns * (2 * ppc * npw + nbp) * 1024 +
+           (size_t)2 * ppc * umax * 4 * wstride * 2;
 }
 
-template <int Q, int R>
-static hipError_t launch_pair_qr(const Stage2Args& a, int nyblk, int nw, hipStream_t st)
+template <int Q, int R, int PPC>
+static hipError_t launch_pair_qrp(const Stage2Args& a, int nyblk, hipStream_t st)
 {
     {
-        const hipError_t e = set_max_lds((const void*)k_stage2_pair<Q, R>, 160 * 1024);
+        const hipError_t e = set_max_lds((const void*)k_stage2_pair<Q, R, PPC>, 160 * 1024);
         if (e != hipSuccess) return e;
     }
     const unsigned ntiles = (unsigned)((a.nvalid + 256 * R - 1) / (256 * R));
     const unsigned nx = a.nwg > 0 && (unsigned)a.nwg < ntiles ? (unsigned)a.nwg : ntiles;
     Stage2Args b = a;
     if (nx == ntiles) b.nwg = 0;
-    hipLaunchKernelGGL((k_stage2_pair<Q, R>), dim3(nx, (unsigned)nyblk), dim3(64 * nw),
-                       stage2_pair_lds_bytes(a.wstride, a.ring_npw, a.ring_nbp, a.nsub, a.umax), st, b, a.off);
+    hipLaunchKernelGGL((k_stage2_pair<Q, R, PPC>), dim3(nx, (unsigned)nyblk), dim3(1024),
+                       stage2_pair_lds_bytes(a.wstride, a.ring_npw, a.ring_nbp, a.nsub, a.umax, PPC), st, b, a.off);
     return hipGetLastError();
 }
 
@@ -2251,12 +2262,14 @@ hipError_t launch_stage2_ring(const Stage2Args& a, int q, int r, hipStream_t st)
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_stage2_pair(const Stage2Args& a, int q, int r, int nw, hipStream_t st)
+hipError_t launch_stage2_pair(const Stage2Args& a, int q, int r, int ppc, hipStream_t st)
 {
     if (a.nvalid <= 0) return hipSuccess;
-    if (nw != 16 && nw != 8) return hipErrorInvalidValue;
+    if (ppc != 1 && ppc != 2) return hipErrorInvalidValue;
     const int nyblk = (a.numdms + a.dms_per_blk - 1) / a.dms_per_blk;
-#define HD_PL(QQ, RR) if (q == QQ && r == RR) return launch_pair_qr<QQ, RR>(a, nyblk, nw, st);
+#define HD_PL(QQ, RR)                                                                             \
+    if (q == QQ && r == RR)                                                                       \
+        return ppc == 2 ? launch_pair_qrp<QQ, RR, 2>(a, nyblk, st) : launch_pair_qrp<QQ, RR, 1>(a, nyblk, st);
     HD_RING_QR(HD_PL)
 #undef HD_PL
     return hipErrorInvalidValue;

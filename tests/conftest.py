@@ -14,8 +14,11 @@ def pytest_configure(config):
 
 
 def gpu_available():
+    """True with a HIP device; a library that does not load raises (HipDedispUnavailable
+    names the cause, e.g. an undefined symbol) instead of reading as 'no device'."""
+    from hipdedisp import _lib, device_count
+    _lib.load()
     try:
-        from hipdedisp import device_count
         return device_count() > 0
     except Exception:
         return False

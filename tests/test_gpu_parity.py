@@ -131,9 +131,14 @@ def test_stage2_pair_ddplan_passes(engine, stage, passnum):
     p = engine.plan(pp)
     p.run_subband()
     outs = []
-    vs = (6, 0, 5, 7)
-    for v in vs:
-        p.set_variant(v)
+    vs = [6, 0, 5, 7]
+    for v in list(vs):
+        try:
+            p.set_variant(v)
+        except PrestoError:                                    # variant 7: when its LDS fits
+            assert v == 7
+            vs.remove(v)
+            continue
         outs.append(p.run_dedisp())
     _, want = OR.run_pass(obs, Opts(), raw, pp, mask=mask, ptsperint=pts, padvals=pad)
     for v, got in zip(vs, outs):
@@ -161,7 +166,11 @@ def test_stage2_pair_persistent_bitexact(engine, stage):
     p.run_subband()
     outs = []
     for v in (6 | (1 << 24), 6 | (2 << 24), 7 | (1 << 24), 7 | (2 << 24)):
-        p.set_variant(v)
+        try:
+            p.set_variant(v)
+        except PrestoError:                                    # variant 7: when its LDS fits
+            assert v & 0xFF == 7
+            continue
         outs.append(p.run_dedisp())
     p.destroy()
     engine.set_mask()
