@@ -64,6 +64,7 @@ class DedispJob:
         self.keep_subbands = keep_subbands
         self.subbanding_time = 0.0
         self.dedispersing_time = 0.0
+        self.singlepulse_time = 0.0     # :539-546 on device (run_pass(single_pulse=...))
         self.ddplans = P.ddplans_for(self.backend)
         self.tempdir = tempfile.mkdtemp(suffix="_tmp", prefix=self.basefilenm,
                                         dir=tmpdir_base or ("/dev/shm" if os.path.isdir("/dev/shm") else None))
@@ -137,13 +138,25 @@ def pass_params(job, ddplan, passnum):
                       ds=ddplan.sub_downsamp, numout=numout)
 
 
-def run_pass(job, ddplan, passnum, maskfilenm, tempdir):
+def _single_pulse(job, plan, ddplan, passnum, tempdir, sp):
+    """:539-546 for the pass's DMs on the device-resident series (hipdedisp.single_pulse):
+    <base>_DM<dm>.singlepulse in sp['workdir'] (or tempdir); adds to job.singlepulse_time."""
+    from .single_pulse import run_single_pulse
+    t, _ = run_single_pulse(plan, os.path.join(tempdir, job.basefilenm), ddplan.dmlist[passnum],
+                            workdir=sp.get("workdir"), maxwidth=sp.get("maxwidth", 0.1),
+                            threshold=sp.get("threshold", 5.0))
+    job.singlepulse_time = getattr(job, "singlepulse_time", 0.0) + t
+
+
+def run_pass(job, ddplan, passnum, maskfilenm, tempdir, single_pulse=None):
     """PALFA2_presto_search.py:498-529 for one pass: subbands (stage 1) then the DM sweep
     (stage 2); writes <tempdir>/<base>_DM<dm>.dat/.inf; returns (t_sub, t_dd).  Without
     subbands (:522-529) the reference makes one prepsubband call, timed as dedispersing
-    time only: t_sub is 0 and the whole pass goes to t_dd."""
+    time only: t_sub is 0 and the whole pass goes to t_dd.  single_pulse (a dict of
+    maxwidth / threshold / workdir, config.searching's singlepulse_*) also runs :539-546 on
+    the series while they are in HBM."""
     if not job.use_subbands:
-        return _run_pass_nosub(job, ddplan, passnum, maskfilenm, tempdir)
+        return _run_pass_nosub(job, ddplan, passnum, maskfilenm, tempdir, single_pulse)
     subbasenm = "%s_DM%s" % (job.basefilenm, ddplan.subdmlist[passnum])
     eng = job.open_engine()
     job.load_mask(maskfilenm)
@@ -164,6 +177,8 @@ def run_pass(job, ddplan, passnum, maskfilenm, tempdir):
         info = job.info_template(pp.nsub, plan.sub_lofreq, plan.sub_chanwid, plan.sub_dt)
         write_dats_device(plan, os.path.join(tempdir, job.basefilenm), ddplan.dmlist[passnum], info, plan.nds)
         t_dd = time.time() - t0
+        if single_pulse is not None:
+            _single_pulse(job, plan, ddplan, passnum, tempdir, single_pulse)
     finally:
         plan.destroy()
     job.subbanding_time += t_sub
@@ -171,7 +186,7 @@ def run_pass(job, ddplan, passnum, maskfilenm, tempdir):
     return t_sub, t_dd
 
 
-def _run_pass_nosub(job, ddplan, passnum, maskfilenm, tempdir):
+def _run_pass_nosub(job, ddplan, passnum, maskfilenm, tempdir, single_pulse=None):
     """PALFA2_presto_search.py:522-529: `prepsubband -mask M -lodm -dmstep -numdms -downsamp
     (dd*sub) -numout N` straight on the raw data: channels (downsampled, float32) are the
     subbands of a nsub = nchan pass."""
@@ -186,19 +201,22 @@ def _run_pass_nosub(job, ddplan, passnum, maskfilenm, tempdir):
         info = job.info_template(pp.nsub, plan.sub_lofreq, plan.sub_chanwid, plan.sub_dt)
         write_dats_device(plan, os.path.join(tempdir, job.basefilenm), ddplan.dmlist[passnum], info, plan.nds)
         t_dd = time.time() - t0
+        if single_pulse is not None:
+            _single_pulse(job, plan, ddplan, passnum, tempdir, single_pulse)
     finally:
         plan.destroy()
     job.dedispersing_time += t_dd
     return 0.0, t_dd
 
 
-def dedisperse_job(job, maskfilenm=None, per_dm=None, remove_dat=False):
-    """The loop of PALFA2_presto_search.py:494-537: every pass of every DDplan stage, then
+def dedisperse_job(job, maskfilenm=None, per_dm=None, remove_dat=False, single_pulse=None):
+    """The loop of PALFA2_presto_search.py:494-537: every pass of every DDplan stage (with
+    the device single-pulse search of :539-546 when single_pulse is given), then
     `per_dm(job, dmstr, basenm)` for each new DM (the reference's downstream tools)."""
     dmstrs = []
     for ddplan in job.ddplans:
         for passnum in range(ddplan.numpasses):
-            run_pass(job, ddplan, passnum, maskfilenm, job.tempdir)
+            run_pass(job, ddplan, passnum, maskfilenm, job.tempdir, single_pulse)
             for dmstr in ddplan.dmlist[passnum]:
                 dmstrs.append(dmstr)
                 basenm = os.path.join(job.tempdir, job.basefilenm + "_DM" + dmstr)

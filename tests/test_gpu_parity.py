@@ -544,9 +544,12 @@ def test_search_stage_dedisperse_job(engine, tmp_path, use_subbands):
         d.numpasses = 1
         ddplans.append(d)
     job.ddplans = ddplans
+    spdir = tmp_path / "sp"
+    spdir.mkdir()
     try:
-        dmstrs = dedisperse_job(job)
+        dmstrs = dedisperse_job(job, single_pulse=dict(maxwidth=0.1, threshold=5.0, workdir=str(spdir)))
         assert len(dmstrs) == sum(d.dmsperpass for d in ddplans)
+        assert job.singlepulse_time > 0
         sobs = job.specinfo.obs_params(0.0)
         for d in ddplans:
             pp = pass_params(job, d, 0)
@@ -560,6 +563,15 @@ def test_search_stage_dedisperse_job(engine, tmp_path, use_subbands):
                 np.testing.assert_allclose(got[nds:], want[k, nds:], rtol=REL_TOL, atol=0)
                 inf = read_inf(base + ".inf")
                 assert inf.N == got.size and "%.2f" % inf.dm == dmstr
+                # :539-546: <base>_DM<dm>.singlepulse in the work dir, equal to the oracle's
+                # single_pulse_search restatement over the .dat just written
+                wl = OR.sp_widths(inf.dt, 0.1)
+                raw, bad = OR.sp_hits(got[None, :], wl, 5.0)
+                ref = OR.sp_candidates(raw, bad, wl, [float(dmstr)], inf.dt, nds, got.size,
+                                       ls=got.size // 1000 * 1000 // 8000 * 8000)[0]
+                text = open(str(spdir / ("%s_DM%s.singlepulse" % (job.basefilenm, dmstr)))).read()
+                assert text == ("# DM      Sigma      Time (s)     Sample    Downfact\n" + "".join(map(str, ref))
+                                if ref else "")
         assert job.dedispersing_time > 0
         assert (job.subbanding_time > 0) == use_subbands
     finally:
