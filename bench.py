@@ -35,9 +35,10 @@ def parse():
     ap.add_argument("--variant", type=int, default=0,
                     help="hd_plan_set_variant value for every plan (0 auto; probe bits are for profiling only)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU-baseline leg")
-    ap.add_argument("--streams", type=int, default=1, choices=(1, 2),
-                    help="stage-2 HIP streams (hd_set_streams): 2 overlaps consecutive passes (no launch tails; "
-                         "per-kernel event times then include the shared time, so the roofline is taken at 1)")
+    ap.add_argument("--streams", type=int, default=1, choices=(1, 2, 3),
+                    help="stage-2 HIP streams (hd_set_streams): 2 overlaps consecutive passes (no launch tails), 3 runs "
+                         "stage 2 on its own stream so the next DDplan stage's stage 1 overlaps it; per-kernel event "
+                         "times then include the shared time, so the roofline is taken at 1")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU work for the baseline sample")
     ap.add_argument("--e2e-beams", type=int, default=1,
                     help="beams run end to end (.dat/.inf files written) after the timed steps; 0 = skip")

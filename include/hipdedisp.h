@@ -151,8 +151,11 @@ HD_API int         hd_sync(hd_ctx* ctx);
 /* Streams for stage 2 (default 1).  With 2, consecutive hd_run_dedisp calls alternate
  * between two HIP streams, so one pass's last tiles share the GPU with the next pass's
  * first ones (no launch tail); stage 1 and hd_set_subbands wait for the second stream's
- * passes, hd_sync waits for both.  Per-plan device times (hd_plan_last_ms) then include
- * the time a kernel shared the GPU with its neighbour.                                */
+ * passes, hd_sync waits for both.  With 3, every hd_run_dedisp runs on the second
+ * stream behind the stage 1 issued before it, and stage 1 waits only for the last stage-2
+ * passes of the plans it rewrites: the next DDplan stage's stage 1 overlaps this stage's
+ * stage 2.  Per-plan device times (hd_plan_last_ms) then include the time a kernel shared
+ * the GPU with others.                                                                  */
 HD_API int         hd_set_streams(hd_ctx* ctx, int32_t n);
 /* Declare the raw block changed outside the library (e.g. written in place through a device
  * pointer): derived layouts (the channel-major copy the 8-bit stage-1 fill reads, built once

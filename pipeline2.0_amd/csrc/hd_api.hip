@@ -89,6 +89,7 @@ struct hd_ctx {
     hd_sp_hit* d_sp_hits = nullptr;
     int64_t sp_hits_cap = 0;
     unsigned long long* d_sp_count = nullptr;
+    double* d_sum_parts = nullptr;  // hd_series_sum partials
     // streaming ingest (hd_push_raw_file): two pinned host blocks, each guarded by the event
     // of the last copy that read it
     void* pin[2] = {nullptr, nullptr};
@@ -101,7 +102,8 @@ struct hd_ctx {
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     bool s2_pending = false;
-    bool dual = false;              // hd_set_streams(ctx, 2)
+    bool dual = false;              // hd_set_streams(ctx, 2 or 3)
+    bool s2all = false;             // hd_set_streams(ctx, 3): every stage-2 pass on stream2
     uint32_t dd_count = 0;
     double* d_partial2 = nullptr;
     size_t partial_bytes2 = 0;
@@ -340,6 +342,7 @@ extern "C" int hd_close(hd_ctx* c)
     dfree(c->d_sp_coef);
     dfree(c->d_sp_hits);
     dfree(c->d_sp_count);
+    dfree(c->d_sum_parts);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
@@ -356,10 +359,11 @@ extern "C" int hd_close(hd_ctx* c)
 extern "C" int hd_set_streams(hd_ctx* c, int32_t n)
 {
     if (!c) return fail(nullptr, HD_E_INVAL, "hd_set_streams: NULL context");
-    if (n != 1 && n != 2) return fail(c, HD_E_INVAL, "hd_set_streams: n must be 1 or 2");
+    if (n < 1 || n > 3) return fail(c, HD_E_INVAL, "hd_set_streams: n must be 1, 2 or 3");
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, sync_all(c));
-    c->dual = n == 2;
+    c->dual = n >= 2;
+    c->s2all = n == 3;
     c->dd_count = 0;
     return HD_OK;
 }
@@ -1943,7 +1947,16 @@ extern "C" int hd_run_subband_multi(hd_plan** plans, int32_t n)
     }
     if (!c->raw_ready) return fail(c, HD_E_STATE, "hd_run_subband: no raw data (hd_push_raw / hd_synth_device)");
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, join_stream2(c));          // a stage-2 pass on stream2 may still read these subbands
+    if (c->s2all) {
+        // stage 2 runs on stream2 behind stage 1: only these plans' own last stage-2 passes
+        // must be done before their subbands are rewritten (the next DDplan stage's stage 1
+        // overlaps the current stage's stage 2)
+        for (int i = 0; i < n; i++)
+            if (plans[i]->ran_dd && plans[i]->dd_stream == c->stream2)
+                HIPCHK(c, hipStreamWaitEvent(c->stream, plans[i]->ev[3], 0));
+    } else {
+        HIPCHK(c, join_stream2(c));      // a stage-2 pass on stream2 may still read these subbands
+    }
     for (int i = 0; i < n; i++) {
         int rc = ensure_sub(c, plans[i]);
         if (rc) return rc;
@@ -2141,13 +2154,15 @@ extern "C" int hd_series_sum(hd_plan* p, int32_t dm, int64_t t0, int64_t count, 
     if (count == 0) return HD_OK;
     HIPCHK(c, hipSetDevice(c->device));
     constexpr int kParts = 512;
-    double* d = nullptr;
-    HIPCHK(c, hipMallocAsync((void**)&d, kParts * sizeof(double), p->dd_stream));
-    HIPCHK(c, hd::launch_series_sum(p->d_out + (size_t)dm * p->out_stride + t0, count, d, kParts, p->dd_stream));
-    std::vector<double> h(kParts);
-    HIPCHK(c, hipMemcpyAsync(h.data(), d, kParts * sizeof(double), hipMemcpyDeviceToHost, p->dd_stream));
-    HIPCHK(c, hipFreeAsync(d, p->dd_stream));
+    // partials in a context buffer (no stream-ordered pool), the stage-2 stream drained
+    // before and after, and a blocking copy into the host vector
+    if (!c->d_sum_parts) HIPCHK(c, hipMalloc(&c->d_sum_parts, kParts * sizeof(double)));
     HIPCHK(c, hipStreamSynchronize(p->dd_stream));
+    HIPCHK(c, hd::launch_series_sum(p->d_out + (size_t)dm * p->out_stride + t0, count, c->d_sum_parts, kParts,
+                                    p->dd_stream));
+    HIPCHK(c, hipStreamSynchronize(p->dd_stream));
+    std::vector<double> h(kParts);
+    HIPCHK(c, hipMemcpy(h.data(), c->d_sum_parts, kParts * sizeof(double), hipMemcpyDeviceToHost));
     double acc = 0.0;
     for (double v : h) acc += v;
     *sum = acc;
@@ -2208,7 +2223,7 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
     const bool pad = p->numout > p->nds;
     // alternate streams between passes (see hd_ctx::stream2); a plan re-run on the other
     // stream first waits for its previous run, which wrote the same series
-    const bool alt = c->dual && (c->dd_count++ & 1u) != 0;
+    const bool alt = c->dual && (c->s2all || (c->dd_count++ & 1u) != 0);
     hipStream_t st = alt ? c->stream2 : c->stream;
     if (alt) {
         HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));

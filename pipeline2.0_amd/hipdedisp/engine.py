@@ -160,7 +160,7 @@ class Engine:
         self._chk(self._L.hd_touch_raw(self._ctx), "hd_touch_raw")
 
     def set_streams(self, n):
-        """1 (default) or 2 HIP streams for stage 2 (hd_set_streams)."""
+        """1 (default), 2 or 3 HIP streams for stage 2 (hd_set_streams)."""
         self._chk(self._L.hd_set_streams(self._ctx, int(n)), "hd_set_streams")
 
     # -- observation state --

@@ -496,6 +496,50 @@ def test_dual_stream_stage2_matches(engine):
             p.destroy()
 
 
+def test_stage2_own_stream_overlap_matches(engine):
+    """hd_set_streams(3): every stage-2 pass on the second stream behind its stage 1, the next
+    DDplan stage's stage 1 overlapping it; beams alternate between two raw contents, so a
+    stage 1 that rewrote subbands before their last stage-2 reader finished, or a stage 2
+    that read them before they were written, would show -- every series equals the
+    single-stream result of its beam."""
+    obs = palfa_obs(N=3 * 8192, nbits=8)
+    engine.set_obs(obs, Opts())
+    stages = []
+    for st, n in ((0, 3), (1, 2), (3, 2)):
+        d = plan.ddplans_for("pdev")[st]
+        stages.append([engine.plan(PassParams(subdm=float(d.subdmlist[i]), lodm=float(d.lodm_arg(i)),
+                                              dmstep=float(d.dmstep_arg()), numdms=d.dmsperpass, nsub=d.numsub,
+                                              ds=d.sub_downsamp, numout=plan.choose_N(obs.N / d.downsamp)))
+                       for i in range(n)])
+    synths = [palfa_synth(beam=0), palfa_synth(beam=1)]
+
+    def beam(k):
+        engine.synth_device(synths[k])
+        for ps in stages:
+            engine.run_subband_multi(ps)
+            for p in ps:
+                p.run_dedisp(to_host=False)
+
+    want = []
+    for k in range(2):
+        beam(k)
+        want.append([p.get_series(0, None, 0, p.numout) for ps in stages for p in ps])
+    engine.set_streams(3)
+    try:
+        for it in range(4):
+            beam((it + 1) % 2)              # queued, not read: the next beam's stage 1 must wait
+            beam(it % 2)                    # for these stage-2 passes per plan
+            got = [p.get_series(0, None, 0, p.numout) for ps in stages for p in ps]
+            for g, w in zip(got, want[it % 2]):
+                assert np.array_equal(g, w), it
+        engine.sync()
+    finally:
+        engine.set_streams(1)
+        for ps in stages:
+            for p in ps:
+                p.destroy()
+
+
 def test_stage1_channel_major_fill(engine):
     """The 8-bit stage-1 kernel fills its LDS tile from a channel-major copy of the raw block
     (built once per raw block): results equal the row-major fill (probe bit 2) and the oracle,
