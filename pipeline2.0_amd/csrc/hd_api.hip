@@ -738,15 +738,29 @@ extern "C" int hd_get_raw_device(hd_ctx* c, void* dev_out, int64_t start, int64_
     return HD_OK;
 }
 
+// Device -> pageable host copies: drain the stream first, then a blocking copy.  (An async
+// copy into pageable memory is staged by the runtime; draining first keeps every read after
+// the kernels that wrote the data whatever the staging does.)
+static hipError_t d2h_2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t height,
+                         hipStream_t st)
+{
+    hipError_t e = hipStreamSynchronize(st);
+    if (e == hipSuccess) e = hipMemcpy2D(dst, dpitch, src, spitch, width, height, hipMemcpyDeviceToHost);
+    return e;
+}
+
+static hipError_t d2h(void* dst, const void* src, size_t bytes, hipStream_t st)
+{
+    return d2h_2d(dst, bytes, src, bytes, bytes, 1, st);
+}
+
 extern "C" int hd_get_raw(hd_ctx* c, void* out, int64_t start, int64_t n)
 {
     if (!c) return fail(nullptr, HD_E_INVAL, "hd_get_raw: NULL context");
     if (!c->raw_ready || !c->d_raw) return fail(c, HD_E_STATE, "hd_get_raw: no raw data");
     if (!out || start < 0 || n < 0 || start + n > c->obs.N) return fail(c, HD_E_INVAL, "hd_get_raw: bad range");
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipMemcpyAsync(out, c->d_raw + (size_t)start * c->rowbytes, (size_t)n * c->rowbytes,
-                             hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, d2h(out, c->d_raw + (size_t)start * c->rowbytes, (size_t)n * c->rowbytes, c->stream));
     return HD_OK;
 }
 
@@ -1559,9 +1573,9 @@ extern "C" int hd_clip_stats(hd_ctx* c, int64_t nown, double* stats)
     }
     const size_t w = (size_t)c->obs.nchan + 3;
     HIPCHK(c, hd::launch_clip_pack(a, c->clip.xbuf, (int)nown, c->stream));
-    HIPCHK(c, hipMemcpyAsync(stats + (size_t)(c->slice_t0 / c->blk) * w, c->clip.xbuf, (size_t)nown * w * 8,
-                             hipMemcpyDefault, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));     // then a blocking copy (stats may be pageable host memory)
+    HIPCHK(c, hipMemcpy(stats + (size_t)(c->slice_t0 / c->blk) * w, c->clip.xbuf, (size_t)nown * w * 8,
+                        hipMemcpyDefault));
     return HD_OK;
 }
 
@@ -1981,9 +1995,7 @@ extern "C" int hd_get_subbands(hd_plan* p, void* host)
     if (!p->sub_valid) return fail(c, HD_E_STATE, "hd_get_subbands: no subbands formed for this plan yet");
     const size_t es = sub_elem(c);
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipMemcpy2DAsync(host, es * p->nds, p->d_sub, es * p->sub_stride, es * p->nds, p->pass.nsub,
-                               hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, d2h_2d(host, es * p->nds, p->d_sub, es * p->sub_stride, es * p->nds, p->pass.nsub, c->stream));
     return HD_OK;
 }
 
@@ -1998,9 +2010,8 @@ extern "C" int hd_get_subbands_window(hd_plan* p, int64_t t0, int64_t count, voi
     if (count == 0) return HD_OK;
     const size_t es = sub_elem(c);
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipMemcpy2DAsync(host, es * count, (const char*)p->d_sub + es * t0, es * p->sub_stride, es * count,
-                               p->pass.nsub, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, d2h_2d(host, es * count, (const char*)p->d_sub + es * t0, es * p->sub_stride, es * count,
+                     p->pass.nsub, c->stream));
     return HD_OK;
 }
 
@@ -2014,10 +2025,8 @@ extern "C" int hd_get_series(hd_plan* p, int32_t dm0, int32_t ndm, int64_t t0, i
                     (long long)p->numout);
     if (count == 0 || ndm == 0) return HD_OK;
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipMemcpy2DAsync(host, sizeof(float) * count, p->d_out + (size_t)dm0 * p->out_stride + t0,
-                               sizeof(float) * p->out_stride, sizeof(float) * count, ndm, hipMemcpyDeviceToHost,
-                               p->dd_stream));
-    HIPCHK(c, hipStreamSynchronize(p->dd_stream));
+    HIPCHK(c, d2h_2d(host, sizeof(float) * count, p->d_out + (size_t)dm0 * p->out_stride + t0,
+                     sizeof(float) * p->out_stride, sizeof(float) * count, ndm, p->dd_stream));
     return HD_OK;
 }
 
@@ -2081,13 +2090,12 @@ extern "C" int hd_single_pulse(hd_plan* p, double dt, double maxwidth, double th
                                      threshold, c->d_sp_hits, c->d_sp_count, c->sp_hits_cap, st));
     }
     unsigned long long cnt = 0;
-    HIPCHK(c, hipMemcpyAsync(&cnt, c->d_sp_count, sizeof(cnt), hipMemcpyDeviceToHost, st));
+    HIPCHK(c, d2h(&cnt, c->d_sp_count, sizeof(cnt), st));
     std::vector<double> coef;
     if (bad_blocks && nblocks > 0) {
         coef.resize((size_t)ndm * nblocks * 4);
-        HIPCHK(c, hipMemcpyAsync(coef.data(), c->d_sp_coef, sizeof(double) * coef.size(), hipMemcpyDeviceToHost, st));
+        HIPCHK(c, d2h(coef.data(), c->d_sp_coef, sizeof(double) * coef.size(), st));
     }
-    HIPCHK(c, hipStreamSynchronize(st));
     if (bad_blocks)
         for (size_t i = 0; i < (size_t)ndm * nblocks; i++) bad_blocks[i] = coef[4 * i + 3] != 0.0;
     *nhits = (int64_t)cnt;
@@ -2162,7 +2170,7 @@ extern "C" int hd_series_sum(hd_plan* p, int32_t dm, int64_t t0, int64_t count, 
                                     p->dd_stream));
     HIPCHK(c, hipStreamSynchronize(p->dd_stream));
     std::vector<double> h(kParts);
-    HIPCHK(c, hipMemcpy(h.data(), c->d_sum_parts, kParts * sizeof(double), hipMemcpyDeviceToHost));
+    HIPCHK(c, d2h(h.data(), c->d_sum_parts, kParts * sizeof(double), p->dd_stream));
     double acc = 0.0;
     for (double v : h) acc += v;
     *sum = acc;
@@ -2325,9 +2333,8 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
     p->ran_dd = true;
     p->dd_stream = st;
     if (host_out) {
-        HIPCHK(c, hipMemcpy2DAsync(host_out, sizeof(float) * p->numout, p->d_out, sizeof(float) * p->out_stride,
-                                   sizeof(float) * p->numout, p->pass.numdms, hipMemcpyDeviceToHost, st));
-        HIPCHK(c, hipStreamSynchronize(st));
+        HIPCHK(c, d2h_2d(host_out, sizeof(float) * p->numout, p->d_out, sizeof(float) * p->out_stride,
+                         sizeof(float) * p->numout, p->pass.numdms, st));
     }
     return HD_OK;
 }
