@@ -101,6 +101,12 @@ struct hd_ctx {
     // main-stream work that rewrites subbands after it; each stream has its own partials.
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // the channel-major raw copy runs on saux beside clip_times' latency-bound kernels
+    // (AS-52 per block, the serial 30-block recurrence): ev_aux0 orders it after the main
+    // stream's work so far, stage 1 waits for ev_aux1
+    hipStream_t saux = nullptr;
+    hipEvent_t ev_aux0 = nullptr, ev_aux1 = nullptr;
+    bool aux_pending = false;
     bool s2_pending = false;
     bool dual = false;              // hd_set_streams(ctx, 2 or 3)
     bool s2all = false;             // hd_set_streams(ctx, 3): every stage-2 pass on stream2
@@ -121,11 +127,13 @@ static hipError_t join_stream2(hd_ctx* c)
 static hipError_t sync_all(hd_ctx* c)
 {
     hipError_t e = hipStreamSynchronize(c->stream);
-    if (c->stream2) {
-        const hipError_t e2 = hipStreamSynchronize(c->stream2);
-        if (e == hipSuccess) e = e2;
-    }
+    for (hipStream_t o : {c->stream2, c->saux})
+        if (o) {
+            const hipError_t e2 = hipStreamSynchronize(o);
+            if (e == hipSuccess) e = e2;
+        }
     c->s2_pending = false;
+    c->aux_pending = false;
     return e;
 }
 
@@ -270,6 +278,9 @@ extern "C" int hd_open(int device, hd_ctx** out)
     c->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->saux, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_aux0, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_aux1, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
         delete c;
@@ -344,6 +355,9 @@ extern "C" int hd_close(hd_ctx* c)
     dfree(c->d_sp_count);
     dfree(c->d_sum_parts);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_aux0) (void)hipEventDestroy(c->ev_aux0);
+    if (c->ev_aux1) (void)hipEventDestroy(c->ev_aux1);
+    if (c->saux) (void)hipStreamDestroy(c->saux);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
     for (int b = 0; b < 2; b++) {
@@ -405,17 +419,37 @@ static bool alloc_rawT(hd_ctx* c, int dmax)
     return true;
 }
 
-static const uint8_t* ensure_rawT(hd_ctx* c, int dmax)
+static const uint8_t* ensure_rawT(hd_ctx* c, int dmax, bool aux = false, bool forked = false)
 {
     if (!alloc_rawT(c, dmax)) return nullptr;
     const int nb = c->obs.nbits;
     if (!c->rawT_valid) {
+        hipStream_t st = c->stream;
+        if (aux) {
+            // on saux after ev_aux0: recorded here (the main stream's work so far) or, when
+            // forked, by clip_times after its full-chip statistics kernels
+            if (!forked && hipEventRecord(c->ev_aux0, c->stream) != hipSuccess) return nullptr;
+            if (hipStreamWaitEvent(c->saux, c->ev_aux0, 0) != hipSuccess) return nullptr;
+            st = c->saux;
+        }
         if (hd::launch_raw_transpose(c->d_raw, c->obs.N, c->obs.nchan, nb, c->opts.nibble_hi_first, c->d_rawT,
-                                     c->rawT_stride, c->stream) != hipSuccess)
+                                     c->rawT_stride, st) != hipSuccess)
             return nullptr;
+        if (aux) {
+            if (hipEventRecord(c->ev_aux1, c->saux) != hipSuccess) return nullptr;
+            c->aux_pending = true;
+        }
         c->rawT_valid = true;
     }
     return c->d_rawT;
+}
+
+// the main stream waits for a channel-major copy still running on saux
+static hipError_t join_aux(hd_ctx* c)
+{
+    if (!c->aux_pending) return hipSuccess;
+    c->aux_pending = false;
+    return hipStreamWaitEvent(c->stream, c->ev_aux1, 0);
 }
 
 extern "C" const char* hd_last_error(const hd_ctx* c) { return c ? c->err.c_str() : g_err.c_str(); }
@@ -1462,7 +1496,7 @@ static int ensure_blocks(hd_ctx* c)
 static int alloc_clip(hd_ctx* c);
 static hd::ClipArgs clip_args(hd_ctx* c);
 
-static int ensure_clip(hd_ctx* c)
+static int ensure_clip(hd_ctx* c, hipEvent_t after_stats = nullptr)
 {
     if (!(c->opts.clip_sigma > 0.0f) || c->clip_valid) return HD_OK;
     if (c->slice_total)
@@ -1470,7 +1504,7 @@ static int ensure_clip(hd_ctx* c)
                     "(hd_clip_stats on every slice, then hd_clip_set_stats) before stage 1");
     int rc = alloc_clip(c);
     if (rc) return rc;
-    HIPCHK(c, hd::launch_clip(clip_args(c), c->stream));
+    HIPCHK(c, hd::launch_clip(clip_args(c), c->stream, after_stats));
     c->clip_valid = true;
     return HD_OK;
 }
@@ -1837,12 +1871,23 @@ static int run_subband_chunk(hd_ctx* c, hd_plan** plans, int n)
     if (rc0) return rc0;
     for (int i = 0; i < n; i++) HIPCHK(c, hipMemsetAsync(plans[i]->d_maxabs, 0, sizeof(int32_t), c->stream));
     HIPCHK(c, hipEventRecord(p0->ev[0], c->stream));
-    if ((rc0 = ensure_clip(c))) return rc0;          // once per raw block, charged to this launch
+    // the channel-major copy (once per raw block) on saux, beside clip_times' serial 30-block
+    // recurrence (one workgroup): forked after clip_times' full-chip statistics kernels, or
+    // now when there is no clipping to run
+    const bool want_rawT = q8 && !(p0->probe & 4);   // probe bit 2: row-major fill
+    const bool clip_runs = c->opts.clip_sigma > 0.0f && !c->clip_valid;
+    const bool fork_clip = want_rawT && clip_runs && !c->rawT_valid && alloc_rawT(c, dmax);
+    const uint8_t* rawT = want_rawT && !fork_clip ? ensure_rawT(c, dmax, true) : nullptr;
+    rc0 = ensure_clip(c, fork_clip ? c->ev_aux0 : nullptr);   // once per raw block, charged to this launch
+    if (fork_clip && !rc0) rawT = ensure_rawT(c, dmax, true, true);
+    const hipError_t ej = join_aux(c);               // (also on failure: nothing may outlive the call)
+    if (rc0) return rc0;
+    HIPCHK(c, ej);
     const bool clip = c->opts.clip_sigma > 0.0f;
     if (q8) {
         m.probe = p0->probe;
         m.rd = raw_desc(c);
-        m.rawT = (p0->probe & 4) ? nullptr : ensure_rawT(c, dmax);   // probe bit 2: row-major fill
+        m.rawT = rawT;
         if (!m.rawT && c->obs.nbits != 8) return fail(c, HD_E_HIP, "stage 1: 4-bit channel-major copy failed");
         m.tstride = c->rawT_stride;
         m.npass = n;

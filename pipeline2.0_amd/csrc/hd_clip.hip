@@ -419,7 +419,7 @@ hipError_t launch_clip_flag(const ClipArgs& a, hipStream_t st)
 }
 
 // per-block statistics of a's spectra (everything before the recurrence)
-hipError_t launch_clip_stats(const ClipArgs& a, hipStream_t st)
+hipError_t launch_clip_stats(const ClipArgs& a, hipStream_t st, hipEvent_t after_stats)
 {
     const RawDesc& rd = a.rd;
     if (rd.N <= 0) return hipSuccess;
@@ -439,13 +439,17 @@ hipError_t launch_clip_stats(const ClipArgs& a, hipStream_t st)
         hipLaunchKernelGGL(k_clip_chan_u4, dim3((unsigned)rd.nblk), dim3(256), 0, st, a);
     else
         hipLaunchKernelGGL(k_clip_chan, dim3((unsigned)(rd.nblk * ((rd.nchan + 255) / 256))), dim3(256), 0, st, a);
+    if (after_stats) {          // the full-chip raw scans are done; the serial recurrence follows
+        const hipError_t e = hipEventRecord(after_stats, st);
+        if (e != hipSuccess) return e;
+    }
     return hipGetLastError();
 }
 
-hipError_t launch_clip(const ClipArgs& a, hipStream_t st)
+hipError_t launch_clip(const ClipArgs& a, hipStream_t st, hipEvent_t after_stats)
 {
     if (a.rd.N <= 0) return hipMemsetAsync(a.nevents, 0, sizeof(int32_t), st);
-    hipError_t e = launch_clip_stats(a, st);
+    hipError_t e = launch_clip_stats(a, st, after_stats);
     if (e == hipSuccess) e = launch_clip_recur(a, st);
     if (e == hipSuccess) e = launch_clip_flag(a, st);
     return e;

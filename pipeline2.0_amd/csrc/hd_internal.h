@@ -154,8 +154,8 @@ struct ClipArgs {
     int32_t* nevents;         // device counter
 };
 int clip_max_block();
-hipError_t launch_clip(const ClipArgs& a, hipStream_t st);       // = stats + recur + flag
-hipError_t launch_clip_stats(const ClipArgs& a, hipStream_t st);
+hipError_t launch_clip(const ClipArgs& a, hipStream_t st, hipEvent_t after_stats = nullptr);   // = stats + recur + flag
+hipError_t launch_clip_stats(const ClipArgs& a, hipStream_t st, hipEvent_t after_stats = nullptr);
 hipError_t launch_clip_recur(const ClipArgs& a, hipStream_t st);
 hipError_t launch_clip_flag(const ClipArgs& a, hipStream_t st);
 // time-sliced contexts: rows [bavg, bstd, numgood, chansum[nchan]] of the first nown blocks
