@@ -309,6 +309,16 @@ HD_API int hd_plan_last_ms(const hd_plan* plan, float* ms_subband, float* ms_ded
  * chunk (half the chunks per tile; HD_E_INVAL when its LDS does not fit). */
 HD_API int hd_plan_set_variant(hd_plan* plan, int32_t variant);
 
+/* ---- rfifind statistics -------------------------------------------------------------
+ * The numeric part of `rfifind -time T -o <base> <files>` (lib/python/PALFA2_presto_search.py:
+ * 482-490) on the raw block in HBM [PRESTO-ext]: for every whole interval of ptsperint spectra
+ * and every channel (ascending frequency), the samples as rfifind reads them (clip_times per
+ * hd_opts, no mask -- call before hd_set_mask), their mean and standard deviation (variance
+ * over n - 1) and the largest power of the interval's real FFT over bins 1 .. ptsperint/2 - 1
+ * normalised by ptsperint * variance.  Outputs float [N / ptsperint][nchan].  The mask and
+ * .stats files are made from these by hipdedisp/rfifind.py.                                */
+HD_API int hd_rfifind_stats(hd_ctx* ctx, int32_t ptsperint, float* dataavg, float* datastd, float* datapow);
+
 /* ---- single-pulse search on the device-resident series -------------------------------
  * Replaces the per-.dat `single_pulse_search.py -p -m maxwidth -t threshold <dat>` of
  * lib/python/PALFA2_presto_search.py:539-546 (maxwidth 0.1 s, threshold 5.0:

@@ -2075,6 +2075,35 @@ extern "C" int hd_get_series(hd_plan* p, int32_t dm0, int32_t ndm, int64_t t0, i
     return HD_OK;
 }
 
+// ---- rfifind statistics (hd_rfi.hip; PALFA2_presto_search.py:482-490) ----------------------
+extern "C" int hd_rfifind_stats(hd_ctx* c, int32_t ptsperint, float* dataavg, float* datastd, float* datapow)
+{
+    if (!c || !dataavg || !datastd || !datapow) return fail(c, HD_E_INVAL, "hd_rfifind_stats: NULL argument");
+    if (!c->raw_ready) return fail(c, HD_E_STATE, "hd_rfifind_stats: no raw data (hd_push_raw / hd_synth_device)");
+    if (!c->h_mask.empty()) return fail(c, HD_E_STATE, "hd_rfifind_stats: rfifind reads the data before any mask");
+    if (c->slice_total) return fail(c, HD_E_STATE, "hd_rfifind_stats: not on a time-sliced context");
+    if (ptsperint < 4 || ptsperint % 2) return fail(c, HD_E_INVAL, "hd_rfifind_stats: ptsperint must be even, >= 4");
+    const int64_t numint = c->obs.N / ptsperint;
+    if (numint < 1) return fail(c, HD_E_INVAL, "hd_rfifind_stats: fewer than ptsperint spectra");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, join_stream2(c));
+    int rc = ensure_clip(c);                         // rfifind's own clip_times (no mask yet)
+    if (rc) return rc;
+    const uint8_t* rawT = ensure_rawT(c, 0);         // one byte per sample for 8/4-bit data
+    if (c->d_scl || c->d_offs || c->d_wts) rawT = nullptr;   // calibrated: the generic decode
+    const size_t n = (size_t)numint * c->obs.nchan;
+    float* d = nullptr;
+    HIPCHK(c, hipMalloc(&d, sizeof(float) * 3 * n));
+    hipError_t e = hd::rfi_stats(raw_desc(c), rawT, c->rawT_stride, ptsperint, (int)numint, d, d + n, d + 2 * n,
+                                 c->stream);
+    if (e == hipSuccess) e = hipMemcpy(dataavg, d, sizeof(float) * n, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(datastd, d + n, sizeof(float) * n, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(datapow, d + 2 * n, sizeof(float) * n, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    HIPCHK(c, e);
+    return HD_OK;
+}
+
 // ---- single-pulse search (hd_sp.hip; replaces single_pulse_search.py per .dat,
 //      PALFA2_presto_search.py:539-546) ----------------------------------------------------
 static const int32_t kSpDownfacts[] = {2, 3, 4, 6, 9, 14, 20, 30, 45, 70, 100, 150, 220, 300};

@@ -173,6 +173,9 @@ hipError_t launch_sp_blocks(const float* x, int64_t stride, int ndm, int nblocks
 hipError_t launch_sp_hits(const float* x, int64_t stride, int ndm, int nblocks, const double* coef, int64_t ls,
                           const int32_t* widths, const double* rsw, int nwidths, double threshold, hd_sp_hit* hits,
                           unsigned long long* count, int64_t cap, hipStream_t st);
+// rfifind statistics (hd_rfi.hip): per interval and channel mean, std, max normalised power
+hipError_t rfi_stats(const RawDesc& rd, const uint8_t* rawT, int64_t tstride, int ptsperint, int numint, float* avg,
+                     float* sd, float* pw, hipStream_t st);
 constexpr int64_t kRawTPad = 65536;   // zero rows after N in each channel-major raw row
 hipError_t launch_raw_transpose(const uint8_t* raw, int64_t N, int32_t nchan, int nbits, int nibble_hi_first,
                                 uint8_t* rawT, int64_t tstride, hipStream_t st);

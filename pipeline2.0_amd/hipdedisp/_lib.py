@@ -39,7 +39,7 @@ EXPORTED = [
     "hd_push_raw_file", "hd_set_streams", "hd_touch_raw", "hd_stats_padvals", "hd_get_clean",
     "hd_get_subbands_window", "hd_get_series", "hd_write_series", "hd_wait_writes",
     "hd_set_slice", "hd_clip_stats", "hd_clip_set_stats", "hd_series_sum", "hd_series_fill",
-    "hd_sp_widths", "hd_single_pulse",
+    "hd_sp_widths", "hd_single_pulse", "hd_rfifind_stats",
 ]
 
 
@@ -153,6 +153,7 @@ def load():
         "hd_clip_set_stats": (ctypes.c_int, [vp, vp]),
         "hd_series_sum": (ctypes.c_int, [vp, i32, i64, i64, P(ctypes.c_double)]),
         "hd_series_fill": (ctypes.c_int, [vp, i64, ctypes.c_float]),
+        "hd_rfifind_stats": (ctypes.c_int, [vp, i32, f32p, f32p, f32p]),
         "hd_sp_widths": (ctypes.c_int, [ctypes.c_double, ctypes.c_double, P(ctypes.c_int32), P(ctypes.c_int32)]),
         "hd_single_pulse": (ctypes.c_int, [vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp, i64, P(i64),
                                            P(ctypes.c_uint8), P(i64)]),

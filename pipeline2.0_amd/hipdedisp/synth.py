@@ -71,10 +71,9 @@ def host_spectra(obs: ObsParams, synth, start=0, count=None):
 
 def rfifind_ptsperint(dt, chunk_time=2 ** 15 * 0.000064, nsblk=PALFA_NSBLK):
     """Samples per rfifind interval for `rfifind -time chunk_time`
-    (searching_example.py:12).  [PRESTO-ext] rfifind rounds the interval to whole
-    PSRFITS rows; restated here as the largest multiple of NSBLK not above chunk_time/dt."""
-    n = int(chunk_time / dt)
-    return max(nsblk, (n // nsblk) * nsblk)
+    (searching_example.py:12): rfifind.ptsperint_for, whole PSRFITS rows."""
+    from .rfifind import ptsperint_for
+    return ptsperint_for(dt, chunk_time, nsblk)
 
 
 def synth_mask(obs: ObsParams, synth, ptsperint, frac=0.02, seed=7):
