@@ -348,6 +348,38 @@ HD_API int hd_sp_widths(double dt, double maxwidth, int32_t* widths, int32_t* n)
 HD_API int hd_single_pulse(hd_plan* plan, double dt, double maxwidth, double threshold, hd_sp_hit* hits,
                            int64_t cap, int64_t* nhits, uint8_t* bad_blocks, int64_t* nblocks);
 
+/* ---- realfft, zapbirds, rednoise on the device-resident series -----------------------
+ * Replace `realfft <dat>; zapbirds -zap -zapfile <zaplist> -baryv <v> <fft>; rednoise <fft>`
+ * per .dat (lib/python/PALFA2_presto_search.py:548-558) [PRESTO-ext, restated; parity with
+ * PRESTO unpinned].  The spectra stay in HBM with the plan ([numdms][numout/2] complex,
+ * PRESTO's packed .fft layout: bin 0 = (DC, Nyquist)); hd_get_fft copies them out.       */
+/* Forward real FFT (no normalisation) of the numout samples of every DM series (after
+ * hd_run_dedisp; numout even).                                                           */
+HD_API int hd_realfft(hd_plan* plan);
+/* Bin ranges [lo, hi) zapped for birdies lobins[i] .. hibins[i] (frequency * T, the
+ * zaplist's freq -+ width/2): lo = floor(lobin), hi = ceil(hibin), clamped to
+ * [1, numbins), empty ones dropped, sorted and merged where they overlap or touch; the
+ * median window [wlo, lo) u [hi, whi) spans side = min(max(50, hi - lo), 2048) bins either
+ * side (clamped).  rng4[4 * k] = {lo, hi, wlo, whi}; cap = room in ranges; *nr = count
+ * (HD_E_NOMEM when more than cap).  Host only.                                           */
+HD_API int hd_zap_ranges(const double* lobins, const double* hibins, int32_t nbirds, int64_t numbins,
+                         int32_t* rng4, int32_t cap, int32_t* nr);
+/* zapbirds -zap: every merged range's bins set to (sqrt(median / ln 2), 0), the median
+ * (element (n-1)/2 of the sorted powers) over its window in the un-zapped spectrum.        */
+HD_API int hd_zapbirds(hd_plan* plan, const double* lobins, const double* hibins, int32_t nbirds);
+/* rednoise's blocks over bins 1 .. numbins - 1: from o = 1, width w(f) = startwidth +
+ * floor((endwidth - startwidth) * ln(1 + f) / ln(1 + endfreq)) at f = o / T Hz below
+ * endfreq, endwidth from there (the last block cut at numbins).  boff[nblk + 1] offsets
+ * (cap = room for offsets), *nblk = count; endwidth <= 128.  Host only.                   */
+HD_API int hd_rednoise_blocks(int64_t numbins, double T, int32_t startwidth, int32_t endwidth, double endfreq,
+                              int32_t* boff, int32_t cap, int32_t* nblk);
+/* rednoise: each block's median power m_j (lower median); bin i scaled by 1/sqrt(m(i)/ln 2),
+ * m linear between the block centres o_j + (w_j - 1)/2 (flat outside them; m <= 0 gives 0);
+ * bin 0 = (1, 0).  T = numout * dt of the series (s); PRESTO's defaults are 6, 100, 6.0.  */
+HD_API int hd_rednoise(hd_plan* plan, int32_t startwidth, int32_t endwidth, double endfreq, double T);
+/* Spectra of DM series dm0 .. dm0 + ndm - 1: out[ndm][numout] floats (numout/2 complex).  */
+HD_API int hd_get_fft(hd_plan* plan, int32_t dm0, int32_t ndm, float* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -179,6 +179,8 @@ struct hd_plan {
     bool copy_pending = false;
     bool ran_sub = false, ran_dd = false;
     hipStream_t dd_stream = nullptr;  // stream of the last hd_run_dedisp (its ev[3] marks the end)
+    hd::FftState* fft = nullptr;    // realfft / zapbirds / rednoise spectra (hd_fft.hip)
+    bool ran_fft = false;
 };
 
 static thread_local std::string g_err;
@@ -972,6 +974,8 @@ static void plan_free(hd_plan* p)
     }
     dfree(p->d_out);
     dfree(p->d_sub);
+    hd::fft_state_free(p->fft);
+    p->fft = nullptr;
     for (auto& e : p->ev)
         if (e) (void)hipEventDestroy(e);
     if (p->ev_copy) (void)hipEventDestroy(p->ev_copy);
@@ -2464,5 +2468,131 @@ extern "C" int hd_plan_last_ms(const hd_plan* p, float* ms_sub, float* ms_dd)
             HIPCHK(c, hipEventElapsedTime(ms_dd, p->ev[2], p->ev[3]));
         }
     }
+    return HD_OK;
+}
+
+// ---- realfft / zapbirds / rednoise (hd_fft.hip; replace the per-.dat PRESTO commands of
+//      PALFA2_presto_search.py:548-558) ---------------------------------------------------
+extern "C" int hd_realfft(hd_plan* p)
+{
+    if (!p) return fail(nullptr, HD_E_INVAL, "hd_realfft: NULL plan");
+    hd_ctx* c = p->ctx;
+    if (!p->ran_dd || !p->d_out) return fail(c, HD_E_STATE, "hd_realfft: run hd_run_dedisp first");
+    if (p->numout < 4 || p->numout % 2) return fail(c, HD_E_INVAL, "hd_realfft: numout %lld must be even, >= 4",
+                                                    (long long)p->numout);
+    if (p->out_stride > INT32_MAX) return fail(c, HD_E_INVAL, "hd_realfft: series stride beyond 2^31");
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t st = p->dd_stream ? p->dd_stream : c->stream;
+    if (!p->fft) p->fft = hd::fft_state_new();
+    HIPCHK(c, hd::fft_series(p->fft, p->d_out, p->out_stride, p->numout, p->pass.numdms, st));
+    p->ran_fft = true;
+    return HD_OK;
+}
+
+extern "C" int hd_zap_ranges(const double* lobins, const double* hibins, int32_t n, int64_t numbins, int32_t* rng4,
+                             int32_t cap, int32_t* nr)
+{
+    if (!nr || n < 0 || (n > 0 && (!lobins || !hibins)) || (cap > 0 && !rng4) || numbins < 2)
+        return fail(nullptr, HD_E_INVAL, "hd_zap_ranges: bad argument");
+    std::vector<std::pair<int64_t, int64_t>> r;
+    for (int32_t i = 0; i < n; i++) {
+        if (!(lobins[i] <= hibins[i])) continue;
+        int64_t lo = (int64_t)std::floor(lobins[i]), hi = (int64_t)std::ceil(hibins[i]);
+        lo = std::max<int64_t>(lo, 1);
+        hi = std::min<int64_t>(hi, numbins);
+        if (lo < hi) r.emplace_back(lo, hi);
+    }
+    std::sort(r.begin(), r.end());
+    std::vector<std::pair<int64_t, int64_t>> m;
+    for (auto& x : r) {
+        if (!m.empty() && x.first <= m.back().second) m.back().second = std::max(m.back().second, x.second);
+        else m.push_back(x);
+    }
+    *nr = (int32_t)m.size();
+    if ((int64_t)m.size() > cap) return fail(nullptr, HD_E_NOMEM, "hd_zap_ranges: %zu ranges > cap %d", m.size(), cap);
+    for (size_t k = 0; k < m.size(); k++) {
+        const int64_t lo = m[k].first, hi = m[k].second;
+        const int64_t side = std::min<int64_t>(std::max<int64_t>(50, hi - lo), 2048);
+        rng4[4 * k + 0] = (int32_t)lo;
+        rng4[4 * k + 1] = (int32_t)hi;
+        rng4[4 * k + 2] = (int32_t)std::max<int64_t>(1, lo - side);
+        rng4[4 * k + 3] = (int32_t)std::min<int64_t>(numbins, hi + side);
+    }
+    return HD_OK;
+}
+
+extern "C" int hd_zapbirds(hd_plan* p, const double* lobins, const double* hibins, int32_t n)
+{
+    if (!p) return fail(nullptr, HD_E_INVAL, "hd_zapbirds: NULL plan");
+    hd_ctx* c = p->ctx;
+    if (!p->ran_fft) return fail(c, HD_E_STATE, "hd_zapbirds: run hd_realfft first");
+    const int64_t nb = p->numout / 2;
+    if (nb > INT32_MAX) return fail(c, HD_E_INVAL, "hd_zapbirds: spectrum beyond 2^31 bins");
+    int32_t nr = 0;
+    int rc = hd_zap_ranges(lobins, hibins, n, nb, nullptr, 0, &nr);
+    if (rc && rc != HD_E_NOMEM) return fail(c, rc, "hd_zapbirds: %s", g_err.c_str());
+    std::vector<int32_t> rng((size_t)4 * std::max(nr, 1));
+    rc = hd_zap_ranges(lobins, hibins, n, nb, rng.data(), nr, &nr);
+    if (rc) return fail(c, rc, "hd_zapbirds: %s", g_err.c_str());
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t st = p->dd_stream ? p->dd_stream : c->stream;
+    HIPCHK(c, hd::fft_zap(p->fft, rng.data(), nr, st));
+    return HD_OK;
+}
+
+extern "C" int hd_rednoise_blocks(int64_t numbins, double T, int32_t startwidth, int32_t endwidth, double endfreq,
+                                  int32_t* boff, int32_t cap, int32_t* nblk)
+{
+    if (!nblk || numbins < 2 || !(T > 0.0) || startwidth < 1 || endwidth < startwidth || endwidth > 128 ||
+        !(endfreq > 0.0) || (cap > 0 && !boff) || numbins > INT32_MAX)
+        return fail(nullptr, HD_E_INVAL, "hd_rednoise_blocks: bad argument");
+    const double lg = std::log(1.0 + endfreq);
+    int64_t o = 1;
+    int32_t k = 0;
+    while (o < numbins) {
+        const double f = (double)o / T;
+        int64_t w = endwidth;
+        if (f < endfreq) w = startwidth + (int64_t)std::floor((double)(endwidth - startwidth) * std::log(1.0 + f) / lg);
+        if (k < cap) boff[k] = (int32_t)o;
+        k++;
+        o = std::min(numbins, o + w);
+    }
+    if (k < cap) boff[k] = (int32_t)numbins;
+    *nblk = k;
+    if (k + 1 > cap) return fail(nullptr, HD_E_NOMEM, "hd_rednoise_blocks: %d offsets > cap %d", k + 1, cap);
+    return HD_OK;
+}
+
+extern "C" int hd_rednoise(hd_plan* p, int32_t startwidth, int32_t endwidth, double endfreq, double T)
+{
+    if (!p) return fail(nullptr, HD_E_INVAL, "hd_rednoise: NULL plan");
+    hd_ctx* c = p->ctx;
+    if (!p->ran_fft) return fail(c, HD_E_STATE, "hd_rednoise: run hd_realfft first");
+    const int64_t nb = p->numout / 2;
+    int32_t nblk = 0;
+    int rc = hd_rednoise_blocks(nb, T, startwidth, endwidth, endfreq, nullptr, 0, &nblk);
+    if (rc && rc != HD_E_NOMEM) return fail(c, rc, "hd_rednoise: %s", g_err.c_str());
+    std::vector<int32_t> boff((size_t)nblk + 1);
+    rc = hd_rednoise_blocks(nb, T, startwidth, endwidth, endfreq, boff.data(), nblk + 1, &nblk);
+    if (rc) return fail(c, rc, "hd_rednoise: %s", g_err.c_str());
+    std::vector<double> cen((size_t)nblk);
+    for (int32_t j = 0; j < nblk; j++) cen[j] = (double)boff[j] + (double)(boff[j + 1] - boff[j] - 1) / 2.0;
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t st = p->dd_stream ? p->dd_stream : c->stream;
+    HIPCHK(c, hd::fft_rednoise(p->fft, boff.data(), cen.data(), nblk, st));
+    return HD_OK;
+}
+
+extern "C" int hd_get_fft(hd_plan* p, int32_t dm0, int32_t ndm, float* out)
+{
+    if (!p || !out) return fail(p ? p->ctx : nullptr, HD_E_INVAL, "hd_get_fft: NULL argument");
+    hd_ctx* c = p->ctx;
+    if (!p->ran_fft) return fail(c, HD_E_STATE, "hd_get_fft: run hd_realfft first");
+    if (dm0 < 0 || ndm < 1 || dm0 + ndm > p->pass.numdms) return fail(c, HD_E_INVAL, "hd_get_fft: bad DM range");
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t st = p->dd_stream ? p->dd_stream : c->stream;
+    const int64_t fs = p->numout / 2 + 1;
+    HIPCHK(c, d2h_2d(out, sizeof(float) * p->numout, hd::fft_buffer(p->fft) + (size_t)dm0 * fs,
+                     sizeof(float2) * fs, sizeof(float) * p->numout, ndm, st));
     return HD_OK;
 }

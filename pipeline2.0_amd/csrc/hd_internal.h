@@ -176,6 +176,14 @@ hipError_t launch_sp_hits(const float* x, int64_t stride, int ndm, int nblocks, 
 // rfifind statistics (hd_rfi.hip): per interval and channel mean, std, max normalised power
 hipError_t rfi_stats(const RawDesc& rd, const uint8_t* rawT, int64_t tstride, int ptsperint, int numint, float* avg,
                      float* sd, float* pw, hipStream_t st);
+// realfft / zapbirds / rednoise of a plan's series (hd_fft.hip)
+struct FftState;
+FftState* fft_state_new();
+void fft_state_free(FftState* s);
+float2* fft_buffer(FftState* s);
+hipError_t fft_series(FftState* s, const float* x, int64_t xstride, int64_t n, int ndm, hipStream_t st);
+hipError_t fft_zap(FftState* s, const int32_t* rng4, int nr, hipStream_t st);
+hipError_t fft_rednoise(FftState* s, const int32_t* boff, const double* cen, int nblk, hipStream_t st);
 constexpr int64_t kRawTPad = 65536;   // zero rows after N in each channel-major raw row
 hipError_t launch_raw_transpose(const uint8_t* raw, int64_t N, int32_t nchan, int nbits, int nibble_hi_first,
                                 uint8_t* rawT, int64_t tstride, hipStream_t st);

@@ -40,6 +40,7 @@ EXPORTED = [
     "hd_get_subbands_window", "hd_get_series", "hd_write_series", "hd_wait_writes",
     "hd_set_slice", "hd_clip_stats", "hd_clip_set_stats", "hd_series_sum", "hd_series_fill",
     "hd_sp_widths", "hd_single_pulse", "hd_rfifind_stats",
+    "hd_realfft", "hd_zap_ranges", "hd_zapbirds", "hd_rednoise_blocks", "hd_rednoise", "hd_get_fft",
 ]
 
 
@@ -154,6 +155,14 @@ def load():
         "hd_series_sum": (ctypes.c_int, [vp, i32, i64, i64, P(ctypes.c_double)]),
         "hd_series_fill": (ctypes.c_int, [vp, i64, ctypes.c_float]),
         "hd_rfifind_stats": (ctypes.c_int, [vp, i32, f32p, f32p, f32p]),
+        "hd_realfft": (ctypes.c_int, [vp]),
+        "hd_zap_ranges": (ctypes.c_int, [P(ctypes.c_double), P(ctypes.c_double), i32, i64, P(ctypes.c_int32), i32,
+                                         P(ctypes.c_int32)]),
+        "hd_zapbirds": (ctypes.c_int, [vp, P(ctypes.c_double), P(ctypes.c_double), i32]),
+        "hd_rednoise_blocks": (ctypes.c_int, [i64, ctypes.c_double, i32, i32, ctypes.c_double, P(ctypes.c_int32), i32,
+                                              P(ctypes.c_int32)]),
+        "hd_rednoise": (ctypes.c_int, [vp, i32, i32, ctypes.c_double, ctypes.c_double]),
+        "hd_get_fft": (ctypes.c_int, [vp, i32, i32, f32p]),
         "hd_sp_widths": (ctypes.c_int, [ctypes.c_double, ctypes.c_double, P(ctypes.c_int32), P(ctypes.c_int32)]),
         "hd_single_pulse": (ctypes.c_int, [vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp, i64, P(i64),
                                            P(ctypes.c_uint8), P(i64)]),

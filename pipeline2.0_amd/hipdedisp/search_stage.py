@@ -65,6 +65,7 @@ class DedispJob:
         self.subbanding_time = 0.0
         self.dedispersing_time = 0.0
         self.singlepulse_time = 0.0     # :539-546 on device (run_pass(single_pulse=...))
+        self.FFT_time = 0.0             # :548-558 on device (run_pass(fft=...))
         self.ddplans = P.ddplans_for(self.backend)
         self.tempdir = tempfile.mkdtemp(suffix="_tmp", prefix=self.basefilenm,
                                         dir=tmpdir_base or ("/dev/shm" if os.path.isdir("/dev/shm") else None))
@@ -148,15 +149,23 @@ def _single_pulse(job, plan, ddplan, passnum, tempdir, sp):
     job.singlepulse_time = getattr(job, "singlepulse_time", 0.0) + t
 
 
-def run_pass(job, ddplan, passnum, maskfilenm, tempdir, single_pulse=None):
+def _fft(job, plan, ddplan, passnum, tempdir, fft):
+    """:548-558 (realfft, zapbirds, rednoise) for the pass's DMs on the device (hipdedisp.fft_stage);
+    adds to job.FFT_time."""
+    from .fft_stage import fft_pass
+    fft_pass(job, plan, ddplan, passnum, tempdir, fft)
+
+
+def run_pass(job, ddplan, passnum, maskfilenm, tempdir, single_pulse=None, fft=None):
     """PALFA2_presto_search.py:498-529 for one pass: subbands (stage 1) then the DM sweep
     (stage 2); writes <tempdir>/<base>_DM<dm>.dat/.inf; returns (t_sub, t_dd).  Without
     subbands (:522-529) the reference makes one prepsubband call, timed as dedispersing
     time only: t_sub is 0 and the whole pass goes to t_dd.  single_pulse (a dict of
     maxwidth / threshold / workdir, config.searching's singlepulse_*) also runs :539-546 on
-    the series while they are in HBM."""
+    the series while they are in HBM; fft (a dict of zaplist / baryv / write) then runs
+    :548-558 on them."""
     if not job.use_subbands:
-        return _run_pass_nosub(job, ddplan, passnum, maskfilenm, tempdir, single_pulse)
+        return _run_pass_nosub(job, ddplan, passnum, maskfilenm, tempdir, single_pulse, fft)
     subbasenm = "%s_DM%s" % (job.basefilenm, ddplan.subdmlist[passnum])
     eng = job.open_engine()
     job.load_mask(maskfilenm)
@@ -179,6 +188,8 @@ def run_pass(job, ddplan, passnum, maskfilenm, tempdir, single_pulse=None):
         t_dd = time.time() - t0
         if single_pulse is not None:
             _single_pulse(job, plan, ddplan, passnum, tempdir, single_pulse)
+        if fft is not None:
+            _fft(job, plan, ddplan, passnum, tempdir, fft)
     finally:
         plan.destroy()
     job.subbanding_time += t_sub
@@ -186,7 +197,7 @@ def run_pass(job, ddplan, passnum, maskfilenm, tempdir, single_pulse=None):
     return t_sub, t_dd
 
 
-def _run_pass_nosub(job, ddplan, passnum, maskfilenm, tempdir, single_pulse=None):
+def _run_pass_nosub(job, ddplan, passnum, maskfilenm, tempdir, single_pulse=None, fft=None):
     """PALFA2_presto_search.py:522-529: `prepsubband -mask M -lodm -dmstep -numdms -downsamp
     (dd*sub) -numout N` straight on the raw data: channels (downsampled, float32) are the
     subbands of a nsub = nchan pass."""
@@ -203,20 +214,22 @@ def _run_pass_nosub(job, ddplan, passnum, maskfilenm, tempdir, single_pulse=None
         t_dd = time.time() - t0
         if single_pulse is not None:
             _single_pulse(job, plan, ddplan, passnum, tempdir, single_pulse)
+        if fft is not None:
+            _fft(job, plan, ddplan, passnum, tempdir, fft)
     finally:
         plan.destroy()
     job.dedispersing_time += t_dd
     return 0.0, t_dd
 
 
-def dedisperse_job(job, maskfilenm=None, per_dm=None, remove_dat=False, single_pulse=None):
+def dedisperse_job(job, maskfilenm=None, per_dm=None, remove_dat=False, single_pulse=None, fft=None):
     """The loop of PALFA2_presto_search.py:494-537: every pass of every DDplan stage (with
     the device single-pulse search of :539-546 when single_pulse is given), then
     `per_dm(job, dmstr, basenm)` for each new DM (the reference's downstream tools)."""
     dmstrs = []
     for ddplan in job.ddplans:
         for passnum in range(ddplan.numpasses):
-            run_pass(job, ddplan, passnum, maskfilenm, job.tempdir, single_pulse)
+            run_pass(job, ddplan, passnum, maskfilenm, job.tempdir, single_pulse, fft)
             for dmstr in ddplan.dmlist[passnum]:
                 dmstrs.append(dmstr)
                 basenm = os.path.join(job.tempdir, job.basefilenm + "_DM" + dmstr)

@@ -1,0 +1,105 @@
+"""CPU checks of the realfft/zapbirds/rednoise row: the library's host layouts
+(hd_zap_ranges, hd_rednoise_blocks) equal the oracle's independent restatement, the zaplist
+reader follows PRESTO's format, and the oracle's numeric steps behave as the tools are meant
+to (white noise normalised to unit mean power, a red-noise slope flattened, birdies replaced
+by the local level).  Parity with PRESTO itself is unpinned (not in this image)."""
+import math
+
+import numpy as np
+import pytest
+
+import fft_oracle as FO
+from hipdedisp import PrestoError
+from hipdedisp import fft_stage as FS
+
+ZAPLIST = """# This file created automatically with makebirds.py
+# Lines beginning with '#' are comments
+# Lines beginning with 'B' are barycentric freqs (i.e. PSR freqs)
+#                 Freq                 Width
+# --------------------  --------------------
+            0.07618684                 0.003
+            0.08317989                 0.004
+
+           60.0                         0.5
+B          29.946923                    0.02
+"""
+
+
+def test_read_zaplist(tmp_path):
+    p = tmp_path / "t.zaplist"
+    p.write_text(ZAPLIST)
+    birds = FS.read_zaplist(str(p))
+    assert birds == [(0.07618684, 0.003, False), (0.08317989, 0.004, False), (60.0, 0.5, False),
+                     (29.946923, 0.02, True)]
+    lo, hi = FS.birdie_bins(birds, 100.0, baryv=1e-4)
+    assert lo[2] == pytest.approx(5975.0) and hi[2] == pytest.approx(6025.0)
+    f = 29.946923 / (1 + 1e-4)
+    assert lo[3] == pytest.approx((f - 0.01) * 100.0) and hi[3] == pytest.approx((f + 0.01) * 100.0)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_zap_ranges_match_oracle(seed):
+    rng = np.random.default_rng(seed)
+    nb = 50000
+    c = rng.uniform(-10, nb + 10, 300)
+    w = rng.exponential(3.0, 300)
+    lo, hi = c - w, c + w
+    lo[:5], hi[:5] = hi[:5], lo[:5]                      # reversed: dropped
+    lo[5], hi[5] = 100.0, 100.0                          # empty after floor/ceil? [100, 100) dropped
+    lo[6], hi[6] = 4000.0, 9000.0                        # wide: window side capped at 2048
+    got = FS.zap_ranges(lo, hi, nb)
+    want = FO.zap_ranges(lo, hi, nb)
+    assert np.array_equal(got, want)
+    assert np.all(got[1:, 0] > got[:-1, 1])              # merged: disjoint, not touching
+    assert np.all((got[:, 0] >= 1) & (got[:, 1] <= nb))
+
+
+def test_zap_ranges_empty():
+    assert FS.zap_ranges([], [], 1000).shape == (0, 4)
+
+
+@pytest.mark.parametrize("numbins,T", [(1 << 21, 274.9), (5000, 10.0), (300000, 1e4), (10, 1.0)])
+def test_rednoise_blocks_match_oracle(numbins, T):
+    got = FS.rednoise_blocks(numbins, T)
+    want = FO.rednoise_blocks(numbins, T)
+    assert np.array_equal(got, want)
+    w = np.diff(got)
+    assert got[0] == 1 and got[-1] == numbins and np.all(w >= 1) and np.all(w <= 100)
+    assert np.all(np.diff(w[:-1]) >= 0)                  # widths never shrink (but the last)
+
+
+def test_rednoise_blocks_rejects():
+    with pytest.raises(PrestoError):
+        FS.rednoise_blocks(1000, 10.0, endwidth=200)
+    with pytest.raises(PrestoError):
+        FS.rednoise_blocks(1000, 0.0)
+
+
+def test_oracle_rednoise_normalises():
+    rng = np.random.default_rng(3)
+    n = 1 << 18
+    T = n * 1e-3
+    f = np.arange(n // 2) / T
+    red = 1.0 + 50.0 / (1.0 + f) ** 1.5                  # red power spectrum
+    z = (rng.normal(size=n // 2) + 1j * rng.normal(size=n // 2)) * np.sqrt(red / 2)
+    F = z.astype(np.complex64)[None, :]
+    G = FO.rednoise(F, FO.rednoise_blocks(n // 2, T))
+    p = np.abs(G[0, 1:].astype(np.complex128)) ** 2
+    assert G[0, 0] == 1.0
+    for a, b in ((1, 200), (200, 5000), (5000, n // 2)):   # unit mean power everywhere
+        assert p[a:b].mean() == pytest.approx(1.0, abs=0.15)
+
+
+def test_oracle_zap_replaces_birdie():
+    rng = np.random.default_rng(4)
+    nb = 20000
+    z = (rng.normal(size=nb) + 1j * rng.normal(size=nb)).astype(np.complex64)
+    z[7000:7003] = 500.0
+    r = FO.zap_ranges([6999.5], [7002.5], nb)
+    assert r.tolist() == [[6999, 7003, 6949, 7053]]
+    G = FO.zap(z[None, :], r)
+    p = np.abs(z.astype(np.complex128)) ** 2
+    w = np.concatenate([p[6949:6999], p[7003:7053]])
+    a = np.float32(math.sqrt(np.sort(w)[(len(w) - 1) // 2] / math.log(2)))
+    assert np.all(G[0, 6999:7003] == a) and np.array_equal(G[0, :6999], z[:6999])
+    assert np.array_equal(G[0, 7003:], z[7003:])

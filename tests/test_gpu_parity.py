@@ -591,9 +591,10 @@ def test_search_stage_dedisperse_job(engine, tmp_path, use_subbands):
     spdir = tmp_path / "sp"
     spdir.mkdir()
     try:
-        dmstrs = dedisperse_job(job, single_pulse=dict(maxwidth=0.1, threshold=5.0, workdir=str(spdir)))
+        dmstrs = dedisperse_job(job, single_pulse=dict(maxwidth=0.1, threshold=5.0, workdir=str(spdir)),
+                                fft=dict(zaplist=None, baryv=0.0, write=True))
         assert len(dmstrs) == sum(d.dmsperpass for d in ddplans)
-        assert job.singlepulse_time > 0
+        assert job.singlepulse_time > 0 and job.FFT_time > 0
         sobs = job.specinfo.obs_params(0.0)
         for d in ddplans:
             pp = pass_params(job, d, 0)
@@ -607,6 +608,9 @@ def test_search_stage_dedisperse_job(engine, tmp_path, use_subbands):
                 np.testing.assert_allclose(got[nds:], want[k, nds:], rtol=REL_TOL, atol=0)
                 inf = read_inf(base + ".inf")
                 assert inf.N == got.size and "%.2f" % inf.dm == dmstr
+                # :548-558: the packed, de-reddened spectrum of the same series
+                spec = np.fromfile(base + ".fft", np.float32)
+                assert spec.size == got.size and spec[0] == 1.0 and spec[1] == 0.0
                 # :539-546: <base>_DM<dm>.singlepulse in the work dir, equal to the oracle's
                 # single_pulse_search restatement over the .dat just written
                 wl = OR.sp_widths(inf.dt, 0.1)
