@@ -210,6 +210,19 @@ typedef struct {
 } hd_rows_src;
 HD_API int hd_push_raw_file(hd_ctx* ctx, const char* path, const hd_rows_src* src, int64_t start,
                             double* io_seconds, double* total_seconds);
+/* Mock ingest in-stream (replaces `combine_mocks <s0> <s1> -o <base>` + `fitsdelrow
+ * <base>_0001.fits[SUBINT] 1 7`, lib/python/datafile.py:494-508): rows of one band's file
+ * whose spectra are spec_bytes long; bytes [src_offset, src_offset + nbytes) of each land at
+ * bytes [dst_offset, dst_offset + nbytes) of device spectrum start + k (the merged row), so
+ * the two halves fill their channel ranges of one raw block with no merged file written.
+ * src->row0 = 7 skips the rows fitsdelrow deletes.                                        */
+HD_API int hd_push_raw_file_band(hd_ctx* ctx, const char* path, const hd_rows_src* src, int64_t start,
+                                 int64_t spec_bytes, int64_t src_offset, int64_t dst_offset, int64_t nbytes,
+                                 double* io_seconds, double* total_seconds);
+/* Spectra [start, start + count) of the raw block set to byte_value in every byte: the
+ * padding between PSRFITS files that start later than the previous one ends
+ * (lib/python/formats/psrfits.py:272-280).                                                */
+HD_API int hd_fill_raw(hd_ctx* ctx, int64_t start, int64_t count, int32_t byte_value);
 /* Fill the device raw block with the synthetic beam (bit-identical to hd_synth_host). */
 HD_API int hd_synth_device(hd_ctx* ctx, const hd_synth* s);
 /* Host generator: spectra [start, start+count) of the same beam into out (file layout).

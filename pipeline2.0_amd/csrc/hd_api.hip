@@ -664,8 +664,11 @@ static int read_full(int fd, void* dst, size_t n, off_t off)
     return 0;
 }
 
-extern "C" int hd_push_raw_file(hd_ctx* c, const char* path, const hd_rows_src* src, int64_t start,
-                                double* io_seconds, double* total_seconds)
+// Spectra of a file whose spectrum is sb bytes: bytes [soff, soff + nb) of each go to bytes
+// [doff, doff + nb) of device spectrum start + k (sb == rowbytes, soff = doff = 0, nb = sb:
+// the whole spectrum, hd_push_raw_file).
+static int push_raw_file_impl(hd_ctx* c, const char* path, const hd_rows_src* src, int64_t start, int64_t sb,
+                              int64_t soff, int64_t doff, int64_t nb, double* io_seconds, double* total_seconds)
 {
     using clk = std::chrono::steady_clock;
     const auto t_all = clk::now();
@@ -673,11 +676,15 @@ extern "C" int hd_push_raw_file(hd_ctx* c, const char* path, const hd_rows_src* 
     if (!c->have_obs) return fail(c, HD_E_STATE, "hd_push_raw_file before hd_set_obs");
     if (!path || !src) return fail(c, HD_E_INVAL, "hd_push_raw_file: NULL argument");
     const int64_t rb = c->rowbytes;
-    if (src->col_bytes <= 0 || src->col_bytes % rb || src->row_bytes < src->col_offset + src->col_bytes ||
+    if (sb <= 0 || src->col_bytes <= 0 || src->col_bytes % sb || src->row_bytes < src->col_offset + src->col_bytes ||
         src->row0 < 0 || src->nrows < 0 || src->table_offset < 0)
         return fail(c, HD_E_INVAL, "hd_push_raw_file: DATA column of %lld bytes is not whole spectra of %lld bytes "
-                    "(or bad row geometry)", (long long)src->col_bytes, (long long)rb);
-    const int64_t spr = src->col_bytes / rb;   // spectra per row (NSBLK)
+                    "(or bad row geometry)", (long long)src->col_bytes, (long long)sb);
+    if (soff < 0 || nb <= 0 || soff + nb > sb || doff < 0 || doff + nb > rb)
+        return fail(c, HD_E_INVAL, "hd_push_raw_file_band: bytes [%lld, %lld) of %lld-byte spectra into [%lld, %lld) "
+                    "of %lld-byte spectra", (long long)soff, (long long)(soff + nb), (long long)sb, (long long)doff,
+                    (long long)(doff + nb), (long long)rb);
+    const int64_t spr = src->col_bytes / sb;   // spectra per row (NSBLK)
     if (start < 0 || start + src->nrows * spr > c->obs.N)
         return fail(c, HD_E_INVAL, "hd_push_raw_file: spectra [%lld, %lld) outside [0, %lld)", (long long)start,
                     (long long)(start + src->nrows * spr), (long long)c->obs.N);
@@ -720,8 +727,13 @@ extern "C" int hd_push_raw_file(hd_ctx* c, const char* path, const hd_rows_src* 
         }
         io += std::chrono::duration<double>(clk::now() - t0).count();
         if (err) break;
-        if (hipMemcpyAsync(c->d_raw + (size_t)(start + r * spr) * rb, dst, (size_t)(nr * src->col_bytes),
-                           hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        const hipError_t ce =
+            (sb == rb && nb == rb)
+                ? hipMemcpyAsync(c->d_raw + (size_t)(start + r * spr) * rb, dst, (size_t)(nr * src->col_bytes),
+                                 hipMemcpyHostToDevice, c->stream)
+                : hipMemcpy2DAsync(c->d_raw + (size_t)(start + r * spr) * rb + doff, (size_t)rb, dst + soff,
+                                   (size_t)sb, (size_t)nb, (size_t)(nr * spr), hipMemcpyHostToDevice, c->stream);
+        if (ce != hipSuccess ||
             hipEventRecord(c->pin_ev[b], c->stream) != hipSuccess) {
             err = HD_E_HIP;
             break;
@@ -738,6 +750,43 @@ extern "C" int hd_push_raw_file(hd_ctx* c, const char* path, const hd_rows_src* 
     c->clip.stats_valid = false;
     if (io_seconds) *io_seconds = io;
     if (total_seconds) *total_seconds = std::chrono::duration<double>(clk::now() - t_all).count();
+    return HD_OK;
+}
+
+extern "C" int hd_push_raw_file(hd_ctx* c, const char* path, const hd_rows_src* src, int64_t start,
+                                double* io_seconds, double* total_seconds)
+{
+    const int64_t rb = c ? c->rowbytes : 0;
+    return push_raw_file_impl(c, path, src, start, rb, 0, 0, rb, io_seconds, total_seconds);
+}
+
+extern "C" int hd_push_raw_file_band(hd_ctx* c, const char* path, const hd_rows_src* src, int64_t start,
+                                     int64_t spec_bytes, int64_t src_offset, int64_t dst_offset, int64_t nbytes,
+                                     double* io_seconds, double* total_seconds)
+{
+    return push_raw_file_impl(c, path, src, start, spec_bytes, src_offset, dst_offset, nbytes, io_seconds,
+                              total_seconds);
+}
+
+extern "C" int hd_fill_raw(hd_ctx* c, int64_t start, int64_t count, int32_t byte_value)
+{
+    if (!c) return fail(nullptr, HD_E_INVAL, "hd_fill_raw: NULL context");
+    if (!c->have_obs) return fail(c, HD_E_STATE, "hd_fill_raw before hd_set_obs");
+    if (start < 0 || count < 0 || start + count > c->obs.N || byte_value < 0 || byte_value > 255)
+        return fail(c, HD_E_INVAL, "hd_fill_raw: spectra [%lld, %lld) outside [0, %lld) or bad value",
+                    (long long)start, (long long)(start + count), (long long)c->obs.N);
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc = ensure_raw(c);
+    if (rc) return rc;
+    if (count) {
+        HIPCHK(c, hipMemsetAsync(c->d_raw + (size_t)start * c->rowbytes, byte_value, (size_t)count * c->rowbytes,
+                                 c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    c->raw_ready = true;
+    c->rawT_valid = false;
+    c->clip_valid = false;
+    c->clip.stats_valid = false;
     return HD_OK;
 }
 

@@ -40,6 +40,7 @@ EXPORTED = [
     "hd_get_subbands_window", "hd_get_series", "hd_write_series", "hd_wait_writes",
     "hd_set_slice", "hd_clip_stats", "hd_clip_set_stats", "hd_series_sum", "hd_series_fill",
     "hd_sp_widths", "hd_single_pulse", "hd_rfifind_stats",
+    "hd_push_raw_file_band", "hd_fill_raw",
     "hd_realfft", "hd_zap_ranges", "hd_zapbirds", "hd_rednoise_blocks", "hd_rednoise", "hd_get_fft",
 ]
 
@@ -149,6 +150,9 @@ def load():
         "hd_get_raw_device": (ctypes.c_int, [vp, vp, i64, i64]),
         "hd_push_raw_file": (ctypes.c_int, [vp, ctypes.c_char_p, P(hd_rows_src), i64, P(ctypes.c_double),
                                             P(ctypes.c_double)]),
+        "hd_push_raw_file_band": (ctypes.c_int, [vp, ctypes.c_char_p, P(hd_rows_src), i64, i64, i64, i64, i64,
+                                                 P(ctypes.c_double), P(ctypes.c_double)]),
+        "hd_fill_raw": (ctypes.c_int, [vp, i64, i64, i32]),
         "hd_set_slice": (ctypes.c_int, [vp, i64, i64]),
         "hd_clip_stats": (ctypes.c_int, [vp, i64, vp]),
         "hd_clip_set_stats": (ctypes.c_int, [vp, vp]),

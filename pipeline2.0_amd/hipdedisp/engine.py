@@ -231,6 +231,24 @@ class Engine:
                                            ctypes.byref(io), ctypes.byref(tot)), "hd_push_raw_file(%s)" % path)
         return io.value, tot.value
 
+    def push_raw_file_band(self, path, table_offset, row_bytes, col_offset, col_bytes, row0, nrows, start,
+                           spec_bytes, src_offset, dst_offset, nbytes, block_bytes=0):
+        """hd_push_raw_file_band: bytes [src_offset, +nbytes) of each spectrum (spec_bytes long) of
+        rows [row0, row0+nrows) into bytes [dst_offset, +nbytes) of device spectra [start, ...)."""
+        src = _lib.hd_rows_src(table_offset=int(table_offset), row_bytes=int(row_bytes), col_offset=int(col_offset),
+                               col_bytes=int(col_bytes), row0=int(row0), nrows=int(nrows),
+                               block_bytes=int(block_bytes))
+        io, tot = ctypes.c_double(), ctypes.c_double()
+        self._chk(self._L.hd_push_raw_file_band(self._ctx, os.fsencode(path), ctypes.byref(src), int(start),
+                                                int(spec_bytes), int(src_offset), int(dst_offset), int(nbytes),
+                                                ctypes.byref(io), ctypes.byref(tot)),
+                  "hd_push_raw_file_band(%s)" % path)
+        return io.value, tot.value
+
+    def fill_raw(self, start, count, byte_value=0):
+        """hd_fill_raw: spectra [start, start+count) set to byte_value (file-gap padding)."""
+        self._chk(self._L.hd_fill_raw(self._ctx, int(start), int(count), int(byte_value)), "hd_fill_raw")
+
     def push_raw_device(self, dev_ptr, start=0, count=None):
         """Raw spectra from device memory of this context's GPU (an int address, e.g. a
         torch tensor's data_ptr() after an RCCL broadcast)."""

@@ -279,21 +279,32 @@ class SpectraInfo:
     def obs_params(self, voverc=0.0):
         """Engine ObsParams for this observation."""
         from ..engine import ObsParams
-        if np.any(self.num_pad > 0):
-            raise ValueError("gaps between PSRFITS files (padding) are not supported yet")
         return ObsParams(nchan=int(self.num_channels), nbits=int(self.bits_per_sample), dt=float(self.dt),
                          lofreq=float(self.lo_freq), df=float(self.df), N=int(self.N),
                          nsblk=int(self.spectra_per_subint), flip=bool(self.need_flipband),
                          npol=int(self.num_polns) if not self.summed_polns else 1, voverc=voverc)
 
+    def gaps(self):
+        """[(start, count)] spectra of padding between files (psrfits.py:272-280): a file that
+        starts after the previous one ends leaves the gap, filled with zero bytes here (PRESTO
+        pads with the mask's pad values, 0 without a mask) [PRESTO-ext]."""
+        out = []
+        for ii in range(1, self.num_files):
+            end = int(self.start_spec[ii - 1]) + int(self.num_spec[ii - 1])
+            if int(self.start_spec[ii]) > end:
+                out.append((end, int(self.start_spec[ii]) - end))
+        return out
+
     def read_spectra(self):
-        """All raw spectra of all files: uint8 [N][nchan*nbits/8] in file order."""
-        parts = []
-        for fn, tab in zip(self.filenames, self._tables):
+        """All raw spectra of all files: uint8 [N][nchan*nbits/8] in file order, gaps zero."""
+        rb = self.num_channels * self.bits_per_sample // 8
+        out = np.zeros((int(self.N), rb), np.uint8)
+        for ii, (fn, tab) in enumerate(zip(self.filenames, self._tables)):
             mm = np.memmap(fn, dtype=np.uint8, mode="r")
-            data = tab.column_bytes(mm, "DATA")
-            parts.append(np.ascontiguousarray(data).reshape(-1, self.num_channels * self.bits_per_sample // 8))
-        return np.concatenate(parts) if len(parts) > 1 else parts[0]
+            data = np.ascontiguousarray(tab.column_bytes(mm, "DATA")).reshape(-1, rb)
+            s0 = int(self.start_spec[ii])
+            out[s0:s0 + data.shape[0]] = data
+        return out
 
     def stream_to(self, engine, block_bytes=0):
         """Stream every file's DATA column into the engine's device raw block through the
@@ -311,6 +322,8 @@ class SpectraInfo:
             io += a
             tot += b
             nbytes += col_bytes * tab.nrows
+        for start, count in self.gaps():
+            engine.fill_raw(start, count, 0)
         return io, tot, nbytes
 
     def read_calib(self):

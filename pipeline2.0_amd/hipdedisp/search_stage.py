@@ -27,6 +27,7 @@ import numpy as np
 from . import plan as P
 from .engine import Engine, Opts, PassParams, PrestoError
 from .formats import psrfits
+from .formats import mock
 from .formats.inf import InfoData
 from .formats.mask import mask_padvals, read_mask
 from .formats.series import write_dats_device, write_subbands
@@ -42,7 +43,13 @@ class DedispJob:
         self.outputdir = resultsdir
         base = os.path.split(self.filenms[0])[1]
         self.basefilenm = base[:-5] if base.endswith(".fits") else base
-        self.specinfo = psrfits.SpectraInfo(self.filenms)
+        if mock.is_complete(self.filenms):
+            # the two Mock halves: merged in-stream (datafile.py:474-508), named as the
+            # merged file the reference would have searched
+            self.specinfo = mock.MockBeam(self.filenms)
+            self.basefilenm = self.specinfo.basename
+        else:
+            self.specinfo = psrfits.SpectraInfo(self.filenms)
         si = self.specinfo
         self.backend = backend or si.backend
         self.MJD = si.start_MJD[0]
