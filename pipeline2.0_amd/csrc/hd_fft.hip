@@ -89,37 +89,41 @@ __global__ __launch_bounds__(256) void k_zap_apply(float2* __restrict__ F, int64
     for (int i = r.x + threadIdx.x; i < r.y; i += blockDim.x) f[i] = make_float2(a, 0.0f);
 }
 
-// One wave per (block, series): the lower median of the block's powers (width <= 128) by
-// rank counting over the block held in LDS (the wave's own stores, read back in order).
+// One wave per (block, series): the lower median of the block's powers (width <= 128): a
+// bitonic sort of 128 slots (+inf past the block) held two per lane (slot lane + 64 h),
+// cross-lane steps by __shfl_xor; the median is slot (n - 1) / 2.
 __global__ __launch_bounds__(256) void k_red_median(const float2* __restrict__ F, int64_t fstride,
                                                     const int32_t* __restrict__ boff, int nblk, int ndm,
                                                     double* __restrict__ med)
 {
-    __shared__ double v[4][128];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int j = blockIdx.x * 4 + w;
+    const int lane = threadIdx.x & 63;
+    const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int d = blockIdx.y;
     if (j >= nblk) return;
     const int o = boff[j], n = boff[j + 1] - o;
     const float2* f = F + (int64_t)d * fstride + o;
-    double* vv = v[w];
-    const double x0 = lane < n ? bin_power(f[lane]) : 0.0;
-    const double x1 = lane + 64 < n ? bin_power(f[lane + 64]) : 0.0;
-    vv[lane] = x0;
-    vv[lane + 64] = x1;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    const int k = (n - 1) / 2;
-    int lt0 = 0, eq0 = 0, lt1 = 0, eq1 = 0;
-    for (int i = 0; i < n; i++) {
-        const double y = vv[i];
-        lt0 += y < x0;
-        eq0 += y == x0;
-        lt1 += y < x1;
-        eq1 += y == x1;
+    double v0 = lane < n ? bin_power(f[lane]) : __builtin_inf();
+    double v1 = lane + 64 < n ? bin_power(f[lane + 64]) : __builtin_inf();
+#pragma unroll
+    for (int k = 2; k <= 128; k <<= 1) {
+#pragma unroll
+        for (int s = k >> 1; s > 0; s >>= 1) {
+            if (s == 64) {                                   // partner: the same lane's other slot
+                const bool up = (lane & k) == 0;             // k == 128: always ascending
+                const double lo = fmin(v0, v1), hi = fmax(v0, v1);
+                v0 = up ? lo : hi;
+                v1 = up ? hi : lo;
+            } else {
+                const bool first = (lane & s) == 0;
+                const bool up0 = (lane & k) == 0, up1 = ((lane + 64) & k) == 0;
+                const double p0 = __shfl_xor(v0, s, 64), p1 = __shfl_xor(v1, s, 64);
+                v0 = (first == up0) ? fmin(v0, p0) : fmax(v0, p0);
+                v1 = (first == up1) ? fmin(v1, p1) : fmax(v1, p1);
+            }
+        }
     }
-    if (lane < n && lt0 <= k && k < lt0 + eq0) med[(int64_t)d * nblk + j] = x0;
-    else if (lane + 64 < n && lt1 <= k && k < lt1 + eq1) med[(int64_t)d * nblk + j] = x1;
+    const int k = (n - 1) / 2;
+    if (lane == (k & 63)) med[(int64_t)d * nblk + j] = k < 64 ? v0 : v1;
 }
 
 // Block j of every series (one workgroup, <= 128 bins, a loop over the series): each bin

@@ -533,6 +533,14 @@ __device__ __forceinline__ void q8_store(const Stage1Multi& a, int p, int s, int
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+// Waves per subband in k_stage1_q8's summing phase: the block has max(4, sg) waves (the fill
+// wants at least 4); with sg < 4 the spare waves take a share of the passes (probe bit 4 of
+// hd_plan_set_variant's probe byte, value 16: one wave per subband, the spare waves idle).
+__host__ __device__ __forceinline__ int q8_waves_per_subband(const Stage1Multi& a)
+{
+    return (a.probe & 16) || a.sg >= 4 ? 1 : 4 / a.sg;
+}
+
 template <int CPS, int DS, int VB>
 __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
 {
@@ -662,8 +670,12 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
     }
     __syncthreads();
 
-    // ---- per-wave subband state (wave = subband)
-    const int sl = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // ---- per-wave subband state: wave w serves subband w / wps and passes p = w % wps (mod
+    //      wps), so every wave of the block (at least 4) sums: sg = 2 gives 2 waves per
+    //      subband instead of 2 summing waves and 2 that only fill
+    const int wps = q8_waves_per_subband(a);
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int sl = wv / wps, pw = wv - sl * wps;
     if (sl >= a.sg) return;                               // fill-only waves (no barrier follows)
     const int lane = threadIdx.x & 63;
     const int s = g * a.sg + sl;
@@ -753,12 +765,12 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
     // pass p is formed, so no global-load latency sits at the head of a pass
     // (unconditional, clamped loads: a branch around them would cost a vmcnt(0) drain)
     const int dlane = c0 + cl0 + min(lane, CPS - 1);
-    int vd = a.dly[0][dlane];
+    int vd = a.dly[min(pw, a.npass - 1)][dlane];
     int pmax = 0;                                         // lane p: max |subband| of pass p
 
     const int npass = (a.probe & 1) ? 0 : a.npass;
-    for (int p = 0; p < npass; p++) {
-        const int vd_next = a.dly[min(p + 1, a.npass - 1)][dlane];
+    for (int p = pw; p < npass; p += wps) {
+        const int vd_next = a.dly[min(p + wps, a.npass - 1)][dlane];
         int dl[CPS];
         int dmx = 0;
 #pragma unroll

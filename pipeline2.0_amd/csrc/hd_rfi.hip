@@ -13,6 +13,8 @@
 
 #include "hd_device.h"
 
+#pragma clang fp contract(off)   // products and sums rounded separately, as the oracle does
+
 namespace hd {
 
 __device__ __forceinline__ double rfi_wave_sum(double v)

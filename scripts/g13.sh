@@ -1,0 +1,6 @@
+cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_fft.py tests/test_gpu_rfifind.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/t13.log 2>&1 &&
+timeout -k 10 300 python scripts/fft_time.py > gpurun_out/fft13.log 2>&1 &&
+timeout -k 10 300 python scripts/rfi_time.py > gpurun_out/rfi13.log 2>&1 &&
+timeout -k 10 300 python scripts/ab_q8.py 8 > gpurun_out/ab13.log 2>&1 &&
+timeout -k 10 300 python scripts/ab_q8.py 4 >> gpurun_out/ab13.log 2>&1
