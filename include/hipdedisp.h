@@ -316,7 +316,8 @@ HD_API int hd_plan_last_ms(const hd_plan* plan, float* ms_subband, float* ms_ded
  * invalid; never set them in production): 1 skip the sums, 2 skip the LDS fill, 4 skip
  * the stage-2 stores, 8 skip the stage-2 expand, 32 skip the stage-1 fixup's block-boundary
  * items, 64 skip its clipped-spectrum items; 128 (valid results, for cross-checks) runs the
- * fixup with the generic per-cell kernel instead of the 8-bit LDS-window one.  Bits 24-25 schedule the pair kernel's
+ * fixup with the generic per-cell kernel instead of the 8-bit LDS-window one; 16 (valid
+ * results) keeps k_stage1_q8 at one summing wave per subband (its spare waves idle).  Bits 24-25 schedule the pair kernel's
  * tiles: 0 or 1 persistent workgroups (one per CU, each over a contiguous tile range; the
  * default), 2 one workgroup per tile.  s2 = 7: the pair kernel with two subband pairs per
  * chunk (half the chunks per tile; HD_E_INVAL when its LDS does not fit). */
