@@ -870,6 +870,11 @@ static size_t fix8_lds_bytes(const Stage1Multi& a, const Fix8Geom& g)
            (size_t)2 * ((a.npass * g.G + 7) & ~7) + (size_t)2 * a.npass * g.SG * 4;
 }
 
+// LDS budget of one k_stage1_fix8 workgroup: smaller windows per workgroup mean more of
+// them in flight on a CU, which this latency-bound kernel wants; measured over the C2 beam's
+// stages (profiles/r02_fix8_lds.txt): 24 KiB best, except at ds >= 10 (wide windows) 40 KiB.
+static size_t fix8_lds_cap(int ds) { return (size_t)(ds >= 10 ? 40 : 24) * 1024; }
+
 // Geometry for k_stage1_fix8, or false when it does not apply (the generic kernel then runs).
 static bool fix8_geom(const Stage1Multi& a, Fix8Geom& g)
 {
@@ -885,7 +890,7 @@ static bool fix8_geom(const Stage1Multi& a, Fix8Geom& g)
         Fix8Geom t = g;
         t.SG = sg;
         t.G = G;
-        if (fix8_lds_bytes(a, t) <= 40 * 1024) {
+        if (fix8_lds_bytes(a, t) <= fix8_lds_cap(a.ds)) {
             g.SG = sg;
             break;
         }
@@ -904,7 +909,12 @@ hipError_t launch_stage1_fixup(const Stage1Multi& a, const int32_t* events, cons
     Fix8Geom g;
     if (!(a.probe & 128) && fix8_geom(a, g)) {           // probe bit 7: the generic kernel
         const unsigned grid = (unsigned)(std::max(1, 4096 / g.nchunk) * g.nchunk);
-        hipLaunchKernelGGL(k_stage1_fix8, dim3(grid), dim3(256), fix8_lds_bytes(a, g), st, a, g, events, nevents,
+        const size_t lb = fix8_lds_bytes(a, g);
+        if (lb > 64 * 1024) {
+            const hipError_t e = set_max_lds((const void*)k_stage1_fix8, (int)lb);
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(k_stage1_fix8, dim3(grid), dim3(256), lb, st, a, g, events, nevents,
                            boundaries);
         return hipGetLastError();
     }

@@ -174,6 +174,7 @@ hipError_t launch_sp_hits(const float* x, int64_t stride, int ndm, int nblocks, 
                           const int32_t* widths, const double* rsw, int nwidths, double threshold, hd_sp_hit* hits,
                           unsigned long long* count, int64_t cap, hipStream_t st);
 // rfifind statistics (hd_rfi.hip): per interval and channel mean, std, max normalised power
+hipError_t set_max_lds(const void* fn, int bytes);
 hipError_t rfi_stats(const RawDesc& rd, const uint8_t* rawT, int64_t tstride, int ptsperint, int numint, float* avg,
                      float* sd, float* pw, hipStream_t st);
 // realfft / zapbirds / rednoise of a plan's series (hd_fft.hip)
