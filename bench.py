@@ -44,6 +44,10 @@ def parse():
                     help="beams run end to end (.dat/.inf files written) after the timed steps; 0 = skip")
     ap.add_argument("--sp-beams", type=int, default=1,
                     help="beams of single-pulse search (hd_single_pulse) timed after the steps; 0 = skip")
+    ap.add_argument("--fft-beams", type=int, default=1,
+                    help="beams of realfft + zapbirds + rednoise (hd_fft.hip) timed after the steps; 0 = skip")
+    ap.add_argument("--rfi-beams", type=int, default=1,
+                    help="beams of rfifind statistics + mask decisions (hd_rfi.hip) timed last; 0 = skip")
     ap.add_argument("--mode", choices=["beam", "slices", "shard"], default="beam",
                     help="beam: one beam per rank (weak scaling, configs[4]); slices: ONE beam cut into per-rank "
                          "time slices, every rank runs all 57 passes on its slice (strong, configs[2]; RCCL carries "
@@ -131,6 +135,57 @@ def single_pulse_leg(eng, stages, beams):
     return {"s_per_beam": s, "candidates_per_beam": ncand // beams,
             "note": "hd_single_pulse over the 57 passes' series in HBM (-m 0.1 -t 5.0): detrend, block stds, "
                     "boxcars, prune_related1 on the GPU; prune_related2 + border cases on the host; wall time"}
+
+
+def fft_leg(eng, stages, beams):
+    """realfft; zapbirds -zap; rednoise over every DM of the beam (PALFA2_presto_search.py:548-558)
+    on each pass's device-resident series: wall seconds per beam (a 60 Hz mains comb and the
+    PALFA zaplist's 0.0762 Hz family as birdies)."""
+    from hipdedisp import fft_stage as FS
+    birds = [(60.0 * k, 0.5, False) for k in range(1, 40)] + [(0.07618684 * k, 0.003, False) for k in range(1, 200)]
+    bins = {}
+
+    def beam():
+        for plans in stages:
+            for p in plans:
+                T = p.numout * p.sub_dt
+                FS.realfft(p)
+                if p.numout not in bins:
+                    bins[p.numout] = FS.birdie_bins(birds, T)
+                FS.zapbirds(p, *bins[p.numout])
+                FS.rednoise(p, T)
+        eng.sync()
+
+    t = time.perf_counter()
+    beam()                                        # hipFFT plans (rocFFT kernel builds) + spectra buffers
+    first = time.perf_counter() - t
+    t = time.perf_counter()
+    for _ in range(beams):
+        beam()
+    s = (time.perf_counter() - t) / beams
+    return {"s_per_beam": s, "first_beam_s": first,
+            "note": "hd_realfft + hd_zapbirds (238 birdies) + hd_rednoise over the 57 passes' series in HBM "
+                    "(spectra stay on the device); wall time with the plans' FFT state built (first_beam_s: "
+                    "including the hipFFT plan builds and buffer allocation)"}
+
+
+def rfifind_leg(eng, obs, beams):
+    """rfifind -time 2^15*64us (PALFA2_presto_search.py:482-490) on the beam in HBM: the device
+    statistics (clip_times, per-interval channel mean/std, max normalised FFT power) and the
+    host mask decisions; wall seconds per beam.  Clears the engine's mask (run last)."""
+    from hipdedisp import rfifind as RF
+    from hipdedisp.synth import rfifind_ptsperint
+    eng.set_mask()
+    pts = rfifind_ptsperint(obs.dt)
+    RF.device_stats(eng, pts)                     # the clip state for the unmasked block
+    eng.sync()
+    t = time.perf_counter()
+    for _ in range(beams):
+        avg, std, pw = RF.device_stats(eng, pts)
+        RF.make_mask(avg, std, pw, pts)
+    s = (time.perf_counter() - t) / beams
+    return {"s_per_beam": s, "intervals": int(avg.shape[0]), "ptsperint": pts,
+            "note": "hd_rfifind_stats + rfifind's mask decisions (host) for the beam; wall time"}
 
 
 def e2e_dir(need_bytes):
@@ -472,6 +527,10 @@ def main():
             line["end_to_end_samples_per_s"] = line["end_to_end"]["samples_per_s"]
     if not (shard or slices) and args.sp_beams > 0:
         line["single_pulse"] = single_pulse_leg(eng, stages, args.sp_beams)
+    if not (shard or slices) and args.fft_beams > 0:
+        line["fft_stage"] = fft_leg(eng, stages, args.fft_beams)
+    if not (shard or slices) and args.rfi_beams > 0:
+        line["rfifind"] = rfifind_leg(eng, obs, args.rfi_beams)
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(obs, synth, ddplans, args.cpu_seconds, mask, pts, pad, omp=False)
         line["cpu_baseline_openmp"] = cpu_baseline(obs, synth, ddplans, args.cpu_seconds, mask, pts, pad, omp=True)

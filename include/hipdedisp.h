@@ -368,7 +368,10 @@ HD_API int hd_single_pulse(hd_plan* plan, double dt, double maxwidth, double thr
  * PRESTO unpinned].  The spectra stay in HBM with the plan ([numdms][numout/2] complex,
  * PRESTO's packed .fft layout: bin 0 = (DC, Nyquist)); hd_get_fft copies them out.       */
 /* Forward real FFT (no normalisation) of the numout samples of every DM series (after
- * hd_run_dedisp; numout even).                                                           */
+ * hd_run_dedisp; numout even).  The hipFFT plan and spectra buffer belong to the context,
+ * one per series geometry (numout, numdms, stride), so consecutive passes of a DDplan stage
+ * reuse them: a later hd_realfft of another plan of the same geometry takes the buffer over,
+ * and hd_zapbirds / hd_rednoise / hd_get_fft of the earlier plan then fail with HD_E_STATE. */
 HD_API int hd_realfft(hd_plan* plan);
 /* Bin ranges [lo, hi) zapped for birdies lobins[i] .. hibins[i] (frequency * T, the
  * zaplist's freq -+ width/2): lo = floor(lobin), hi = ceil(hibin), clamped to

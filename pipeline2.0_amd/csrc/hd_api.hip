@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <cmath>
 #include <map>
+#include <tuple>
 #include <chrono>
 #include <string>
 #include <thread>
@@ -114,6 +115,10 @@ struct hd_ctx {
     double* d_partial2 = nullptr;
     size_t partial_bytes2 = 0;
     hd::Writer* writer = nullptr;   // .dat output path (hd_io.hip), opened on first use
+    // realfft state per series geometry (numout, numdms, stride): hipFFT plan + spectra
+    // buffer, shared by the plans of that geometry -- each pass's hd_realfft takes it over
+    // (the owner), so a beam builds 6 hipFFT plans, not 57
+    std::map<std::tuple<int64_t, int, int64_t>, hd::FftState*> fft_cache;
 };
 
 // main-stream work from here on runs after every stage-2 pass queued on stream2
@@ -179,7 +184,7 @@ struct hd_plan {
     bool copy_pending = false;
     bool ran_sub = false, ran_dd = false;
     hipStream_t dd_stream = nullptr;  // stream of the last hd_run_dedisp (its ev[3] marks the end)
-    hd::FftState* fft = nullptr;    // realfft / zapbirds / rednoise spectra (hd_fft.hip)
+    hd::FftState* fft = nullptr;    // realfft state (hd_fft.hip, from hd_ctx::fft_cache)
     bool ran_fft = false;
 };
 
@@ -367,6 +372,8 @@ extern "C" int hd_close(hd_ctx* c)
         if (c->pin_ev[b]) (void)hipEventDestroy(c->pin_ev[b]);
     }
     clear_special_cache(c);
+    for (auto& kv : c->fft_cache) hd::fft_state_free(kv.second);
+    c->fft_cache.clear();
     (void)hipStreamDestroy(c->stream);
     delete c;
     return HD_OK;
@@ -1023,7 +1030,7 @@ static void plan_free(hd_plan* p)
     }
     dfree(p->d_out);
     dfree(p->d_sub);
-    hd::fft_state_free(p->fft);
+    if (p->fft && hd::fft_owner(p->fft) == p) hd::fft_set_owner(p->fft, nullptr);   // the context owns it
     p->fft = nullptr;
     for (auto& e : p->ev)
         if (e) (void)hipEventDestroy(e);
@@ -2532,8 +2539,13 @@ extern "C" int hd_realfft(hd_plan* p)
     if (p->out_stride > INT32_MAX) return fail(c, HD_E_INVAL, "hd_realfft: series stride beyond 2^31");
     HIPCHK(c, hipSetDevice(c->device));
     hipStream_t st = p->dd_stream ? p->dd_stream : c->stream;
-    if (!p->fft) p->fft = hd::fft_state_new();
+    const auto key = std::make_tuple(p->numout, p->pass.numdms, p->out_stride);
+    hd::FftState*& st_fft = c->fft_cache[key];
+    if (!st_fft) st_fft = hd::fft_state_new();
+    p->fft = st_fft;
+    hd::fft_set_owner(p->fft, nullptr);            // (a failed transform leaves no owner)
     HIPCHK(c, hd::fft_series(p->fft, p->d_out, p->out_stride, p->numout, p->pass.numdms, st));
+    hd::fft_set_owner(p->fft, p);
     p->ran_fft = true;
     return HD_OK;
 }
@@ -2575,6 +2587,8 @@ extern "C" int hd_zapbirds(hd_plan* p, const double* lobins, const double* hibin
     if (!p) return fail(nullptr, HD_E_INVAL, "hd_zapbirds: NULL plan");
     hd_ctx* c = p->ctx;
     if (!p->ran_fft) return fail(c, HD_E_STATE, "hd_zapbirds: run hd_realfft first");
+    if (hd::fft_owner(p->fft) != p)
+        return fail(c, HD_E_STATE, "hd_zapbirds: the spectra were replaced by another plan's hd_realfft (same geometry)");
     const int64_t nb = p->numout / 2;
     if (nb > INT32_MAX) return fail(c, HD_E_INVAL, "hd_zapbirds: spectrum beyond 2^31 bins");
     int32_t nr = 0;
@@ -2617,6 +2631,8 @@ extern "C" int hd_rednoise(hd_plan* p, int32_t startwidth, int32_t endwidth, dou
     if (!p) return fail(nullptr, HD_E_INVAL, "hd_rednoise: NULL plan");
     hd_ctx* c = p->ctx;
     if (!p->ran_fft) return fail(c, HD_E_STATE, "hd_rednoise: run hd_realfft first");
+    if (hd::fft_owner(p->fft) != p)
+        return fail(c, HD_E_STATE, "hd_rednoise: the spectra were replaced by another plan's hd_realfft (same geometry)");
     const int64_t nb = p->numout / 2;
     int32_t nblk = 0;
     int rc = hd_rednoise_blocks(nb, T, startwidth, endwidth, endfreq, nullptr, 0, &nblk);
@@ -2637,6 +2653,8 @@ extern "C" int hd_get_fft(hd_plan* p, int32_t dm0, int32_t ndm, float* out)
     if (!p || !out) return fail(p ? p->ctx : nullptr, HD_E_INVAL, "hd_get_fft: NULL argument");
     hd_ctx* c = p->ctx;
     if (!p->ran_fft) return fail(c, HD_E_STATE, "hd_get_fft: run hd_realfft first");
+    if (hd::fft_owner(p->fft) != p)
+        return fail(c, HD_E_STATE, "hd_get_fft: the spectra were replaced by another plan's hd_realfft (same geometry)");
     if (dm0 < 0 || ndm < 1 || dm0 + ndm > p->pass.numdms) return fail(c, HD_E_INVAL, "hd_get_fft: bad DM range");
     HIPCHK(c, hipSetDevice(c->device));
     hipStream_t st = p->dd_stream ? p->dd_stream : c->stream;

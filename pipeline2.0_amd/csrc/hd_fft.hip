@@ -162,6 +162,7 @@ __global__ __launch_bounds__(128) void k_red_scale(float2* __restrict__ F, int64
 // ---- host side --------------------------------------------------------------------------
 
 struct FftState {
+    const void* owner = nullptr;    // the plan whose spectra d_fft holds (hd_api.hip)
     hipfftHandle plan = 0;
     bool have_plan = false;
     int64_t n = 0;
@@ -189,6 +190,11 @@ void fft_state_free(FftState* s)
 }
 
 float2* fft_buffer(FftState* s) { return s ? s->d_fft : nullptr; }
+const void* fft_owner(const FftState* s) { return s ? s->owner : nullptr; }
+void fft_set_owner(FftState* s, const void* owner)
+{
+    if (s) s->owner = owner;
+}
 
 hipError_t fft_series(FftState* s, const float* x, int64_t xstride, int64_t n, int ndm, hipStream_t st)
 {

@@ -182,6 +182,8 @@ struct FftState;
 FftState* fft_state_new();
 void fft_state_free(FftState* s);
 float2* fft_buffer(FftState* s);
+const void* fft_owner(const FftState* s);
+void fft_set_owner(FftState* s, const void* owner);
 hipError_t fft_series(FftState* s, const float* x, int64_t xstride, int64_t n, int ndm, hipStream_t st);
 hipError_t fft_zap(FftState* s, const int32_t* rng4, int nr, hipStream_t st);
 hipError_t fft_rednoise(FftState* s, const int32_t* boff, const double* cen, int nblk, hipStream_t st);

@@ -126,3 +126,29 @@ def test_fft_state_errors(engine, beam):
             FS.get_fft(p, 3, 2)
     finally:
         p.destroy()
+
+
+def test_fft_state_shared_per_geometry(engine, beam):
+    """Two passes of one geometry share the context's hipFFT plan and spectra buffer: the
+    second hd_realfft takes it over, the first plan's spectra calls then fail loudly."""
+    mk = lambda sd: PassParams(subdm=sd, lodm=sd - 5.0, dmstep=0.5, numdms=8, nsub=96, ds=3,
+                               numout=P.choose_N(beam.N / 3))
+    p1, p2 = engine.plan(mk(71.0)), engine.plan(mk(90.0))
+    try:
+        for p in (p1, p2):
+            p.run_subband()
+            p.run_dedisp(to_host=False)
+        FS.realfft(p1)
+        a = FS.get_fft(p1)
+        FS.realfft(p2)
+        with pytest.raises(PrestoError):
+            FS.get_fft(p1)
+        with pytest.raises(PrestoError):
+            FS.rednoise(p1, 10.0)
+        b = FS.get_fft(p2)
+        assert not np.array_equal(a, b)
+        FS.realfft(p1)                                    # and back
+        assert np.array_equal(FS.get_fft(p1), a)
+    finally:
+        p1.destroy()
+        p2.destroy()
