@@ -103,3 +103,13 @@ def test_oracle_zap_replaces_birdie():
     a = np.float32(math.sqrt(np.sort(w)[(len(w) - 1) // 2] / math.log(2)))
     assert np.all(G[0, 6999:7003] == a) and np.array_equal(G[0, :6999], z[:6999])
     assert np.array_equal(G[0, 7003:], z[7003:])
+
+
+def test_layout_edge_cases():
+    # a spectrum of 2 bins: one block of one bin
+    assert FS.rednoise_blocks(2, 1.0).tolist() == [1, 2]
+    assert np.array_equal(FS.rednoise_blocks(7, 0.5), FO.rednoise_blocks(7, 0.5))
+    # birdies wholly outside [1, numbins) or reversed vanish; one touching bin 0 is clamped
+    r = FS.zap_ranges([-5.0, 2000.0, 10.0, -0.4], [-1.0, 2100.0, 9.0, 2.5], 1000)
+    assert r.tolist() == [[1, 3, 1, 53]]
+    assert np.array_equal(r, FO.zap_ranges([-5.0, 2000.0, 10.0, -0.4], [-1.0, 2100.0, 9.0, 2.5], 1000))
