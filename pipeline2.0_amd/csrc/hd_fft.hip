@@ -126,9 +126,9 @@ __global__ __launch_bounds__(256) void k_red_median(const float2* __restrict__ F
     if (lane == (k & 63)) med[(int64_t)d * nblk + j] = k < 64 ? v0 : v1;
 }
 
-// Block j of every series (one workgroup, <= 128 bins, a loop over the series): each bin
-// scaled by 1 / sqrt(m / ln 2), m interpolated between the medians of the neighbouring block
-// centres cen[] (double).  Block 0's workgroup also sets bin 0 to (1, 0).
+// Block j (blockIdx.x, <= 128 bins) of series blockIdx.y: each bin scaled by
+// 1 / sqrt(m / ln 2), m interpolated between the medians of the neighbouring block centres
+// cen[] (double).  Block 0's workgroup also sets bin 0 to (1, 0).
 __global__ __launch_bounds__(128) void k_red_scale(float2* __restrict__ F, int64_t fstride,
                                                    const int32_t* __restrict__ boff, const double* __restrict__ cen,
                                                    int nblk, int ndm, const double* __restrict__ med)
@@ -140,10 +140,11 @@ __global__ __launch_bounds__(128) void k_red_scale(float2* __restrict__ F, int64
     const double c = cen[j];
     const bool left = (double)i < c;
     const int ja = left ? j - 1 : j, jb = left ? j : j + 1;
-    for (int d = 0; d < ndm; d++) {
+    {
+        const int d = blockIdx.y;
         float2* f = F + (int64_t)d * fstride;
         if (j == 0 && t == 0) f[0] = make_float2(1.0f, 0.0f);
-        if (t >= n) continue;
+        if (t >= n) return;
         const double* m = med + (int64_t)d * nblk;
         double mi;
         if (ja < 0) mi = m[0];
@@ -265,8 +266,8 @@ hipError_t fft_rednoise(FftState* s, const int32_t* boff, const double* cen, int
     const int64_t fs = s->n / 2 + 1;
     hipLaunchKernelGGL(k_red_median, dim3((nblk + 3) / 4, s->ndm), dim3(256), 0, st, s->d_fft, fs, s->d_boff, nblk,
                        s->ndm, s->d_med);
-    hipLaunchKernelGGL(k_red_scale, dim3(nblk), dim3(128), 0, st, s->d_fft, fs, s->d_boff, s->d_cen, nblk, s->ndm,
-                       s->d_med);
+    hipLaunchKernelGGL(k_red_scale, dim3(nblk, s->ndm), dim3(128), 0, st, s->d_fft, fs, s->d_boff, s->d_cen, nblk,
+                       s->ndm, s->d_med);
     return hipGetLastError();
 }
 
