@@ -269,32 +269,57 @@ __global__ __launch_bounds__(256) void k_clip_chan_u4(ClipArgs a)
 }
 
 // ---- the serial recurrence over blocks (one workgroup, thread = channel) -------------
-__global__ __launch_bounds__(1024) void k_clip_recur(ClipArgs a)
+// One thread per channel, spread over single-wave workgroups on as many CUs: the recurrence
+// is serial over blocks and issue-bound in double precision, so one 1024-thread workgroup on
+// one CU ran it 16 waves deep on 4 SIMDs.  Every thread carries the (channel-independent)
+// running avg / std itself; thread 0 of workgroup 0 publishes them.
+__global__ __launch_bounds__(64) void k_clip_recur(ClipArgs a)
 {
     const int nch = a.rd.nchan;
     const float clip_sigma = a.clip_sigma;
     const int nloop = nch > 0 ? nch : 1;
     constexpr int U = 8;                                // chansum loads in flight per thread
-    for (int c0 = 0; c0 < nloop; c0 += blockDim.x) {
+    for (int c0 = blockIdx.x * blockDim.x; c0 < nloop; c0 += gridDim.x * blockDim.x) {
         const int c = c0 + threadIdx.x;
         const bool own = c < nch;
         float ravg = 0.0f, rstd = 0.0f, cra = 0.0f;
         float lev = own && a.padvals0 ? a.padvals0[c] : 0.0f;
         int nread = 0;
-        for (int b8 = 0; b8 < a.rd.nblk; b8 += U) {
-          double csv[U];
-          int ngv[U];
+        // the per-block inputs do not depend on the recurrence: group g + 1's loads are in
+        // flight while group g is folded (software pipelining; the chain itself is short)
+        double ncsv[U], nbav[U], nbsd[U];
+        int nngv[U];
+        bool nazv[U];
+        auto fetch = [&](int b8) {
 #pragma unroll
-          for (int u = 0; u < U; u++) {                 // independent of the recurrence: issue first
-              const int b = min(b8 + u, a.rd.nblk - 1);
-              csv[u] = own ? a.chansum[(int64_t)b * nch + c] : 0.0;
-              ngv[u] = a.numgood[b];
+            for (int u = 0; u < U; u++) {
+                const int b = min(b8 + u, a.rd.nblk - 1);
+                ncsv[u] = own ? a.chansum[(int64_t)b * nch + c] : 0.0;
+                nngv[u] = a.numgood[b];
+                nbav[u] = a.bavg[b];
+                nbsd[u] = a.bstd[b];
+                nazv[u] = a.allzap && a.allzap[b];
+            }
+        };
+        fetch(0);
+        for (int b8 = 0; b8 < a.rd.nblk; b8 += U) {
+          double csv[U], bav[U], bsd[U];
+          int ngv[U];
+          bool azv[U];
+#pragma unroll
+          for (int u = 0; u < U; u++) {
+              csv[u] = ncsv[u];
+              bav[u] = nbav[u];
+              bsd[u] = nbsd[u];
+              ngv[u] = nngv[u];
+              azv[u] = nazv[u];
           }
+          if (b8 + U < a.rd.nblk) fetch(b8 + U);
 #pragma unroll
           for (int u = 0; u < U; u++) {
             const int b = b8 + u;
             if (b >= a.rd.nblk) break;
-            const bool run = clip_sigma > 0.0f && !(a.allzap && a.allzap[b]);
+            const bool run = clip_sigma > 0.0f && !azv[u];
             if (run) {
                 const int ng = ngv[u];
                 double cur_avg, cur_std, cat;
@@ -303,8 +328,8 @@ __global__ __launch_bounds__(1024) void k_clip_recur(ClipArgs a)
                     cur_std = (double)rstd;
                     cat = (double)cra;
                 } else {
-                    cur_avg = a.bavg[b];
-                    cur_std = a.bstd[b];
+                    cur_avg = bav[u];
+                    cur_std = bsd[u];
                     cat = csv[u] / (double)ng;
                 }
                 if (nread) {
@@ -322,7 +347,7 @@ __global__ __launch_bounds__(1024) void k_clip_recur(ClipArgs a)
                 lev = cra;
                 nread++;
             }
-            if (c0 == 0 && threadIdx.x == 0) {
+            if (c0 == 0 && threadIdx.x == 0) {              // workgroup 0, thread 0
                 a.doclip[b] = run;
                 a.ravg[b] = ravg;
                 a.trig[b] = clip_sigma * rstd;
@@ -401,10 +426,11 @@ hipError_t launch_clip_unpack(const ClipArgs& g, const double* in, hipStream_t s
     return hipGetLastError();
 }
 
-// the serial recurrence over a.rd.nblk blocks (a's arrays), one workgroup
+// the serial recurrence over a.rd.nblk blocks (a's arrays), one wave per 64 channels
 hipError_t launch_clip_recur(const ClipArgs& a, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_clip_recur, dim3(1), dim3(1024), 0, st, a);
+    const unsigned g = (unsigned)std::max(1, (a.rd.nchan + 63) / 64);
+    hipLaunchKernelGGL(k_clip_recur, dim3(g), dim3(64), 0, st, a);
     return hipGetLastError();
 }
 
