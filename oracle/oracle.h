@@ -98,6 +98,18 @@ int64_t or_clip_prepare(const or_obs* obs, const or_opts* opts, const uint8_t* r
                         const float* scl, const float* offs, const float* wts,
                         const uint8_t* allzap, const float* padvals0, int blk, int nblk,
                         float* pad, uint8_t* clipped);
+/* The same clip_times split at a time slice's exchange (hd_clip_stats / hd_clip_set_stats):
+ * or_clip_rows writes the rows {avg, std, numgood, chansum[nchan]} of global read blocks
+ * [b0, b0 + nrows) from raw = spectra b0*blk.. of the observation (obs->N its full length);
+ * or_clip_finish runs the recurrence over the summed table of all nblk rows and flags the
+ * spectra [t0, t0 + n) that raw holds.  or_clip_prepare == rows over all blocks + finish. */
+int     or_clip_rows(const or_obs* obs, const or_opts* opts, const uint8_t* raw, const float* scl,
+                     const float* offs, const float* wts, const uint8_t* allzap, int blk, int64_t b0,
+                     int64_t nrows, double* rows);
+int64_t or_clip_finish(const or_obs* obs, const or_opts* opts, const uint8_t* raw, const float* scl,
+                       const float* offs, const float* wts, const uint8_t* allzap, const float* padvals0,
+                       int blk, int nblk, const double* table, int64_t t0, int64_t n, float* pad,
+                       uint8_t* clipped);
 
 /* ---- stage 1: raw -> subbands, output samples [t0, t0+count) of every subband ----
  * out: [nsub][out_stride] int16 or f32 (opts->sub_dtype); column index = t - t0.

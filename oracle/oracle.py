@@ -57,6 +57,10 @@ def lib(omp=False):
         L.or_check_mask_blocks.restype = None
         L.or_clip_prepare.argtypes = [P(or_obs), P(or_opts), vp, vp, vp, vp, vp, vp, ci, ci, vp, vp]
         L.or_clip_prepare.restype = i64
+        L.or_clip_rows.argtypes = [P(or_obs), P(or_opts), vp, vp, vp, vp, vp, ci, i64, i64, vp]
+        L.or_clip_rows.restype = ci
+        L.or_clip_finish.argtypes = [P(or_obs), P(or_opts), vp, vp, vp, vp, vp, vp, ci, ci, vp, i64, i64, vp, vp]
+        L.or_clip_finish.restype = i64
         L.or_stage1.argtypes = [P(or_obs), P(or_opts), vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, vp,
                                 i64, i64, vp, i64]
         L.or_stage2.argtypes = [vp, ci, i64, i64, ci, vp, ci, i64, i64, vp, i64]
@@ -71,6 +75,8 @@ def lib(omp=False):
         L.or_delay_from_dm.argtypes = [d, d]
         L.sp_oracle_hits.argtypes = [vp, i64, ci, i64, vp, ci, d, vp, i64, vp]
         L.sp_oracle_hits.restype = i64
+        L.sp_prune_related1.argtypes = [vp, vp, i64, ci, vp]
+        L.sp_prune_related1.restype = None
         _libs[key] = L
     return _libs[key]
 
@@ -164,6 +170,40 @@ def prepare(obs, opts, raw, calib=(None, None, None), mask=None, ptsperint=0, pa
     if n < 0:
         raise ValueError("or_clip_prepare rejected its arguments")
     return Clean(blk, nblk, zap, allzap, pad, clipped, int(n))
+
+
+def clip_rows(obs, opts, raw, b0, nrows, mask=None, ptsperint=0, blk=None, omp=False):
+    """clip_times' exchange rows [nrows][nchan + 3] of global read blocks [b0, b0 + nrows)
+    (hd_clip_stats' layout) from raw = the observation's spectra b0 * blk onward; obs.N is
+    the whole observation's length."""
+    blk = int(blk or obs.nsblk)
+    _, allzap = block_masks(obs, mask, ptsperint, blk=blk)
+    rows = np.zeros((nrows, obs.nchan + 3), np.float64)
+    raw = np.ascontiguousarray(raw, np.uint8)
+    o, p = _obs(obs), _opts(opts)
+    if lib(omp).or_clip_rows(ctypes.byref(o), ctypes.byref(p), _ptr(raw), None, None, None, _ptr(allzap), blk,
+                             int(b0), int(nrows), _ptr(rows)):
+        raise ValueError("or_clip_rows rejected its arguments")
+    return rows
+
+
+def clip_finish(obs, opts, raw, table, t0, n, mask=None, ptsperint=0, padvals=None, blk=None):
+    """clip_times' recurrence over the summed exchange table -> (pad [nblk][nchan], clipped
+    flags of spectra [t0, t0 + n), count clipped among them); raw holds those spectra."""
+    blk = int(blk or obs.nsblk)
+    nblk = (obs.N + blk - 1) // blk
+    _, allzap = block_masks(obs, mask, ptsperint, blk=blk)
+    pad = np.zeros((nblk, obs.nchan), np.float32)
+    clipped = np.zeros(n, np.uint8)
+    pv = None if padvals is None else np.ascontiguousarray(padvals, np.float32)
+    table = np.ascontiguousarray(table, np.float64)
+    raw = np.ascontiguousarray(raw, np.uint8)
+    o, p = _obs(obs), _opts(opts)
+    k = lib().or_clip_finish(ctypes.byref(o), ctypes.byref(p), _ptr(raw), None, None, None, _ptr(allzap), _ptr(pv),
+                             blk, nblk, _ptr(table), int(t0), int(n), _ptr(pad), _ptr(clipped))
+    if k < 0:
+        raise ValueError("or_clip_finish rejected its arguments")
+    return pad, clipped, int(k)
 
 
 def stage1(obs, opts, raw, nsub, ds, subdm, t0=0, count=None, calib=(None, None, None),
@@ -276,18 +316,15 @@ class SpCand:
         return "%7.2f %7.2f %13.6f %10d     %3d\n" % (self.DM, self.sigma, self.time, self.bin, self.downfact)
 
 
-def _prune_related1_localmax(bins, sig, half, ls):
-    """prune_related1 as the local-maximum rule (sp_oracle.c / hd_sp.hip): keep a hit when
-    no hit within half bins is stronger -- a later one that is equal also removes it."""
-    if half == 0 or len(bins) == 0:
-        return np.ones(len(bins), bool)
-    dense = np.full(ls + 2 * half + 2, -np.inf)
-    dense[bins + half] = sig
-    keep = np.ones(len(bins), bool)
-    for d in range(1, half + 1):
-        keep &= ~(dense[bins + half + d] >= sig)
-        keep &= ~(dense[bins + half - d] > sig)
-    return keep
+def prune_related1(bins, sig, downfact):
+    """The script's prune_related1 greedy walk (sp_oracle.c, literal): bool mask of the kept
+    entries of one (chunk, width) hit list in bin order."""
+    bins = np.ascontiguousarray(bins, dtype=np.int32)
+    sig = np.ascontiguousarray(sig, dtype=np.float64)
+    rem = np.zeros(len(bins), np.uint8)
+    if len(bins) > 1:
+        lib(False).sp_prune_related1(_ptr(bins), _ptr(sig), len(bins), int(downfact), _ptr(rem))
+    return rem == 0
 
 
 def _prune_related2(cands, downfacts):
@@ -331,24 +368,34 @@ def _prune_border_cases(cands, offregions):
 
 def sp_candidates(hits, bad, widths, dms, dt, nds=None, numout=None, ls=None):
     """single_pulse_search.py's per-DM candidate list from the raw hits (every boxcar value
-    above threshold in [0, ls)): prune_related1 per width (local-maximum rule), hits in bad
-    blocks dropped, the rest in bin order (widths ascending among equal bins: the script's
-    append + bisect.insort), prune_related2 across widths and, for padded series,
-    prune_border_cases.  -> [list of SpCand per DM]"""
+    above threshold in [0, ls)), chunk by chunk (8000 samples) as the script builds it:
+    width-1 hits outside bad blocks; per width > 1 the chunk's hits through prune_related1
+    (the greedy walk) and then the script's `zip(hibins, hivals, hiblocks)` -- survivor m
+    kept when the block of the m-th UNPRUNED hit is good; the list in bin order (widths
+    ascending among equal bins: the script's append + bisect.insort), prune_related2 across
+    widths and, for padded series, prune_border_cases.  -> [list of SpCand per DM]"""
     downfacts = list(widths[1:])
-    if ls is None:
-        ls = int(hits["bin"].max()) + 1 if len(hits) else 0
     out = []
     for d in range(len(dms)):
         hd = hits[hits["dm"] == d]
         kept = []
         for wi, w in enumerate(widths):
             hw = hd[hd["widx"] == wi]
-            k = _prune_related1_localmax(hw["bin"].astype(np.int64), hw["sigma"], w // 2, ls)
-            hw = hw[k]
-            blk = hw["bin"] // 1000
-            ok = bad[d][blk] == 0 if bad.size else np.ones(len(hw), bool)
-            kept += [(int(b), wi, float(v)) for b, v in zip(hw["bin"][ok], hw["sigma"][ok])]
+            hw = hw[np.argsort(hw["bin"], kind="stable")]
+            b_all = hw["bin"].astype(np.int64)
+            if wi == 0:
+                ok = bad[d][b_all // 1000] == 0 if bad.size else np.ones(len(hw), bool)
+                kept += [(int(b), wi, float(v)) for b, v in zip(b_all[ok], hw["sigma"][ok])]
+                continue
+            chunk = b_all // 8000
+            for c in np.unique(chunk):
+                sel = chunk == c
+                bins, sig = b_all[sel], hw["sigma"][sel]
+                k = prune_related1(bins, sig, w)
+                blocks = bins // 1000                               # hiblocks of the unpruned list
+                for m, (b, v) in enumerate(zip(bins[k], sig[k])):
+                    if not (bad.size and bad[d][blocks[m]]):
+                        kept.append((int(b), wi, float(v)))
         kept.sort(key=lambda r: (r[0], r[1]))
         cl = [SpCand(dms[d], v, b * dt, b, widths[wi]) for b, wi, v in kept]
         cl = _prune_related2(cl, downfacts)

@@ -336,8 +336,9 @@ static void clip_block_stats(const float* rawdata, int ptsperblk, int numchan, f
         double var;
         avg_var(median_temp, numgoodpts, &bs->avg, &var);
         bs->std = sqrt(var);
-        for (int jj = 0; jj < numchan; jj++) chan_avg_temp[jj] /= numgoodpts;
     }
+    /* chan_avg_temp keeps the SUMS here: the exchange rows of a time-sliced beam carry them,
+     * and clip_finish divides by numgood exactly where clip_times does */
     free(median_temp);
 }
 
@@ -383,54 +384,120 @@ static int clip_update(const float* zero_dm_block, int ptsperblk, int numchan, f
     return clipped;
 }
 
+static void zero_dm(const float* rawdata, int ptsperblk, int numchan, float* zero_dm_block)
+{
+    for (int ii = 0; ii < ptsperblk; ii++) {
+        zero_dm_block[ii] = 0.0f;
+        for (int jj = 0; jj < numchan; jj++) zero_dm_block[ii] += rawdata[(int64_t)ii * numchan + jj];
+    }
+}
+
+/* Exchange rows of clip_times' per-block statistics (the layout of hd_clip_stats): for the
+ * global read blocks [b0, b0 + nrows), row r = {avg, std, numgood, chansum[nchan]} (zeros for
+ * a block whose every channel is masked).  raw holds the observation's spectra from
+ * t0 = b0 * blk on (a time slice's own rows); obs->N is the whole observation's length.   */
+int or_clip_rows(const or_obs* obs, const or_opts* opts, const uint8_t* raw, const float* scl, const float* offs,
+                 const float* wts, const uint8_t* allzap, int blk, int64_t b0, int64_t nrows, double* rows)
+{
+    const int nchan = obs->nchan;
+    const int64_t nblk = (obs->N + blk - 1) / blk;
+    if (blk <= 0 || b0 < 0 || nrows < 0 || b0 + nrows > nblk) return -1;
+    memset(rows, 0, sizeof(double) * (size_t)nrows * (nchan + 3));
+    const int64_t rowbytes = (int64_t)nchan * obs->nbits / 8;
+#pragma omp parallel
+    {
+        float* X = (float*)malloc(sizeof(float) * (size_t)blk * nchan);
+        float* zdm = (float*)malloc(sizeof(float) * (size_t)blk);
+#pragma omp for schedule(dynamic, 1)
+        for (int64_t r = 0; r < nrows; r++) {
+            const int64_t b = b0 + r;
+            if (allzap && allzap[b]) continue;
+            const int64_t t0 = b * blk;
+            const int nb = (int)((t0 + blk <= obs->N) ? blk : obs->N - t0);
+            for (int ii = 0; ii < nb; ii++)
+                decode_row(obs, opts, raw + (t0 - b0 * blk + ii) * rowbytes, scl, offs, wts, X + (int64_t)ii * nchan);
+            blockstat bs;
+            double* row = rows + r * (nchan + 3);
+            clip_block_stats(X, nb, nchan, zdm, &bs, row + 3);
+            row[0] = bs.avg;
+            row[1] = bs.std;
+            row[2] = (double)bs.numgood;
+        }
+        free(zdm);
+        free(X);
+    }
+    return 0;
+}
+
+/* clip_times' block-order recurrence over the exchange rows table[nblk][nchan + 3] of the
+ * whole observation: pad[nblk][nchan] (the channel levels in force per block) and the
+ * clipped flags of spectra [t0, t0 + n) of raw (which holds those spectra; t0 a multiple of
+ * blk).  Returns the number of clipped spectra among them.                                */
+int64_t or_clip_finish(const or_obs* obs, const or_opts* opts, const uint8_t* raw, const float* scl,
+                       const float* offs, const float* wts, const uint8_t* allzap, const float* padvals0, int blk,
+                       int nblk, const double* table, int64_t t0, int64_t n, float* pad, uint8_t* clipped)
+{
+    const int nchan = obs->nchan;
+    if (blk <= 0 || nblk != (int)((obs->N + blk - 1) / blk) || t0 % blk || t0 < 0 || t0 + n > obs->N) return -1;
+    memset(clipped, 0, (size_t)n);
+    float* padvals = (float*)calloc((size_t)nchan, sizeof(float));
+    if (padvals0) memcpy(padvals, padvals0, sizeof(float) * nchan);
+    const int clip = opts->clip_sigma > 0.0f;
+    const int64_t rowbytes = (int64_t)nchan * obs->nbits / 8;
+    float* X = (float*)malloc(sizeof(float) * (size_t)blk * nchan);
+    float* zdm = (float*)malloc(sizeof(float) * (size_t)blk);
+    uint8_t* scratch = (uint8_t*)malloc((size_t)blk);
+    double* cat = (double*)malloc(sizeof(double) * nchan);
+    clipstate st = {0.0f, 0.0f, 0, (float*)calloc((size_t)nchan, sizeof(float))};
+    int64_t total = 0;
+    for (int b = 0; b < nblk; b++) {
+        const int64_t s0 = (int64_t)b * blk;
+        const int nb = (int)((s0 + blk <= obs->N) ? blk : obs->N - s0);
+        const int mine = s0 >= t0 && s0 < t0 + n;
+        if (clip && !(allzap && allzap[b])) {
+            const double* row = table + (int64_t)b * (nchan + 3);
+            blockstat bs = {(int)row[2], row[0], row[1]};
+            for (int jj = 0; jj < nchan; jj++) cat[jj] = bs.numgood >= 1 ? row[3 + jj] / bs.numgood : row[3 + jj];
+            uint8_t* flags = scratch;
+            memset(scratch, 0, (size_t)blk);
+            if (mine) {
+                for (int ii = 0; ii < nb; ii++)
+                    decode_row(obs, opts, raw + (s0 - t0 + ii) * rowbytes, scl, offs, wts, X + (int64_t)ii * nchan);
+                zero_dm(X, nb, nchan, zdm);
+                flags = clipped + (s0 - t0);
+            } else {
+                for (int ii = 0; ii < nb; ii++) zdm[ii] = st.running_avg;   /* flags of other slices: unused */
+            }
+            const int k = clip_update(zdm, nb, nchan, opts->clip_sigma, &bs, cat, padvals, &st, flags);
+            if (mine) total += k;
+        }
+        memcpy(pad + (int64_t)b * nchan, padvals, sizeof(float) * nchan);
+    }
+    free(st.chan_running_avg);
+    free(cat);
+    free(scratch);
+    free(zdm);
+    free(X);
+    free(padvals);
+    return total;
+}
+
 int64_t or_clip_prepare(const or_obs* obs, const or_opts* opts, const uint8_t* raw,
                         const float* scl, const float* offs, const float* wts,
                         const uint8_t* allzap, const float* padvals0, int blk, int nblk,
                         float* pad, uint8_t* clipped)
 {
-    const int nchan = obs->nchan;
-    if (blk <= 0 || nblk != (int)((obs->N + blk - 1) / blk)) return -1;
-    memset(clipped, 0, (size_t)obs->N);
-    float* padvals = (float*)calloc((size_t)nchan, sizeof(float));
-    if (padvals0) memcpy(padvals, padvals0, sizeof(float) * nchan);
     /* the reference's -sub command leaves prepsubband's default clip on; a block whose
      * every channel is masked is neither clipped nor counted (read_psrdata) */
-    const int clip = opts->clip_sigma > 0.0f;
-    float* zdm = clip ? (float*)malloc(sizeof(float) * (size_t)obs->N) : NULL;
-    blockstat* bs = clip ? (blockstat*)calloc((size_t)nblk, sizeof(blockstat)) : NULL;
-    double* cat = clip ? (double*)malloc(sizeof(double) * (size_t)nblk * nchan) : NULL;
-    if (clip) {
-        const int64_t rowbytes = (int64_t)nchan * obs->nbits / 8;
-#pragma omp parallel
-        {
-            float* X = (float*)malloc(sizeof(float) * (size_t)blk * nchan);
-#pragma omp for schedule(dynamic, 1)
-            for (int b = 0; b < nblk; b++) {
-                if (allzap && allzap[b]) continue;
-                const int64_t t0 = (int64_t)b * blk;
-                const int nb = (int)((t0 + blk <= obs->N) ? blk : obs->N - t0);
-                for (int ii = 0; ii < nb; ii++)
-                    decode_row(obs, opts, raw + (t0 + ii) * rowbytes, scl, offs, wts, X + (int64_t)ii * nchan);
-                clip_block_stats(X, nb, nchan, zdm + t0, bs + b, cat + (int64_t)b * nchan);
-            }
-            free(X);
-        }
+    if (blk <= 0 || nblk != (int)((obs->N + blk - 1) / blk)) return -1;
+    double* table = NULL;
+    if (opts->clip_sigma > 0.0f) {
+        table = (double*)malloc(sizeof(double) * (size_t)nblk * (obs->nchan + 3));
+        or_clip_rows(obs, opts, raw, scl, offs, wts, allzap, blk, 0, nblk, table);
     }
-    clipstate st = {0.0f, 0.0f, 0, (float*)calloc((size_t)nchan, sizeof(float))};
-    int64_t total = 0;
-    for (int b = 0; b < nblk; b++) {
-        const int64_t t0 = (int64_t)b * blk;
-        const int nb = (int)((t0 + blk <= obs->N) ? blk : obs->N - t0);
-        if (clip && !(allzap && allzap[b]))
-            total += clip_update(zdm + t0, nb, nchan, opts->clip_sigma, bs + b, cat + (int64_t)b * nchan,
-                                 padvals, &st, clipped + t0);
-        memcpy(pad + (int64_t)b * nchan, padvals, sizeof(float) * nchan);
-    }
-    free(st.chan_running_avg);
-    free(padvals);
-    free(zdm);
-    free(bs);
-    free(cat);
+    const int64_t total = or_clip_finish(obs, opts, raw, scl, offs, wts, allzap, padvals0, blk, nblk, table, 0,
+                                         obs->N, pad, clipped);
+    free(table);
     return total;
 }
 

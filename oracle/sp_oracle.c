@@ -10,7 +10,9 @@
  *   per DM: sort the stds, locut/hicut at the largest jumps of the lower/upper halves,
  *     pseudo-median and population std of [locut, hicut), bad = outside +-4 std;
  *   normalised data (bad blocks 0) over the first numchunks*8000 samples (0 beyond);
- *   hits: every boxcar value (1/sqrt(w) kernel at PRESTO's offsets) above threshold.
+ *   hits: every boxcar value (1/sqrt(w) kernel at PRESTO's offsets) above threshold;
+ *   sp_prune_related1: the script's prune_related1 greedy walk, literally (quadratic; the
+ *     device uses the O(n) form it reduces to).
  *
  * The summation orders are the ones hd_sp.hip defines (64 lane partials over the block's
  * samples 16l..16l+15, then a xor butterfly; per 8000-sample chunk a prefix over 256
@@ -202,4 +204,24 @@ int64_t sp_oracle_hits(const float* x, int64_t stride, int ndm, int64_t n, const
     free(P);
     free(coef);
     return cnt;
+}
+
+/* prune_related1(hibins, hivals, downfact) of single_pulse_search.py, step for step:
+ *   for ii in range(len-1): skip removed ii; for jj > ii: break when |bin_jj - bin_ii| >
+ *   downfact/2 (integer); skip removed jj; remove jj if val_ii > val_jj, else remove ii.
+ * bins ascending; removed[n] receives 1 for every removed entry.                          */
+void sp_prune_related1(const int32_t* bins, const double* vals, int64_t n, int downfact, uint8_t* removed)
+{
+    memset(removed, 0, (size_t)n);
+    const int half = downfact / 2;
+    for (int64_t ii = 0; ii + 1 < n; ii++) {
+        if (removed[ii]) continue;
+        for (int64_t jj = ii + 1; jj < n; jj++) {
+            const int gap = bins[jj] - bins[ii];
+            if ((gap < 0 ? -gap : gap) > half) break;
+            if (removed[jj]) continue;
+            if (vals[ii] > vals[jj]) removed[jj] = 1;
+            else removed[ii] = 1;
+        }
+    }
 }

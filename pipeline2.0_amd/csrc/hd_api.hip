@@ -13,6 +13,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <map>
 #include <tuple>
@@ -2225,6 +2226,20 @@ extern "C" int hd_single_pulse(hd_plan* p, double dt, double maxwidth, double th
     }
     unsigned long long cnt = 0;
     HIPCHK(c, d2h(&cnt, c->d_sp_count, sizeof(cnt), st));
+    if ((int64_t)cnt > c->sp_hits_cap) {
+        // the device list overflowed: grow it to the count and search again (once per size)
+        HIPCHK(c, hipStreamSynchronize(st));
+        dfree(c->d_sp_hits);
+        c->d_sp_hits = nullptr;
+        c->sp_hits_cap = 0;
+        const int64_t ncap = (int64_t)cnt + (int64_t)cnt / 4;
+        HIPCHK(c, hipMalloc(&c->d_sp_hits, sizeof(hd_sp_hit) * (size_t)ncap));
+        c->sp_hits_cap = ncap;
+        HIPCHK(c, hipMemsetAsync(c->d_sp_count, 0, sizeof(unsigned long long), st));
+        HIPCHK(c, hd::launch_sp_hits(p->d_out, p->out_stride, ndm, (int)nblocks, c->d_sp_coef, ls, widths, rsw, nw,
+                                     threshold, c->d_sp_hits, c->d_sp_count, c->sp_hits_cap, st));
+        HIPCHK(c, d2h(&cnt, c->d_sp_count, sizeof(cnt), st));
+    }
     std::vector<double> coef;
     if (bad_blocks && nblocks > 0) {
         coef.resize((size_t)ndm * nblocks * 4);
@@ -2233,28 +2248,33 @@ extern "C" int hd_single_pulse(hd_plan* p, double dt, double maxwidth, double th
     if (bad_blocks)
         for (size_t i = 0; i < (size_t)ndm * nblocks; i++) bad_blocks[i] = coef[4 * i + 3] != 0.0;
     *nhits = (int64_t)cnt;
-    if ((int64_t)cnt > cap || (int64_t)cnt > c->sp_hits_cap)
+    if ((int64_t)cnt > cap)
         return fail(c, HD_E_NOMEM, "hd_single_pulse: %llu hits > capacity %lld (call again with room)", cnt,
-                    (long long)std::min(cap, c->sp_hits_cap));
+                    (long long)cap);
     if (!cnt) return HD_OK;
     HIPCHK(c, hipMemcpy(hits, c->d_sp_hits, sizeof(hd_sp_hit) * cnt, hipMemcpyDeviceToHost));
-    // the script's dm_candlist order: by bin, widths in increasing order among equal bins
-    // (width-1 hits appended first, every downfactor's bisect.insort after equals)
-    std::sort(hits, hits + cnt, [](const hd_sp_hit& a, const hd_sp_hit& b) {
-        return a.dm != b.dm ? a.dm < b.dm : a.bin != b.bin ? a.bin < b.bin : a.widx < b.widx;
-    });
-    // prune_related2 (exact greedy walk, per DM) and prune_border_cases (padded series: data
-    // ends at nds - 1, padding runs to numout - 1 -- the .inf on/off pairs)
+    // per DM (in parallel): the script's dm_candlist order -- by bin, widths in increasing
+    // order among equal bins (width-1 hits appended first, every downfactor's bisect.insort
+    // after equals) -- then prune_related2 (its greedy walk, literally) and prune_border_cases
+    // (padded series: data ends at nds - 1, padding runs to numout - 1 -- the .inf on/off pair)
+    std::vector<int64_t> dstart((size_t)ndm + 1, 0);
+    for (unsigned long long i = 0; i < cnt; i++) dstart[(size_t)hits[i].dm + 1]++;
+    for (int d = 0; d < ndm; d++) dstart[d + 1] += dstart[d];
+    {
+        std::vector<hd_sp_hit> tmp(hits, hits + cnt);
+        std::vector<int64_t> pos(dstart.begin(), dstart.end() - 1);
+        for (const hd_sp_hit& h : tmp) hits[pos[(size_t)h.dm]++] = h;
+    }
     const int reach = nw > 1 ? widths[nw - 1] / 2 : 0;
     const bool padded = p->numout > p->nds;
-    int64_t out = 0;
-    std::vector<char> gone;
-    for (int64_t d0 = 0; d0 < (int64_t)cnt;) {
-        int64_t d1 = d0;
-        while (d1 < (int64_t)cnt && hits[d1].dm == hits[d0].dm) d1++;
-        const int64_t n = d1 - d0;
-        hd_sp_hit* h = hits + d0;
-        gone.assign((size_t)n, 0);
+    std::vector<int64_t> kept((size_t)ndm, 0);
+    auto prune_dm = [&](int d) {
+        hd_sp_hit* h = hits + dstart[d];
+        const int64_t n = dstart[d + 1] - dstart[d];
+        std::sort(h, h + n, [](const hd_sp_hit& x, const hd_sp_hit& y) {
+            return x.bin != y.bin ? x.bin < y.bin : x.widx < y.widx;
+        });
+        std::vector<char> gone((size_t)n, 0);
         for (int64_t i = 0; i + 1 < n; i++) {
             if (gone[i]) continue;
             for (int64_t j = i + 1; j < n; j++) {
@@ -2276,9 +2296,27 @@ extern "C" int hd_single_pulse(hd_plan* p, double dt, double maxwidth, double th
                 if (hi > off && lo < on) gone[i] = 1;
             }
         }
+        int64_t k = 0;
         for (int64_t i = 0; i < n; i++)
-            if (!gone[i]) hits[out++] = h[i];
-        d0 = d1;
+            if (!gone[i]) h[k++] = h[i];
+        kept[(size_t)d] = k;
+    };
+    const unsigned nth = std::max(1u, std::min({16u, std::thread::hardware_concurrency(), (unsigned)ndm}));
+    if (nth <= 1 || cnt < 4096) {
+        for (int d = 0; d < ndm; d++) prune_dm(d);
+    } else {
+        std::vector<std::thread> th;
+        std::atomic<int> next{0};
+        for (unsigned t = 0; t < nth; t++)
+            th.emplace_back([&]() {
+                for (int d = next++; d < ndm; d = next++) prune_dm(d);
+            });
+        for (auto& t : th) t.join();
+    }
+    int64_t out = 0;
+    for (int d = 0; d < ndm; d++) {
+        if (out != dstart[d]) memmove(hits + out, hits + dstart[d], sizeof(hd_sp_hit) * (size_t)kept[(size_t)d]);
+        out += kept[(size_t)d];
     }
     *nhits = out;
     return HD_OK;

@@ -12,11 +12,14 @@
 //     (1, 2, 3, 4, 6, 9, 14, 20, 30, 45, 70, 100, 150, 220, 300 samples, kernel
 //     1/sqrt(w) at PRESTO's offsets) over the first numchunks * 8000 samples (zero beyond);
 //     a value above threshold outside the bad blocks is a hit;
-//   * prune_related1 (per width, drop hits within downfact/2 of a stronger one) as the
-//     local-maximum rule its greedy walk reduces to: a hit of width w > 1 survives when no
-//     other hit of that width within w/2 bins is stronger (equal: the later one wins, as
-//     the walk removes the earlier).  It is evaluated here, per hit, in parallel; the walk
-//     itself is sequential (and quadratic on dense pulsar trains).
+//   * prune_related1 per (chunk, width > 1) exactly as the script's greedy walk, in the O(n)
+//     form it reduces to: in bin order a hit is a "pivot" unless the
+//     last pivot lies within h = w/2 bins and is strictly stronger; a pivot survives when
+//     the next pivot is more than h bins later (or there is none).  One lane walks one
+//     (chunk, width) over a bitmask of its above-threshold bins;
+//   * the script's bad-block test after the walk: survivor m is paired with the block of the
+//     m-th UNPRUNED hit (`zip(hibins, hivals, hiblocks)` with hiblocks taken before
+//     prune_related1); width-1 hits are tested against their own block.
 // The survivors go to the host (hd_api.hip) for prune_related2 and the border cases.
 // Arithmetic is double with a fixed summation order (lane partials in index order, then a
 // xor butterfly over the 64 lanes; per-chunk prefix sums over 256 segments of 34 samples),
@@ -29,9 +32,11 @@ namespace hd {
 
 constexpr int kSpBlock = 1000;               // detrendlen
 constexpr int kSpChunk = 8000;               // chunklen
-constexpr int kSpHalo = 352;                 // >= max downfact (its window + the prune reach)
-constexpr int kSpSeg = 34;                   // prefix-sum segment per thread
-constexpr int kSpWin = 256 * kSpSeg;         // kSpChunk + 2 * kSpHalo = 8704
+constexpr int kSpHalo = 224;                 // >= max downfact / 2 + 1 (a boxcar's reach)
+constexpr int kSpSeg = 33;                   // prefix-sum segment per thread
+constexpr int kSpWin = 256 * kSpSeg;         // kSpChunk + 2 * kSpHalo = 8448
+constexpr int kSpWords = kSpChunk / 32;      // hit bitmask words per (chunk, width)
+constexpr int kSpRound = 7;                  // widths walked per round (bitmask LDS: 7 KB)
 
 __device__ __forceinline__ double wave_sum_f64(double v)
 {
@@ -219,14 +224,30 @@ struct SpArgs {
     int64_t cap;
 };
 
+__device__ __forceinline__ void sp_emit(const SpArgs& a, int dm, int64_t bin, int wi, double s)
+{
+    const unsigned long long slot = atomicAdd(a.count, 1ull);
+    if ((int64_t)slot < a.cap) {
+        hd_sp_hit h;
+        h.dm = dm;
+        h.bin = (int32_t)bin;
+        h.widx = wi;
+        h.pad = 0;
+        h.sigma = s;
+        a.hits[slot] = h;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_sp_hits(SpArgs a)
 {
     __shared__ double P[kSpWin + 1];
     __shared__ double tot[257];
+    __shared__ uint32_t bits[kSpRound][kSpWords];
     const int dm = blockIdx.x / a.nchunks, ch = blockIdx.x - dm * a.nchunks;
     const float* xs = a.x + (int64_t)dm * a.stride;
     const double* cf = a.coef + (int64_t)dm * a.nblocks * 4;
     const int64_t w0 = (int64_t)ch * kSpChunk - kSpHalo;     // sample of window element 0
+    const int64_t c0 = (int64_t)ch * kSpChunk;               // first bin of the chunk
     const int tid = threadIdx.x;
     double loc[kSpSeg];
     double run = 0.0;
@@ -251,46 +272,65 @@ __global__ __launch_bounds__(256) void k_sp_hits(SpArgs a)
 #pragma unroll
     for (int j = 0; j < kSpSeg; j++) P[tid * kSpSeg + j + 1] = base + loc[j];
     __syncthreads();
-    // boxcar value of width index wi at window element k (sample w0 + k)
-    auto boxcar = [&](int wi, int k) -> double {
+    // boxcar value (width index wi > 0) at chunk bin o
+    auto boxcar = [&](int wi, int o) -> double {
         const int w = a.widths[wi];
-        if (w == 1) return (double)sp_norm(xs, cf, w0 + k, a.ls);
+        const int k = o + kSpHalo;
         const int lo = k - w / 2, hi = k + ((w & 1) ? w / 2 : w / 2 - 1) + 1;
         return (P[hi] - P[lo]) * a.rsw[wi];
     };
+    auto bad = [&](int o) { return cf[((c0 + o) / kSpBlock) * 4 + 3] != 0.0; };
+    // width 1: every value above threshold outside the bad blocks (no prune_related1)
     for (int o = tid; o < kSpChunk; o += 256) {
-        const int64_t i = (int64_t)ch * kSpChunk + o;
-        if (i >= a.ls) break;
-        if (cf[(i / kSpBlock) * 4 + 3] != 0.0) continue;     // bad block: not searched
-        const int k = o + kSpHalo;
-        for (int wi = 0; wi < a.nwidths; wi++) {
-            const double s = boxcar(wi, k);
-            if (!(s > a.threshold)) continue;
-            // prune_related1: a stronger hit (later one on ties) within w/2 removes it
-            const int half = a.widths[wi] / 2;
-            bool keep = true;
-            for (int d = 1; d <= half && keep; d++) {
-                if (i + d < a.ls) {
-                    const double t = boxcar(wi, k + d);
-                    keep = !(t >= s);
-                }
-                if (keep && i - d >= 0) {
-                    const double t = boxcar(wi, k - d);
-                    keep = !(t > s);
-                }
-            }
-            if (!keep) continue;
-            const unsigned long long slot = atomicAdd(a.count, 1ull);
-            if ((int64_t)slot < a.cap) {
-                hd_sp_hit h;
-                h.dm = dm;
-                h.bin = (int32_t)i;
-                h.widx = wi;
-                h.pad = 0;
-                h.sigma = s;
-                a.hits[slot] = h;
-            }
+        if (bad(o)) continue;
+        const double s = (double)sp_norm(xs, cf, c0 + o, a.ls);
+        if (s > a.threshold) sp_emit(a, dm, c0 + o, 0, s);
+    }
+    const int wv = tid >> 6, ln = tid & 63;
+    for (int r0 = 1; r0 < a.nwidths; r0 += kSpRound) {
+        const int nr = min(kSpRound, a.nwidths - r0);
+        // the above-threshold bins of widths r0 .. r0+nr-1 (bad blocks included: the script
+        // prunes before it looks at blocks)
+        for (int t = tid; t < nr * kSpWords; t += 256) {
+            const int j = t / kSpWords, wd = t - j * kSpWords;
+            uint32_t m = 0;
+            for (int b = 0; b < 32; b++)
+                if (boxcar(r0 + j, 32 * wd + b) > a.threshold) m |= 1u << b;
+            bits[j][wd] = m;
         }
+        __syncthreads();
+        // prune_related1: width r0 + j walked by lane j >> 2 of wave j & 3
+        const int j = wv + 4 * ln;
+        if (ln < 2 && j < nr) {
+            const int wi = r0 + j;
+            const int h = a.widths[wi] / 2;
+            const uint32_t* bm = bits[j];
+            int lpb = 0, zw = 0;
+            double lpx = 0.0;
+            bool have = false;
+            uint32_t zm = bm[0];
+            auto survivor = [&](int b, double x) {
+                while (zm == 0) zm = bm[++zw];                // the m-th unpruned hit (m <= current)
+                const int hb = 32 * zw + __builtin_ctz(zm);
+                zm &= zm - 1;
+                if (!bad(hb)) sp_emit(a, dm, c0 + b, wi, x);
+            };
+            for (int wd = 0; wd < kSpWords; wd++) {
+                uint32_t m = bm[wd];
+                while (m) {
+                    const int b = 32 * wd + __builtin_ctz(m);
+                    m &= m - 1;
+                    const double x = boxcar(wi, b);
+                    if (have && b - lpb <= h && lpx > x) continue;     // removed by the last pivot
+                    if (have && b - lpb > h) survivor(lpb, lpx);       // else the new pivot removes it
+                    lpb = b;
+                    lpx = x;
+                    have = true;
+                }
+            }
+            if (have) survivor(lpb, lpx);
+        }
+        __syncthreads();
     }
 }
 
@@ -324,7 +364,7 @@ hipError_t launch_sp_hits(const float* x, int64_t stride, int ndm, int nblocks, 
     a.nwidths = nwidths;
     if (nwidths < 1 || nwidths > 16) return hipErrorInvalidValue;
     for (int i = 0; i < nwidths; i++) {
-        if (widths[i] < 1 || widths[i] / 2 > kSpHalo) return hipErrorInvalidValue;
+        if (widths[i] < 1 || widths[i] / 2 + 1 > kSpHalo) return hipErrorInvalidValue;
         a.widths[i] = widths[i];
         a.rsw[i] = rsw[i];
     }

@@ -8,8 +8,9 @@ The reference runs, for every .dat a pass writes (lib/python/PALFA2_presto_searc
 wall time to job.singlepulse_time and moves <base>_DM<dm>.singlepulse to the work dir.  Here
 the whole search runs in libhipdedisp over the series still in HBM (hd_single_pulse):
 per-block detrend and trimmed std, bad blocks, normalisation, the boxcar hits of every
-downfactor and prune_related1 on the GPU (csrc/hd_sp.hip), prune_related2 and the border
-cases on the host (csrc/hd_api.hip).  This module turns the candidates into the script's
+downfactor, prune_related1 (the script's greedy walk per 8000-sample chunk and width) and its
+bad-block test on the GPU (csrc/hd_sp.hip), prune_related2 and the border cases on the host
+(csrc/hd_api.hip, one thread per DM).  This module turns the candidates into the script's
 `.singlepulse` text: "# DM      Sigma      Time (s)     Sample    Downfact" and one
 "%7.2f %7.2f %13.6f %10d     %3d" line per candidate (the file exists, empty, when a DM has
 none).  [PRESTO-ext] restated; there is no CPU fallback.
@@ -57,15 +58,16 @@ def device_candidates(plan, dt, maxwidth=0.1, threshold=5.0):
     eng = plan.eng
     nb = plan.numout // 1000
     bad = np.zeros((plan.pp.numdms, max(nb, 1)), np.uint8)
-    cap = 1 << 16
+    cap = getattr(eng, "_sp_cap", 1 << 20)                   # room for the device hits (pre prune_related2)
     while True:
-        hits = np.zeros(cap, HIT)
+        hits = np.empty(cap, HIT)
         n, nbk = ctypes.c_int64(), ctypes.c_int64()
         rc = eng._L.hd_single_pulse(plan._p, float(dt), float(maxwidth), float(threshold),
                                     hits.ctypes.data_as(ctypes.c_void_p), cap, ctypes.byref(n),
                                     bad.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), ctypes.byref(nbk))
         if rc == _lib.HD_E_NOMEM and n.value > cap:           # room for every device hit
-            cap = int(n.value)
+            cap = int(n.value) + int(n.value) // 4
+            eng._sp_cap = cap
             continue
         eng._chk(rc, "single_pulse_search.py")
         return hits[:n.value], bad[:, :nb]

@@ -206,54 +206,72 @@ def test_time_slices_halo_covers_every_pass():
             assert last_row < nloc
 
 
-class _FakeSliceEngine:
-    """Stands in for a sliced Engine in the exchange test: per-block statistics are a known
-    function of the global block index."""
-
-    def __init__(self, t0, blk, nchan):
-        self.t0, self.blk, self.nchan = t0, blk, nchan
-
-    def clip_stats(self, nown, table):
-        g0 = self.t0 // self.blk
-        for b in range(nown):
-            table[g0 + b] = (g0 + b) * 1000.0 + np.arange(self.nchan + 3)
-
-
 def _slice_worker(rank, world, port, q):
+    """One rank of a sliced beam on CPU: the clip statistics of its own read blocks from its
+    own spectra (the oracle's clip_times rows stand in for hd_clip_stats, same layout), the
+    gloo all-reduce, then clip_times finished over the summed table for its own spectra;
+    the padding sums' all-reduce."""
     import torch
     import torch.distributed as dist
+    import oracle as OR
+    from hipdedisp import Opts
+    from hipdedisp.synth import host_spectra, palfa_synth, synth_mask
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        obs = palfa_obs(N=(1 << 20) + 777, nchan=96)
+        obs, s, pts, mask, pad = _slice_beam()
         ts = S.TimeSlices(obs, P.ddplans_for("pdev"), world)
+        t0, own, nloc = ts.slice(rank)
+        raw = host_spectra(obs, s, t0, nloc)                # this rank's spectra only
         t = torch.zeros((ts.nblk_total, obs.nchan + 3), dtype=torch.float64)
-        ts.contribute_clip_stats(_FakeSliceEngine(ts.slice(rank)[0], ts.blk, obs.nchan), rank, t.numpy())
+        b0, nb = t0 // ts.blk, ts.nown_blocks(rank)
+        t.numpy()[b0:b0 + nb] = OR.clip_rows(obs, Opts(), raw, b0, nb, mask=mask, ptsperint=pts)
         dist.all_reduce(t)                                   # phase A exchange
+        lpad, lclip, k = OR.clip_finish(obs, Opts(), raw[:own], t.numpy(), t0, own, mask=mask, ptsperint=pts,
+                                        padvals=pad)
         sums = torch.tensor([float(rank + 1), 2.0 * (rank + 1)], dtype=torch.float64)
         dist.all_reduce(sums)                                # phase C exchange
-        q.put((rank, t.numpy().copy(), sums.tolist()))
+        q.put((rank, t0, own, lpad, lclip, k, sums.tolist()))
     finally:
         dist.destroy_process_group()
 
 
+def _slice_beam():
+    from hipdedisp.synth import palfa_synth, rfifind_ptsperint, synth_mask
+    obs = palfa_obs(N=(1 << 18) + 3 * 30720 + 777, nbits=8)
+    s = palfa_synth()
+    s.spike_frac, s.spike_amp = 0.003, 40.0                 # zero-DM spikes for clip_times
+    pts = 16384
+    mask, pad = synth_mask(obs, s, pts, frac=0.03)
+    return obs, s, pts, mask, pad
+
+
 def test_time_slice_exchanges_gloo_world2():
-    """The two all-reduces of a sliced beam on gloo at world size 2: the summed clip
-    statistics table has every read block's row exactly once, and the padding sums add."""
+    """The two all-reduces of a sliced beam on gloo at world size 2, on real clip_times
+    statistics: each rank's pad values and clip flags after the exchange equal clip_times
+    over the whole beam (oracle.prepare), and the padding sums add."""
     import torch.multiprocessing as mp
+    import oracle as OR
+    from hipdedisp import Opts
+    from hipdedisp.synth import host_spectra
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_slice_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=120) for _ in procs]
+    res = [q.get(timeout=240) for _ in procs]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    nblk = res[0][1].shape[0]
-    want = np.arange(nblk)[:, None] * 1000.0 + np.arange(res[0][1].shape[1])[None, :]
-    for rank, table, sums in res:
-        assert np.array_equal(table, want)
+    obs, s, pts, mask, pad = _slice_beam()
+    whole = OR.prepare(obs, Opts(), host_spectra(obs, s), mask=mask, ptsperint=pts, padvals=pad)
+    assert whole.nclipped > 100
+    total = 0
+    for rank, t0, own, lpad, lclip, k, sums in res:
+        assert np.array_equal(lpad, whole.pad), rank          # the recurrence ran over every block
+        assert np.array_equal(lclip, whole.clipped[t0:t0 + own]), rank
+        total += k
         assert sums == [3.0, 6.0]
+    assert total == whole.nclipped

@@ -99,8 +99,9 @@ def test_candidates_find_injected_pulses():
 
 
 def test_candidate_bookkeeping_follows_script():
-    """prune_related1 within a width (local-maximum rule), bad blocks, prune_related2 across
-    widths and border pruning on a padded series, on a hand-made hit list."""
+    """prune_related1 within a width (the greedy walk), the script's bad-block zip (survivor m
+    takes the block of the m-th unpruned hit), prune_related2 across widths and border
+    pruning on a padded series, on a hand-made hit list."""
     rows = [(0, 100, 0, 6.0), (0, 5000, 0, 5.5),                 # width 1
             (0, 101, 1, 7.0), (0, 102, 1, 6.5),                 # width 2: 102 within 1 of 101 -> pruned
             (0, 2990, 2, 8.0), (0, 2991, 2, 8.5), (0, 4000, 2, 6.0),   # width 3, blocks 2, 2, 4
@@ -112,35 +113,85 @@ def test_candidate_bookkeeping_follows_script():
     bad[0, 2] = 1
     cl = OR.sp_candidates(hits, bad, [1, 2, 3], [5.0], 1e-3, nds=7995, numout=8000)[0]
     got = [(c.bin, c.downfact) for c in cl]
-    # width 3: 2990 loses to 2991, which sits in the bad block 2; 100 (w1, 6.0) loses to
-    # 101 (w2, 7.0) within max(1, 1, 1); 7999 (w3) reaches the padding after nds - 1 = 7994
-    assert got == [(101, 2), (4000, 3), (5000, 1), (7990, 2)]
+    # width 3: 2990 loses to 2991; the survivors 2991, 4000, 7999 are zipped with the blocks
+    # of the unpruned hits 2990, 2991, 4000 -> blocks 2, 2, 4: 2991 and 4000 both read the bad
+    # block 2 (the script's quirk), 7999 reads block 4 and reaches the padding after
+    # nds - 1 = 7994; 100 (w1, 6.0) loses to 101 (w2, 7.0) within max(1, 1, 1)
+    assert got == [(101, 2), (5000, 1), (7990, 2)]
 
 
-def test_prune_related1_local_max_equals_greedy_walk_on_peaks():
-    """On separated peaks (and on the chains the script's walk resolves), the local-maximum
-    rule keeps what the greedy walk of prune_related1 keeps."""
-    def greedy(bins, vals, downfact):
-        gone = set()
-        for ii in range(len(bins) - 1):
-            if ii in gone:
+def greedy_walk(bins, vals, downfact):
+    """prune_related1 of single_pulse_search.py, transcribed (kept bins)."""
+    gone = set()
+    for ii in range(len(bins) - 1):
+        if ii in gone:
+            continue
+        for jj in range(ii + 1, len(bins)):
+            if abs(bins[jj] - bins[ii]) > downfact // 2:
+                break
+            if jj in gone:
                 continue
-            for jj in range(ii + 1, len(bins)):
-                if abs(bins[jj] - bins[ii]) > downfact // 2:
-                    break
-                if jj in gone:
-                    continue
-                gone.add(jj if vals[ii] > vals[jj] else ii)
-        return [b for k, b in enumerate(bins) if k not in gone]
+            if vals[ii] > vals[jj]:
+                gone.add(jj)
+            else:
+                gone.add(ii)
+    return [b for k, b in enumerate(bins) if k not in gone]
+
+
+def pivot_walk(bins, vals, downfact):
+    """The O(n) form hd_sp.hip's k_sp_hits walks: a hit is a pivot unless the last pivot
+    lies within h = downfact // 2 bins and is strictly stronger; a pivot is kept when the
+    next pivot lies more than h bins after it (or there is none)."""
+    h = downfact // 2
+    out, lp = [], None
+    for b, x in zip(bins, vals):
+        if lp is not None and b - lp[0] <= h and lp[1] > x:
+            continue
+        if lp is not None and b - lp[0] > h:
+            out.append(lp[0])
+        lp = (b, x)
+    if lp is not None:
+        out.append(lp[0])
+    return out
+
+
+def _hit_lists(rng):
+    """Hit lists of one (chunk, width): random sparse/dense bins, monotone chains, wide humps,
+    plateaus with ties, trains of pulses closer than the width."""
+    kind = rng.integers(0, 5)
+    n = int(rng.integers(1, 400))
+    if kind == 0:                                              # random bins, random values
+        bins = np.sort(rng.choice(2000, size=min(n, 2000), replace=False))
+        vals = rng.normal(7.0, 1.0, len(bins)).round(int(rng.integers(0, 3)))
+    elif kind == 1:                                            # one falling / rising chain
+        bins = np.arange(n) + 5
+        vals = 10.0 - 0.01 * np.arange(n) if rng.integers(0, 2) else 5.0 + 0.01 * np.arange(n)
+    elif kind == 2:                                            # humps longer than the width
+        c = np.arange(n)
+        vals = 8.0 + 3.0 * np.sin(c / rng.uniform(2.0, 40.0)) ** 2
+        bins = c[vals > 8.5]
+        vals = vals[vals > 8.5]
+    elif kind == 3:                                            # plateaus: many equal values
+        bins = np.sort(rng.choice(600, size=min(n, 600), replace=False))
+        vals = rng.integers(5, 8, len(bins)).astype(np.float64)
+    else:                                                      # a pulse train, gaps in it
+        per = int(rng.integers(2, 80))
+        c = np.arange(2000)
+        vals = 6.0 + 4.0 * np.exp(-((c % per) - per / 2) ** 2 / rng.uniform(0.5, 30.0)) + rng.normal(0, 0.3, c.size)
+        bins, vals = c[vals > 7.0], vals[vals > 7.0]
+    return [int(b) for b in bins], [float(v) for v in vals]
+
+
+def test_prune_related1_walks_agree():
+    """The script's walk (transcribed here), the oracle's C transcription and the device's
+    O(n) pivot form keep the same hits on monotone chains, wide humps, ties, dense trains."""
     rng = np.random.default_rng(5)
-    for trial in range(200):
-        w = int(rng.choice([2, 3, 4, 6, 9, 14, 20]))
-        centres = np.sort(rng.choice(5000, 12, replace=False)) * (w + 3)
-        bins, vals = [], []
-        for c in centres:                                     # one peak per cluster
-            width = int(rng.integers(1, w + 1))
-            for k in range(width):
-                bins.append(int(c + k))
-                vals.append(10.0 - abs(k - width // 2) - 0.01 * k)
-        keep = OR._prune_related1_localmax(np.array(bins), np.array(vals), w // 2, max(bins) + 1)
-        assert [b for b, k in zip(bins, keep) if k] == greedy(bins, vals, w)
+    for trial in range(600):
+        w = int(rng.choice([2, 3, 4, 6, 9, 14, 20, 30, 45, 70, 100, 150, 220, 300]))
+        bins, vals = _hit_lists(rng)
+        want = greedy_walk(bins, vals, w)
+        keep = OR.prune_related1(np.array(bins, np.int32), np.array(vals), w)
+        assert [b for b, k in zip(bins, keep) if k] == want, (trial, w)
+        assert pivot_walk(bins, vals, w) == want, (trial, w)
+    # the advisor's example: 10, 9, 8 at consecutive bins with downfact 2 keeps bins 0 and 2
+    assert greedy_walk([0, 1, 2], [10.0, 9.0, 8.0], 2) == [0, 2] == pivot_walk([0, 1, 2], [10.0, 9.0, 8.0], 2)
