@@ -139,10 +139,10 @@ def single_pulse_leg(eng, stages, beams):
 
 def fft_leg(eng, stages, beams):
     """realfft; zapbirds -zap; rednoise over every DM of the beam (PALFA2_presto_search.py:548-558)
-    on each pass's device-resident series: wall seconds per beam (a 60 Hz mains comb and the
-    PALFA zaplist's 0.0762 Hz family as birdies)."""
+    on each pass's device-resident series: wall seconds per beam, with the reference's own
+    zaplist (lib/zaplists/PALFA.zaplist, committed as tests/golden/palfa_zaplist.json)."""
     from hipdedisp import fft_stage as FS
-    birds = [(60.0 * k, 0.5, False) for k in range(1, 40)] + [(0.07618684 * k, 0.003, False) for k in range(1, 200)]
+    birds = [tuple(b) for b in json.load(open(os.path.join(ROOT, "tests", "golden", "palfa_zaplist.json")))["birdies"]]
     bins = {}
 
     def beam():
@@ -164,7 +164,7 @@ def fft_leg(eng, stages, beams):
         beam()
     s = (time.perf_counter() - t) / beams
     return {"s_per_beam": s, "first_beam_s": first,
-            "note": "hd_realfft + hd_zapbirds (238 birdies) + hd_rednoise over the 57 passes' series in HBM "
+            "note": "hd_realfft + hd_zapbirds (the 221 PALFA.zaplist birdies) + hd_rednoise over the 57 passes' series in HBM "
                     "(spectra stay on the device); wall time with the plans' FFT state built (first_beam_s: "
                     "including the hipFFT plan builds and buffer allocation)"}
 

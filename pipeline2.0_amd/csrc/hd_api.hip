@@ -2523,9 +2523,13 @@ extern "C" int hd_write_series(hd_plan* p, const char* const* paths, int32_t wai
     if (!p->ev_copy) HIPCHK(c, hipEventCreateWithFlags(&p->ev_copy, hipEventDisableTiming));
     std::string err;
     int rc = hd::writer_series(c->writer, p->ev[3], p->d_out, p->out_stride, p->pass.numdms, p->numout, paths, err);
-    if (rc == 0) {
-        HIPCHK(c, hipEventRecord(p->ev_copy, hd::writer_stream(c->writer)));
-        p->copy_pending = true;
+    // even after a failure part-way (a file that cannot be created, a copy that fails), the
+    // chunks queued before it keep copying from p->d_out: a later hd_run_dedisp of this plan
+    // must wait for them, so the copy event is recorded whatever rc is
+    {
+        const hipError_t e = hipEventRecord(p->ev_copy, hd::writer_stream(c->writer));
+        if (e == hipSuccess) p->copy_pending = true;
+        if (e != hipSuccess && rc == 0) HIPCHK(c, e);
     }
     if (rc) return fail(c, rc, "hd_write_series: %s", err.c_str());
     if (wait) return hd_wait_writes(c, nullptr, nullptr);
@@ -2697,7 +2701,9 @@ extern "C" int hd_get_fft(hd_plan* p, int32_t dm0, int32_t ndm, float* out)
     HIPCHK(c, hipSetDevice(c->device));
     hipStream_t st = p->dd_stream ? p->dd_stream : c->stream;
     const int64_t fs = p->numout / 2 + 1;
+    HIPCHK(c, hd::fft_begin(p->fft, st));          // after the last op on the shared spectra
     HIPCHK(c, d2h_2d(out, sizeof(float) * p->numout, hd::fft_buffer(p->fft) + (size_t)dm0 * fs,
                      sizeof(float2) * fs, sizeof(float) * p->numout, ndm, st));
+    HIPCHK(c, hd::fft_end(p->fft, st));
     return HD_OK;
 }

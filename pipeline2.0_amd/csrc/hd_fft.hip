@@ -174,6 +174,10 @@ struct FftState {
     int32_t* d_boff = nullptr;
     double* d_cen = nullptr;
     size_t rng_cap = 0, med_cap = 0, boff_cap = 0, cen_cap = 0;
+    // plans of the same geometry share this state from different stage-2 streams: every op
+    // on it waits for the last one's event and records its own (fft_begin / fft_end)
+    hipEvent_t done = nullptr;
+    bool pending = false;
 };
 
 FftState* fft_state_new() { return new FftState(); }
@@ -181,6 +185,8 @@ FftState* fft_state_new() { return new FftState(); }
 void fft_state_free(FftState* s)
 {
     if (!s) return;
+    if (s->pending) (void)hipEventSynchronize(s->done);
+    if (s->done) (void)hipEventDestroy(s->done);
     if (s->have_plan) hipfftDestroy(s->plan);
     (void)hipFree(s->d_fft);
     (void)hipFree(s->d_rng);
@@ -197,9 +203,30 @@ void fft_set_owner(FftState* s, const void* owner)
     if (s) s->owner = owner;
 }
 
+// Order work on the shared state after the previous op (whatever its stream) / record its end.
+hipError_t fft_begin(FftState* s, hipStream_t st)
+{
+    if (!s->done) {
+        hipError_t e = hipEventCreateWithFlags(&s->done, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+    }
+    return s->pending ? hipStreamWaitEvent(st, s->done, 0) : hipSuccess;
+}
+
+hipError_t fft_end(FftState* s, hipStream_t st)
+{
+    hipError_t e = hipEventRecord(s->done, st);
+    s->pending = e == hipSuccess;
+    return e;
+}
+
 hipError_t fft_series(FftState* s, const float* x, int64_t xstride, int64_t n, int ndm, hipStream_t st)
 {
     if (n < 4 || (n & 1) || ndm < 1) return hipErrorInvalidValue;
+    {
+        hipError_t e = fft_begin(s, st);
+        if (e != hipSuccess) return e;
+    }
     const int64_t fs = n / 2 + 1;
     if (s->n != n || s->ndm != ndm || !s->d_fft) {
         if (s->have_plan) hipfftDestroy(s->plan);
@@ -221,7 +248,8 @@ hipError_t fft_series(FftState* s, const float* x, int64_t xstride, int64_t n, i
         hipfftExecR2C(s->plan, (hipfftReal*)x, (hipfftComplex*)s->d_fft) != HIPFFT_SUCCESS)
         return hipErrorUnknown;
     hipLaunchKernelGGL(k_fft_pack, dim3((ndm + 63) / 64), dim3(64), 0, st, s->d_fft, fs, n / 2, ndm);
-    return hipGetLastError();
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? fft_end(s, st) : e;
 }
 
 template <class T>
@@ -242,7 +270,8 @@ hipError_t fft_zap(FftState* s, const int32_t* rng4, int nr, hipStream_t st)
 {
     if (!s->d_fft) return hipErrorInvalidValue;
     if (nr == 0) return hipSuccess;
-    hipError_t e = grow(&s->d_rng, &s->rng_cap, (size_t)nr, st);
+    hipError_t e = fft_begin(s, st);
+    if (e == hipSuccess) e = grow(&s->d_rng, &s->rng_cap, (size_t)nr, st);
     if (e == hipSuccess) e = grow(&s->d_med, &s->med_cap, (size_t)nr * s->ndm, st);
     if (e == hipSuccess) e = hipMemcpyAsync(s->d_rng, rng4, sizeof(int4) * nr, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);     // rng4 is the caller's (pageable) memory
@@ -250,13 +279,15 @@ hipError_t fft_zap(FftState* s, const int32_t* rng4, int nr, hipStream_t st)
     const int64_t fs = s->n / 2 + 1;
     hipLaunchKernelGGL(k_zap_median, dim3(nr, s->ndm), dim3(256), 0, st, s->d_fft, fs, s->d_rng, s->d_med, nr);
     hipLaunchKernelGGL(k_zap_apply, dim3(nr, s->ndm), dim3(256), 0, st, s->d_fft, fs, s->d_rng, s->d_med, nr);
-    return hipGetLastError();
+    e = hipGetLastError();
+    return e == hipSuccess ? fft_end(s, st) : e;
 }
 
 hipError_t fft_rednoise(FftState* s, const int32_t* boff, const double* cen, int nblk, hipStream_t st)
 {
     if (!s->d_fft || nblk < 1) return hipErrorInvalidValue;
-    hipError_t e = grow(&s->d_boff, &s->boff_cap, (size_t)nblk + 1, st);
+    hipError_t e = fft_begin(s, st);
+    if (e == hipSuccess) e = grow(&s->d_boff, &s->boff_cap, (size_t)nblk + 1, st);
     if (e == hipSuccess) e = grow(&s->d_cen, &s->cen_cap, (size_t)nblk, st);
     if (e == hipSuccess) e = grow(&s->d_med, &s->med_cap, (size_t)nblk * s->ndm, st);
     if (e == hipSuccess) e = hipMemcpyAsync(s->d_boff, boff, sizeof(int32_t) * (nblk + 1), hipMemcpyHostToDevice, st);
@@ -268,7 +299,8 @@ hipError_t fft_rednoise(FftState* s, const int32_t* boff, const double* cen, int
                        s->ndm, s->d_med);
     hipLaunchKernelGGL(k_red_scale, dim3(nblk, s->ndm), dim3(128), 0, st, s->d_fft, fs, s->d_boff, s->d_cen, nblk,
                        s->ndm, s->d_med);
-    return hipGetLastError();
+    e = hipGetLastError();
+    return e == hipSuccess ? fft_end(s, st) : e;
 }
 
 }  // namespace hd

@@ -181,6 +181,8 @@ hipError_t rfi_stats(const RawDesc& rd, const uint8_t* rawT, int64_t tstride, in
 struct FftState;
 FftState* fft_state_new();
 void fft_state_free(FftState* s);
+hipError_t fft_begin(FftState* s, hipStream_t st);
+hipError_t fft_end(FftState* s, hipStream_t st);
 float2* fft_buffer(FftState* s);
 const void* fft_owner(const FftState* s);
 void fft_set_owner(FftState* s, const void* owner);

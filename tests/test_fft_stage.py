@@ -3,7 +3,9 @@
 reader follows PRESTO's format, and the oracle's numeric steps behave as the tools are meant
 to (white noise normalised to unit mean power, a red-noise slope flattened, birdies replaced
 by the local level).  Parity with PRESTO itself is unpinned (not in this image)."""
+import json
 import math
+import os
 
 import numpy as np
 import pytest
@@ -35,6 +37,49 @@ def test_read_zaplist(tmp_path):
     assert lo[2] == pytest.approx(5975.0) and hi[2] == pytest.approx(6025.0)
     f = 29.946923 / (1 + 1e-4)
     assert lo[3] == pytest.approx((f - 0.01) * 100.0) and hi[3] == pytest.approx((f + 0.01) * 100.0)
+
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "palfa_zaplist.json")
+REF_ZAPLIST = "/root/reference/lib/zaplists/PALFA.zaplist"
+
+
+def palfa_birdies():
+    return [(f, w, b) for f, w, b in json.load(open(GOLDEN))["birdies"]]
+
+
+def test_palfa_zaplist_fixture_shape():
+    """The reference's PALFA.zaplist (lib/zaplists/, the default zaplist of search_job,
+    PALFA2_presto_search.py:472-474, 548-553) as committed: 226 lines, 5 comments, 221
+    topocentric birdies -- the 0.0762/0.0832 Hz families and the 60 Hz mains comb."""
+    g = json.load(open(GOLDEN))
+    assert g["lines"] == 226 and g["comment_lines"] == 5
+    birds = palfa_birdies()
+    assert len(birds) == 221 and not any(b for _, _, b in birds)
+    assert birds[0] == (0.07618684, 0.003, False) and birds[-1] == (300.0, 0.5, False)
+    assert [(f, w) for f, w, _ in birds[-5:]] == [(60.0, 0.1), (120.0, 0.2), (180.0, 0.3), (240.0, 0.4), (300.0, 0.5)]
+
+
+def test_read_zaplist_palfa(tmp_path):
+    """read_zaplist on the reference's file (when the reference is present) and on the same
+    lines rewritten from the fixture (with a 'B' line added) gives the fixture's birdies."""
+    if os.path.exists(REF_ZAPLIST):
+        assert FS.read_zaplist(REF_ZAPLIST) == palfa_birdies()
+    p = tmp_path / "PALFA.zaplist"
+    body = "".join("%22r%22r\n" % (f, w) for f, w, _ in palfa_birdies())
+    p.write_text("# Freq Width\n" + body + "B 29.946923 0.02\n")
+    assert FS.read_zaplist(str(p)) == palfa_birdies() + [(29.946923, 0.02, True)]
+
+
+def test_palfa_zaplist_ranges_match_oracle():
+    """The PALFA birdies of a C2 stage-0 series (2^22 x 65.476 us) and of a ds-10 series as
+    merged bin ranges: library == oracle; the 60 Hz comb lands at its bins."""
+    for n, dt in ((1 << 22, 65.476e-6), (419432, 654.76e-6)):
+        T = n * dt
+        lo, hi = FS.birdie_bins(palfa_birdies(), T, baryv=0.0)
+        got = FS.zap_ranges(lo, hi, n // 2)
+        assert np.array_equal(got, FO.zap_ranges(lo, hi, n // 2))
+        k60 = int(math.floor((60.0 - 0.05) * T))
+        assert any(r[0] <= k60 < r[1] for r in got)
 
 
 @pytest.mark.parametrize("seed", [0, 1, 2])

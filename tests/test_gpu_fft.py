@@ -84,6 +84,34 @@ def test_fft_zap_rednoise_match_oracle(engine, beam, ds, numdms, tmp_path):
         p.destroy()
 
 
+def test_zapbirds_palfa_zaplist_matches_oracle(engine, beam):
+    """zapbirds with the reference's own zaplist (lib/zaplists/PALFA.zaplist, committed as
+    tests/golden/palfa_zaplist.json): every one of its 221 birdies zapped on the device
+    exactly as the oracle zaps the device's own spectrum."""
+    import json
+    import os
+    g = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "palfa_zaplist.json")))
+    birdies = [tuple(b) for b in g["birdies"]]
+    pp = PassParams(subdm=71.0, lodm=65.0, dmstep=0.5, numdms=8, nsub=96, ds=1, numout=beam.N)
+    p = engine.plan(pp)
+    try:
+        p.run_subband()
+        p.run_dedisp(to_host=False)
+        T = p.numout * p.sub_dt
+        FS.realfft(p)
+        F0 = FS.spectra_complex(FS.get_fft(p))
+        nb = p.numout // 2
+        lo, hi = FS.birdie_bins(birdies, T, baryv=0.0)
+        r = FS.zap_ranges(lo, hi, nb)
+        assert len(r) > 100
+        FS.zapbirds(p, lo, hi)
+        F1 = FS.spectra_complex(FS.get_fft(p))
+        assert np.array_equal(F1, FO.zap(F0, r))
+        assert not np.array_equal(F1, F0)
+    finally:
+        p.destroy()
+
+
 def test_run_fft_writes_packed_files(engine, beam, tmp_path):
     obs = beam
     d = P.ddplans_for("pdev")[1]
