@@ -103,7 +103,7 @@ def test_zapbirds_palfa_zaplist_matches_oracle(engine, beam):
         nb = p.numout // 2
         lo, hi = FS.birdie_bins(birdies, T, baryv=0.0)
         r = FS.zap_ranges(lo, hi, nb)
-        assert len(r) > 100
+        assert len(r) >= 20                          # the low-frequency families merge
         FS.zapbirds(p, lo, hi)
         F1 = FS.spectra_complex(FS.get_fft(p))
         assert np.array_equal(F1, FO.zap(F0, r))
