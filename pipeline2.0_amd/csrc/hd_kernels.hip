@@ -760,7 +760,6 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
     cadd0 = __builtin_amdgcn_readfirstlane(cadd0);
     cadd1 = __builtin_amdgcn_readfirstlane(cadd1);
     cadd2 = __builtin_amdgcn_readfirstlane(cadd2);
-    const bool fast_out = a.sub_dtype == 0 && !mean;      // int16 sums stored as they are
     // channel delays of pass p live in lanes 0..CPS-1 of vd; pass p+1's are loaded while
     // pass p is formed, so no global-load latency sits at the head of a pass
     // (unconditional, clamped loads: a branch around them would cost a vmcnt(0) drain)
@@ -781,32 +780,88 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
         int amax = 0;
         if (intpath) {
             uint32_t ae[M], ao[M];
+            if (brow >= (1 << 30)) {                   // uniform: the tile lies in one read block
+                const uint32_t kk = (uint32_t)cadd0 | ((uint32_t)cadd0 << 16);
 #pragma unroll
-            for (int m = 0; m < M; m++) {
-                // quarter q of output j: the constant of the block its last row lies in
-                const int lastrow = (lane + 64 * m) * DS + DS - 1 + dmx;
-                auto kof = [&](int row) {
-                    return (uint32_t)(row < brow ? cadd0 : (!THREE || row < brow2) ? cadd1 : cadd2);
-                };
-                const uint32_t k0 = kof(lastrow), k1 = kof(lastrow + S), k2 = kof(lastrow + 2 * S),
-                               k3 = kof(lastrow + 3 * S);
-                ae[m] = k0 | (k2 << 16);
-                ao[m] = k1 | (k3 << 16);
+                for (int m = 0; m < M; m++) ae[m] = ao[m] = kk;
+            } else {
+#pragma unroll
+                for (int m = 0; m < M; m++) {
+                    // quarter q of output j: the constant of the block its last row lies in
+                    const int lastrow = (lane + 64 * m) * DS + DS - 1 + dmx;
+                    auto kof = [&](int row) {
+                        return (uint32_t)(row < brow ? cadd0 : (!THREE || row < brow2) ? cadd1 : cadd2);
+                    };
+                    const uint32_t k0 = kof(lastrow), k1 = kof(lastrow + S), k2 = kof(lastrow + 2 * S),
+                                   k3 = kof(lastrow + 3 * S);
+                    ae[m] = k0 | (k2 << 16);
+                    ao[m] = k1 | (k3 << 16);
+                }
             }
+            // the channel sums, branch-free so every LDS read of the pass can be in flight
+            // before the first add; channels masked in every block of the tile (their pads are
+            // in the constants) are ANDed away by a uniform mask
+            if (zall == 0) {
+                // all reads of a group of channels first (a scheduling barrier keeps the
+                // compiler from interleaving a wait after every read pair), then the adds
+                constexpr int PER = M * DS, CG = PER * CPS <= 48 ? CPS : (CPS + 1) / 2;
 #pragma unroll
-            for (int cc = 0; cc < CPS; cc++) {
-                if (zall & (1u << cc)) continue;       // masked channel: its pads are in the constants
-                const uint32_t* b = lbase + lrb[cc] + dl[cc];
+                for (int c0g = 0; c0g < CPS; c0g += CG) {
+                    uint32_t xs[CG * PER];
 #pragma unroll
-                for (int m = 0; m < M; m++)
+                    for (int cc = 0; cc < CG; cc++) {
+                        const uint32_t* b = lbase + lrb[min(c0g + cc, CPS - 1)] + dl[min(c0g + cc, CPS - 1)];
 #pragma unroll
-                    for (int k = 0; k < DS; k++) {
-                        const uint32_t x = b[m * 64 * DS + k];
-                        ae[m] += x & 0x00FF00FFu;                              // quarters 0, 2
-                        ao[m] += __builtin_amdgcn_perm(0u, x, 0x0c030c01u);    // quarters 1, 3
+                        for (int m = 0; m < M; m++)
+#pragma unroll
+                            for (int k = 0; k < DS; k++) xs[cc * PER + m * DS + k] = b[m * 64 * DS + k];
                     }
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int cc = 0; cc < CG; cc++) {
+                        if (c0g + cc >= CPS) break;
+#pragma unroll
+                        for (int m = 0; m < M; m++)
+#pragma unroll
+                            for (int k = 0; k < DS; k++) {
+                                const uint32_t x = xs[cc * PER + m * DS + k];
+                                ae[m] += x & 0x00FF00FFu;                              // quarters 0, 2
+                                ao[m] += __builtin_amdgcn_perm(0u, x, 0x0c030c01u);    // quarters 1, 3
+                            }
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int cc = 0; cc < CPS; cc++) {
+                    const uint32_t keep = ((zall >> cc) & 1u) ? 0u : 0xFFFFFFFFu;
+                    const uint32_t* b = lbase + lrb[cc] + dl[cc];
+#pragma unroll
+                    for (int m = 0; m < M; m++)
+#pragma unroll
+                        for (int k = 0; k < DS; k++) {
+                            const uint32_t x = b[m * 64 * DS + k] & keep;
+                            ae[m] += x & 0x00FF00FFu;
+                            ao[m] += __builtin_amdgcn_perm(0u, x, 0x0c030c01u);
+                        }
+                }
             }
-            if (fast_out) {   // int16 sums (< 32768: host check): store the u16 halves directly
+            if (a.sub_dtype == 0) {
+                // int16 outputs, stored from the packed halves; mean mode divides each 16-bit
+                // half by DS exactly (v = kD + r < 2^16: v * fl(1/D) + 0.5/D stays within
+                // 0.5/D - 2^-7 of k + (r + 0.5)/D, so truncation gives k)
+                if (mean && DS > 1) {
+                    const float inv = 1.0f / (float)DS, half = 0.5f / (float)DS;
+                    auto divpk = [&](uint32_t v) {
+                        const uint32_t lo = (uint32_t)((float)(v & 0xFFFFu) * inv + half);
+                        const uint32_t hi = (uint32_t)((float)(v >> 16) * inv + half);
+                        return lo | (hi << 16);
+                    };
+#pragma unroll
+                    for (int m = 0; m < M; m++) {
+                        ae[m] = divpk(ae[m]);
+                        ao[m] = divpk(ao[m]);
+                    }
+                }
                 u16x2 mx = {0, 0};
                 int16_t* o = (int16_t*)a.out[p] + (int64_t)s * a.ostride[p] + tO0 + lane;
 #pragma unroll
