@@ -1947,6 +1947,9 @@ static int run_subband_chunk(hd_ctx* c, hd_plan** plans, int n)
     const bool clip = c->opts.clip_sigma > 0.0f;
     if (q8) {
         m.probe = p0->probe;
+        // clipped-spectrum and block-boundary outputs recomputed inside k_stage1_q8 (probe bits
+        // 5-7 keep the separate fixup kernels for cross-checks)
+        m.qfix = clip && !(p0->probe & (32 | 64 | 128)) ? 1 : 0;
         m.rd = raw_desc(c);
         m.rawT = rawT;
         if (!m.rawT && c->obs.nbits != 8) return fail(c, HD_E_HIP, "stage 1: 4-bit channel-major copy failed");
@@ -1988,9 +1991,11 @@ static int run_subband_chunk(hd_ctx* c, hd_plan** plans, int n)
             }
             HIPCHK(c, hd::launch_stage1_tiled(f, fvw, d_sp, nsp, true, c->stream));
         }
-        // clipped spectra, and the block-boundary outputs of the per-block pad constants
-        // (probe bits 5/6 skip the boundary / clipped-spectrum items: profiling only)
-        if (clip && !(p0->probe & 64))
+        // clipped spectra, and the block-boundary outputs of the per-block pad constants, when
+        // k_stage1_q8 did not redo them itself (probe bits 5/6 skip the boundary /
+        // clipped-spectrum items: profiling only)
+        if (m.qfix) {
+        } else if (clip && !(p0->probe & 64))
             HIPCHK(c, hd::launch_stage1_fixup(m, c->clip.events, c->clip.nevents,
                                               m.rd.zidx != nullptr && !(p0->probe & 32), c->stream));
         else if (clip && !(p0->probe & 32) && m.rd.zidx)

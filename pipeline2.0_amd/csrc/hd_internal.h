@@ -56,6 +56,8 @@ struct Stage1Multi {
     int32_t W;                // 8-bit integer path: LDS dwords per channel row (>= S + dmax)
     int32_t two_ok;           // read-block boundaries a non-special tile may straddle (0, 1; q8 ds >= 10: 2)
     int32_t probe;            // profiling only: bit0 skip subband formation, bit1 skip fill
+    int32_t qfix;             // 8-bit integer path: recompute clipped-spectrum / read-block-boundary
+                              // outputs inside k_stage1_q8 (no separate fixup launch)
     double tie_eps;           // 8-bit integer path: margin the rounding of a masked subband's pad
                               // constant needs (float-fold error, plus the /ds rounding in mean mode)
     int32_t ntiles, ngroups;

@@ -159,9 +159,10 @@ __device__ __forceinline__ float s1_sample(const Stage1Multi& a, const uint8_t* 
         x = (st.zap[cc] & (second ? 2 : 1)) ? (second ? st.pad1[cc] : st.pad0[cc]) : x;
     } else if (MODE == kModeGen) {
         const int row = jk + st.dly[cc];
-        const int b = livr[row];
+        const int lv = livr[row];
+        const int b = lv & 0x3FFFFFFF;
         const int c = st.zap[cc];
-        if ((TAIL && row >= rows_valid) || zap_at(a.rd, b, c)) x = pad_at(a.rd, b, c);
+        if ((TAIL && row >= rows_valid) || (lv >> 30) || zap_at(a.rd, b, c)) x = pad_at(a.rd, b, c);
     }   // kModeClean: no mask logic at all
     return x;
 }
@@ -260,8 +261,15 @@ void k_stage1_tiled(Stage1Multi a, const int* __restrict__ special_tiles)
         mode = b_last == b0 ? kModeFast : (b_last == b0 + 1 ? kModeTwo : kModeGen);
     }
     if (SPECIAL && tail) mode = kModeGen;          // rows past N read the last block's pads
+    // the special tiles of the 8-bit integer path replace clipped spectra themselves (that
+    // path has no separate fixup launch): GEN mode, bit 30 of the row table = clipped
+    const bool sp_clip = SPECIAL && a.qfix && a.rd.clipped;
+    if (sp_clip) mode = kModeGen;
     if (SPECIAL && mode == kModeGen)
-        for (int r = threadIdx.x; r < rows; r += blockDim.x) livr[r] = (int)blk_of(a.rd, tR0 + r);
+        for (int r = threadIdx.x; r < rows; r += blockDim.x) {
+            const int64_t t = tR0 + r;
+            livr[r] = (int)blk_of(a.rd, t) | (sp_clip && t < a.rd.N && a.rd.clipped[t] ? (1 << 30) : 0);
+        }
 
     // ---- fill: VW-byte global loads, dword LDS stores
     {
@@ -668,6 +676,27 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
                 }
         }
     }
+    // in-kernel fixup state (qfix): [clip bits of the tile's rows][pads [3][G]][zap bits [G]]
+    const int rows_t = 4 * S + a.dmax;
+    const int nwc = (rows_t + 31) >> 5;
+    uint32_t* cflag = lds + G * W;
+    float* fpad = (float*)(cflag + nwc);
+    uint8_t* fzb = (uint8_t*)(fpad + 3 * G);
+    __shared__ int amax_fix[kMaxPass];
+    __shared__ uint8_t fneed[8];                          // per subband: bit b = boundary b needs outputs redone
+    if (a.qfix) {
+        for (int w = threadIdx.x; w < nwc; w += blockDim.x) {
+            uint32_t bits = 0;
+            if (a.rd.clipped)
+                for (int b = 0; b < 32; b++) {
+                    const int r = 32 * w + b;
+                    if (r < rows_t && a.rd.clipped[tR0 + r]) bits |= 1u << b;
+                }
+            cflag[w] = bits;
+        }
+        if (threadIdx.x < kMaxPass) amax_fix[threadIdx.x] = 0;
+        if (threadIdx.x < 8) fneed[threadIdx.x] = 0;
+    }
     __syncthreads();
 
     // ---- per-wave subband state: wave w serves subband w / wps and passes p = w % wps (mod
@@ -676,15 +705,8 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
     const int wps = q8_waves_per_subband(a);
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int sl = wv / wps, pw = wv - sl * wps;
-    if (sl >= a.sg) return;                               // fill-only waves (no barrier follows)
     const int lane = threadIdx.x & 63;
-    const int s = g * a.sg + sl;
-    const int cl0 = sl * CPS;
-    int lrb[CPS];
-    float pad0[CPS], pad1[CPS], pad2[THREE ? CPS : 1];
-    // read blocks: the tile lies in block b0, or straddles b0 | b0+1 at row brow (and, for
-    // THREE, b0+1 | b0+2 at row brow2: the 2560-row tiles of ds >= 6 outgrow a 2048-row block)
-    uint32_t z0 = 0, z1 = 0, z2 = 0;
+    // brow / brow2: the tile's read-block boundaries (tile-relative rows), uniform per workgroup
     int brow = 1 << 30, brow2 = 1 << 30;
     const int64_t b0 = tR0 / a.rd.blk;
     {
@@ -692,6 +714,15 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
         if (b < 4 * S + a.dmax) brow = (int)b;
         if (THREE && b + a.rd.blk < 4 * S + a.dmax) brow2 = (int)(b + a.rd.blk);
     }
+    const bool mean = a.ds_mode == 1;
+    if (sl < a.sg) {                                      // waves past sg only filled
+    const int s = g * a.sg + sl;
+    const int cl0 = sl * CPS;
+    int lrb[CPS];
+    float pad0[CPS], pad1[CPS], pad2[THREE ? CPS : 1];
+    // read blocks: the tile lies in block b0, or straddles b0 | b0+1 at row brow (and, for
+    // THREE, b0+1 | b0+2 at row brow2: the 2560-row tiles of ds >= 6 outgrow a 2048-row block)
+    uint32_t z0 = 0, z1 = 0, z2 = 0;
     const int64_t b1 = brow < (1 << 30) ? b0 + 1 : b0;
     const int64_t b2 = brow2 < (1 << 30) ? b0 + 2 : b1;
 #pragma unroll
@@ -713,7 +744,6 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
     const uint32_t zany = z0 | z1 | z2, zall = z0 & z1 & z2, zsplit = (z0 ^ z1) | (z1 ^ z2);
     const int fz = zany ? __builtin_ctz(zany) : CPS;      // first channel off the integer path
     const uint32_t* lbase = lds + lane * DS;
-    const bool mean = a.ds_mode == 1;
     // Masked channels without a float fold.  With int16 output, a subband whose masked
     // channels are the same in both blocks of the tile outputs Q(D(F)), F = the oracle's float
     // fold of integers and pad values, D = /DS (mean) or identity (sum), Q = floor(x + 1/2)
@@ -760,6 +790,37 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
     cadd0 = __builtin_amdgcn_readfirstlane(cadd0);
     cadd1 = __builtin_amdgcn_readfirstlane(cadd1);
     cadd2 = __builtin_amdgcn_readfirstlane(cadd2);
+    if (a.qfix && pw == 0) {
+        // the fixup phase below folds single outputs of any subband of the tile: its channels'
+        // pads and zap flags per block slot; and whether the integer path's per-block
+        // constants are wrong for outputs straddling a boundary (a channel masked in both
+        // blocks whose pads differ)
+        if (lane < CPS) {
+            const int cc = lane, lc = cl0 + cc;
+            float q0 = pad0[0], q1 = pad1[0], q2 = THREE ? pad2[0] : pad1[0];
+#pragma unroll
+            for (int k = 1; k < CPS; k++)
+                if (cc == k) {
+                    q0 = pad0[k];
+                    q1 = pad1[k];
+                    q2 = THREE ? pad2[k] : pad1[k];
+                }
+            fpad[lc] = q0;
+            fpad[G + lc] = q1;
+            fpad[2 * G + lc] = q2;
+            fzb[lc] = (uint8_t)(((z0 >> cc) & 1u) | (((z1 >> cc) & 1u) << 1) | (((z2 >> cc) & 1u) << 2));
+        }
+        if (lane == 0 && intpath) {
+            uint8_t nd = 0;
+#pragma unroll
+            for (int cc = 0; cc < CPS; cc++)
+                if (zall & (1u << cc)) {
+                    if (brow < (1 << 30) && pad0[cc] != pad1[cc]) nd |= 1;
+                    if (THREE && brow2 < (1 << 30) && pad1[cc] != pad2[THREE ? cc : 0]) nd |= 2;
+                }
+            fneed[sl] = nd;
+        }
+    }
     // channel delays of pass p live in lanes 0..CPS-1 of vd; pass p+1's are loaded while
     // pass p is formed, so no global-load latency sits at the head of a pass
     // (unconditional, clamped loads: a branch around them would cost a vmcnt(0) drain)
@@ -789,8 +850,11 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
                 for (int m = 0; m < M; m++) {
                     // quarter q of output j: the constant of the block its last row lies in
                     const int lastrow = (lane + 64 * m) * DS + DS - 1 + dmx;
-                    auto kof = [&](int row) {
-                        return (uint32_t)(row < brow ? cadd0 : (!THREE || row < brow2) ? cadd1 : cadd2);
+                    const uint32_t k0c = (uint32_t)cadd0, k1c = (uint32_t)cadd1, k2c = (uint32_t)cadd2;
+                    const int br1 = brow, br2 = brow2;
+                    // arithmetic select (a ?: chain becomes a scratch lookup table at ds >= 10)
+                    auto kof = [=](int row) {
+                        return k0c + (row >= br1 ? k1c - k0c : 0u) + (THREE && row >= br2 ? k2c - k1c : 0u);
                     };
                     const uint32_t k0 = kof(lastrow), k1 = kof(lastrow + S), k2 = kof(lastrow + 2 * S),
                                    k3 = kof(lastrow + 3 * S);
@@ -804,7 +868,7 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
             if (zall == 0) {
                 // all reads of a group of channels first (a scheduling barrier keeps the
                 // compiler from interleaving a wait after every read pair), then the adds
-                constexpr int PER = M * DS, CG = PER * CPS <= 48 ? CPS : (CPS + 1) / 2;
+                constexpr int PER = M * DS, CG = PER * CPS <= 40 ? CPS : (40 / PER < 1 ? 1 : 40 / PER);
 #pragma unroll
                 for (int c0g = 0; c0g < CPS; c0g += CG) {
                     uint32_t xs[CG * PER];
@@ -944,9 +1008,122 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
         vd = vd_next;
     }
     if (a.sub_dtype == 0 && lane < a.npass) publish_max(a.maxabs[lane], pmax);
+    }                                                     // per-wave section
+
+    if (!a.qfix) return;                                  // uniform
+    // ---- fixup phase: every output of the tile that a clipped spectrum touches, and (integer
+    //      path) every output whose rows straddle a read-block boundary where a masked
+    //      channel's pads differ, recomputed as the oracle's exact float fold from the tile
+    //      still in LDS.  Tasks are spread over all threads with their pass index per lane.
+    //      Ordering: this wave's integer stores have landed in L2 before the barrier, so the
+    //      fixup store of the same element (from any wave of the workgroup) lands after them.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int nthr = blockDim.x;
+    auto fold_store = [&](int p, int sl2, int jt, const int* dd) {
+        const int q = jt / JQ, jq = jt - q * JQ;
+        float acc = 0.0f;
+        for (int k = 0; k < DS; k++) {
+            float sk = 0.0f;
+#pragma unroll
+            for (int cc = 0; cc < CPS; cc++) {
+                const int lc = sl2 * CPS + cc;
+                const int lr = a.rd.flip ? G - 1 - lc : lc;
+                const int row = jt * DS + k + dd[cc];                    // tile-relative raw row
+                const uint32_t wd = lds[lr * W + jq * DS + k + dd[cc]];
+                const float xb = (float)((wd >> (8 * q)) & 0xFFu);
+                const int slot = row < brow ? 0 : (!THREE || row < brow2) ? 1 : 2;
+                const bool rep = ((cflag[row >> 5] >> (row & 31)) & 1u) || ((fzb[lc] >> slot) & 1u);
+                sk += rep ? fpad[slot * G + lc] : xb;
+            }
+            acc += sk;
+        }
+        if (mean) acc = acc / (float)DS;
+        const int s2 = g * a.sg + sl2;
+        if (a.sub_dtype == 0) {
+            const int16_t v = to_i16(acc, a.sub_round);
+            ((int16_t*)a.out[p])[(int64_t)s2 * a.ostride[p] + tO0 + jt] = v;
+            const int av = v < 0 ? -(int)v : (int)v;
+            if (av > 0) atomicMax(&amax_fix[p], av);
+        } else {
+            ((float*)a.out[p])[(int64_t)s2 * a.ostride[p] + tO0 + jt] = acc;
+        }
+    };
+    const int np = (a.probe & 1) ? 0 : a.npass;
+    // clipped spectra: per flag word (uniform loop), tasks (pass, set bit, channel of the
+    // tile): the output channel c maps the clipped row to, unless channel c - 1 of its subband
+    // maps it to the same output (delays fall with frequency, so equal outputs are adjacent)
+    for (int w = 0; w < nwc; w++) {
+        const uint32_t word = cflag[w];
+        if (!word) continue;
+        const int nb = __builtin_popcount(word);
+        const int ntask = np * nb * G;
+        for (int t = threadIdx.x; t < ntask; t += nthr) {
+            const int p = t / (nb * G), r2 = t - p * (nb * G);
+            const int i = r2 / G, lc = r2 - i * G;
+            uint32_t wb = word;
+            for (int k = 0; k < i; k++) wb &= wb - 1;
+            const int R = 32 * w + __builtin_ctz(wb);
+            const int sl2 = lc / CPS, cc = lc - sl2 * CPS;
+            const int32_t* dp = a.dly[p] + c0 + sl2 * CPS;
+            const int jn = R - dp[cc];
+            if (jn < 0) continue;
+            const int jt = jn / DS;
+            if (jt >= 4 * JQ) continue;
+            if (cc > 0) {
+                const int jp = R - dp[cc - 1];
+                if (jp >= 0 && jp / DS == jt) continue;
+            }
+            int dd[CPS];
+#pragma unroll
+            for (int k = 0; k < CPS; k++) dd[k] = dp[k];
+            fold_store(p, sl2, jt, dd);
+        }
+    }
+    // read-block boundaries: the outputs whose rows hold both B - 1 and B
+#pragma unroll
+    for (int bi = 0; bi < (THREE ? 2 : 1); bi++) {
+        const int B = bi == 0 ? brow : brow2;
+        if (B >= (1 << 30)) continue;
+        uint32_t anyneed = 0;
+        for (int k = 0; k < a.sg; k++) anyneed |= fneed[k];
+        if (!((anyneed >> bi) & 1u)) continue;
+        const int JB = (a.dmax + DS - 1) / DS + 2;
+        const int ntask = np * a.sg * JB;
+        for (int t = threadIdx.x; t < ntask; t += nthr) {
+            const int p = t / (a.sg * JB), r2 = t - p * (a.sg * JB);
+            const int sl2 = r2 / JB, jj = r2 - sl2 * JB;
+            if (!((fneed[sl2] >> bi) & 1u)) continue;
+            const int32_t* dp = a.dly[p] + c0 + sl2 * CPS;
+            int dd[CPS], mind = 1 << 30, maxd = 0;
+#pragma unroll
+            for (int k = 0; k < CPS; k++) {
+                dd[k] = dp[k];
+                mind = min(mind, dd[k]);
+                maxd = max(maxd, dd[k]);
+            }
+            int lo = B - (DS - 1) - maxd, hi = B - 1 - mind;
+            lo = lo <= 0 ? 0 : (lo + DS - 1) / DS;
+            hi = hi < 0 ? -1 : min(hi / DS, 4 * JQ - 1);
+            const int jt = lo + jj;
+            if (jt > hi) continue;
+            fold_store(p, sl2, jt, dd);
+        }
+    }
+    __syncthreads();
+    if (a.sub_dtype == 0 && threadIdx.x < np) publish_max(a.maxabs[threadIdx.x], amax_fix[threadIdx.x]);
 }
 
-size_t stage1_q8_lds_bytes(const Stage1Multi& a) { return (size_t)a.sg * a.cps * a.W * 4; }
+size_t stage1_q8_lds_bytes(const Stage1Multi& a)
+{
+    size_t b = (size_t)a.sg * a.cps * a.W * 4;
+    if (a.qfix) {
+        const int rows = 4 * stage1_q8_quarter_rows(a.ds) + a.dmax;
+        const int G = a.sg * a.cps;
+        b += (size_t)((rows + 31) >> 5) * 4 + (size_t)3 * G * 4 + (size_t)((G + 15) & ~15);
+    }
+    return b;
+}
 
 template <int CPS, int DS>
 static hipError_t launch_q8_ds(const Stage1Multi& a, int vb, size_t lds, hipStream_t st)
