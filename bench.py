@@ -11,6 +11,7 @@ output samples of all ranks / max-over-ranks wall time.
   torchrun --nproc-per-node N ... bench.py --gpus N ...     (one rank per GPU)
 """
 import argparse
+import glob
 import json
 import os
 import sys
@@ -449,33 +450,40 @@ def main():
         dist.all_reduce(tt)
         total_out = tt.item()
 
-    # per-kernel device time of the last step (hipEvents on the engine's stream)
+    # per-kernel device time of the last step (hipEvents on the engine's stream); stage 2 is
+    # grouped by the kernel each plan launched (hd_plan_kernel, the names rocprofv3 prints)
     ms1 = ms2 = 0.0
+    per_kernel = {}
     for p in plans:
         a, b = p.last_ms()
         ms1 += a
         ms2 += b
+        k = per_kernel.setdefault(p.kernel(), {"ms": 0.0, "launches": 0, "units": 0})
+        k["ms"] += b
+        k["launches"] += 1
+        k["units"] += p.pp.numdms * (ts.out_range(rank, p.pp.ds)[1] if slices else p.nds)
     raw_bytes = (ts.slice(rank)[1] if slices else obs.N) * obs.rowbytes
-    sub_bytes = sum(p.pp.nsub * p.nds * 2 for p in plans)
     adds2 = sum(p.pp.numdms * p.nds * p.pp.nsub for p in plans)
     # algorithmic bytes per output sample (SURVEY §8d compulsory model): raw once + 4 B out
     b_unit = (raw_bytes + 4.0 * out_per_step) / out_per_step
-    if ms2 >= ms1:
-        dom = "k_stage2 (DM sweep)"
-        achieved = out_per_step * b_unit / (ms2 * 1e-3) / 1e9
-        launch_ms = ms2 / len(plans)
-    else:
-        dom = "k_stage1 (subband formation)"
-        n1 = sum((len(st) + 31) // 32 for st in stages)      # stage-1 launches per step
-        achieved = (n1 * raw_bytes + sub_bytes) / (ms1 * 1e-3) / 1e9
-        launch_ms = ms1 / n1
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_r02.json")
-    if os.path.exists(pmc):
+    dom = max(per_kernel, key=lambda k: per_kernel[k]["ms"])
+    kd = per_kernel[dom]
+    achieved = kd["units"] * b_unit / (kd["ms"] * 1e-3) / 1e9
+    launch_ms = kd["ms"] / kd["launches"]
+    alg_per_launch = kd["units"] * b_unit / kd["launches"]
+    # HBM traffic of exactly this kernel from the committed PMC summary (scripts/pmc_summary.py;
+    # keyed by kernel name -- a figure for any other kernel is refused)
+    traffic, traffic_src = None, None
+    for pmc in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_r*.json")), reverse=True):
         try:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch", {}).get(dom.split()[0])
+            j = json.load(open(pmc))
         except Exception:
-            traffic = None
+            continue
+        e = j.get("kernels", {}).get(dom)
+        if e and e.get("hbm_bytes"):
+            traffic = e["hbm_bytes"]
+            traffic_src = "%s (commit %s)" % (os.path.relpath(pmc, ROOT), j.get("commit", "?"))
+            break
     step_s = dt_max / args.steps
     line = {
         "metric": METRIC,
@@ -500,8 +508,12 @@ def main():
                    else "beam-per-GPU x%d" % world},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "avg_launch_ms": launch_ms, "bytes_per_unit": b_unit},
+                     "traffic_source": traffic_src, "algorithmic_bytes_per_launch": alg_per_launch,
+                     "launches_per_step": kd["launches"], "avg_launch_ms": launch_ms, "bytes_per_unit": b_unit},
         "kernel_ms_per_step": {"stage1": ms1, "stage2": ms2},
+        "stage2_kernels": {k: {"ms": v["ms"], "launches": v["launches"],
+                               "GBps_alg": v["units"] * b_unit / (v["ms"] * 1e-3) / 1e9 if v["ms"] > 0 else None}
+                           for k, v in sorted(per_kernel.items(), key=lambda kv: -kv[1]["ms"])},
         "stage2_streams": args.streams,
         "step_compulsory_hbm_frac": (raw_bytes + 4.0 * out_per_step) / step_s / (HBM_PEAK_GBS * 1e9),
         "stage2_valu_frac": adds2 / (ms2 * 1e-3) / VALU_ADD_PEAK if ms2 > 0 else None,

@@ -146,6 +146,7 @@ static hipError_t sync_all(hd_ctx* c)
 struct hd_plan {
     hd_ctx* ctx = nullptr;
     hd_pass pass{};
+    char s2name[64] = {0};          // stage-2 kernel of the last hd_run_dedisp (hd_plan_kernel)
     int64_t nds = 0, numout = 0, nvalid = 0;
     int64_t sub_stride = 0, out_stride = 0;
     double sub_lofreq = 0, sub_chanwid = 0, sub_dt = 0;
@@ -2492,12 +2493,19 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         else if (wk == 1) HIPCHK(c, hd::launch_stage2_wide2(a, w.q, w.r, w.nw, st));
         else if (wk == 2) HIPCHK(c, hd::launch_stage2_ring(a, w.q, w.r, st));
         else HIPCHK(c, hd::launch_stage2_pair(a, w.q, w.r, wk == 4 ? 2 : 1, st));
+        // the names rocprofv3 prints (template arguments as the compiler spells them)
+        if (wk == 0) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_wide<%d, %d, %d>", w.q, w.r, w.sc);
+        else if (wk == 1) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_wide2<%d, %d, %d>", w.q, w.r, w.sc);
+        else if (wk == 2) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_ring<%d, %d>", w.q, w.r);
+        else snprintf(p->s2name, sizeof(p->s2name), "k_stage2_pair<%d, %d, %d>", w.q, w.r, wk == 4 ? 2 : 1);
     } else if (use_lds) {
         a.off = p->d_boff;
         HIPCHK(c, hd::launch_stage2_lds(a, p->q, st));
+        snprintf(p->s2name, sizeof(p->s2name), "k_stage2_lds<%d>", p->q);
     } else {
         a.off = p->d_off;
         HIPCHK(c, hd::launch_stage2_direct(a, st));
+        snprintf(p->s2name, sizeof(p->s2name), "k_stage2_direct");
     }
     if (pad)
         HIPCHK(c, hd::launch_pad(p->d_out, p->out_stride, p->pass.numdms, p->nds, p->numout, partial, ntiles,
@@ -2576,6 +2584,14 @@ extern "C" int hd_plan_last_ms(const hd_plan* p, float* ms_sub, float* ms_dd)
 
 // ---- realfft / zapbirds / rednoise (hd_fft.hip; replace the per-.dat PRESTO commands of
 //      PALFA2_presto_search.py:548-558) ---------------------------------------------------
+extern "C" int hd_plan_kernel(const hd_plan* p, char* name, int32_t cap)
+{
+    if (!p || !name || cap < 1) return fail(p ? p->ctx : nullptr, HD_E_INVAL, "hd_plan_kernel: bad argument");
+    if (!p->ran_dd) return fail(p->ctx, HD_E_STATE, "hd_plan_kernel: run hd_run_dedisp first");
+    snprintf(name, (size_t)cap, "%s", p->s2name);
+    return HD_OK;
+}
+
 extern "C" int hd_realfft(hd_plan* p)
 {
     if (!p) return fail(nullptr, HD_E_INVAL, "hd_realfft: NULL plan");

@@ -34,7 +34,7 @@ EXPORTED = [
     "hd_close", "hd_last_error", "hd_sync", "hd_set_obs", "hd_set_chan_calib", "hd_set_mask",
     "hd_push_raw", "hd_synth_device", "hd_synth_host", "hd_plan_create", "hd_plan_destroy",
     "hd_plan_get_delays", "hd_plan_sub_params", "hd_run_subband", "hd_get_subbands",
-    "hd_set_subbands", "hd_run_dedisp", "hd_plan_last_ms", "hd_plan_set_variant",
+    "hd_set_subbands", "hd_run_dedisp", "hd_plan_last_ms", "hd_plan_kernel", "hd_plan_set_variant",
     "hd_get_raw", "hd_plan_tables", "hd_run_subband_multi", "hd_push_raw_device", "hd_get_raw_device",
     "hd_push_raw_file", "hd_set_streams", "hd_touch_raw", "hd_stats_padvals", "hd_get_clean",
     "hd_get_subbands_window", "hd_get_series", "hd_write_series", "hd_wait_writes",
@@ -143,6 +143,7 @@ def load():
         "hd_set_subbands": (ctypes.c_int, [vp, vp]),
         "hd_run_dedisp": (ctypes.c_int, [vp, f32p]),
         "hd_plan_last_ms": (ctypes.c_int, [vp, f32p, f32p]),
+        "hd_plan_kernel": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int32]),
         "hd_plan_set_variant": (ctypes.c_int, [vp, i32]),
         "hd_get_raw": (ctypes.c_int, [vp, vp, i64, i64]),
         "hd_run_subband_multi": (ctypes.c_int, [P(vp), i32]),

@@ -406,6 +406,13 @@ class Plan:
         arr = (ctypes.c_char_p * len(paths))(*[os.fsencode(p) for p in paths])
         self.eng._chk(self.eng._L.hd_write_series(self._p, arr, int(bool(wait))), "hd_write_series")
 
+    def kernel(self):
+        """Name of the stage-2 kernel of the last run_dedisp (hd_plan_kernel), as rocprofv3
+        prints it without namespace and arguments."""
+        buf = ctypes.create_string_buffer(64)
+        self.eng._chk(self.eng._L.hd_plan_kernel(self._p, buf, 64), "hd_plan_kernel")
+        return buf.value.decode()
+
     def last_ms(self):
         a, b = ctypes.c_float(), ctypes.c_float()
         self.eng._chk(self.eng._L.hd_plan_last_ms(self._p, ctypes.byref(a), ctypes.byref(b)), "hd_plan_last_ms")

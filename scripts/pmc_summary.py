@@ -20,9 +20,27 @@ def family(name):
     return m.group(1) if m else name.split("(")[0]
 
 
+def short(name):
+    """'void hd::k_stage2_pair<5, 3, 2>(hd::Stage2Args, int const*)' -> 'k_stage2_pair<5, 3, 2>'
+    (the name hd_plan_kernel reports)."""
+    s = re.sub(r"^void ", "", name.strip())
+    s = re.sub(r"^hd::", "", s)
+    depth, out = 0, []
+    for ch in s:
+        if ch == "(" and depth == 0:
+            break
+        depth += ch == "<"
+        depth -= ch == ">"
+        out.append(ch)
+    return "".join(out)
+
+
+_DISP = defaultdict(set)                                   # (kernel, counter) -> dispatches
+
+
 def load(root):
     acc = defaultdict(lambda: defaultdict(float))        # kernel -> counter -> sum
-    disp = defaultdict(set)
+    disp = _DISP
     dur = defaultdict(dict)
     for f in glob.glob(os.path.join(root, "*", "*_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
@@ -59,6 +77,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("root")
     ap.add_argument("--json")
+    ap.add_argument("--commit", default="")
     a = ap.parse_args()
     rows = load(a.root)
     fam = {}
@@ -73,15 +92,24 @@ def main():
         if "hbm_bytes" in d:
             fam.setdefault(family(k), []).append(d["hbm_bytes"])
     if a.json:
-        per_launch = {f: sum(v) / len(v) for f, v in fam.items()}
-        for pre in ("k_stage1", "k_stage2"):       # the families bench.py reports
-            vals = [b for f, v in fam.items() if f.startswith(pre) for b in v]
-            if vals:
-                per_launch[pre] = sum(vals) / len(vals)
-        json.dump({"source": a.root,
-                   "note": "HBM bytes per launch = 2*FETCH_SIZE + WRITE_SIZE (KiB -> B), mean over the "
-                           "instantiations of a kernel family (gfx950 FETCH_SIZE correction, MI355X_MICROARCH.md)",
-                   "hbm_bytes_per_launch": per_launch}, open(a.json, "w"), indent=1)
+        kernels = {}
+        for k, r in rows.items():
+            d = derive(r)
+            if "hbm_bytes" not in d:
+                continue
+            e = {"launches": len(next(iter(v for kk, v in _DISP.items() if kk[0] == k), [])) or None,
+                 "dispatch_ms": r["dispatch_ms"]}
+            e.update({c: d[c] for c in ("hbm_read_bytes", "hbm_write_bytes", "hbm_bytes") if c in d})
+            for c in ("valu_active_per_wave_cycle", "lds_conflict_share"):
+                if c in d:
+                    e[c] = d[c]
+            kernels[short(k)] = e
+        json.dump({"source": a.root, "commit": a.commit,
+                   "note": "per launch, mean over the kernel's dispatches in the profiled run: hbm_bytes = "
+                           "2*FETCH_SIZE + WRITE_SIZE (KiB -> B; gfx950 FETCH_SIZE counts half of a wide "
+                           "streaming read, MI355X_MICROARCH.md); keys are the exact kernel names "
+                           "(hd_plan_kernel), so bench.py only takes a traffic figure for the kernel it times",
+                   "kernels": kernels}, open(a.json, "w"), indent=1)
 
 
 if __name__ == "__main__":
