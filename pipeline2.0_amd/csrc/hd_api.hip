@@ -61,6 +61,7 @@ struct hd_ctx {
     struct ClipBufs {
         float* zdm = nullptr;
         uint8_t *good = nullptr, *clipped = nullptr;
+        uint32_t* clipbits = nullptr;       // clipped, bit-packed (k_stage1_q8's in-kernel fixup)
         int32_t *numgood = nullptr, *doclip = nullptr, *events = nullptr, *nevents = nullptr;
         int32_t* nzero = nullptr;           // a device 0 (profiling: a fixup over no clipped spectra)
         double *bavg = nullptr, *bstd = nullptr, *chansum = nullptr;
@@ -314,7 +315,7 @@ static void free_blocks(hd_ctx* c)
 static void free_clip(hd_ctx* c)
 {
     hd_ctx::ClipBufs& b = c->clip;
-    for (void* p : {(void*)b.zdm, (void*)b.good, (void*)b.clipped, (void*)b.numgood, (void*)b.doclip,
+    for (void* p : {(void*)b.zdm, (void*)b.good, (void*)b.clipped, (void*)b.clipbits, (void*)b.numgood, (void*)b.doclip,
                     (void*)b.events, (void*)b.nevents, (void*)b.nzero, (void*)b.bavg, (void*)b.bstd, (void*)b.chansum,
                     (void*)b.ravg, (void*)b.trig, (void*)b.pad, (void*)b.numgood_g, (void*)b.doclip_g,
                     (void*)b.bavg_g, (void*)b.bstd_g, (void*)b.chansum_g, (void*)b.xbuf, (void*)b.ravg_g,
@@ -1486,6 +1487,7 @@ static hd::RawDesc raw_desc(const hd_ctx* c)
     rd.pad = clip ? cpad : c->d_padvals;
     rd.pad_stride = clip ? c->obs.nchan : 0;
     rd.clipped = clip ? c->clip.clipped : nullptr;
+    rd.clipbits = clip ? c->clip.clipbits : nullptr;
     return rd;
 }
 
@@ -1585,6 +1587,7 @@ static int alloc_clip(hd_ctx* c)
         al((void**)&b.zdm, N * 4);
         al((void**)&b.good, N);
         al((void**)&b.clipped, N);
+        al((void**)&b.clipbits, (N + 63) / 64 * 8);
         al((void**)&b.events, N * 4);
         al((void**)&b.nevents, 4);
         al((void**)&b.nzero, 4);
@@ -1644,6 +1647,7 @@ static hd::ClipArgs clip_args(hd_ctx* c)
     a.trig = b.trig;
     a.doclip = b.doclip;
     a.clipped = b.clipped;
+    a.clipbits = b.clipbits;
     a.pad = b.pad;
     a.events = b.events;
     a.nevents = b.nevents;
@@ -1948,9 +1952,13 @@ static int run_subband_chunk(hd_ctx* c, hd_plan** plans, int n)
     const bool clip = c->opts.clip_sigma > 0.0f;
     if (q8) {
         m.probe = p0->probe;
-        // clipped-spectrum and block-boundary outputs recomputed inside k_stage1_q8 (probe bits
-        // 5-7 keep the separate fixup kernels for cross-checks)
-        m.qfix = clip && !(p0->probe & (32 | 64 | 128)) ? 1 : 0;
+        // clipped-spectrum and block-boundary outputs: the separate fixup kernel (k_stage1_fix8)
+        // by default; HD_QFIX=1 in the environment recomputes them inside k_stage1_q8 instead
+        // (measured 36.5 vs 34.4 ms of stage 1 per C2 beam: the in-kernel fixup's store drain and
+        // barrier cost every tile, and nearly every tile holds a clipped spectrum; probe bits
+        // 5-7 also select the separate kernels)
+        const bool env_qfix = getenv("HD_QFIX") && atoi(getenv("HD_QFIX")) != 0;
+        m.qfix = clip && env_qfix && !(p0->probe & (32 | 64 | 128)) ? 1 : 0;
         m.rd = raw_desc(c);
         m.rawT = rawT;
         if (!m.rawT && c->obs.nbits != 8) return fail(c, HD_E_HIP, "stage 1: 4-bit channel-major copy failed");

@@ -368,10 +368,11 @@ __global__ __launch_bounds__(256) void k_clip_flag(ClipArgs a)
         clip = a.doclip[b] && fabsf(a.zdm[t] - a.ravg[b]) > a.trig[b];
         a.clipped[t] = clip;
     }
-    // wave-aggregated append
+    // bit-packed flags (a wave covers 64 rows from a multiple of 64), then a wave-aggregated append
     const uint64_t bal = __ballot(clip);
+    const int lane = threadIdx.x & 63;
+    if (lane == 0 && t < a.rd.N) *(uint2*)(a.clipbits + (t >> 5)) = make_uint2((uint32_t)bal, (uint32_t)(bal >> 32));
     if (bal) {
-        const int lane = threadIdx.x & 63;
         int base = 0;
         if (lane == __ffsll((unsigned long long)bal) - 1) base = atomicAdd(a.nevents, __popcll(bal));
         base = __shfl(base, __ffsll((unsigned long long)bal) - 1, 64);

@@ -28,6 +28,7 @@ struct RawDesc {
     const float* pad;         // [nblk][nchan] (pad_stride = nchan) or [1][nchan] (stride 0), or nullptr (0)
     int32_t pad_stride;
     const uint8_t* clipped;   // [N] 1 = spectrum replaced by clip_times, or nullptr
+    const uint32_t* clipbits; // the same flags bit-packed: bit t % 32 of word t / 32 (with clipped)
 };
 
 struct Stage1Args {
@@ -151,6 +152,7 @@ struct ClipArgs {
     float* trig;              // [nblk] clip_sigma * running_std after the block
     int32_t* doclip;          // [nblk] clip_times ran on the block
     uint8_t* clipped;         // [N] out
+    uint32_t* clipbits;       // [2 * ceil(N / 64)] out: clipped, bit-packed
     float* pad;               // [nblk][nchan] out: pad values in force for the block
     int32_t* events;          // [N] out: clipped spectra (any order)
     int32_t* nevents;         // device counter

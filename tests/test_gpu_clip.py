@@ -2,6 +2,8 @@
 read block (check_mask), PRESTO clip_times on the device (hd_clip.hip), the exact fixup of
 clipped spectra and of the integer path's block-boundary outputs, and the subband rounding
 and downsampling switches.  Bar: bit-exact against the oracle."""
+import os
+
 import numpy as np
 import pytest
 
@@ -162,8 +164,9 @@ def test_rfimask_file_and_stats_pads(engine, tmp_path):
 @pytest.mark.parametrize("stage", [0, 1, 3, 5])
 def test_fixup_kernels_agree_full_stage(engine, stage):
     """All passes of a Mock DDplan stage in one launch (28 at stage 0: the LDS-window fixup's
-    largest delay table), masked, with spikes: the 8-bit LDS-window fixup and the generic
-    per-cell fixup (probe bit 128) give identical subbands, and pass 0 equals the oracle."""
+    largest delay table), masked, with spikes: the 8-bit LDS-window fixup, the fixup inside
+    k_stage1_q8 (HD_QFIX=1) and the generic per-cell fixup (probe bit 128) give identical
+    subbands, and pass 0 equals the oracle."""
     obs = palfa_obs(N=1 << 17, nbits=8, nsblk=2048)
     raw, s = beam(engine, obs, Opts(), spiky_synth())
     pts = 16384
@@ -176,6 +179,13 @@ def test_fixup_kernels_agree_full_stage(engine, stage):
     try:
         engine.run_subband_multi(plans)
         fast = [p.get_subbands() for p in plans]
+        os.environ["HD_QFIX"] = "1"
+        try:
+            engine.run_subband_multi(plans)
+        finally:
+            del os.environ["HD_QFIX"]
+        for i, p in enumerate(plans):
+            assert np.array_equal(p.get_subbands(), fast[i]), ("in-kernel fixup", i)
         for p in plans:
             p.set_variant(128 << 16)
         engine.run_subband_multi(plans)
