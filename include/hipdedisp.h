@@ -291,6 +291,22 @@ HD_API int hd_get_series(hd_plan* plan, int32_t dm0, int32_t ndm, int64_t t0, in
  * (prepsubband's first-DM mean) is the observation's, not the slice's.                 */
 HD_API int hd_series_sum(hd_plan* plan, int32_t dm, int64_t t0, int64_t count, double* sum);
 HD_API int hd_series_fill(hd_plan* plan, int64_t t0, float value);
+
+/* ---- barycentric output (prepsubband without -nobary) ---------------------------------
+ * The reference's stage-2 command passes no -nobary (PALFA2_presto_search.py:514-520), so
+ * PRESTO resamples every DM series to the solar-system barycentre [PRESTO-ext]: from a TEMPO
+ * table of topocentric times topo[n] and their barycentric times bary[n] (MJD, spaced tdt
+ * seconds -- what presto.barycenter returns, the call the reference makes in get_baryv,
+ * :43-57) it lists the output bins where one bin is added (value > 0: a padding sample
+ * before topocentric sample v) or removed (value < 0: topocentric sample -v dropped), in
+ * units of the output sample time dsdt.  hd_bary_diffbins restates that list (host only,
+ * no device); *ndiff receives the count (HD_E_INVAL when it exceeds cap, diffbins holding the
+ * first cap).  hd_plan_set_bary makes the plan's stage 2 write the barycentred series
+ * (numout samples; added bins and the tail take the plan's padding value, hd_opts.pad_mode);
+ * ndiff = 0 (or diffbins NULL) turns it off.  Not for time-sliced plans (HD_E_INVAL).   */
+HD_API int hd_bary_diffbins(const double* topo, const double* bary, int32_t n, double tdt, double dsdt,
+                            int32_t* diffbins, int32_t cap, int32_t* ndiff);
+HD_API int hd_plan_set_bary(hd_plan* plan, const int32_t* diffbins, int32_t ndiff);
 /* The .dat output path (replaces the files prepsubband leaves in the tempdir,
  * PALFA2_presto_search.py:514-520, 532-537): queue the device-resident series of the last
  * hd_run_dedisp of this plan to paths[numdms] -- raw little-endian float32, numout samples,

@@ -264,6 +264,82 @@ def run_pass(obs, opts, raw, pp, calib=(None, None, None), mask=None, ptsperint=
     return sub, out
 
 
+def _nearest_long(x):
+    return int(x - 0.5) if x < 0 else int(x + 0.5)       # PRESTO's NEAREST_LONG (truncating casts)
+
+
+def bary_diffbins(topo, bary, tdt, dsdt):
+    """prepsubband's add/remove-bin list [PRESTO-ext restatement, parity unpinned: PRESTO is not
+    in the reference]: the barycentric - topocentric time of each TEMPO table point relative to
+    the first, in output bins; between points ii-1 and ii every half-bin crossing of its nearest
+    integer gives one entry, NEAREST_LONG of the crossing linearly interpolated onto the points'
+    output-bin positions ((ii-1)*tdt/dsdt, ii*tdt/dsdt), negated when the difference falls.
+    Reference call site: PALFA2_presto_search.py:514-520 (stage-2 prepsubband, no -nobary)."""
+    SECPERDAY = 86400.0
+    dtmp = bary[0] - topo[0]
+    b = [((bary[i] - topo[i]) - dtmp) * SECPERDAY / dsdt for i in range(len(topo))]
+    out = []
+    oldbin = 0
+    for ii in range(1, len(b)):
+        currentbin = _nearest_long(b[ii])
+        if currentbin != oldbin:
+            if currentbin > 0:
+                calcpt = oldbin + 0.5
+                lobin = (ii - 1) * tdt / dsdt
+                hibin = ii * tdt / dsdt
+            else:
+                calcpt = oldbin - 0.5
+                lobin = -((ii - 1) * tdt / dsdt)
+                hibin = -(ii * tdt / dsdt)
+            while abs(calcpt) < abs(b[ii]):
+                out.append(_nearest_long((calcpt - b[ii - 1]) * (hibin - lobin) / (b[ii] - b[ii - 1]) + lobin))
+                calcpt = calcpt + 1.0 if currentbin > 0 else calcpt - 1.0
+            oldbin = currentbin
+    return np.array(out, np.int32)
+
+
+def pad_values(topo, nds, pad_mode):
+    """The padding value per DM of a [numdms][>= min(nds, numout)] topocentric series, as k_pad /
+    or_pad define it: 1 zero; 2 (prepsubband's one avg) the first DM's sum / nds for every DM;
+    0 each DM's own."""
+    nd = topo.shape[0]
+    if pad_mode == 1 or nds <= 0:
+        return np.zeros(nd, np.float32)
+    n = min(nds, topo.shape[1])
+    sums = np.sum(topo[:, :n].astype(np.float64), axis=1)
+    if pad_mode == 2:
+        sums[:] = sums[0]
+    return (sums / float(nds)).astype(np.float32)
+
+
+def bary_series(topo, nvalid, numout, diffbins, padv):
+    """Barycentred series [numdms][numout] from topocentric ones [numdms][>= nvalid], written
+    sample by sample as prepsubband's output loop does: before topocentric sample |v| a
+    padding sample (v > 0) or sample |v| dropped (v < 0); entries at or past nvalid unused;
+    truncated to numout, then padded."""
+    nd = topo.shape[0]
+    out = np.empty((nd, numout), np.float32)
+    for d in range(nd):
+        col = []
+        k = 0
+        for t in range(nvalid):
+            skip = False
+            while k < len(diffbins) and abs(int(diffbins[k])) == t:
+                if diffbins[k] > 0:
+                    col.append(padv[d])
+                else:
+                    skip = True
+                k += 1
+            if not skip:
+                col.append(topo[d, t])
+            if len(col) >= numout:
+                break
+        col = col[:numout]
+        out[d, :len(col)] = col
+        out[d, len(col):] = padv[d]
+    return out
+
+
 def stats_padvals(dataavg):
     """determine_padvals from rfifind .stats interval averages [numint][numchan]."""
     a = np.ascontiguousarray(dataavg, np.float32)

@@ -172,6 +172,7 @@ struct hd_plan {
     } wide[5];                      // [2]: k_stage2_ring (16 waves, LDS-DMA staging ring);
                                     // [3]: k_stage2_pair (the ring over subband-pair partials),
                                     // [4]: the same with two pairs per chunk (half the chunks)
+    bool sub_nonneg = false;        // every subband value >= 0 (known on the host with sub_bound)
     int32_t sub_bound = -1;         // bound on |subband| known on the host (-1: none), set when
                                     // the subbands are formed or uploaded (pair variant gate)
     int32_t variant = 0;
@@ -189,6 +190,14 @@ struct hd_plan {
     hipStream_t dd_stream = nullptr;  // stream of the last hd_run_dedisp (its ev[3] marks the end)
     hd::FftState* fft = nullptr;    // realfft state (hd_fft.hip, from hd_ctx::fft_cache)
     bool ran_fft = false;
+    // barycentric output (hd_plan_set_bary): stage 2 writes the topocentric series to d_topo,
+    // then k_bary copies its segments to d_out; d_bseg [nbseg][3] = {out0, src0 (-1: padding),
+    // len}; d_padv [numdms] the padding values
+    int32_t nbseg = 0;
+    bool bary_adds = false;         // some bin is added (the padding value is needed)
+    int32_t* d_bseg = nullptr;
+    float* d_topo = nullptr;
+    float* d_padv = nullptr;
 };
 
 static thread_local std::string g_err;
@@ -1033,6 +1042,9 @@ static void plan_free(hd_plan* p)
     }
     dfree(p->d_out);
     dfree(p->d_sub);
+    dfree(p->d_bseg);
+    dfree(p->d_topo);
+    dfree(p->d_padv);
     if (p->fft && hd::fft_owner(p->fft) == p) hd::fft_set_owner(p->fft, nullptr);   // the context owns it
     p->fft = nullptr;
     for (auto& e : p->ev)
@@ -1278,6 +1290,17 @@ static void pair_tables(hd_plan* p, bool i16, int ppc, hd_plan::Wide& w, std::ve
     w.npw = npw;
     w.nbp = nbp;
     w.umax = umax;
+}
+
+// Subbands formed by stage 1 on the device are >= 0 when the samples are unsigned integers
+// (<= 8 bits, no calibration) and every pad value is >= 0: mask pads from the .stats file
+// (h_padvals) and clip_times' running channel means (means of unsigned samples).
+static bool stage1_sub_nonneg(const hd_ctx* c)
+{
+    if (c->d_scl || c->d_offs || c->d_wts || c->obs.nbits > 8) return false;
+    for (float v : c->h_padvals)
+        if (!(v >= 0.0f)) return false;
+    return true;
 }
 
 // Static bound on |subband| for subbands formed by stage 1 on the device (-1: none): integer
@@ -2061,6 +2084,7 @@ static int run_subband_chunk(hd_ctx* c, hd_plan** plans, int n)
     for (int i = 0; i < n; i++) {
         plans[i]->sub_valid = true;
         plans[i]->sub_bound = stage1_sub_bound(c, plans[i]);
+        plans[i]->sub_nonneg = plans[i]->sub_bound >= 0 && stage1_sub_nonneg(c);
         plans[i]->ran_sub = (i == 0);   // the launch's time is attributed to its first plan
     }
     return HD_OK;
@@ -2390,14 +2414,132 @@ extern "C" int hd_set_subbands(hd_plan* p, const void* host)
         int32_t m = 0;
         const int16_t* h = (const int16_t*)host;
         const size_t n = (size_t)p->pass.nsub * p->nds;
-        for (size_t i = 0; i < n; i++) m = std::max(m, h[i] < 0 ? -(int32_t)h[i] : (int32_t)h[i]);
+        bool neg = false;
+        for (size_t i = 0; i < n; i++) {
+            m = std::max(m, h[i] < 0 ? -(int32_t)h[i] : (int32_t)h[i]);
+            neg |= h[i] < 0;
+        }
         HIPCHK(c, hipMemcpyAsync(p->d_maxabs, &m, sizeof m, hipMemcpyHostToDevice, c->stream));
         p->sub_bound = m;
+        p->sub_nonneg = !neg;
     } else {
         p->sub_bound = -1;
+        p->sub_nonneg = false;
     }
     HIPCHK(c, hipStreamSynchronize(c->stream));
     p->sub_valid = true;
+    return HD_OK;
+}
+
+// ---- barycentric output ---------------------------------------------------------------
+// prepsubband's add/remove-bin list [PRESTO-ext, restated; reference call site
+// PALFA2_presto_search.py:514-520, which passes no -nobary]: the barycentric minus topocentric
+// time of each table point, relative to the first point, in output bins; wherever its nearest
+// integer changes between points ii-1 and ii, one bin per half-bin crossing, at the output
+// bin the crossing interpolates to (NEAREST_LONG(LININTERP(...)) of the crossing point
+// between the two points' bin positions); negative when the difference falls (bins removed).
+static long nearest_long_c(double x) { return x < 0.0 ? (long)(x - 0.5) : (long)(x + 0.5); }
+
+extern "C" int hd_bary_diffbins(const double* topo, const double* bary, int32_t n, double tdt, double dsdt,
+                                int32_t* diffbins, int32_t cap, int32_t* ndiff)
+{
+    if (!topo || !bary || !ndiff || (cap > 0 && !diffbins)) return fail(nullptr, HD_E_INVAL, "hd_bary_diffbins: NULL argument");
+    if (n < 2 || !(tdt > 0.0) || !(dsdt > 0.0)) return fail(nullptr, HD_E_INVAL, "hd_bary_diffbins: need n >= 2, tdt > 0, dsdt > 0");
+    std::vector<double> b((size_t)n);
+    const double d0 = bary[0] - topo[0];
+    for (int i = 0; i < n; i++) b[i] = ((bary[i] - topo[i]) - d0) * 86400.0 / dsdt;
+    int32_t cnt = 0;
+    long oldbin = 0;
+    for (int ii = 1; ii < n; ii++) {
+        const long currentbin = nearest_long_c(b[ii]);
+        if (currentbin == oldbin) continue;
+        double calcpt, lobin, hibin;
+        if (currentbin > 0) {
+            calcpt = (double)oldbin + 0.5;
+            lobin = (ii - 1) * tdt / dsdt;
+            hibin = ii * tdt / dsdt;
+        } else {
+            calcpt = (double)oldbin - 0.5;
+            lobin = -((ii - 1) * tdt / dsdt);
+            hibin = -(ii * tdt / dsdt);
+        }
+        while (std::fabs(calcpt) < std::fabs(b[ii])) {
+            const double y = (calcpt - b[ii - 1]) * (hibin - lobin) / (b[ii] - b[ii - 1]) + lobin;
+            const long v = nearest_long_c(y);
+            if (cnt < cap) diffbins[cnt] = (int32_t)v;
+            cnt++;
+            calcpt = currentbin > 0 ? calcpt + 1.0 : calcpt - 1.0;
+        }
+        oldbin = currentbin;
+    }
+    *ndiff = cnt;
+    if (cnt > cap) return fail(nullptr, HD_E_INVAL, "hd_bary_diffbins: %d bins > cap %d", (int)cnt, (int)cap);
+    return HD_OK;
+}
+
+// Segments of the barycentred series from the diffbins, applied in PRESTO's order while the
+// topocentric samples [0, nvalid) are written: the samples before |v|, then one padding sample
+// (v > 0) or sample |v| skipped (v < 0); the rest, then padding to numout.
+static void bary_segments(const int32_t* dv, int32_t nd, int64_t nvalid, int64_t numout, std::vector<int32_t>& seg,
+                          bool& adds)
+{
+    seg.clear();
+    adds = false;
+    int64_t out = 0, src = 0;
+    auto put = [&](int64_t s, int64_t len) {
+        len = std::min<int64_t>(len, numout - out);
+        if (len <= 0) return;
+        const size_t k = seg.size();
+        if (s < 0 && k >= 3 && seg[k - 2] < 0) {              // merge padding runs
+            seg[k - 1] += (int32_t)len;
+        } else {
+            seg.push_back((int32_t)out);
+            seg.push_back((int32_t)s);
+            seg.push_back((int32_t)len);
+        }
+        if (s < 0) adds = true;
+        out += len;
+    };
+    for (int32_t i = 0; i < nd && out < numout; i++) {
+        const int64_t p = dv[i] < 0 ? -(int64_t)dv[i] : (int64_t)dv[i];
+        if (p >= nvalid) break;
+        put(src, p - src);
+        src = p;
+        if (dv[i] > 0) put(-1, 1);
+        else src = p + 1;
+    }
+    put(src, nvalid - src);
+    put(-1, numout - out);
+}
+
+extern "C" int hd_plan_set_bary(hd_plan* p, const int32_t* diffbins, int32_t ndiff)
+{
+    if (!p) return fail(nullptr, HD_E_INVAL, "hd_plan_set_bary: NULL plan");
+    hd_ctx* c = p->ctx;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, sync_all(c));
+    if (p->copy_pending && c->writer) HIPCHK(c, hipEventSynchronize(p->ev_copy));
+    dfree(p->d_bseg);
+    p->d_bseg = nullptr;
+    p->nbseg = 0;
+    if (!diffbins || ndiff <= 0) {
+        dfree(p->d_topo);
+        p->d_topo = nullptr;
+        return HD_OK;
+    }
+    if (c->slice_total > 0) return fail(c, HD_E_INVAL, "hd_plan_set_bary: not for a time-sliced context");
+    for (int32_t i = 1; i < ndiff; i++)
+        if (std::abs((int64_t)diffbins[i]) < std::abs((int64_t)diffbins[i - 1]))
+            return fail(c, HD_E_INVAL, "hd_plan_set_bary: |diffbins| must not decrease (entry %d)", (int)i);
+    if (p->numout >= ((int64_t)1 << 31)) return fail(c, HD_E_INVAL, "hd_plan_set_bary: numout >= 2^31");
+    std::vector<int32_t> seg;
+    bary_segments(diffbins, ndiff, p->nvalid, p->numout, seg, p->bary_adds);
+    const size_t bytes = sizeof(int32_t) * seg.size();
+    HIPCHK(c, hipMalloc(&p->d_bseg, std::max<size_t>(bytes, 16)));
+    if (bytes) HIPCHK(c, hipMemcpy(p->d_bseg, seg.data(), bytes, hipMemcpyHostToDevice));
+    p->nbseg = (int32_t)(seg.size() / 3);
+    if (!p->d_padv) HIPCHK(c, hipMalloc(&p->d_padv, sizeof(float) * (size_t)std::max(p->pass.numdms, 1)));
+    p->ran_dd = false;                 // the device series no longer match the settings
     return HD_OK;
 }
 
@@ -2414,7 +2556,16 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
             return fail(c, HD_E_NOMEM, "cannot allocate %zu bytes of DM series", bytes);
         }
     }
-    const bool pad = p->numout > p->nds;
+    const bool bary = p->nbseg > 0;
+    if (bary && !p->d_topo) {
+        const size_t bytes = sizeof(float) * (size_t)p->pass.numdms * p->out_stride;
+        if (hipMalloc(&p->d_topo, bytes) != hipSuccess) {
+            p->d_topo = nullptr;
+            return fail(c, HD_E_NOMEM, "cannot allocate %zu bytes of topocentric DM series", bytes);
+        }
+    }
+    // barycentric output: the padding value is needed for added bins and the tail
+    const bool pad = bary || p->numout > p->nds;
     // alternate streams between passes (see hd_ctx::stream2); a plan re-run on the other
     // stream first waits for its previous run, which wrote the same series
     const bool alt = c->dual && (c->s2all || (c->dd_count++ & 1u) != 0);
@@ -2474,7 +2625,7 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
     a.nds = p->nds;
     a.sub_stride = p->sub_stride;
     a.nvalid = p->nvalid;
-    a.out = p->d_out;
+    a.out = bary ? p->d_topo : p->d_out;
     a.out_stride = p->out_stride;
     a.partial = partial;
     a.ntiles = ntiles;
@@ -2496,6 +2647,7 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         a.ring_nbp = w.nbp;
         a.ptab = w.d_omin;
         a.umax = w.umax;
+        a.nonneg = p->sub_nonneg ? 1 : 0;
         a.nwg = p->pair_persist != 2 ? c->ncu : 0;   // persistent by default (measured 1.29 vs 1.36 ms, stage-0 pass)
         if (wk == 0) HIPCHK(c, hd::launch_stage2_wide(a, w.q, w.r, w.nw, st));
         else if (wk == 1) HIPCHK(c, hd::launch_stage2_wide2(a, w.q, w.r, w.nw, st));
@@ -2505,7 +2657,8 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         if (wk == 0) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_wide<%d, %d, %d>", w.q, w.r, w.sc);
         else if (wk == 1) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_wide2<%d, %d, %d>", w.q, w.r, w.sc);
         else if (wk == 2) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_ring<%d, %d>", w.q, w.r);
-        else snprintf(p->s2name, sizeof(p->s2name), "k_stage2_pair<%d, %d, %d>", w.q, w.r, wk == 4 ? 2 : 1);
+        else snprintf(p->s2name, sizeof(p->s2name), "k_stage2_pair<%d, %d, %d, %s>", w.q, w.r, wk == 4 ? 2 : 1,
+                      a.nonneg && !(p->probe & 64) ? "true" : "false");
     } else if (use_lds) {
         a.off = p->d_boff;
         HIPCHK(c, hd::launch_stage2_lds(a, p->q, st));
@@ -2515,7 +2668,10 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         HIPCHK(c, hd::launch_stage2_direct(a, st));
         snprintf(p->s2name, sizeof(p->s2name), "k_stage2_direct");
     }
-    if (pad)
+    if (bary)
+        HIPCHK(c, hd::launch_bary(p->d_topo, p->d_out, p->out_stride, p->pass.numdms, p->numout, p->d_bseg, p->nbseg,
+                                  partial, ntiles, p->nds, c->opts.pad_mode, p->d_padv, st));
+    else if (pad)
         HIPCHK(c, hd::launch_pad(p->d_out, p->out_stride, p->pass.numdms, p->nds, p->numout, partial, ntiles,
                                  c->opts.pad_mode, st));
     HIPCHK(c, hipEventRecord(p->ev[3], st));

@@ -95,6 +95,7 @@ struct Stage2Args {
     // the largest U of the plan (expanded copies per pair = 4*umax)
     const int32_t* ptab;
     int32_t umax;
+    int32_t nonneg;           // pair variant: every subband value is >= 0 (unsigned packed halves)
 };
 
 hipError_t launch_stage1_direct(const Stage1Args& a, hipStream_t st);
@@ -179,6 +180,10 @@ hipError_t launch_sp_hits(const float* x, int64_t stride, int ndm, int nblocks, 
                           unsigned long long* count, int64_t cap, hipStream_t st);
 // rfifind statistics (hd_rfi.hip): per interval and channel mean, std, max normalised power
 hipError_t set_max_lds(const void* fn, int bytes);
+// barycentric output: padding values (as k_pad) then the segments {out0, src0 | -1, len}
+hipError_t launch_bary(const float* topo, float* out, int64_t stride, int numdms, int64_t numout, const int32_t* seg,
+                       int nseg, const double* partial, int ntiles, int64_t nds, int pad_mode, float* padv,
+                       hipStream_t st);
 hipError_t rfi_stats(const RawDesc& rd, const uint8_t* rawT, int64_t tstride, int ptsperint, int numint, float* avg,
                      float* sd, float* pw, hipStream_t st);
 // realfft / zapbirds / rednoise of a plan's series (hd_fft.hip)

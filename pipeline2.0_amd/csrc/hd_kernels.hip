@@ -1323,6 +1323,91 @@ hipError_t launch_pad(float* out, int64_t out_stride, int numdms, int64_t nds, i
     return hipGetLastError();
 }
 
+// ---- barycentric output: padding values, then the segments of the barycentred series ----
+__global__ __launch_bounds__(256) void k_padvals(const double* partial, int ntiles, int64_t nds, int pad_mode,
+                                                float* padv)
+{
+    __shared__ double red[256];
+    const int d = blockIdx.x;
+    const int dsrc = pad_mode == 2 ? 0 : d;                 // as k_pad
+    double s = 0.0;
+    if (pad_mode != 1 && partial)
+        for (int i = threadIdx.x; i < ntiles; i += 256) s += partial[(int64_t)dsrc * ntiles + i];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w >= 1; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) padv[d] = (pad_mode != 1 && nds > 0 && partial) ? (float)(red[0] / (double)nds) : 0.0f;
+}
+
+// One workgroup per (2048 output samples, DM): each sample finds its segment {out0, src0, len}
+// (binary search over the segment starts staged in LDS in pieces of kBarySegLds), then copies
+// topo[src0 + j - out0] or writes the padding value.  Reads are contiguous within a segment.
+constexpr int kBarySegLds = 2048;
+__global__ __launch_bounds__(256) void k_bary(const float* __restrict__ topo, float* __restrict__ out, int64_t stride,
+                                             int64_t numout, const int32_t* __restrict__ seg, int nseg,
+                                             const float* __restrict__ padv)
+{
+    __shared__ int32_t s_out0[kBarySegLds];
+    __shared__ int lo_s, hi_s;
+    const int d = blockIdx.y;
+    const int64_t j0 = (int64_t)blockIdx.x * 2048;
+    const int64_t j1 = j0 + 2048 < numout ? j0 + 2048 : numout;
+    if (threadIdx.x == 0) {
+        // segments overlapping [j0, j1): first = last k with out0[k] <= j0
+        int lo = 0, hi = nseg - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (seg[3 * mid] <= j0) lo = mid;
+            else hi = mid - 1;
+        }
+        int last = lo;
+        while (last + 1 < nseg && seg[3 * (last + 1)] < j1) last++;
+        lo_s = lo;
+        hi_s = last;
+    }
+    __syncthreads();
+    const int k0 = lo_s, nk = hi_s - lo_s + 1;
+    const float pv = padv[d];
+    const float* tp = topo + (int64_t)d * stride;
+    float* op = out + (int64_t)d * stride;
+    if (nk == 1) {                                            // uniform: one segment
+        const int64_t o0 = seg[3 * k0], s0 = seg[3 * k0 + 1];
+        for (int64_t j = j0 + threadIdx.x; j < j1; j += 256) op[j] = s0 < 0 ? pv : tp[s0 + (j - o0)];
+        return;
+    }
+    for (int i = threadIdx.x; i < nk && i < kBarySegLds; i += 256) s_out0[i] = seg[3 * (k0 + i)];
+    __syncthreads();
+    const int nl = nk < kBarySegLds ? nk : kBarySegLds;
+    for (int64_t j = j0 + threadIdx.x; j < j1; j += 256) {
+        int lo = 0, hi = nl - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_out0[mid] <= j) lo = mid;
+            else hi = mid - 1;
+        }
+        int k = k0 + lo;
+        while (k + 1 < nseg && seg[3 * (k + 1)] <= j) k++;     // beyond the staged piece (rare)
+        const int64_t o0 = seg[3 * k], s0 = seg[3 * k + 1];
+        op[j] = s0 < 0 ? pv : tp[s0 + (j - o0)];
+    }
+}
+
+hipError_t launch_bary(const float* topo, float* out, int64_t stride, int numdms, int64_t numout, const int32_t* seg,
+                       int nseg, const double* partial, int ntiles, int64_t nds, int pad_mode, float* padv,
+                       hipStream_t st)
+{
+    if (numdms <= 0 || numout <= 0 || nseg <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_padvals, dim3((unsigned)numdms), dim3(256), 0, st, partial, ntiles, nds, pad_mode, padv);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_bary, dim3((unsigned)((numout + 2047) / 2048), (unsigned)numdms), dim3(256), 0, st, topo, out,
+                       stride, numout, seg, nseg, padv);
+    return hipGetLastError();
+}
+
 // ---- series sums and fills (time-sliced passes: the padding value is the observation's) --
 __global__ __launch_bounds__(256) void k_series_sum(const float* __restrict__ x, int64_t n, double* __restrict__ part)
 {

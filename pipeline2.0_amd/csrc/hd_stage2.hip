@@ -840,7 +840,36 @@ __device__ __forceinline__ void load8_shift(const uint32_t* w32, int x, uint32_t
     for (int m = 0; m < 4; m++) o[m] = __builtin_amdgcn_alignbit(w[m + 1], w[m], sh);
 }
 
-template <int Q, int R, int PPC>
+// The same 8 elements from two 8-byte-aligned ds_read_b64 and one ds_read_b32 (the five
+// ds_read_b32 above, 8 bytes apart across lanes, run 2-way bank-conflicted): the first dword
+// x >> 1 is even (b64, b64, b32) or odd (b32, b64, b64); its parity is uniform per window.
+__device__ __forceinline__ void load8_shift64(const uint32_t* w32, int x, uint32_t (&o)[4])
+{
+    const int j = x >> 1;
+    const uint32_t sh = (uint32_t)(x & 1) * 16u;
+    uint32_t w[5];
+    if ((j & 1) == 0) {
+        const uint2 p = *(const uint2*)(w32 + j);
+        const uint2 q = *(const uint2*)(w32 + j + 2);
+        w[0] = p.x;
+        w[1] = p.y;
+        w[2] = q.x;
+        w[3] = q.y;
+        w[4] = w32[j + 4];
+    } else {
+        w[0] = w32[j];
+        const uint2 p = *(const uint2*)(w32 + j + 1);
+        const uint2 q = *(const uint2*)(w32 + j + 3);
+        w[1] = p.x;
+        w[2] = p.y;
+        w[3] = q.x;
+        w[4] = q.y;
+    }
+#pragma unroll
+    for (int m = 0; m < 4; m++) o[m] = __builtin_amdgcn_alignbit(w[m + 1], w[m], sh);
+}
+
+template <int Q, int R, int PPC, bool NN>
 __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, const int32_t* __restrict__ boff)
 {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
@@ -886,7 +915,10 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, const int32_
 
     int maxabs = *a.maxabs;
     maxabs = maxabs < 1 ? 1 : maxabs;
-    int G = 32767 / (2 * maxabs);                      // pairs per packed-int16 group
+    // pairs per packed-16-bit group: signed halves hold |sum| <= 32767; with subbands known
+    // non-negative (host) the halves are unsigned and hold sums <= 65535 (twice the group)
+    constexpr bool nonneg = NN;                        // (a runtime switch here spills registers)
+    int G = (nonneg ? 65535 : 32767) / (2 * maxabs);
     G = G < 1 ? 1 : (G > 64 ? 64 : G);
     G = __builtin_amdgcn_readfirstlane(G);
 
@@ -903,6 +935,29 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, const int32_
         }
     int gcount = 0;
     const bool loader = wave < 2 * PPC * npw + nbp;
+    // packed 16-bit group -> int32 accumulators (zero- or sign-extended halves)
+    auto widen = [&]() {
+#pragma unroll
+        for (int qq = 0; qq < Q; qq++)
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                if (nonneg) {
+                    const uint32_t lo = __builtin_bit_cast(uint32_t, acc16[qq][r][0]);
+                    const uint32_t hi = __builtin_bit_cast(uint32_t, acc16[qq][r][1]);
+                    acc32[qq][r][0] += (int)(lo & 0xFFFFu);
+                    acc32[qq][r][1] += (int)(lo >> 16);
+                    acc32[qq][r][2] += (int)(hi & 0xFFFFu);
+                    acc32[qq][r][3] += (int)(hi >> 16);
+                } else {
+                    acc32[qq][r][0] += acc16[qq][r][0].x;
+                    acc32[qq][r][1] += acc16[qq][r][0].y;
+                    acc32[qq][r][2] += acc16[qq][r][1].x;
+                    acc32[qq][r][3] += acc16[qq][r][1].y;
+                }
+                acc16[qq][r][0] = short2v{0, 0};
+                acc16[qq][r][1] = short2v{0, 0};
+            }
+    };
 
     const int ntot = ntl * nchunk;
     int dchunk = 0, dtile = 0, dcount = 0;             // source chunk of the next DMA (clamped at the end)
@@ -947,8 +1002,8 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, const int32_
                 for (int m = 1; m < kPairUMax; m++)
                     if (uu >= upw) { uu -= upw; u++; }
                 uint32_t A[4], B[4], P[4];
-                load8_shift(S0, k0 + 4 * uu, A);
-                load8_shift(S1, pt[3 + u] + 4 * uu, B);
+                load8_shift64(S0, k0 + 4 * uu, A);
+                load8_shift64(S1, pt[3 + u] + 4 * uu, B);
 #pragma unroll
                 for (int m = 0; m < 4; m++)
                     P[m] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(short2v, A[m]) + __builtin_bit_cast(short2v, B[m]));
@@ -966,6 +1021,7 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, const int32_
 
     auto flush = [&](int tile) {
         const int64_t t0 = (int64_t)tile * T;
+        widen();
     #pragma unroll
         for (int q = 0; q < Q; q++) {
             const int dl = wave * Q + q;
@@ -974,10 +1030,6 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, const int32_
             int64_t part = 0;
     #pragma unroll
             for (int r = 0; r < R; r++) {
-                acc32[q][r][0] += acc16[q][r][0].x;
-                acc32[q][r][1] += acc16[q][r][0].y;
-                acc32[q][r][2] += acc16[q][r][1].x;
-                acc32[q][r][3] += acc16[q][r][1].y;
                 const int64_t tl = t0 + 256 * r + 4 * lane;
                 if (dv && !(a.probe & 4)) {
                     float* o = a.out + (int64_t)d * a.out_stride + tl;
@@ -1058,17 +1110,7 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, const int32_
                 }
                 if (q == Q - 1 && ++gcount == G) {                // one pair done: widen every G pairs
                     gcount = 0;
-#pragma unroll
-                    for (int qq = 0; qq < Q; qq++)
-#pragma unroll
-                        for (int r = 0; r < R; r++) {
-                            acc32[qq][r][0] += acc16[qq][r][0].x;
-                            acc32[qq][r][1] += acc16[qq][r][0].y;
-                            acc32[qq][r][2] += acc16[qq][r][1].x;
-                            acc32[qq][r][3] += acc16[qq][r][1].y;
-                            acc16[qq][r][0] = short2v{0, 0};
-                            acc16[qq][r][1] = short2v{0, 0};
-                        }
+                    widen();
                 }
             }
         }
@@ -1089,20 +1131,29 @@ size_t stage2_pair_lds_bytes(int wstride, int npw, int nbp, int nsub, int umax, 
            (size_t)2 * ppc * umax * 4 * wstride * 2;
 }
 
-template <int Q, int R, int PPC>
-static hipError_t launch_pair_qrp(const Stage2Args& a, int nyblk, hipStream_t st)
+template <int Q, int R, int PPC, bool NN>
+static hipError_t launch_pair_qrpn(const Stage2Args& a, int nyblk, hipStream_t st)
 {
     {
-        const hipError_t e = set_max_lds((const void*)k_stage2_pair<Q, R, PPC>, 160 * 1024);
+        const hipError_t e = set_max_lds((const void*)k_stage2_pair<Q, R, PPC, NN>, 160 * 1024);
         if (e != hipSuccess) return e;
     }
     const unsigned ntiles = (unsigned)((a.nvalid + 256 * R - 1) / (256 * R));
     const unsigned nx = a.nwg > 0 && (unsigned)a.nwg < ntiles ? (unsigned)a.nwg : ntiles;
     Stage2Args b = a;
     if (nx == ntiles) b.nwg = 0;
-    hipLaunchKernelGGL((k_stage2_pair<Q, R, PPC>), dim3(nx, (unsigned)nyblk), dim3(1024),
+    hipLaunchKernelGGL((k_stage2_pair<Q, R, PPC, NN>), dim3(nx, (unsigned)nyblk), dim3(1024),
                        stage2_pair_lds_bytes(a.wstride, a.ring_npw, a.ring_nbp, a.nsub, a.umax, PPC), st, b, a.off);
     return hipGetLastError();
+}
+
+// non-negative subbands (host-known): unsigned packed halves, twice the group (probe 64 keeps
+// the signed kernel for A/B)
+template <int Q, int R, int PPC>
+static hipError_t launch_pair_qrp(const Stage2Args& a, int nyblk, hipStream_t st)
+{
+    if (a.nonneg && !(a.probe & 64)) return launch_pair_qrpn<Q, R, PPC, true>(a, nyblk, st);
+    return launch_pair_qrpn<Q, R, PPC, false>(a, nyblk, st);
 }
 
 // Two workgroups per CU: 8 waves x Q DMs (<= 40) per workgroup, one LDS window buffer, no

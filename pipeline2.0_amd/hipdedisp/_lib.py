@@ -42,6 +42,7 @@ EXPORTED = [
     "hd_sp_widths", "hd_single_pulse", "hd_rfifind_stats",
     "hd_push_raw_file_band", "hd_fill_raw",
     "hd_realfft", "hd_zap_ranges", "hd_zapbirds", "hd_rednoise_blocks", "hd_rednoise", "hd_get_fft",
+    "hd_bary_diffbins", "hd_plan_set_bary",
 ]
 
 
@@ -168,6 +169,9 @@ def load():
                                               P(ctypes.c_int32)]),
         "hd_rednoise": (ctypes.c_int, [vp, i32, i32, ctypes.c_double, ctypes.c_double]),
         "hd_get_fft": (ctypes.c_int, [vp, i32, i32, f32p]),
+        "hd_bary_diffbins": (ctypes.c_int, [P(ctypes.c_double), P(ctypes.c_double), i32, ctypes.c_double,
+                                            ctypes.c_double, P(ctypes.c_int32), i32, P(ctypes.c_int32)]),
+        "hd_plan_set_bary": (ctypes.c_int, [vp, P(ctypes.c_int32), i32]),
         "hd_sp_widths": (ctypes.c_int, [ctypes.c_double, ctypes.c_double, P(ctypes.c_int32), P(ctypes.c_int32)]),
         "hd_single_pulse": (ctypes.c_int, [vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp, i64, P(i64),
                                            P(ctypes.c_uint8), P(i64)]),

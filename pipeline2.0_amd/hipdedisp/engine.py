@@ -110,6 +110,29 @@ def plan_tables(obs: "ObsParams", opts: "Opts", pp: "PassParams"):
     return idd, off, (a.value, b.value, c.value)
 
 
+def bary_diffbins(topo, bary, tdt, dsdt):
+    """prepsubband's add/remove-bin list [PRESTO-ext] from a TEMPO table (hd_bary_diffbins;
+    host only): topo/bary MJDs spaced tdt s, output sample time dsdt s.  int32 array, > 0 =
+    a padding bin before topocentric sample v, < 0 = sample -v removed."""
+    t = np.ascontiguousarray(topo, dtype=np.float64)
+    b = np.ascontiguousarray(bary, dtype=np.float64)
+    if t.shape != b.shape or t.ndim != 1:
+        raise PrestoError("topo and bary must be 1-D arrays of the same length")
+    L = _lib.load()
+    D = ctypes.POINTER(ctypes.c_double)
+    I32 = ctypes.POINTER(ctypes.c_int32)
+    n = ctypes.c_int32(0)
+    rc = L.hd_bary_diffbins(t.ctypes.data_as(D), b.ctypes.data_as(D), len(t), float(tdt), float(dsdt), None, 0,
+                            ctypes.byref(n))
+    if rc and n.value == 0:                       # bad arguments (the count query itself fails)
+        _check(rc, "hd_bary_diffbins")
+    cap = max(n.value, 1)
+    out = np.zeros(cap, np.int32)
+    _check(L.hd_bary_diffbins(t.ctypes.data_as(D), b.ctypes.data_as(D), len(t), float(tdt), float(dsdt),
+                              out.ctypes.data_as(I32), cap, ctypes.byref(n)), "hd_bary_diffbins")
+    return out[:n.value]
+
+
 def stats_padvals(dataavg):
     """determine_padvals [PRESTO-ext] from rfifind .stats interval averages [numint][numchan]
     (hd_stats_padvals; host only)."""
@@ -342,6 +365,16 @@ class Plan:
 
     def set_variant(self, v):
         self.eng._chk(self.eng._L.hd_plan_set_variant(self._p, int(v)), "hd_plan_set_variant")
+
+    def set_bary(self, diffbins=None):
+        """Barycentred output (hd_plan_set_bary): the add/remove-bin list of bary_diffbins for
+        this plan's output sample time; None or empty = topocentric."""
+        if diffbins is None or len(diffbins) == 0:
+            self.eng._chk(self.eng._L.hd_plan_set_bary(self._p, None, 0), "hd_plan_set_bary")
+            return
+        d = np.ascontiguousarray(diffbins, dtype=np.int32)
+        self.eng._chk(self.eng._L.hd_plan_set_bary(self._p, d.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), len(d)),
+                      "hd_plan_set_bary")
 
     def run_subband(self):
         self.eng._chk(self.eng._L.hd_run_subband(self._p), "prepsubband -sub -subdm %.2f" % self.pp.subdm)

@@ -37,7 +37,7 @@ class DedispJob:
     """The part of obs_info (PALFA2_presto_search.py:231-294) the dedispersion stage uses."""
 
     def __init__(self, filenms, resultsdir=".", tmpdir_base=None, device=0, opts=None,
-                 use_subbands=True, keep_subbands=False, backend=None, voverc=0.0):
+                 use_subbands=True, keep_subbands=False, backend=None, voverc=0.0, bary_table=None):
         self.filenms = list(filenms)
         self.filenmstr = " ".join(self.filenms)
         self.outputdir = resultsdir
@@ -63,9 +63,14 @@ class DedispJob:
         self.samp_per_row = si.spectra_per_subint
         self.fctr = si.fctr
         # average barycentric v/c (the reference's obs_info.baryv, :269-270, from TEMPO): it
-        # enters PRESTO's delay tables; the barycentric resampling of the output series needs
-        # TEMPO and is not performed -- 0 is prepsubband -nobary
+        # enters PRESTO's delay tables -- 0 is prepsubband -nobary.  bary_table = (topo, bary,
+        # tdt): the TEMPO table (MJDs every tdt s from the start of the data, as
+        # presto.barycenter returns them, :43-57) that makes the series barycentred, as the
+        # reference's stage-2 command (no -nobary, :514-520) leaves them; without one (TEMPO is
+        # not in this image) the series stay topocentric and the .inf says so
         self.baryv = voverc
+        self.bary_table = bary_table
+        self._diffbins = {}
         self.hostname = socket.gethostname()
         self.use_subbands = use_subbands
         self.keep_subbands = keep_subbands
@@ -123,11 +128,26 @@ class DedispJob:
             self.engine.close()
             self.engine = None
 
-    def info_template(self, nsub, lofreq, chanwid, dt):
+    def set_bary(self, plan):
+        """Barycentred output for a plan (its output sample time) when a TEMPO table is set."""
+        if self.bary_table is None:
+            return
+        from .engine import bary_diffbins
+        topo, bary, tdt = self.bary_table
+        dsdt = plan.sub_dt
+        if dsdt not in self._diffbins:
+            self._diffbins[dsdt] = bary_diffbins(topo, bary, tdt, dsdt)
+        plan.set_bary(self._diffbins[dsdt])
+
+    def info_template(self, nsub, lofreq, chanwid, dt, series=False):
+        """.inf fields; series=True for the stage-2 .dat files, which are barycentred (bary = 1,
+        epoch = the barycentric MJD of the first sample) when a TEMPO table is set."""
+        bary = series and self.bary_table is not None
+        mjd = float(self.bary_table[1][0]) if bary else float(self.MJD)
         return InfoData(name="", telescope=self.specinfo.telescope or "Arecibo",
                         instrument=self.backend, object=self.specinfo.source or "Unknown",
                         ra=self.ra_string, dec=self.dec_string, observer=self.specinfo.observer or "Unknown",
-                        mjd=float(self.MJD), bary=0, dt=dt, freq=lofreq, freqband=nsub * chanwid,
+                        mjd=mjd, bary=int(bary), dt=dt, freq=lofreq, freqband=nsub * chanwid,
                         num_chan=nsub, chan_wid=chanwid)
 
 
@@ -189,8 +209,9 @@ def run_pass(job, ddplan, passnum, maskfilenm, tempdir, single_pulse=None, fft=N
             write_subbands(os.path.join(tempdir, "subbands", subbasenm), plan.get_subbands(), info)
         t_sub = time.time() - t0
         t0 = time.time()
+        job.set_bary(plan)
         plan.run_dedisp(to_host=False)
-        info = job.info_template(pp.nsub, plan.sub_lofreq, plan.sub_chanwid, plan.sub_dt)
+        info = job.info_template(pp.nsub, plan.sub_lofreq, plan.sub_chanwid, plan.sub_dt, series=True)
         write_dats_device(plan, os.path.join(tempdir, job.basefilenm), ddplan.dmlist[passnum], info, plan.nds)
         t_dd = time.time() - t0
         if single_pulse is not None:
@@ -215,8 +236,9 @@ def _run_pass_nosub(job, ddplan, passnum, maskfilenm, tempdir, single_pulse=None
     try:
         t0 = time.time()
         plan.run_subband()
+        job.set_bary(plan)
         plan.run_dedisp(to_host=False)
-        info = job.info_template(pp.nsub, plan.sub_lofreq, plan.sub_chanwid, plan.sub_dt)
+        info = job.info_template(pp.nsub, plan.sub_lofreq, plan.sub_chanwid, plan.sub_dt, series=True)
         write_dats_device(plan, os.path.join(tempdir, job.basefilenm), ddplan.dmlist[passnum], info, plan.nds)
         t_dd = time.time() - t0
         if single_pulse is not None:
