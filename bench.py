@@ -49,6 +49,8 @@ def parse():
                     help="beams of realfft + zapbirds + rednoise (hd_fft.hip) timed after the steps; 0 = skip")
     ap.add_argument("--rfi-beams", type=int, default=1,
                     help="beams of rfifind statistics + mask decisions (hd_rfi.hip) timed last; 0 = skip")
+    ap.add_argument("--stream-beams", type=int, default=3,
+                    help="beams of the overlapped PSRFITS-streaming leg (configs[4]; prefetch thread), run last; 0 = skip")
     ap.add_argument("--mode", choices=["beam", "slices", "shard"], default="beam",
                     help="beam: one beam per rank (weak scaling, configs[4]); slices: ONE beam cut into per-rank "
                          "time slices, every rank runs all 57 passes on its slice (strong, configs[2]; RCCL carries "
@@ -187,6 +189,45 @@ def rfifind_leg(eng, obs, beams):
     s = (time.perf_counter() - t) / beams
     return {"s_per_beam": s, "intervals": int(avg.shape[0]), "ptsperint": pts,
             "note": "hd_rfifind_stats + rfifind's mask decisions (host) for the beam; wall time"}
+
+
+def stream_leg(eng, stages, obs, synth_beams, beams):
+    """configs[4]'s overlapped PSRFITS streaming (one beam per job, queue_managers/pbs.py:67):
+    two beams written as PSRFITS files (tmpfs); per timed beam the NEXT beam's file is read on
+    the library's prefetch thread + copy stream (hd_prefetch_raw_file) while this beam's 57
+    passes run, then hd_swap_raw.  Wall seconds per beam, and the reads' own rate."""
+    import shutil
+    from hipdedisp.formats import psrfits
+    nbytes = obs.N * obs.rowbytes
+    d = e2e_dir(2.2 * nbytes)
+    if d is None:
+        return None
+    files = []
+    try:
+        for k, sy in enumerate(synth_beams):
+            eng.synth_device(sy)
+            fn = os.path.join(d, "beam%d.fits" % k)
+            psrfits.write_psrfits(fn, eng.get_raw(), obs, beam=k)
+            files.append(psrfits.SpectraInfo([fn]))
+        files[0].stream_to(eng, prefetch=True)
+        eng.swap_raw()
+        eng.sync()
+        io = 0.0
+        t = time.perf_counter()
+        for k in range(beams):
+            files[(k + 1) % len(files)].stream_to(eng, prefetch=True)
+            run_step(eng, stages)
+            a, _ = eng.swap_raw()
+            io += a
+        eng.sync()
+        s = (time.perf_counter() - t) / beams
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    return {"s_per_beam": s, "samples_per_s": sum(p.pp.numdms * p.nds for st in stages for p in st) / s,
+            "read_GBps": nbytes / (io / beams) / 1e9 if io > 0 else None, "pread_s_per_beam": io / beams,
+            "dir": os.path.dirname(d),
+            "note": "configs[4] per GPU: each beam's PSRFITS read (pread -> pinned -> HBM on the prefetch thread and "
+                    "copy stream) overlapped with the previous beam's 57 passes; wall time per beam"}
 
 
 def e2e_dir(need_bytes):
@@ -543,6 +584,10 @@ def main():
         line["fft_stage"] = fft_leg(eng, stages, args.fft_beams)
     if not (shard or slices) and args.rfi_beams > 0:
         line["rfifind"] = rfifind_leg(eng, obs, args.rfi_beams)
+    if not (shard or slices) and args.stream_beams > 0:
+        st = stream_leg(eng, stages, obs, [synth, palfa_synth(beam=rank + 8, nbits=args.nbits)], args.stream_beams)
+        if st:
+            line["stream_beams"] = st
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(obs, synth, ddplans, args.cpu_seconds, mask, pts, pad, omp=False)
         line["cpu_baseline_openmp"] = cpu_baseline(obs, synth, ddplans, args.cpu_seconds, mask, pts, pad, omp=True)

@@ -223,6 +223,22 @@ HD_API int hd_push_raw_file_band(hd_ctx* ctx, const char* path, const hd_rows_sr
  * padding between PSRFITS files that start later than the previous one ends
  * (lib/python/formats/psrfits.py:272-280).                                                */
 HD_API int hd_fill_raw(hd_ctx* ctx, int64_t start, int64_t count, int32_t byte_value);
+/* Overlapped ingest of the next beam (BASELINE configs[4]: the 7 beams of an ALFA pointing,
+ * one beam per job as queue_managers/pbs.py:67 runs them): hd_prefetch_raw_file / _band /
+ * hd_prefetch_fill queue the work of hd_push_raw_file / _band / hd_fill_raw for the NEXT
+ * beam into the context's second raw slot and return at once -- a reader thread preads into
+ * pinned blocks of its own and copies on a stream of its own while the current beam computes.
+ * hd_swap_raw waits for the queued reads (not for compute), orders the context's streams after
+ * their copies and makes the prefetched block current; the previous block becomes the next
+ * prefetch target, reused only after the work already queued on it.  Same hd_set_obs for both
+ * beams (a new hd_set_obs drops the prefetch).  *io_seconds: pread time, *total_seconds:
+ * first queued job to the swap.  HD_E_STATE when nothing was prefetched; a read or copy error
+ * of any queued job is returned here.                                                      */
+HD_API int hd_prefetch_raw_file(hd_ctx* ctx, const char* path, const hd_rows_src* src, int64_t start);
+HD_API int hd_prefetch_raw_file_band(hd_ctx* ctx, const char* path, const hd_rows_src* src, int64_t start,
+                                     int64_t spec_bytes, int64_t src_offset, int64_t dst_offset, int64_t nbytes);
+HD_API int hd_prefetch_fill(hd_ctx* ctx, int64_t start, int64_t count, int32_t byte_value);
+HD_API int hd_swap_raw(hd_ctx* ctx, double* io_seconds, double* total_seconds);
 /* Fill the device raw block with the synthetic beam (bit-identical to hd_synth_host). */
 HD_API int hd_synth_device(hd_ctx* ctx, const hd_synth* s);
 /* Host generator: spectra [start, start+count) of the same beam into out (file layout).

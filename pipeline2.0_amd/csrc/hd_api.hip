@@ -15,6 +15,9 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
 #include <map>
 #include <tuple>
 #include <chrono>
@@ -27,6 +30,26 @@
 #include "../../include/hipdedisp.h"
 
 #define HD_VERSION_STR "hipdedisp 0.1.0 (gfx950)"
+
+// Pinned host blocks of the file ingest: kReaders reader threads x 2 blocks, each guarded by
+// the event of the last copy that read it.
+constexpr int kReaders = 4;
+struct PinSet {
+    void* pin[2 * kReaders] = {};
+    hipEvent_t ev[2 * kReaders] = {};
+    size_t bytes = 0;
+    void release()
+    {
+        for (int b = 0; b < 2 * kReaders; b++) {
+            if (ev[b]) (void)hipEventSynchronize(ev[b]);
+            if (pin[b]) (void)hipHostFree(pin[b]);
+            if (ev[b]) (void)hipEventDestroy(ev[b]);
+            pin[b] = nullptr;
+            ev[b] = nullptr;
+        }
+        bytes = 0;
+    }
+};
 
 struct hd_ctx {
     int device = -1;
@@ -93,11 +116,8 @@ struct hd_ctx {
     int64_t sp_hits_cap = 0;
     unsigned long long* d_sp_count = nullptr;
     double* d_sum_parts = nullptr;  // hd_series_sum partials
-    // streaming ingest (hd_push_raw_file): two pinned host blocks, each guarded by the event
-    // of the last copy that read it
-    void* pin[2] = {nullptr, nullptr};
-    size_t pin_bytes = 0;
-    hipEvent_t pin_ev[2] = {nullptr, nullptr};
+    // streaming ingest (hd_push_raw_file): pinned host blocks of the reader threads
+    PinSet pins;
     // stage 2 alternates between the main stream and stream2, so one pass's last tiles and
     // the next pass's first ones share the GPU (no tail between launches).  ev_fork orders
     // stream2 after the main stream's work so far; ev_join (after each stream2 pass) orders
@@ -121,6 +141,35 @@ struct hd_ctx {
     // buffer, shared by the plans of that geometry -- each pass's hd_realfft takes it over
     // (the owner), so a beam builds 6 hipFFT plans, not 57
     std::map<std::tuple<int64_t, int, int64_t>, hd::FftState*> fft_cache;
+    // overlapped ingest of the next beam (hd_prefetch_*, hd_swap_raw): a second raw slot filled
+    // by a reader thread through its own pinned blocks on its own copy stream
+    struct Prefetch;
+    Prefetch* pf = nullptr;
+};
+
+struct PfJob {
+    bool fill = false;
+    std::string path;
+    hd_rows_src src{};
+    int64_t start = 0, sb = 0, soff = 0, doff = 0, nb = 0, count = 0;
+    int32_t byte_value = 0;
+};
+
+struct hd_ctx::Prefetch {
+    uint8_t* d_next = nullptr;       // the idle raw slot
+    hipStream_t st = nullptr;        // copy stream
+    hipEvent_t ev_free = nullptr;    // recorded at a swap: the work queued on the old block
+    hipEvent_t ev_done = nullptr;    // recorded at a swap: the prefetch copies
+    bool wait_free = false;          // the next queued job first waits for ev_free
+    PinSet pins;
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<PfJob> q;
+    bool busy = false, stop = false, any = false;
+    int err = 0;
+    std::string errmsg;
+    double io = 0.0, t0 = 0.0;       // pread seconds, steady-clock seconds of the first job
 };
 
 // main-stream work from here on runs after every stage-2 pass queued on stream2
@@ -335,8 +384,11 @@ static void free_clip(hd_ctx* c)
     c->clip.stats_valid = false;
 }
 
+static void pf_stop(hd_ctx* c);
+
 static void free_obs_buffers(hd_ctx* c)
 {
+    pf_stop(c);                        // the prefetched block has the old geometry
     dfree(c->d_raw); c->d_raw = nullptr;
     dfree(c->d_rawT); c->d_rawT = nullptr;
     c->rawT_valid = false;
@@ -379,10 +431,7 @@ extern "C" int hd_close(hd_ctx* c)
     if (c->saux) (void)hipStreamDestroy(c->saux);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
-    for (int b = 0; b < 2; b++) {
-        if (c->pin[b]) (void)hipHostFree(c->pin[b]);
-        if (c->pin_ev[b]) (void)hipEventDestroy(c->pin_ev[b]);
-    }
+    c->pins.release();
     clear_special_cache(c);
     for (auto& kv : c->fft_cache) hd::fft_state_free(kv.second);
     c->fft_cache.clear();
@@ -683,85 +732,118 @@ static int read_full(int fd, void* dst, size_t n, off_t off)
     return 0;
 }
 
-// Spectra of a file whose spectrum is sb bytes: bytes [soff, soff + nb) of each go to bytes
-// [doff, doff + nb) of device spectrum start + k (sb == rowbytes, soff = doff = 0, nb = sb:
-// the whole spectrum, hd_push_raw_file).
+// Rows of a PSRFITS table to device spectra: kReaders threads, each with two pinned host blocks,
+// take blocks of rows in turn (block k: thread k % kReaders); a thread's pread of its next block
+// overlaps the copy of its previous one (each block is guarded by the event of the last copy
+// that read it; a never-recorded event is complete), and the threads' preads run in parallel
+// (one thread reads tmpfs at ~10 GB/s).  Spectra of the file are sb bytes: bytes
+// [soff, soff + nb) of each go to bytes [doff, doff + nb) of device spectrum start + k (sb ==
+// rb, soff = doff = 0, nb = sb: whole spectra).  Returns 0, HD_E_IO or HD_E_HIP; copies may
+// still be in flight on st.
+static int rows_to_device(int device, uint8_t* d_raw, int64_t rb, hipStream_t st, PinSet& ps, const char* path,
+                          const hd_rows_src* src, int64_t start, int64_t sb, int64_t soff, int64_t doff, int64_t nb,
+                          double& io)
+{
+    using clk = std::chrono::steady_clock;
+    const int64_t spr = src->col_bytes / sb;   // spectra per row (NSBLK)
+    const size_t want = src->block_bytes > 0 ? (size_t)src->block_bytes : (size_t)32 << 20;
+    const int64_t rows_blk = std::max<int64_t>(1, (int64_t)(want / (size_t)src->col_bytes));
+    const size_t blk_bytes = (size_t)rows_blk * (size_t)src->col_bytes;
+    const int64_t nblocks = (src->nrows + rows_blk - 1) / rows_blk;
+    const int nthr = (int)std::min<int64_t>(kReaders, std::max<int64_t>(nblocks, 1));
+    if (ps.bytes < blk_bytes) {
+        ps.release();
+        for (int b = 0; b < 2 * kReaders; b++)
+            if (hipHostMalloc(&ps.pin[b], blk_bytes, hipHostMallocDefault) != hipSuccess) return HD_E_HIP;
+        ps.bytes = blk_bytes;
+    }
+    for (int b = 0; b < 2 * kReaders; b++)
+        if (!ps.ev[b] && hipEventCreateWithFlags(&ps.ev[b], hipEventDisableTiming) != hipSuccess) return HD_E_HIP;
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) return HD_E_IO;
+    std::atomic<int> err{0};
+    std::vector<double> tio((size_t)nthr, 0.0);
+    auto reader = [&](int t) {
+        if (t > 0 && hipSetDevice(device) != hipSuccess) {
+            err = HD_E_HIP;
+            return;
+        }
+        for (int64_t k = t, i = 0; k < nblocks && !err.load(); k += nthr, i++) {
+            const int b = 2 * t + (int)(i & 1);
+            const int64_t r = k * rows_blk;
+            const int64_t nr = std::min(rows_blk, src->nrows - r);
+            if (hipEventSynchronize(ps.ev[b]) != hipSuccess) { err = HD_E_HIP; break; }
+            const auto t0 = clk::now();
+            char* dst = (char*)ps.pin[b];
+            bool bad = false;
+            if (src->col_offset == 0 && src->col_bytes == src->row_bytes) {
+                bad = read_full(fd, dst, (size_t)(nr * src->col_bytes),
+                                (off_t)(src->table_offset + (src->row0 + r) * src->row_bytes)) != 0;
+            } else {
+                for (int64_t q = 0; q < nr && !bad; q++)
+                    bad = read_full(fd, dst + q * src->col_bytes, (size_t)src->col_bytes,
+                                    (off_t)(src->table_offset + (src->row0 + r + q) * src->row_bytes + src->col_offset)) != 0;
+            }
+            tio[t] += std::chrono::duration<double>(clk::now() - t0).count();
+            if (bad) { err = HD_E_IO; break; }
+            const hipError_t ce =
+                (sb == rb && nb == rb)
+                    ? hipMemcpyAsync(d_raw + (size_t)(start + r * spr) * rb, dst, (size_t)(nr * src->col_bytes),
+                                     hipMemcpyHostToDevice, st)
+                    : hipMemcpy2DAsync(d_raw + (size_t)(start + r * spr) * rb + doff, (size_t)rb, dst + soff,
+                                       (size_t)sb, (size_t)nb, (size_t)(nr * spr), hipMemcpyHostToDevice, st);
+            if (ce != hipSuccess || hipEventRecord(ps.ev[b], st) != hipSuccess) { err = HD_E_HIP; break; }
+        }
+    };
+    std::vector<std::thread> helpers;
+    for (int t = 1; t < nthr; t++) helpers.emplace_back(reader, t);
+    reader(0);
+    for (auto& h : helpers) h.join();
+    close(fd);
+    double m = 0.0;                            // pread time: the busiest reader's
+    for (double v : tio) m = std::max(m, v);
+    io += m;
+    return err.load();
+}
+
+// Argument checks shared by the synchronous and the prefetching file ingest.
+static int check_rows_src(hd_ctx* c, const char* what, const char* path, const hd_rows_src* src, int64_t start,
+                          int64_t sb, int64_t soff, int64_t doff, int64_t nb)
+{
+    if (!c) return fail(nullptr, HD_E_INVAL, "%s: NULL context", what);
+    if (!c->have_obs) return fail(c, HD_E_STATE, "%s before hd_set_obs", what);
+    if (!path || !src) return fail(c, HD_E_INVAL, "%s: NULL argument", what);
+    const int64_t rb = c->rowbytes;
+    if (sb <= 0 || src->col_bytes <= 0 || src->col_bytes % sb || src->row_bytes < src->col_offset + src->col_bytes ||
+        src->row0 < 0 || src->nrows < 0 || src->table_offset < 0)
+        return fail(c, HD_E_INVAL, "%s: DATA column of %lld bytes is not whole spectra of %lld bytes "
+                    "(or bad row geometry)", what, (long long)src->col_bytes, (long long)sb);
+    if (soff < 0 || nb <= 0 || soff + nb > sb || doff < 0 || doff + nb > rb)
+        return fail(c, HD_E_INVAL, "%s: bytes [%lld, %lld) of %lld-byte spectra into [%lld, %lld) "
+                    "of %lld-byte spectra", what, (long long)soff, (long long)(soff + nb), (long long)sb, (long long)doff,
+                    (long long)(doff + nb), (long long)rb);
+    const int64_t spr = src->col_bytes / sb;
+    if (start < 0 || start + src->nrows * spr > c->obs.N)
+        return fail(c, HD_E_INVAL, "%s: spectra [%lld, %lld) outside [0, %lld)", what, (long long)start,
+                    (long long)(start + src->nrows * spr), (long long)c->obs.N);
+    return HD_OK;
+}
+
 static int push_raw_file_impl(hd_ctx* c, const char* path, const hd_rows_src* src, int64_t start, int64_t sb,
                               int64_t soff, int64_t doff, int64_t nb, double* io_seconds, double* total_seconds)
 {
     using clk = std::chrono::steady_clock;
     const auto t_all = clk::now();
-    if (!c) return fail(nullptr, HD_E_INVAL, "hd_push_raw_file: NULL context");
-    if (!c->have_obs) return fail(c, HD_E_STATE, "hd_push_raw_file before hd_set_obs");
-    if (!path || !src) return fail(c, HD_E_INVAL, "hd_push_raw_file: NULL argument");
-    const int64_t rb = c->rowbytes;
-    if (sb <= 0 || src->col_bytes <= 0 || src->col_bytes % sb || src->row_bytes < src->col_offset + src->col_bytes ||
-        src->row0 < 0 || src->nrows < 0 || src->table_offset < 0)
-        return fail(c, HD_E_INVAL, "hd_push_raw_file: DATA column of %lld bytes is not whole spectra of %lld bytes "
-                    "(or bad row geometry)", (long long)src->col_bytes, (long long)sb);
-    if (soff < 0 || nb <= 0 || soff + nb > sb || doff < 0 || doff + nb > rb)
-        return fail(c, HD_E_INVAL, "hd_push_raw_file_band: bytes [%lld, %lld) of %lld-byte spectra into [%lld, %lld) "
-                    "of %lld-byte spectra", (long long)soff, (long long)(soff + nb), (long long)sb, (long long)doff,
-                    (long long)(doff + nb), (long long)rb);
-    const int64_t spr = src->col_bytes / sb;   // spectra per row (NSBLK)
-    if (start < 0 || start + src->nrows * spr > c->obs.N)
-        return fail(c, HD_E_INVAL, "hd_push_raw_file: spectra [%lld, %lld) outside [0, %lld)", (long long)start,
-                    (long long)(start + src->nrows * spr), (long long)c->obs.N);
-    HIPCHK(c, hipSetDevice(c->device));
-    int rc = ensure_raw(c);
+    int rc = check_rows_src(c, "hd_push_raw_file", path, src, start, sb, soff, doff, nb);
     if (rc) return rc;
-    const size_t want = src->block_bytes > 0 ? (size_t)src->block_bytes : (size_t)32 << 20;
-    const int64_t rows_blk = std::max<int64_t>(1, (int64_t)(want / (size_t)src->col_bytes));
-    const size_t blk_bytes = (size_t)rows_blk * (size_t)src->col_bytes;
-    if (c->pin_bytes < blk_bytes) {
-        for (int b = 0; b < 2; b++) {
-            if (c->pin[b]) HIPCHK(c, hipHostFree(c->pin[b]));
-            c->pin[b] = nullptr;
-        }
-        c->pin_bytes = 0;
-        for (int b = 0; b < 2; b++) HIPCHK(c, hipHostMalloc(&c->pin[b], blk_bytes, hipHostMallocDefault));
-        c->pin_bytes = blk_bytes;
-    }
-    for (int b = 0; b < 2; b++)
-        if (!c->pin_ev[b]) HIPCHK(c, hipEventCreateWithFlags(&c->pin_ev[b], hipEventDisableTiming));
-    const int fd = open(path, O_RDONLY);
-    if (fd < 0) return fail(c, HD_E_IO, "hd_push_raw_file: cannot open %s", path);
+    HIPCHK(c, hipSetDevice(c->device));
+    rc = ensure_raw(c);
+    if (rc) return rc;
     double io = 0.0;
-    int err = 0;
-    bool used[2] = {false, false};
-    for (int64_t r = 0, k = 0; r < src->nrows && !err; r += rows_blk, k++) {
-        const int b = (int)(k & 1);
-        const int64_t nr = std::min(rows_blk, src->nrows - r);
-        if (used[b] && hipEventSynchronize(c->pin_ev[b]) != hipSuccess) { err = HD_E_HIP; break; }
-        const auto t0 = clk::now();
-        char* dst = (char*)c->pin[b];
-        if (src->col_offset == 0 && src->col_bytes == src->row_bytes) {
-            if (read_full(fd, dst, (size_t)(nr * src->col_bytes), (off_t)(src->table_offset + (src->row0 + r) * src->row_bytes)))
-                err = HD_E_IO;
-        } else {
-            for (int64_t i = 0; i < nr && !err; i++)
-                if (read_full(fd, dst + i * src->col_bytes, (size_t)src->col_bytes,
-                              (off_t)(src->table_offset + (src->row0 + r + i) * src->row_bytes + src->col_offset)))
-                    err = HD_E_IO;
-        }
-        io += std::chrono::duration<double>(clk::now() - t0).count();
-        if (err) break;
-        const hipError_t ce =
-            (sb == rb && nb == rb)
-                ? hipMemcpyAsync(c->d_raw + (size_t)(start + r * spr) * rb, dst, (size_t)(nr * src->col_bytes),
-                                 hipMemcpyHostToDevice, c->stream)
-                : hipMemcpy2DAsync(c->d_raw + (size_t)(start + r * spr) * rb + doff, (size_t)rb, dst + soff,
-                                   (size_t)sb, (size_t)nb, (size_t)(nr * spr), hipMemcpyHostToDevice, c->stream);
-        if (ce != hipSuccess ||
-            hipEventRecord(c->pin_ev[b], c->stream) != hipSuccess) {
-            err = HD_E_HIP;
-            break;
-        }
-        used[b] = true;
-    }
-    close(fd);
+    const int err = rows_to_device(c->device, c->d_raw, c->rowbytes, c->stream, c->pins, path, src, start, sb, soff,
+                                   doff, nb, io);
     const hipError_t se = hipStreamSynchronize(c->stream);
-    if (err == HD_E_IO) return fail(c, HD_E_IO, "hd_push_raw_file: short read from %s", path);
+    if (err == HD_E_IO) return fail(c, HD_E_IO, "hd_push_raw_file: cannot read %s", path);
     if (err || se != hipSuccess) return fail(c, HD_E_HIP, "hd_push_raw_file: HIP copy failed");
     c->raw_ready = true;
     c->rawT_valid = false;
@@ -769,6 +851,212 @@ static int push_raw_file_impl(hd_ctx* c, const char* path, const hd_rows_src* sr
     c->clip.stats_valid = false;
     if (io_seconds) *io_seconds = io;
     if (total_seconds) *total_seconds = std::chrono::duration<double>(clk::now() - t_all).count();
+    return HD_OK;
+}
+
+// ---- overlapped ingest of the next beam ------------------------------------------------
+static double now_s()
+{
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+static void pf_worker(hd_ctx* c, int device)
+{
+    hd_ctx::Prefetch* pf = c->pf;
+    (void)hipSetDevice(device);
+    const int64_t rb = c->rowbytes;
+    for (;;) {
+        PfJob j;
+        {
+            std::unique_lock<std::mutex> lk(pf->mu);
+            pf->cv.wait(lk, [&] { return pf->stop || !pf->q.empty(); });
+            if (pf->q.empty()) return;               // stop with nothing queued
+            j = pf->q.front();
+            pf->q.pop_front();
+            pf->busy = true;
+        }
+        int err = 0;
+        double io = 0.0;
+        bool skip;
+        {
+            std::lock_guard<std::mutex> lk(pf->mu);
+            skip = pf->err != 0;                     // after a failure only drain the queue
+        }
+        if (!skip) {
+            if (j.fill) {
+                if (j.count && hipMemsetAsync(pf->d_next + (size_t)j.start * rb, j.byte_value, (size_t)j.count * rb,
+                                              pf->st) != hipSuccess)
+                    err = HD_E_HIP;
+            } else {
+                err = rows_to_device(device, pf->d_next, rb, pf->st, pf->pins, j.path.c_str(), &j.src, j.start, j.sb,
+                                     j.soff, j.doff, j.nb, io);
+            }
+        }
+        {
+            std::lock_guard<std::mutex> lk(pf->mu);
+            pf->io += io;
+            if (err && !pf->err) {
+                pf->err = err;
+                pf->errmsg = err == HD_E_IO ? "hd_prefetch_raw_file: cannot read " + j.path
+                                            : std::string("hd_prefetch: HIP copy failed");
+            }
+            pf->busy = false;
+        }
+        pf->cv.notify_all();
+    }
+}
+
+static void pf_stop(hd_ctx* c)
+{
+    hd_ctx::Prefetch* pf = c->pf;
+    if (!pf) return;
+    {
+        std::lock_guard<std::mutex> lk(pf->mu);
+        pf->stop = true;
+        pf->q.clear();
+    }
+    pf->cv.notify_all();
+    if (pf->th.joinable()) pf->th.join();
+    if (pf->st) (void)hipStreamSynchronize(pf->st);
+    dfree(pf->d_next);
+    pf->pins.release();
+    if (pf->ev_free) (void)hipEventDestroy(pf->ev_free);
+    if (pf->ev_done) (void)hipEventDestroy(pf->ev_done);
+    if (pf->st) (void)hipStreamDestroy(pf->st);
+    delete pf;
+    c->pf = nullptr;
+}
+
+static int pf_queue(hd_ctx* c, PfJob&& j)
+{
+    HIPCHK(c, hipSetDevice(c->device));
+    if (!c->pf) {
+        c->pf = new hd_ctx::Prefetch();
+        hd_ctx::Prefetch* pf = c->pf;
+        const size_t bytes = (size_t)c->obs.N * c->rowbytes;
+        if (hipMalloc(&pf->d_next, bytes) != hipSuccess) {
+            pf->d_next = nullptr;
+            pf_stop(c);
+            return fail(c, HD_E_NOMEM, "cannot allocate %zu bytes for the prefetched raw block", bytes);
+        }
+        if (hipStreamCreateWithFlags(&pf->st, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&pf->ev_free, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&pf->ev_done, hipEventDisableTiming) != hipSuccess) {
+            pf_stop(c);
+            return fail(c, HD_E_HIP, "hd_prefetch: cannot create the copy stream");
+        }
+        pf->th = std::thread(pf_worker, c, c->device);
+    }
+    hd_ctx::Prefetch* pf = c->pf;
+    std::lock_guard<std::mutex> lk(pf->mu);
+    if (pf->wait_free) {                             // the slot still holds the previous beam
+        HIPCHK(c, hipStreamWaitEvent(pf->st, pf->ev_free, 0));
+        pf->wait_free = false;
+    }
+    if (!pf->any) {
+        pf->any = true;
+        pf->t0 = now_s();
+        pf->io = 0.0;
+    }
+    pf->q.push_back(std::move(j));
+    pf->cv.notify_all();
+    return HD_OK;
+}
+
+extern "C" int hd_prefetch_raw_file(hd_ctx* c, const char* path, const hd_rows_src* src, int64_t start)
+{
+    const int64_t rb = c ? c->rowbytes : 0;
+    int rc = check_rows_src(c, "hd_prefetch_raw_file", path, src, start, rb, 0, 0, rb);
+    if (rc) return rc;
+    PfJob j;
+    j.path = path;
+    j.src = *src;
+    j.start = start;
+    j.sb = j.nb = rb;
+    return pf_queue(c, std::move(j));
+}
+
+extern "C" int hd_prefetch_raw_file_band(hd_ctx* c, const char* path, const hd_rows_src* src, int64_t start,
+                                         int64_t spec_bytes, int64_t src_offset, int64_t dst_offset, int64_t nbytes)
+{
+    int rc = check_rows_src(c, "hd_prefetch_raw_file_band", path, src, start, spec_bytes, src_offset, dst_offset,
+                            nbytes);
+    if (rc) return rc;
+    PfJob j;
+    j.path = path;
+    j.src = *src;
+    j.start = start;
+    j.sb = spec_bytes;
+    j.soff = src_offset;
+    j.doff = dst_offset;
+    j.nb = nbytes;
+    return pf_queue(c, std::move(j));
+}
+
+extern "C" int hd_prefetch_fill(hd_ctx* c, int64_t start, int64_t count, int32_t byte_value)
+{
+    if (!c) return fail(nullptr, HD_E_INVAL, "hd_prefetch_fill: NULL context");
+    if (!c->have_obs) return fail(c, HD_E_STATE, "hd_prefetch_fill before hd_set_obs");
+    if (start < 0 || count < 0 || start + count > c->obs.N || byte_value < 0 || byte_value > 255)
+        return fail(c, HD_E_INVAL, "hd_prefetch_fill: spectra [%lld, %lld) outside [0, %lld) or bad value",
+                    (long long)start, (long long)(start + count), (long long)c->obs.N);
+    PfJob j;
+    j.fill = true;
+    j.start = start;
+    j.count = count;
+    j.byte_value = byte_value;
+    return pf_queue(c, std::move(j));
+}
+
+extern "C" int hd_swap_raw(hd_ctx* c, double* io_seconds, double* total_seconds)
+{
+    if (!c) return fail(nullptr, HD_E_INVAL, "hd_swap_raw: NULL context");
+    hd_ctx::Prefetch* pf = c->pf;
+    if (!pf || !pf->any) return fail(c, HD_E_STATE, "hd_swap_raw: nothing prefetched");
+    HIPCHK(c, hipSetDevice(c->device));
+    int err;
+    std::string msg;
+    double io, t0;
+    {
+        std::unique_lock<std::mutex> lk(pf->mu);
+        pf->cv.wait(lk, [&] { return pf->q.empty() && !pf->busy; });
+        err = pf->err;
+        msg = pf->errmsg;
+        io = pf->io;
+        t0 = pf->t0;
+        pf->err = 0;
+        pf->errmsg.clear();
+        pf->any = false;
+    }
+    if (err) {
+        (void)hipStreamSynchronize(pf->st);
+        return fail(c, err, "%s", msg.c_str());
+    }
+    // the context's streams run after the copies; the old block is free once the work queued
+    // on it so far is done (the next prefetch into it waits for ev_free)
+    HIPCHK(c, hipEventRecord(pf->ev_done, pf->st));
+    HIPCHK(c, join_stream2(c));
+    HIPCHK(c, join_aux(c));
+    HIPCHK(c, hipEventRecord(pf->ev_free, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, pf->ev_done, 0));
+    {
+        std::lock_guard<std::mutex> lk(pf->mu);
+        pf->wait_free = true;
+    }
+    if (!c->d_raw) {
+        const size_t bytes = (size_t)c->obs.N * c->rowbytes;
+        if (hipMalloc(&c->d_raw, bytes) != hipSuccess) {
+            c->d_raw = nullptr;
+            return fail(c, HD_E_NOMEM, "cannot allocate %zu bytes of raw data", bytes);
+        }
+    }
+    std::swap(c->d_raw, pf->d_next);
+    c->raw_ready = true;
+    c->rawT_valid = false;
+    c->clip_valid = false;
+    c->clip.stats_valid = false;
+    if (io_seconds) *io_seconds = io;
+    if (total_seconds) *total_seconds = now_s() - t0;
     return HD_OK;
 }
 

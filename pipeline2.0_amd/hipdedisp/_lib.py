@@ -43,6 +43,7 @@ EXPORTED = [
     "hd_push_raw_file_band", "hd_fill_raw",
     "hd_realfft", "hd_zap_ranges", "hd_zapbirds", "hd_rednoise_blocks", "hd_rednoise", "hd_get_fft",
     "hd_bary_diffbins", "hd_plan_set_bary",
+    "hd_prefetch_raw_file", "hd_prefetch_raw_file_band", "hd_prefetch_fill", "hd_swap_raw",
 ]
 
 
@@ -172,6 +173,10 @@ def load():
         "hd_bary_diffbins": (ctypes.c_int, [P(ctypes.c_double), P(ctypes.c_double), i32, ctypes.c_double,
                                             ctypes.c_double, P(ctypes.c_int32), i32, P(ctypes.c_int32)]),
         "hd_plan_set_bary": (ctypes.c_int, [vp, P(ctypes.c_int32), i32]),
+        "hd_prefetch_raw_file": (ctypes.c_int, [vp, ctypes.c_char_p, P(hd_rows_src), i64]),
+        "hd_prefetch_raw_file_band": (ctypes.c_int, [vp, ctypes.c_char_p, P(hd_rows_src), i64, i64, i64, i64, i64]),
+        "hd_prefetch_fill": (ctypes.c_int, [vp, i64, i64, i32]),
+        "hd_swap_raw": (ctypes.c_int, [vp, P(ctypes.c_double), P(ctypes.c_double)]),
         "hd_sp_widths": (ctypes.c_int, [ctypes.c_double, ctypes.c_double, P(ctypes.c_int32), P(ctypes.c_int32)]),
         "hd_single_pulse": (ctypes.c_int, [vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp, i64, P(i64),
                                            P(ctypes.c_uint8), P(i64)]),

@@ -268,6 +268,34 @@ class Engine:
                   "hd_push_raw_file_band(%s)" % path)
         return io.value, tot.value
 
+    def prefetch_raw_file(self, path, table_offset, row_bytes, col_offset, col_bytes, row0, nrows, start=0,
+                          block_bytes=0, band=None):
+        """hd_prefetch_raw_file(_band): queue rows of a PSRFITS table for the NEXT beam (the
+        context's second raw slot, read on a background thread while this beam computes);
+        band = (spec_bytes, src_offset, dst_offset, nbytes) for a Mock half.  Returns at once."""
+        src = _lib.hd_rows_src(table_offset=int(table_offset), row_bytes=int(row_bytes), col_offset=int(col_offset),
+                               col_bytes=int(col_bytes), row0=int(row0), nrows=int(nrows),
+                               block_bytes=int(block_bytes))
+        if band is None:
+            self._chk(self._L.hd_prefetch_raw_file(self._ctx, os.fsencode(path), ctypes.byref(src), int(start)),
+                      "hd_prefetch_raw_file(%s)" % path)
+        else:
+            sb, so, do, nb = (int(x) for x in band)
+            self._chk(self._L.hd_prefetch_raw_file_band(self._ctx, os.fsencode(path), ctypes.byref(src), int(start),
+                                                        sb, so, do, nb), "hd_prefetch_raw_file_band(%s)" % path)
+
+    def prefetch_fill(self, start, count, byte_value=0):
+        """hd_prefetch_fill: a file gap of the NEXT beam."""
+        self._chk(self._L.hd_prefetch_fill(self._ctx, int(start), int(count), int(byte_value)), "hd_prefetch_fill")
+
+    def swap_raw(self):
+        """hd_swap_raw: the prefetched beam becomes the current raw block once its reads are
+        done (compute already queued keeps running).  Returns (pread s, s since the first
+        prefetch call)."""
+        io, tot = ctypes.c_double(), ctypes.c_double()
+        self._chk(self._L.hd_swap_raw(self._ctx, ctypes.byref(io), ctypes.byref(tot)), "hd_swap_raw")
+        return io.value, tot.value
+
     def fill_raw(self, start, count, byte_value=0):
         """hd_fill_raw: spectra [start, start+count) set to byte_value (file-gap padding)."""
         self._chk(self._L.hd_fill_raw(self._ctx, int(start), int(count), int(byte_value)), "hd_fill_raw")

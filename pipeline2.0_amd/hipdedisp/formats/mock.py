@@ -137,9 +137,10 @@ class MockBeam:
         return ObsParams(nchan=self.nchan, nbits=self.nbits, dt=float(self.dt), lofreq=float(self.lofreq),
                          df=float(self.df), N=int(self.N), nsblk=self.nsblk, flip=self.flip, npol=1, voverc=voverc)
 
-    def stream_to(self, engine, block_bytes=0):
+    def stream_to(self, engine, block_bytes=0, prefetch=False):
         """Both halves into the engine's raw block (hd_set_obs(obs_params()) first), rows from
-        rows_deleted on; returns (seconds in pread, seconds total, bytes read)."""
+        rows_deleted on; returns (seconds in pread, seconds total, bytes read).  prefetch=True
+        queues them for the NEXT beam (hd_prefetch_raw_file_band; engine.swap_raw() after)."""
         io = tot = 0.0
         nbytes = 0
         for part, s_off, nb, d_off in self.bands:
@@ -147,11 +148,16 @@ class MockBeam:
             off, rep, code = tab.cols["DATA"]
             col_bytes = rep * _TFORM_SIZES[code]
             spec_bytes = col_bytes // self.nsblk
-            x, y = engine.push_raw_file_band(part.filenames[0], tab.data_offset, tab.rowlen, off, col_bytes,
-                                             self.rows_deleted, self.nrows, 0, spec_bytes, s_off, d_off, nb,
-                                             block_bytes=block_bytes)
-            io += x
-            tot += y
+            if prefetch:
+                engine.prefetch_raw_file(part.filenames[0], tab.data_offset, tab.rowlen, off, col_bytes,
+                                         self.rows_deleted, self.nrows, 0, block_bytes=block_bytes,
+                                         band=(spec_bytes, s_off, d_off, nb))
+            else:
+                x, y = engine.push_raw_file_band(part.filenames[0], tab.data_offset, tab.rowlen, off, col_bytes,
+                                                 self.rows_deleted, self.nrows, 0, spec_bytes, s_off, d_off, nb,
+                                                 block_bytes=block_bytes)
+                io += x
+                tot += y
             nbytes += col_bytes * self.nrows
         return io, tot, nbytes
 

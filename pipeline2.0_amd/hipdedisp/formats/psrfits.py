@@ -306,10 +306,12 @@ class SpectraInfo:
             out[s0:s0 + data.shape[0]] = data
         return out
 
-    def stream_to(self, engine, block_bytes=0):
+    def stream_to(self, engine, block_bytes=0, prefetch=False):
         """Stream every file's DATA column into the engine's device raw block through the
         library's pinned double-buffered reader (hd_push_raw_file), file after file at its
-        start spectrum.  Returns (seconds in pread, seconds total, bytes)."""
+        start spectrum.  Returns (seconds in pread, seconds total, bytes).  prefetch=True
+        queues the same reads for the NEXT beam (hd_prefetch_raw_file, background; times 0)
+        -- engine.swap_raw() then makes it current."""
         if self.num_polns > 1 and not self.summed_polns:
             raise ValueError("multi-polarisation PSRFITS DATA is not supported by the stream reader")
         io = tot = 0.0
@@ -317,13 +319,20 @@ class SpectraInfo:
         for ii, (fn, tab) in enumerate(zip(self.filenames, self._tables)):
             off, rep, code = tab.cols["DATA"]
             col_bytes = rep * _TFORM_SIZES[code]
-            a, b = engine.push_raw_file(fn, tab.data_offset, tab.rowlen, off, col_bytes, 0, tab.nrows,
-                                        start=int(self.start_spec[ii]), block_bytes=block_bytes)
-            io += a
-            tot += b
+            if prefetch:
+                engine.prefetch_raw_file(fn, tab.data_offset, tab.rowlen, off, col_bytes, 0, tab.nrows,
+                                         start=int(self.start_spec[ii]), block_bytes=block_bytes)
+            else:
+                a, b = engine.push_raw_file(fn, tab.data_offset, tab.rowlen, off, col_bytes, 0, tab.nrows,
+                                            start=int(self.start_spec[ii]), block_bytes=block_bytes)
+                io += a
+                tot += b
             nbytes += col_bytes * tab.nrows
         for start, count in self.gaps():
-            engine.fill_raw(start, count, 0)
+            if prefetch:
+                engine.prefetch_fill(start, count, 0)
+            else:
+                engine.fill_raw(start, count, 0)
         return io, tot, nbytes
 
     def read_calib(self):

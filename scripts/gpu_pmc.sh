@@ -6,7 +6,7 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 rm -rf gpurun_out/pmc && mkdir -p gpurun_out/pmc
-B="python3 bench.py --steps 1 --warmup 0 --no-cpu --e2e-beams 0 --sp-beams 0 --fft-beams 0 --rfi-beams 0"
+B="python3 bench.py --steps 1 --warmup 0 --no-cpu --e2e-beams 0 --sp-beams 0 --fft-beams 0 --rfi-beams 0 --stream-beams 0"
 run() {  # name counters...
   local n=$1; shift
   timeout -s KILL 240 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pmc/$n -o $n --pmc "$@" -- $B \

@@ -5,7 +5,7 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 rm -rf gpurun_out/tlb && mkdir -p gpurun_out/tlb
-B="python3 bench.py --steps 1 --warmup 0 --no-cpu --e2e-beams 0 --sp-beams 0 --fft-beams 0 --rfi-beams 0"
+B="python3 bench.py --steps 1 --warmup 0 --no-cpu --e2e-beams 0 --sp-beams 0 --fft-beams 0 --rfi-beams 0 --stream-beams 0"
 A="python3 scripts/ab_stage2.py 0 --probes=0 --reps=1"
 run() {  # dir cmd counters...
   local n=$1 cmd=$2; shift 2
