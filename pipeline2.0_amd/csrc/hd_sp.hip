@@ -26,6 +26,8 @@
 // so oracle/sp_oracle.c reproduces every value bit for bit; PRESTO's float32 FFT
 // convolution is replaced by exact window sums (no circular wrap of windows wider than its
 // 96-sample chunk overlap).
+#include <stdlib.h>
+
 #include "hd_internal.h"
 
 namespace hd {
@@ -222,6 +224,7 @@ struct SpArgs {
     hd_sp_hit* hits;
     unsigned long long* count;
     int64_t cap;
+    int32_t probe;                               // profiling (HD_SP_PROBE): 1 no walk, 2 no width-1, 4 no bitmask
 };
 
 __device__ __forceinline__ void sp_emit(const SpArgs& a, int dm, int64_t bin, int wi, double s)
@@ -281,7 +284,7 @@ __global__ __launch_bounds__(256) void k_sp_hits(SpArgs a)
     };
     auto bad = [&](int o) { return cf[((c0 + o) / kSpBlock) * 4 + 3] != 0.0; };
     // width 1: every value above threshold outside the bad blocks (no prune_related1)
-    for (int o = tid; o < kSpChunk; o += 256) {
+    for (int o = tid; o < kSpChunk && !(a.probe & 2); o += 256) {
         if (bad(o)) continue;
         const double s = (double)sp_norm(xs, cf, c0 + o, a.ls);
         if (s > a.threshold) sp_emit(a, dm, c0 + o, 0, s);
@@ -294,14 +297,14 @@ __global__ __launch_bounds__(256) void k_sp_hits(SpArgs a)
         for (int t = tid; t < nr * kSpWords; t += 256) {
             const int j = t / kSpWords, wd = t - j * kSpWords;
             uint32_t m = 0;
-            for (int b = 0; b < 32; b++)
+            for (int b = 0; b < 32 && !(a.probe & 4); b++)
                 if (boxcar(r0 + j, 32 * wd + b) > a.threshold) m |= 1u << b;
             bits[j][wd] = m;
         }
         __syncthreads();
         // prune_related1: width r0 + j walked by lane j >> 2 of wave j & 3
         const int j = wv + 4 * ln;
-        if (ln < 2 && j < nr) {
+        if (ln < 2 && j < nr && !(a.probe & 1)) {
             const int wi = r0 + j;
             const int h = a.widths[wi] / 2;
             const uint32_t* bm = bits[j];
@@ -371,6 +374,7 @@ hipError_t launch_sp_hits(const float* x, int64_t stride, int ndm, int nblocks, 
     a.hits = hits;
     a.count = count;
     a.cap = cap;
+    a.probe = getenv("HD_SP_PROBE") ? atoi(getenv("HD_SP_PROBE")) : 0;
     if (a.nchunks <= 0 || ndm <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_sp_hits, dim3((unsigned)(ndm * a.nchunks)), dim3(256), 0, st, a);
     return hipGetLastError();
