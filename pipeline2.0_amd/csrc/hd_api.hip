@@ -115,6 +115,10 @@ struct hd_ctx {
     hd_sp_hit* d_sp_hits = nullptr;
     int64_t sp_hits_cap = 0;
     unsigned long long* d_sp_count = nullptr;
+    uint8_t* d_sp_bad = nullptr;    // bad-block flags as bytes
+    size_t sp_bad_bytes = 0;
+    void* sp_pin = nullptr;         // pinned staging of the hits / flags D2H
+    size_t sp_pin_bytes = 0;
     double* d_sum_parts = nullptr;  // hd_series_sum partials
     // streaming ingest (hd_push_raw_file): pinned host blocks of the reader threads
     PinSet pins;
@@ -424,6 +428,8 @@ extern "C" int hd_close(hd_ctx* c)
     dfree(c->d_sp_coef);
     dfree(c->d_sp_hits);
     dfree(c->d_sp_count);
+    dfree(c->d_sp_bad);
+    if (c->sp_pin) (void)hipHostFree(c->sp_pin);
     dfree(c->d_sum_parts);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_aux0) (void)hipEventDestroy(c->ev_aux0);
@@ -2566,19 +2572,42 @@ extern "C" int hd_single_pulse(hd_plan* p, double dt, double maxwidth, double th
                                      threshold, c->d_sp_hits, c->d_sp_count, c->sp_hits_cap, st));
         HIPCHK(c, d2h(&cnt, c->d_sp_count, sizeof(cnt), st));
     }
-    std::vector<double> coef;
-    if (bad_blocks && nblocks > 0) {
-        coef.resize((size_t)ndm * nblocks * 4);
-        HIPCHK(c, d2h(coef.data(), c->d_sp_coef, sizeof(double) * coef.size(), st));
-    }
-    if (bad_blocks)
-        for (size_t i = 0; i < (size_t)ndm * nblocks; i++) bad_blocks[i] = coef[4 * i + 3] != 0.0;
+    // the bad-block flags as bytes (device-packed), and the hits, through the context's pinned
+    // staging block (pageable copies of a few MB cost milliseconds per pass)
+    const size_t nbad = bad_blocks && nblocks > 0 ? (size_t)ndm * nblocks : 0;
     *nhits = (int64_t)cnt;
-    if ((int64_t)cnt > cap)
+    const bool fits = (int64_t)cnt <= cap;
+    const size_t hbytes = fits ? sizeof(hd_sp_hit) * cnt : 0;
+    const size_t need = std::max(hbytes, nbad);
+    if (need > c->sp_pin_bytes) {
+        HIPCHK(c, hipStreamSynchronize(st));
+        if (c->sp_pin) HIPCHK(c, hipHostFree(c->sp_pin));
+        c->sp_pin = nullptr;
+        c->sp_pin_bytes = 0;
+        HIPCHK(c, hipHostMalloc(&c->sp_pin, need + need / 4, hipHostMallocDefault));
+        c->sp_pin_bytes = need + need / 4;
+    }
+    if (nbad) {
+        if (c->sp_bad_bytes < nbad) {
+            HIPCHK(c, hipStreamSynchronize(st));
+            dfree(c->d_sp_bad);
+            c->d_sp_bad = nullptr;
+            c->sp_bad_bytes = 0;
+            HIPCHK(c, hipMalloc(&c->d_sp_bad, nbad));
+            c->sp_bad_bytes = nbad;
+        }
+        HIPCHK(c, hd::launch_sp_badflags(c->d_sp_coef, (int64_t)nbad, c->d_sp_bad, st));
+        HIPCHK(c, hipMemcpyAsync(c->sp_pin, c->d_sp_bad, nbad, hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipStreamSynchronize(st));
+        memcpy(bad_blocks, c->sp_pin, nbad);
+    }
+    if (!fits)
         return fail(c, HD_E_NOMEM, "hd_single_pulse: %llu hits > capacity %lld (call again with room)", cnt,
                     (long long)cap);
     if (!cnt) return HD_OK;
-    HIPCHK(c, hipMemcpy(hits, c->d_sp_hits, sizeof(hd_sp_hit) * cnt, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpyAsync(c->sp_pin, c->d_sp_hits, hbytes, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    memcpy(hits, c->sp_pin, hbytes);
     // per DM (in parallel): the script's dm_candlist order -- by bin, widths in increasing
     // order among equal bins (width-1 hits appended first, every downfactor's bisect.insort
     // after equals) -- then prune_related2 (its greedy walk, literally) and prune_border_cases

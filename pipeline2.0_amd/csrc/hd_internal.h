@@ -174,6 +174,7 @@ hipError_t launch_stage1_fixup(const Stage1Multi& a, const int32_t* events, cons
 // single-pulse search (hd_sp.hip): per-block detrend/std + per-DM bad blocks -> coef
 // [ndm][nblocks][4] (mean, slope, std, bad); boxcar hits above threshold
 int sp_max_blocks();
+hipError_t launch_sp_badflags(const double* coef, int64_t n, uint8_t* bad, hipStream_t st);
 hipError_t launch_sp_blocks(const float* x, int64_t stride, int ndm, int nblocks, double* coef, hipStream_t st);
 hipError_t launch_sp_hits(const float* x, int64_t stride, int ndm, int nblocks, const double* coef, int64_t ls,
                           const int32_t* widths, const double* rsw, int nwidths, double threshold, hd_sp_hit* hits,

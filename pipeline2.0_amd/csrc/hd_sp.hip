@@ -16,7 +16,11 @@
 //     form it reduces to: in bin order a hit is a "pivot" unless the
 //     last pivot lies within h = w/2 bins and is strictly stronger; a pivot survives when
 //     the next pivot is more than h bins later (or there is none).  One lane walks one
-//     (chunk, width) over a bitmask of its above-threshold bins;
+//     (chunk, width) over a bitmask of its above-threshold bins (made by wave ballots, one
+//     lane per bin, so the prefix-sum reads are bank-conflict free).  Splitting the walk into
+//     independent runs (a hit more than h bins after the previous one starts a new run) over
+//     the 64 lanes measured slower: a bright pulse is one run of thousands of hits, still
+//     walked by one lane, and the lanes' second pass for the zip costs more than it saves;
 //   * the script's bad-block test after the walk: survivor m is paired with the block of the
 //     m-th UNPRUNED hit (`zip(hibins, hivals, hiblocks)` with hiblocks taken before
 //     prune_related1); width-1 hits are tested against their own block.
@@ -38,7 +42,7 @@ constexpr int kSpHalo = 224;                 // >= max downfact / 2 + 1 (a boxca
 constexpr int kSpSeg = 33;                   // prefix-sum segment per thread
 constexpr int kSpWin = 256 * kSpSeg;         // kSpChunk + 2 * kSpHalo = 8448
 constexpr int kSpWords = kSpChunk / 32;      // hit bitmask words per (chunk, width)
-constexpr int kSpRound = 7;                  // widths walked per round (bitmask LDS: 7 KB)
+constexpr int kSpRound = 8;                  // widths per round (bitmask LDS: 8 KB), walked by lanes 0-1 of each wave
 
 __device__ __forceinline__ double wave_sum_f64(double v)
 {
@@ -252,6 +256,7 @@ __global__ __launch_bounds__(256) void k_sp_hits(SpArgs a)
     const int64_t w0 = (int64_t)ch * kSpChunk - kSpHalo;     // sample of window element 0
     const int64_t c0 = (int64_t)ch * kSpChunk;               // first bin of the chunk
     const int tid = threadIdx.x;
+    const int wv = tid >> 6, ln = tid & 63;
     double loc[kSpSeg];
     double run = 0.0;
 #pragma unroll
@@ -289,17 +294,19 @@ __global__ __launch_bounds__(256) void k_sp_hits(SpArgs a)
         const double s = (double)sp_norm(xs, cf, c0 + o, a.ls);
         if (s > a.threshold) sp_emit(a, dm, c0 + o, 0, s);
     }
-    const int wv = tid >> 6, ln = tid & 63;
     for (int r0 = 1; r0 < a.nwidths; r0 += kSpRound) {
         const int nr = min(kSpRound, a.nwidths - r0);
         // the above-threshold bins of widths r0 .. r0+nr-1 (bad blocks included: the script
-        // prunes before it looks at blocks)
-        for (int t = tid; t < nr * kSpWords; t += 256) {
-            const int j = t / kSpWords, wd = t - j * kSpWords;
-            uint32_t m = 0;
-            for (int b = 0; b < 32 && !(a.probe & 4); b++)
-                if (boxcar(r0 + j, 32 * wd + b) > a.threshold) m |= 1u << b;
-            bits[j][wd] = m;
+        // prunes before it looks at blocks): lane = bin, one ballot per 64 bins (consecutive
+        // lanes read consecutive P entries: no bank conflicts)
+        for (int t = wv; t < nr * (kSpChunk / 64); t += 4) {
+            const int j = t / (kSpChunk / 64), q = t - j * (kSpChunk / 64);
+            const bool hit = !(a.probe & 4) && boxcar(r0 + j, 64 * q + ln) > a.threshold;
+            const uint64_t m = __ballot(hit);
+            if (ln == 0) {
+                bits[j][2 * q] = (uint32_t)m;
+                bits[j][2 * q + 1] = (uint32_t)(m >> 32);
+            }
         }
         __syncthreads();
         // prune_related1: width r0 + j walked by lane j >> 2 of wave j & 3
@@ -335,6 +342,20 @@ __global__ __launch_bounds__(256) void k_sp_hits(SpArgs a)
         }
         __syncthreads();
     }
+}
+
+// The bad-block flags as bytes (the host needs ndm * nblocks bytes, not the 32-byte records).
+__global__ __launch_bounds__(256) void k_sp_badflags(const double* __restrict__ coef, int64_t n, uint8_t* __restrict__ bad)
+{
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) bad[i] = coef[4 * i + 3] != 0.0;
+}
+
+hipError_t launch_sp_badflags(const double* coef, int64_t n, uint8_t* bad, hipStream_t st)
+{
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_sp_badflags, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, coef, n, bad);
+    return hipGetLastError();
 }
 
 int sp_max_blocks() { return kSpMaxBlocks; }
