@@ -731,36 +731,66 @@ struct Fix8Geom {
     int nchunk, jmax;         // chunks per item; boundary outputs per (pass, subband) at most
 };
 
+// The oracle's fold of one output (k outer, channel inner, from 0.0f) over the LDS window.
+// CPS / DS > 0 are compile-time (the channel loop unrolls; each channel's delay and its two
+// blocks' zap flags are read once, not once per k); 0 = runtime values.
+template <int CPS, int DS>
 __device__ __forceinline__ float fix8_fold(const Stage1Multi& a, const uint8_t* lraw, const uint8_t* flg,
                                            const uint8_t* zap, const float* pad, const int16_t* dl, int Wp, int G,
-                                           int lc0, int64_t trel, int bndrel)
+                                           int lc0, int trel, int bndrel)
 {
     // trel = j*ds - wlo: window row of (k = 0, delay 0); dl: this pass's delays of the chunk
-    const int ds = a.ds, cps = a.cps;
+    const int ds = DS ? DS : a.ds, cps = CPS ? CPS : a.cps;
     float acc = 0.0f;
-    for (int k = 0; k < ds; k++) {
-        float sk = 0.0f;
-        for (int cc = 0; cc < cps; cc++) {
-            const int lc = lc0 + cc;
-            const int lr = (int)trel + k + dl[lc];
-            const int part = lr >= bndrel;
-            const bool rep = flg[lr] | zap[part * G + lc];
-            const float x = rep ? pad[part * G + lc] : (float)lraw[lc * Wp + lr];
-            sk += x;
+    if constexpr (CPS > 0) {
+        int d[CPS];
+        uint32_t zb = 0;                                   // bit cc: zapped in block slot 0; 16 + cc: slot 1
+#pragma unroll
+        for (int cc = 0; cc < CPS; cc++) {
+            d[cc] = trel + dl[lc0 + cc];
+            zb |= (uint32_t)zap[lc0 + cc] << cc;
+            zb |= (uint32_t)zap[G + lc0 + cc] << (16 + cc);
         }
-        acc += sk;
+#pragma unroll
+        for (int k = 0; k < ds; k++) {
+            float sk = 0.0f;
+#pragma unroll
+            for (int cc = 0; cc < CPS; cc++) {
+                const int lr = d[cc] + k;
+                const int part = lr >= bndrel;
+                const bool rep = flg[lr] | ((zb >> (16 * part + cc)) & 1u);
+                const float x = rep ? pad[part * G + lc0 + cc] : (float)lraw[(lc0 + cc) * Wp + lr];
+                sk += x;
+            }
+            acc += sk;
+        }
+    } else {
+        for (int k = 0; k < ds; k++) {
+            float sk = 0.0f;
+            for (int cc = 0; cc < cps; cc++) {
+                const int lc = lc0 + cc;
+                const int lr = trel + k + dl[lc];
+                const int part = lr >= bndrel;
+                const bool rep = flg[lr] | zap[part * G + lc];
+                const float x = rep ? pad[part * G + lc] : (float)lraw[lc * Wp + lr];
+                sk += x;
+            }
+            acc += sk;
+        }
     }
     if (a.ds_mode == 1) acc = acc / (float)ds;
     return acc;
 }
 
+template <int CPS, int DS>
 __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm, const int32_t* __restrict__ events,
                                                     const int32_t* __restrict__ nevents, int boundaries)
 {
     // dynamic LDS: raw [G][Wp] | flags [Wp] | zap [2][G] | pad [2][G] f32 | dly [npass][G] i16
     //              | lo, cnt [npass][SG] (boundary items)
     extern __shared__ __attribute__((aligned(16))) char fsm[];
-    const int G = gm.G, Wp = gm.Wp, SG = gm.SG, npass = a.npass, cps = a.cps, ds = a.ds;
+    const int G = gm.G, Wp = gm.Wp, SG = gm.SG, npass = a.npass;
+    const int cps = CPS ? CPS : a.cps, ds = DS ? DS : a.ds;
     uint8_t* lraw = (uint8_t*)fsm;
     uint8_t* flg = lraw + G * Wp;
     float* pad = (float*)(flg + Wp);                      // Wp is a multiple of 16
@@ -850,13 +880,14 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
                 const int j = jn / ds;
                 if (j >= nds) continue;
                 const int lc0 = lc - lc % cps;
-                bool dup = false;
-                for (int l2 = lc0; l2 < lc; l2++) {
-                    const int jn2 = r - dl[l2];
-                    dup |= jn2 >= 0 && jn2 / ds == j;
+                // delays fall with frequency within a subband, so the outputs its channels map
+                // r to rise with the channel and equal ones are adjacent: only channel lc - 1
+                // can name j first
+                if (lc > lc0) {
+                    const int jn2 = r - dl[lc - 1];
+                    if (jn2 >= 0 && jn2 / ds == j) continue;
                 }
-                if (dup) continue;
-                const float acc = fix8_fold(a, lraw, flg, zap, pad, dl, Wp, G, lc0, (int64_t)j * ds - wlo, bndrel);
+                const float acc = fix8_fold<CPS, DS>(a, lraw, flg, zap, pad, dl, Wp, G, lc0, j * ds - wlo, bndrel);
                 const int s = (c0 + lc0) / cps;
                 if (a.sub_dtype == 0) {
                     const int16_t q = to_i16(acc, a.sub_round);
@@ -874,7 +905,7 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
                 const int p = ps / SG, sl = ps - p * SG;
                 const int j = lo_s[ps] + jj;
                 const int16_t* dl = dly + p * G;
-                const float acc = fix8_fold(a, lraw, flg, zap, pad, dl, Wp, G, sl * cps, (int64_t)j * ds - wlo, bndrel);
+                const float acc = fix8_fold<CPS, DS>(a, lraw, flg, zap, pad, dl, Wp, G, sl * cps, j * ds - wlo, bndrel);
                 const int s = chunk * SG + sl;
                 if (a.sub_dtype == 0) {
                     const int16_t q = to_i16(acc, a.sub_round);
@@ -937,13 +968,19 @@ hipError_t launch_stage1_fixup(const Stage1Multi& a, const int32_t* events, cons
     if (!(a.probe & 128) && fix8_geom(a, g)) {           // probe bit 7: the generic kernel
         const unsigned grid = (unsigned)(std::max(1, 4096 / g.nchunk) * g.nchunk);
         const size_t lb = fix8_lds_bytes(a, g);
+        // compile-time (cps, ds) for the Mock DDplan's stages (16 bits of zap flags per
+        // channel set: cps <= 16), else the runtime kernel
+        const void* fn = (const void*)k_stage1_fix8<0, 0>;
+#define HD_F8(C, D) if (a.cps == C && a.ds == D) fn = (const void*)k_stage1_fix8<C, D>;
+        HD_F8(10, 1) HD_F8(10, 2) HD_F8(10, 3) HD_F8(10, 5) HD_F8(10, 6) HD_F8(10, 10)
+        HD_F8(8, 1) HD_F8(16, 1)
+#undef HD_F8
         if (lb > 64 * 1024) {
-            const hipError_t e = set_max_lds((const void*)k_stage1_fix8, (int)lb);
+            const hipError_t e = set_max_lds(fn, (int)lb);
             if (e != hipSuccess) return e;
         }
-        hipLaunchKernelGGL(k_stage1_fix8, dim3(grid), dim3(256), lb, st, a, g, events, nevents,
-                           boundaries);
-        return hipGetLastError();
+        void* args[] = {(void*)&a, (void*)&g, (void*)&events, (void*)&nevents, (void*)&boundaries};
+        return hipLaunchKernel(fn, dim3(grid), dim3(256), args, lb, st);
     }
     // boundary items scan one subband per thread (nsub <= blockDim); clipped-spectrum items loop
     // over channels, so any nsub (e.g. the nsub = nchan no-subband pass) takes them
