@@ -41,16 +41,20 @@ def parse():
                          "stage 2 on its own stream so the next DDplan stage's stage 1 overlaps it; per-kernel event "
                          "times then include the shared time, so the roofline is taken at 1")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU work for the baseline sample")
-    ap.add_argument("--e2e-beams", type=int, default=1,
+    # the legs after the timed steps characterise one GPU: by default (-1) they run at world
+    # size 1 only (8 ranks each writing a beam's 47 GB of .dat files, or two 4 GB PSRFITS
+    # beams, would share one host's tmpfs)
+    ap.add_argument("--e2e-beams", type=int, default=-1,
                     help="beams run end to end (.dat/.inf files written) after the timed steps; 0 = skip")
-    ap.add_argument("--sp-beams", type=int, default=1,
+    ap.add_argument("--sp-beams", type=int, default=-1,
                     help="beams of single-pulse search (hd_single_pulse) timed after the steps; 0 = skip")
-    ap.add_argument("--fft-beams", type=int, default=1,
+    ap.add_argument("--fft-beams", type=int, default=-1,
                     help="beams of realfft + zapbirds + rednoise (hd_fft.hip) timed after the steps; 0 = skip")
-    ap.add_argument("--rfi-beams", type=int, default=1,
+    ap.add_argument("--rfi-beams", type=int, default=-1,
                     help="beams of rfifind statistics + mask decisions (hd_rfi.hip) timed last; 0 = skip")
-    ap.add_argument("--stream-beams", type=int, default=3,
-                    help="beams of the overlapped PSRFITS-streaming leg (configs[4]; prefetch thread), run last; 0 = skip")
+    ap.add_argument("--stream-beams", type=int, default=-1,
+                    help="beams of the overlapped PSRFITS-streaming leg (configs[4]; prefetch thread; 3 at world "
+                         "size 1), run last; 0 = skip")
     ap.add_argument("--mode", choices=["beam", "slices", "shard"], default="beam",
                     help="beam: one beam per rank (weak scaling, configs[4]); slices: ONE beam cut into per-rank "
                          "time slices, every rank runs all 57 passes on its slice (strong, configs[2]; RCCL carries "
@@ -423,6 +427,9 @@ def cpu_baseline(obs, synth, ddplans, target_s, mask, pts, pad, omp):
 def main():
     args = parse()
     world, rank, local, dist, torch = dist_setup(args)
+    for leg, n1 in (("e2e_beams", 1), ("sp_beams", 1), ("fft_beams", 1), ("rfi_beams", 1), ("stream_beams", 3)):
+        if getattr(args, leg) < 0:
+            setattr(args, leg, n1 if world == 1 else 0)
     from hipdedisp import Engine, Opts, plan as P
     from hipdedisp.synth import palfa_obs, palfa_synth, rfifind_ptsperint, synth_mask
 

@@ -325,18 +325,41 @@ __global__ __launch_bounds__(256) void k_sp_hits(SpArgs a)
                 zm &= zm - 1;
                 if (!bad(hb)) sp_emit(a, dm, c0 + b, wi, x);
             };
-            for (int wd = 0; wd < kSpWords; wd++) {
-                uint32_t m = bm[wd];
-                while (m) {
-                    const int b = 32 * wd + __builtin_ctz(m);
-                    m &= m - 1;
-                    const double x = boxcar(wi, b);
-                    if (have && b - lpb <= h && lpx > x) continue;     // removed by the last pivot
-                    if (have && b - lpb > h) survivor(lpb, lpx);       // else the new pivot removes it
-                    lpb = b;
-                    lpx = x;
-                    have = true;
+            // the hits in bin order, their boxcar values read kSpLook hits ahead of the walk
+            // (a dense run is thousands of hits: the walk must not wait for each value's LDS
+            // reads in turn)
+            int rw = 0;
+            uint32_t rm = bm[0];
+            auto next_bit = [&]() -> int {
+                while (!rm && rw < kSpWords - 1) rm = bm[++rw];
+                if (!rm) return -1;
+                const int b = 32 * rw + __builtin_ctz(rm);
+                rm &= rm - 1;
+                return b;
+            };
+            constexpr int kSpLook = 4;
+            int qb[kSpLook];
+            double qx[kSpLook];
+#pragma unroll
+            for (int k = 0; k < kSpLook; k++) {
+                qb[k] = next_bit();
+                qx[k] = qb[k] >= 0 ? boxcar(wi, qb[k]) : 0.0;
+            }
+            while (qb[0] >= 0) {
+                const int b = qb[0];
+                const double x = qx[0];
+#pragma unroll
+                for (int k = 0; k + 1 < kSpLook; k++) {
+                    qb[k] = qb[k + 1];
+                    qx[k] = qx[k + 1];
                 }
+                qb[kSpLook - 1] = next_bit();
+                qx[kSpLook - 1] = qb[kSpLook - 1] >= 0 ? boxcar(wi, qb[kSpLook - 1]) : 0.0;
+                if (have && b - lpb <= h && lpx > x) continue;         // removed by the last pivot
+                if (have && b - lpb > h) survivor(lpb, lpx);           // else the new pivot removes it
+                lpb = b;
+                lpx = x;
+                have = true;
             }
             if (have) survivor(lpb, lpx);
         }

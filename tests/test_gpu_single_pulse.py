@@ -104,3 +104,46 @@ def test_single_pulse_many_hits_and_short_series(engine, beam, tmp_path):
         assert len(got) == 0 and bad.shape == (76, 6)
     finally:
         p.destroy()
+
+
+def test_candidate_lists_end_to_end_clip_vs_noclip(engine):
+    """North-star 'identical candidate lists' on two independent paths, end to end: the
+    product (stage 1 + stage 2 on the GPU, then hd_single_pulse on the series still in HBM)
+    against the oracle (the C prepsubband restatement's own series, then sp_oracle's search),
+    for a low-DM pass of a beam with zero-DM spikes, once with clipping on (-clip 6, what the
+    reference's commands leave on) and once with -noclip.  The two settings give different
+    series, so the test also asserts the candidate lists follow them: without clipping the
+    spikes make thousands of DM ~ 0 candidates that clip_times removes."""
+    N = 1 << 18
+    obs = palfa_obs(N=N, nbits=8)
+    s = palfa_synth()
+    raw = host_spectra(obs, s)
+    pp = PassParams(subdm=3.8, lodm=0.0, dmstep=0.1, numdms=76, nsub=96, ds=1, numout=plan.choose_N(N))
+    dms = [0.1 * i for i in range(76)]
+    lists = {}
+    for clip in (6.0, 0.0):
+        opts = Opts(clip_sigma=clip)
+        engine.set_obs(obs, opts)
+        engine.synth_device(s)
+        p = engine.plan(pp)
+        try:
+            p.run_subband()
+            p.run_dedisp(to_host=False)
+            dt = p.sub_dt
+            wl = SP.widths(dt, 0.1)
+            got, gbad = SP.device_candidates(p, dt, 0.1, 5.0)
+            have = [(r[0], r[1], wl[r[2]], r[4]) for r in got.tolist()]
+            nds, numout = p.nds, p.numout
+        finally:
+            p.destroy()
+        _, series = OR.run_pass(obs, opts, raw, pp, omp=True)      # the oracle's own series
+        hits, bad = OR.sp_hits(series, wl, 5.0)
+        ref = OR.sp_candidates(hits, bad, wl, dms, dt, nds, numout, ls=series.shape[1] // 1000 * 1000 // 8000 * 8000)
+        want = [(d, c.bin, c.downfact, c.sigma) for d, cl in enumerate(ref) for c in cl]
+        assert np.array_equal(gbad, bad)
+        assert have == want, "clip %g: device and oracle candidate lists differ" % clip
+        lists[clip] = have
+    low = {k: sum(1 for c in v if c[0] < 20) for k, v in lists.items()}     # DM < 2
+    assert lists[6.0] != lists[0.0]
+    assert low[0.0] > 10 * max(low[6.0], 1) and len(lists[0.0]) > 5 * len(lists[6.0])
+    engine.set_obs(obs, Opts())
