@@ -1554,8 +1554,9 @@ static void pair_tables(hd_plan* p, bool i16, int ppc, hd_plan::Wide& w, std::ve
             span0 = std::max(span0, hi - lo);
             umax = std::max(umax, (int)r.size());
         }
-    const int ws = (int)round_up((size_t)(256 * R + span0 + 4), 4);
-    const int npw = (int)((((size_t)ws + 10 + k1max) * 2 + 1023) / 1024);
+    // a multiple of 8 elements: the expand stores 8-element (16-byte) pieces of each copy
+    const int ws = (int)round_up((size_t)(256 * R + span0 + 4), 8);
+    const int npw = (int)((((size_t)ws + 14 + k1max) * 2 + 1023) / 1024);
     const int nbp = (int)(((size_t)ppc * dpb * 4 + 1023) / 1024);
     if (2 * ppc * npw + nbp > nw || hd::stage2_pair_lds_bytes(ws, npw, nbp, nsub, umax, ppc) > 160 * 1024 ||
         !hd::stage2_pair_supports(Q, R))

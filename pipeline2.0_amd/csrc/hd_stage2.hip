@@ -869,6 +869,45 @@ __device__ __forceinline__ void load8_shift64(const uint32_t* w32, int x, uint32
     for (int m = 0; m < 4; m++) o[m] = __builtin_amdgcn_alignbit(w[m + 1], w[m], sh);
 }
 
+// Twelve int16 elements x .. x+11 of a staging window (any parity) as 6 packed pairs, from
+// three reads of the 7 dwords j = x >> 1 .. j + 6: one ds_read_b128 at the 16-byte-aligned
+// dword, one ds_read_b64 and one ds_read_b32 around it (the split depends on j & 3, uniform per
+// window).  Lanes 16 bytes apart (8-element items) keep the b128 reads conflict-free.
+__device__ __forceinline__ void load12_shift(const uint32_t* w32, int x, uint32_t (&o)[6])
+{
+    const int j = x >> 1;
+    const uint32_t sh = (uint32_t)(x & 1) * 16u;
+    uint32_t w[7];
+    switch (j & 3) {
+    case 0: {
+        const uint4 a = *(const uint4*)(w32 + j);
+        const uint2 b = *(const uint2*)(w32 + j + 4);
+        w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y; w[6] = w32[j + 6];
+        break;
+    }
+    case 1: {
+        const uint2 b = *(const uint2*)(w32 + j + 1);
+        const uint4 a = *(const uint4*)(w32 + j + 3);
+        w[0] = w32[j]; w[1] = b.x; w[2] = b.y; w[3] = a.x; w[4] = a.y; w[5] = a.z; w[6] = a.w;
+        break;
+    }
+    case 2: {
+        const uint2 b = *(const uint2*)(w32 + j);
+        const uint4 a = *(const uint4*)(w32 + j + 2);
+        w[0] = b.x; w[1] = b.y; w[2] = a.x; w[3] = a.y; w[4] = a.z; w[5] = a.w; w[6] = w32[j + 6];
+        break;
+    }
+    default: {
+        const uint4 a = *(const uint4*)(w32 + j + 1);
+        const uint2 b = *(const uint2*)(w32 + j + 5);
+        w[0] = w32[j]; w[1] = a.x; w[2] = a.y; w[3] = a.z; w[4] = a.w; w[5] = b.x; w[6] = b.y;
+        break;
+    }
+    }
+#pragma unroll
+    for (int m = 0; m < 6; m++) o[m] = __builtin_amdgcn_alignbit(w[m + 1], w[m], sh);
+}
+
 template <int Q, int R, int PPC, bool NN>
 __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, const int32_t* __restrict__ boff)
 {
@@ -895,7 +934,6 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, const int32_
     const int dpb = a.dms_per_blk;
     const int dblk0 = yb * dpb;
     const int ws = a.wstride;
-    const int upw = ws >> 2;
     const int npw = a.ring_npw;                       // 1 KiB DMA pieces per window
     const int nbp = a.ring_nbp;                       // pieces of a chunk's offset block
     const int umax = a.umax;
@@ -996,25 +1034,29 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, const int32_
             const int k0 = pt[0] & 1;
             const int U = pt[2];
             int16_t* buf = (int16_t*)(lds_raw + exp0) + ((cc & 1) * PPC + k) * (umax * 4 * ws);
-            for (int idx = threadIdx.x; idx < U * upw; idx += nthr) {
+            // item = 8 elements of every copy (ws is a multiple of 8: 16-byte stores)
+            const int up8 = ws >> 3;
+            for (int idx = threadIdx.x; idx < U * up8; idx += nthr) {
                 int u = 0, uu = idx;
 #pragma unroll
                 for (int m = 1; m < kPairUMax; m++)
-                    if (uu >= upw) { uu -= upw; u++; }
-                uint32_t A[4], B[4], P[4];
-                load8_shift64(S0, k0 + 4 * uu, A);
-                load8_shift64(S1, pt[3 + u] + 4 * uu, B);
+                    if (uu >= up8) { uu -= up8; u++; }
+                uint32_t A[6], B[6], P[6];
+                load12_shift(S0, k0 + 8 * uu, A);
+                load12_shift(S1, pt[3 + u] + 8 * uu, B);
 #pragma unroll
-                for (int m = 0; m < 4; m++)
+                for (int m = 0; m < 6; m++)
                     P[m] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(short2v, A[m]) + __builtin_bit_cast(short2v, B[m]));
-                uint2* dst0 = (uint2*)(buf + (u * 4) * ws);
+                uint4* dst0 = (uint4*)(buf + (u * 4) * ws);
                 const uint32_t h1 = __builtin_amdgcn_alignbit(P[1], P[0], 16);
                 const uint32_t h3 = __builtin_amdgcn_alignbit(P[2], P[1], 16);
                 const uint32_t h5 = __builtin_amdgcn_alignbit(P[3], P[2], 16);
-                dst0[uu] = make_uint2(P[0], P[1]);
-                dst0[upw + uu] = make_uint2(h1, h3);
-                dst0[2 * upw + uu] = make_uint2(P[1], P[2]);
-                dst0[3 * upw + uu] = make_uint2(h3, h5);
+                const uint32_t h7 = __builtin_amdgcn_alignbit(P[4], P[3], 16);
+                const uint32_t h9 = __builtin_amdgcn_alignbit(P[5], P[4], 16);
+                dst0[uu] = make_uint4(P[0], P[1], P[2], P[3]);
+                dst0[up8 + uu] = make_uint4(h1, h3, h5, h7);
+                dst0[2 * up8 + uu] = make_uint4(P[1], P[2], P[3], P[4]);
+                dst0[3 * up8 + uu] = make_uint4(h3, h5, h7, h9);
             }
         }
     };
