@@ -2162,14 +2162,20 @@ static bool stage1_q8_tiling(const hd_ctx* c, int nsub, int ds, int dmax, hd::St
     const int W = S + ((dmax + 15) & ~15);            // whole 16-row fill units (16-byte LDS stores)
     int sg = 0, v = 0;
     size_t best = 0;
+    // HD_Q8_SG_CAP (profiling): at most this many subbands per workgroup
+    const int sgcap = getenv("HD_Q8_SG_CAP") ? atoi(getenv("HD_Q8_SG_CAP")) : 4;
     for (int cand : {4, 2, 1}) {
-        if (nsub % cand) continue;
+        if (nsub % cand || (cand > sgcap && cand > 1)) continue;
         const int G = cand * cps;
         const int cv = (G % 8 == 0 && nchan % 8 == 0) ? 8 : (G % 4 == 0 && nchan % 4 == 0) ? 4 : 0;
         if (!cv) continue;
         const size_t lds = (size_t)G * W * 4;
         if (lds > 160 * 1024) continue;
-        if (lds <= 64 * 1024) {
+        // the most subbands whose tile leaves room for 3 workgroups per CU: at ds 2 the
+        // 4-subband tile (56 KiB, 2 per CU) measured 5.19 ms per 12-pass launch against 4.30 at
+        // 2 subbands; at ds 1 and 3 (48 KiB, 3 per CU) 4 subbands stay faster (8.06 vs 8.26,
+        // 2.60 vs 3.45 ms; HD_Q8_SG_CAP=2, scripts/ab_bench.sh)
+        if (3 * lds <= 160 * 1024) {
             sg = cand;
             v = cv;
             break;
