@@ -931,7 +931,15 @@ static size_t fix8_lds_bytes(const Stage1Multi& a, const Fix8Geom& g)
 // LDS budget of one k_stage1_fix8 workgroup: smaller windows per workgroup mean more of
 // them in flight on a CU, which this latency-bound kernel wants; measured over the C2 beam's
 // stages (profiles/r02_fix8_lds.txt): 24 KiB best, except at ds >= 10 (wide windows) 40 KiB.
-static size_t fix8_lds_cap(int ds) { return (size_t)(ds >= 10 ? 40 : 24) * 1024; }
+static size_t fix8_lds_cap(int ds)
+{
+    // HD_FIX8_LDS_KB (profiling): the cap in KiB for every ds
+    if (getenv("HD_FIX8_LDS_KB")) return (size_t)atoi(getenv("HD_FIX8_LDS_KB")) * 1024;
+    // measured per stage of the C2 beam (scripts/ab_fix8_lds.sh, 16/24/32/48 KiB): ds 1 best at
+    // 16-24 (1.77 ms), ds 2-3 at 32 (1.33 / 0.84), ds 5-10 at 48 (2.00 / 1.18 / 1.42): wider
+    // windows need room for more channels per workgroup
+    return (size_t)(ds <= 1 ? 24 : ds <= 3 ? 32 : 48) * 1024;
+}
 
 // Geometry for k_stage1_fix8, or false when it does not apply (the generic kernel then runs).
 static bool fix8_geom(const Stage1Multi& a, Fix8Geom& g)
