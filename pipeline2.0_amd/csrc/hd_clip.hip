@@ -272,88 +272,95 @@ __global__ __launch_bounds__(256) void k_clip_chan_u4(ClipArgs a)
 // One thread per channel, spread over single-wave workgroups on as many CUs: the recurrence
 // is serial over blocks and issue-bound in double precision, so one 1024-thread workgroup on
 // one CU ran it 16 waves deep on 4 SIMDs.  Every thread carries the (channel-independent)
-// running avg / std itself; thread 0 of workgroup 0 publishes them.
+// running avg / std itself; thread 0 of workgroup 0 publishes them.  The per-block scalars
+// are staged in LDS per segment and only the channel sums are global loads (16 blocks
+// ahead): 0.85 ms per C2 beam against 2.25 with every input a global load 8 blocks ahead.
+constexpr int kRecurSeg = 1024;               // blocks of per-block scalars staged in LDS at a time
+
 __global__ __launch_bounds__(64) void k_clip_recur(ClipArgs a)
 {
+    // the per-block scalars (numgood, block avg / std, all-zapped) of kRecurSeg blocks at a
+    // time in LDS: the chain then reads them at LDS latency; the per-channel sums are the only
+    // global loads, U blocks ahead in registers
+    __shared__ double s_bav[kRecurSeg], s_bsd[kRecurSeg];
+    __shared__ int s_ng[kRecurSeg];
+    __shared__ uint8_t s_az[kRecurSeg];
     const int nch = a.rd.nchan;
+    const int nblk = a.rd.nblk;
     const float clip_sigma = a.clip_sigma;
     const int nloop = nch > 0 ? nch : 1;
-    constexpr int U = 8;                                // chansum loads in flight per thread
+    constexpr int U = 16;                               // chansum loads in flight per thread
+    static_assert(kRecurSeg % U == 0, "segment of whole prefetch groups");
     for (int c0 = blockIdx.x * blockDim.x; c0 < nloop; c0 += gridDim.x * blockDim.x) {
         const int c = c0 + threadIdx.x;
         const bool own = c < nch;
         float ravg = 0.0f, rstd = 0.0f, cra = 0.0f;
         float lev = own && a.padvals0 ? a.padvals0[c] : 0.0f;
         int nread = 0;
-        // the per-block inputs do not depend on the recurrence: group g + 1's loads are in
-        // flight while group g is folded (software pipelining; the chain itself is short)
-        double ncsv[U], nbav[U], nbsd[U];
-        int nngv[U];
-        bool nazv[U];
-        auto fetch = [&](int b8) {
+        double ncsv[U];
+        auto fetch = [&](int b0) {
 #pragma unroll
             for (int u = 0; u < U; u++) {
-                const int b = min(b8 + u, a.rd.nblk - 1);
+                const int b = min(b0 + u, nblk - 1);
                 ncsv[u] = own ? a.chansum[(int64_t)b * nch + c] : 0.0;
-                nngv[u] = a.numgood[b];
-                nbav[u] = a.bavg[b];
-                nbsd[u] = a.bstd[b];
-                nazv[u] = a.allzap && a.allzap[b];
             }
         };
         fetch(0);
-        for (int b8 = 0; b8 < a.rd.nblk; b8 += U) {
-          double csv[U], bav[U], bsd[U];
-          int ngv[U];
-          bool azv[U];
-#pragma unroll
-          for (int u = 0; u < U; u++) {
-              csv[u] = ncsv[u];
-              bav[u] = nbav[u];
-              bsd[u] = nbsd[u];
-              ngv[u] = nngv[u];
-              azv[u] = nazv[u];
-          }
-          if (b8 + U < a.rd.nblk) fetch(b8 + U);
-#pragma unroll
-          for (int u = 0; u < U; u++) {
-            const int b = b8 + u;
-            if (b >= a.rd.nblk) break;
-            const bool run = clip_sigma > 0.0f && !azv[u];
-            if (run) {
-                const int ng = ngv[u];
-                double cur_avg, cur_std, cat;
-                if (ng < 1) {
-                    cur_avg = (double)ravg;
-                    cur_std = (double)rstd;
-                    cat = (double)cra;
-                } else {
-                    cur_avg = bav[u];
-                    cur_std = bsd[u];
-                    cat = csv[u] / (double)ng;
-                }
-                if (nread) {
-                    const float r29 = ravg * (float)(kBlocksToAvg - 1);
-                    const float s29 = rstd * (float)(kBlocksToAvg - 1);
-                    const float c29 = cra * (float)(kBlocksToAvg - 1);
-                    ravg = (float)(((double)r29 + cur_avg) / (double)kBlocksToAvg);
-                    rstd = (float)(((double)s29 + cur_std) / (double)kBlocksToAvg);
-                    cra = (float)(((double)c29 + cat) / (double)kBlocksToAvg);
-                } else {
-                    ravg = (float)cur_avg;
-                    rstd = (float)cur_std;
-                    cra = (float)cat;
-                }
-                lev = cra;
-                nread++;
+        for (int s0 = 0; s0 < nblk; s0 += kRecurSeg) {
+            const int ns = min(kRecurSeg, nblk - s0);
+            __syncthreads();                              // the previous segment is consumed
+            for (int i = threadIdx.x; i < ns; i += blockDim.x) {
+                s_bav[i] = a.bavg[s0 + i];
+                s_bsd[i] = a.bstd[s0 + i];
+                s_ng[i] = a.numgood[s0 + i];
+                s_az[i] = a.allzap ? a.allzap[s0 + i] : 0;
             }
-            if (c0 == 0 && threadIdx.x == 0) {              // workgroup 0, thread 0
-                a.doclip[b] = run;
-                a.ravg[b] = ravg;
-                a.trig[b] = clip_sigma * rstd;
+            __syncthreads();
+            for (int g0 = 0; g0 < ns; g0 += U) {
+                double csv[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) csv[u] = ncsv[u];
+                if (s0 + g0 + U < nblk) fetch(s0 + g0 + U);
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const int bl = g0 + u, b = s0 + bl;
+                    if (bl >= ns) continue;                      // (the segment's last group)
+                    const bool run = clip_sigma > 0.0f && !s_az[bl];
+                    if (run) {
+                        const int ng = s_ng[bl];
+                        double cur_avg, cur_std, cat;
+                        if (ng < 1) {
+                            cur_avg = (double)ravg;
+                            cur_std = (double)rstd;
+                            cat = (double)cra;
+                        } else {
+                            cur_avg = s_bav[bl];
+                            cur_std = s_bsd[bl];
+                            cat = csv[u] / (double)ng;
+                        }
+                        if (nread) {
+                            const float r29 = ravg * (float)(kBlocksToAvg - 1);
+                            const float s29 = rstd * (float)(kBlocksToAvg - 1);
+                            const float c29 = cra * (float)(kBlocksToAvg - 1);
+                            ravg = (float)(((double)r29 + cur_avg) / (double)kBlocksToAvg);
+                            rstd = (float)(((double)s29 + cur_std) / (double)kBlocksToAvg);
+                            cra = (float)(((double)c29 + cat) / (double)kBlocksToAvg);
+                        } else {
+                            ravg = (float)cur_avg;
+                            rstd = (float)cur_std;
+                            cra = (float)cat;
+                        }
+                        lev = cra;
+                        nread++;
+                    }
+                    if (c0 == 0 && threadIdx.x == 0) {          // workgroup 0, thread 0
+                        a.doclip[b] = run;
+                        a.ravg[b] = ravg;
+                        a.trig[b] = clip_sigma * rstd;
+                    }
+                    if (own) a.pad[(int64_t)b * nch + c] = lev;
+                }
             }
-            if (own) a.pad[(int64_t)b * nch + c] = lev;
-          }
         }
     }
 }
@@ -458,6 +465,14 @@ hipError_t launch_clip_stats(const ClipArgs& a, hipStream_t st, hipEvent_t after
         hipLaunchKernelGGL(k_clip_zdm_u4, dim3((unsigned)((rd.N + 3) / 4)), dim3(256), 0, st, rd, a.zdm);
     else
         hipLaunchKernelGGL(k_clip_zdm, dim3((unsigned)((rd.N + 255) / 256)), dim3(256), 0, st, rd, a.zdm);
+    // the channel-major copy forks after the channel sums (beside the recurrence); forking it
+    // here instead (HD_FORK_EARLY=1), beside the block medians, AS-52 and channel sums too,
+    // measured 79.9 vs 78.8 ms per C2 beam: it competes with the channel sums' raw scan
+    const bool late = !(getenv("HD_FORK_EARLY") && atoi(getenv("HD_FORK_EARLY")) != 0);
+    if (after_stats && !late) {
+        const hipError_t e = hipEventRecord(after_stats, st);
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(k_clip_block, dim3((unsigned)rd.nblk), dim3(1024), 0, st, a);
     hipLaunchKernelGGL(k_clip_as52, dim3((unsigned)((rd.nblk + 63) / 64)), dim3(64), 0, st, a);
     if (rd.nbits == 8 && !calib && rd.rowbytes % 4 == 0)
@@ -466,7 +481,7 @@ hipError_t launch_clip_stats(const ClipArgs& a, hipStream_t st, hipEvent_t after
         hipLaunchKernelGGL(k_clip_chan_u4, dim3((unsigned)rd.nblk), dim3(256), 0, st, a);
     else
         hipLaunchKernelGGL(k_clip_chan, dim3((unsigned)(rd.nblk * ((rd.nchan + 255) / 256))), dim3(256), 0, st, a);
-    if (after_stats) {          // the full-chip raw scans are done; the serial recurrence follows
+    if (after_stats && late) {  // the full-chip raw scans are done; the serial recurrence follows
         const hipError_t e = hipEventRecord(after_stats, st);
         if (e != hipSuccess) return e;
     }
