@@ -40,6 +40,9 @@ def parse():
                     help="stage-2 HIP streams (hd_set_streams): 2 overlaps consecutive passes (no launch tails), 3 runs "
                          "stage 2 on its own stream so the next DDplan stage's stage 1 overlaps it; per-kernel event "
                          "times then include the shared time, so the roofline is taken at 1")
+    ap.add_argument("--dd-single", action="store_true",
+                    help="stage 2 as one launch per pass (hd_run_dedisp) instead of one launch per DDplan stage "
+                         "(hd_run_dedisp_multi)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU work for the baseline sample")
     # the legs after the timed steps characterise one GPU: by default (-1) they run at world
     # size 1 only (8 ranks each writing a beam's 47 GB of .dat files, or two 4 GB PSRFITS
@@ -120,9 +123,21 @@ def run_step(eng, stages):
         if not plans:
             continue
         eng.run_subband_multi(plans)
+        run_dedisp_stage(eng, plans)
+    eng.sync()
+
+
+DD_MULTI = True
+
+
+def run_dedisp_stage(eng, plans):
+    """Stage 2 of one DDplan stage's passes: one pair-kernel launch for all of them
+    (hd_run_dedisp_multi), or one per pass with --dd-single."""
+    if DD_MULTI:
+        eng.run_dedisp_multi(plans)
+    else:
         for p in plans:
             p.run_dedisp(to_host=False)
-    eng.sync()
 
 
 def single_pulse_leg(eng, stages, beams):
@@ -269,8 +284,8 @@ def end_to_end(eng, stages, obs, outdir):
         if not plans:
             continue
         eng.run_subband_multi(plans)
+        run_dedisp_stage(eng, plans)
         for p in plans:
-            p.run_dedisp(to_host=False)
             info.dt, info.freq, info.chan_wid, info.num_chan = p.sub_dt, p.sub_lofreq, p.sub_chanwid, p.pp.nsub
             info.freqband = p.pp.nsub * p.sub_chanwid
             write_dats_device(p, base, p.dmstrs, info, p.nds, wait=False)
@@ -426,6 +441,8 @@ def cpu_baseline(obs, synth, ddplans, target_s, mask, pts, pad, omp):
 
 def main():
     args = parse()
+    global DD_MULTI
+    DD_MULTI = not args.dd_single
     world, rank, local, dist, torch = dist_setup(args)
     for leg, n1 in (("e2e_beams", 1), ("sp_beams", 1), ("fft_beams", 1), ("rfi_beams", 1), ("stream_beams", 3)):
         if getattr(args, leg) < 0:
@@ -508,7 +525,7 @@ def main():
         ms2 += b
         k = per_kernel.setdefault(p.kernel(), {"ms": 0.0, "launches": 0, "units": 0})
         k["ms"] += b
-        k["launches"] += 1
+        k["launches"] += 1 if p.launch_passes() > 0 else 0      # passes sharing a launch count once
         k["units"] += p.pp.numdms * (ts.out_range(rank, p.pp.ds)[1] if slices else p.nds)
     raw_bytes = (ts.slice(rank)[1] if slices else obs.N) * obs.rowbytes
     adds2 = sum(p.pp.numdms * p.nds * p.pp.nsub for p in plans)
@@ -563,6 +580,7 @@ def main():
                                "GBps_alg": v["units"] * b_unit / (v["ms"] * 1e-3) / 1e9 if v["ms"] > 0 else None}
                            for k, v in sorted(per_kernel.items(), key=lambda kv: -kv[1]["ms"])},
         "stage2_streams": args.streams,
+        "stage2_launch": "one per pass" if args.dd_single else "one per DDplan stage (hd_run_dedisp_multi)",
         "step_compulsory_hbm_frac": (raw_bytes + 4.0 * out_per_step) / step_s / (HBM_PEAK_GBS * 1e9),
         "stage2_valu_frac": adds2 / (ms2 * 1e-3) / VALU_ADD_PEAK if ms2 > 0 else None,
     }

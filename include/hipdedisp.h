@@ -298,6 +298,17 @@ HD_API int hd_set_subbands(hd_plan* plan, const void* host);
 /* Stage 2: subbands -> numdms series of numout f32 samples.  host_out [numdms][numout]
  * receives them when non-NULL; otherwise they stay resident on the device.          */
 HD_API int hd_run_dedisp(hd_plan* plan, float* host_out);
+/* Stage 2 of several passes (the reference's per-pass prepsubband calls of one DDplan stage,
+ * PALFA2_presto_search.py:512-529), series left on the device: passes that take the pair
+ * kernel with the same geometry (one DDplan stage) share ONE launch of up to 28 passes, so the
+ * tail of one pass's persistent workgroups overlaps the next pass instead of idling the GPU;
+ * any other plan runs as hd_run_dedisp(plan, NULL).  Results are identical to per-plan runs.
+ * Device time of a shared launch is attributed to its first plan (hd_plan_last_ms of the
+ * others reports 0; hd_plan_launch_passes tells which plan led how many passes).        */
+HD_API int hd_run_dedisp_multi(hd_plan* const* plans, int32_t n);
+/* Passes carried by the last stage-2 launch this plan led: 1 for hd_run_dedisp, n for the
+ * first plan of a shared launch, 0 for a plan whose stage 2 ran inside another's.         */
+HD_API int hd_plan_launch_passes(const hd_plan* plan, int32_t* npass);
 /* Samples [t0, t0+count) of DMs [dm0, dm0+ndm) of the device-resident series of the last
  * hd_run_dedisp, host layout [ndm][count] (t0+count <= numout).                        */
 HD_API int hd_get_series(hd_plan* plan, int32_t dm0, int32_t ndm, int64_t t0, int64_t count, float* host);

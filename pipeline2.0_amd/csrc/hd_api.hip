@@ -201,6 +201,8 @@ struct hd_plan {
     hd_ctx* ctx = nullptr;
     hd_pass pass{};
     char s2name[64] = {0};          // stage-2 kernel of the last hd_run_dedisp (hd_plan_kernel)
+    int32_t s2passes = 1;           // passes the last stage-2 launch this plan led carried (0: it
+                                    // ran inside another plan's launch, hd_run_dedisp_multi)
     int64_t nds = 0, numout = 0, nvalid = 0;
     int64_t sub_stride = 0, out_stride = 0;
     double sub_lofreq = 0, sub_chanwid = 0, sub_dt = 0;
@@ -3005,10 +3007,186 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
     }
     p->ran_dd = true;
     p->dd_stream = st;
+    p->s2passes = 1;
     if (host_out) {
         HIPCHK(c, d2h_2d(host_out, sizeof(float) * p->numout, p->d_out, sizeof(float) * p->out_stride,
                          sizeof(float) * p->numout, p->pass.numdms, st));
     }
+    return HD_OK;
+}
+
+// ---- stage 2 of several passes in one launch ---------------------------------------------
+// A plan joins a multi-pass launch when it takes the two-pairs-per-chunk pair kernel (auto or
+// variant 7) on the topocentric grid; plans with the same kernel and geometry (one DDplan
+// stage) share a launch of at most kS2MaxPass passes, the rest run one by one.
+static bool dedisp_multi_ok(const hd_plan* p)
+{
+    const bool pair_bound = p->sub_bound >= 0 && 2 * p->sub_bound <= 32767;
+    return p->sub_valid && (p->variant == 0 || p->variant == 7) && p->wide[4].ok && pair_bound && p->nbseg == 0 &&
+           p->pair_persist != 2;
+}
+
+static bool dedisp_same_group(const hd_plan* a, const hd_plan* b)
+{
+    const hd_plan::Wide &x = a->wide[4], &y = b->wide[4];
+    return a->ctx == b->ctx && x.q == y.q && x.r == y.r && x.dpb == y.dpb && a->pass.numdms == b->pass.numdms &&
+           a->pass.nsub == b->pass.nsub && a->nds == b->nds && a->nvalid == b->nvalid && a->numout == b->numout &&
+           a->out_stride == b->out_stride && a->sub_nonneg == b->sub_nonneg && a->probe == b->probe;
+}
+
+static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
+{
+    hd_plan* p0 = g[0];
+    const hd_plan::Wide& w0 = p0->wide[4];
+    // hd_set_streams(2 or 3): the shared launch runs on stream2, so the main stream goes on
+    // to the next DDplan stage's stage 1 (other plans' subbands) beside it
+    const bool alt = c->dual;
+    hipStream_t st = alt ? c->stream2 : c->stream;
+    if (alt) {
+        HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
+        HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
+    } else {
+        HIPCHK(c, join_stream2(c));
+    }
+    for (int i = 0; i < n; i++) {
+        hd_plan* p = g[i];
+        if (!p->d_out) {
+            const size_t bytes = sizeof(float) * (size_t)p->pass.numdms * p->out_stride;
+            if (hipMalloc(&p->d_out, bytes) != hipSuccess) {
+                p->d_out = nullptr;
+                return fail(c, HD_E_NOMEM, "cannot allocate %zu bytes of DM series", bytes);
+            }
+        }
+        if (p->ran_dd && p->dd_stream != st) HIPCHK(c, hipStreamWaitEvent(st, p->ev[3], 0));
+        if (p->copy_pending) {
+            HIPCHK(c, hipStreamWaitEvent(st, p->ev_copy, 0));
+            p->copy_pending = false;
+        }
+    }
+    const bool pad = p0->numout > p0->nds;
+    const int tile = 256 * w0.r;
+    const int ntiles = (int)((p0->nvalid + tile - 1) / tile);
+    const size_t per = (size_t)p0->pass.numdms * std::max(ntiles, 1);
+    double* partial = nullptr;
+    if (pad && c->opts.pad_mode != HD_PAD_ZERO) {
+        const size_t need = sizeof(double) * per * n;
+        double*& buf = alt ? c->d_partial2 : c->d_partial;
+        size_t& have = alt ? c->partial_bytes2 : c->partial_bytes;
+        if (have < need) {
+            HIPCHK(c, hipStreamSynchronize(st));
+            dfree(buf);
+            buf = nullptr;
+            have = 0;
+            HIPCHK(c, hipMalloc(&buf, need));
+            have = need;
+        }
+        partial = buf;
+    }
+    hd::Stage2Args a{};
+    a.sub = p0->d_sub;
+    a.sub_dtype = c->opts.sub_dtype;
+    a.nsub = p0->pass.nsub;
+    a.numdms = p0->pass.numdms;
+    a.nds = p0->nds;
+    a.sub_stride = p0->sub_stride;
+    a.nvalid = p0->nvalid;
+    a.out = p0->d_out;
+    a.out_stride = p0->out_stride;
+    a.partial = partial;
+    a.ntiles = ntiles;
+    a.tile = tile;
+    a.maxabs = p0->d_maxabs;
+    a.off = w0.d_boff;
+    a.omin = w0.d_omin;
+    a.wstride = w0.ws;
+    a.dms_per_blk = w0.dpb;
+    a.sc = w0.sc;
+    a.probe = p0->probe;
+    a.ring_npw = w0.npw;
+    a.ring_nbp = w0.nbp;
+    a.ptab = w0.d_omin;
+    a.umax = w0.umax;
+    a.nonneg = p0->sub_nonneg ? 1 : 0;
+    a.nwg = c->ncu;
+    hd::S2Multi m{};
+    m.npass = n;
+    for (int i = 0; i < n; i++) {
+        const hd_plan* p = g[i];
+        const hd_plan::Wide& w = p->wide[4];
+        hd::S2Pass& q = m.p[i];
+        q.sub = p->d_sub;
+        q.ptab = w.d_omin;
+        q.off = w.d_boff;
+        q.maxabs = p->d_maxabs;
+        q.out = p->d_out;
+        q.partial = partial ? partial + per * i : nullptr;
+        q.sub_stride = p->sub_stride;
+        q.ws = w.ws;
+        q.npw = w.npw;
+        q.nbp = w.nbp;
+        q.umax = w.umax;
+    }
+    HIPCHK(c, hipEventRecord(p0->ev[2], st));
+    HIPCHK(c, hd::launch_stage2_pair_multi(a, m, w0.q, w0.r, 2, st));
+    if (pad)
+        for (int i = 0; i < n; i++)
+            HIPCHK(c, hd::launch_pad(g[i]->d_out, g[i]->out_stride, g[i]->pass.numdms, g[i]->nds, g[i]->numout,
+                                     m.p[i].partial, ntiles, c->opts.pad_mode, st));
+    for (int i = 0; i < n; i++) {
+        hd_plan* p = g[i];
+        if (i > 0) HIPCHK(c, hipEventRecord(p->ev[2], st));
+        HIPCHK(c, hipEventRecord(p->ev[3], st));
+        p->ran_dd = true;
+        p->dd_stream = st;
+        p->s2passes = i == 0 ? n : 0;
+        snprintf(p->s2name, sizeof(p->s2name), "k_stage2_pair<%d, %d, 2, %s>", w0.q, w0.r,
+                 a.nonneg && !(a.probe & 64) ? "true" : "false");
+    }
+    if (alt) {
+        HIPCHK(c, hipEventRecord(c->ev_join, st));
+        c->s2_pending = true;
+    }
+    return HD_OK;
+}
+
+extern "C" int hd_run_dedisp_multi(hd_plan* const* plans, int32_t n)
+{
+    if (!plans || n <= 0) return fail(nullptr, HD_E_INVAL, "hd_run_dedisp_multi: need n >= 1 plans");
+    for (int32_t i = 0; i < n; i++)
+        if (!plans[i]) return fail(nullptr, HD_E_INVAL, "hd_run_dedisp_multi: plan %d is NULL", (int)i);
+    hd_ctx* c = plans[0]->ctx;
+    for (int32_t i = 1; i < n; i++)
+        if (plans[i]->ctx != c) return fail(c, HD_E_INVAL, "hd_run_dedisp_multi: plans of different contexts");
+    for (int32_t i = 0; i < n; i++)
+        for (int32_t j = 0; j < i; j++)
+            if (plans[i] == plans[j]) return fail(c, HD_E_INVAL, "hd_run_dedisp_multi: plan %d repeated", (int)i);
+    HIPCHK(c, hipSetDevice(c->device));
+    std::vector<bool> done((size_t)n, false);
+    for (int32_t i = 0; i < n; i++) {
+        if (done[i]) continue;
+        if (!dedisp_multi_ok(plans[i]) || getenv("HD_DD_SINGLE")) {
+            const int rc = hd_run_dedisp(plans[i], nullptr);
+            if (rc) return rc;
+            done[i] = true;
+            continue;
+        }
+        std::vector<hd_plan*> g;
+        for (int32_t j = i; j < n && (int)g.size() < hd::kS2MaxPass; j++)
+            if (!done[j] && dedisp_multi_ok(plans[j]) && dedisp_same_group(plans[i], plans[j])) {
+                g.push_back(plans[j]);
+                done[j] = true;
+            }
+        const int rc = run_dedisp_group(c, g.data(), (int)g.size());
+        if (rc) return rc;
+    }
+    return HD_OK;
+}
+
+extern "C" int hd_plan_launch_passes(const hd_plan* p, int32_t* npass)
+{
+    if (!p || !npass) return fail(p ? p->ctx : nullptr, HD_E_INVAL, "hd_plan_launch_passes: NULL argument");
+    if (!p->ran_dd) return fail(p->ctx, HD_E_STATE, "hd_plan_launch_passes: run hd_run_dedisp first");
+    *npass = p->s2passes;
     return HD_OK;
 }
 
@@ -3064,7 +3242,7 @@ extern "C" int hd_plan_last_ms(const hd_plan* p, float* ms_sub, float* ms_dd)
         *ms_dd = 0.0f;
         if (p->ran_dd) {
             HIPCHK(c, hipEventSynchronize(p->ev[3]));
-            HIPCHK(c, hipEventElapsedTime(ms_dd, p->ev[2], p->ev[3]));
+            if (p->s2passes > 0) HIPCHK(c, hipEventElapsedTime(ms_dd, p->ev[2], p->ev[3]));
         }
     }
     return HD_OK;

@@ -126,7 +126,27 @@ hipError_t launch_stage2_ring(const Stage2Args& a, int q, int r, hipStream_t st)
 constexpr int kPairUMax = 6, kPairTab = 16;   // pair variant: patterns per pair, table ints per pair
 size_t stage2_pair_lds_bytes(int wstride, int npw, int nbp, int nsub, int umax, int ppc);
 bool stage2_pair_supports(int q, int r);
+// Per-pass buffers and table geometry of one pass in a pair launch.  One launch may carry up
+// to kS2MaxPass passes that share everything else in Stage2Args (nsub, numdms, nvalid, ntiles,
+// out_stride, dms_per_blk, nonneg, probe): every pass of a DDplan stage.
+struct S2Pass {
+    const void* sub;
+    const int32_t* ptab;
+    const int32_t* off;
+    const int32_t* maxabs;
+    float* out;
+    double* partial;
+    int64_t sub_stride;
+    int32_t ws, npw, nbp, umax;
+};
+constexpr int kS2MaxPass = 28;
+struct S2Multi {
+    int32_t npass, nyblk;     // nyblk: set by the launcher
+    S2Pass p[kS2MaxPass];
+};
+S2Pass stage2_pass_of(const Stage2Args& a);
 hipError_t launch_stage2_pair(const Stage2Args& a, int q, int r, int ppc, hipStream_t st);
+hipError_t launch_stage2_pair_multi(const Stage2Args& a, const S2Multi& m, int q, int r, int ppc, hipStream_t st);
 hipError_t launch_stage2_wide2(const Stage2Args& a, int q, int r, int nw, hipStream_t st);
 hipError_t launch_stage2_direct(const Stage2Args& a, hipStream_t st);
 hipError_t launch_stage2_lds(const Stage2Args& a, int q, hipStream_t st);

@@ -909,9 +909,14 @@ __device__ __forceinline__ void load12_shift(const uint32_t* w32, int x, uint32_
 }
 
 template <int Q, int R, int PPC, bool NN>
-__global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, const int32_t* __restrict__ boff)
+__global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, S2Multi m)
 {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+    // the pass of this workgroup: blockIdx.y = pass * nyblk + y-block (one launch may carry
+    // every pass of a DDplan stage; their per-pass buffers and table geometry come from m)
+    const int pi = (int)blockIdx.y / m.nyblk;
+    const S2Pass& P = m.p[pi];
+    const int32_t* __restrict__ boff = P.off;
     // PPC subband pairs per chunk: two halve the chunks (barriers, DMA/offset bookkeeping) per
     // tile; their staging ring has one slot less (4) so the doubled expanded buffers fit
     constexpr int NS = PPC == 2 ? 4 : kRingNS, T = 256 * R;
@@ -927,16 +932,16 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, const int32_
         tb = (int)((int64_t)blockIdx.x * nt / gridDim.x);
         ntl = (int)((int64_t)(blockIdx.x + 1) * nt / gridDim.x) - tb;
     }
-    const int yb = blockIdx.y;
+    const int yb = (int)blockIdx.y - pi * m.nyblk;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nthr = blockDim.x;
     const int dpb = a.dms_per_blk;
     const int dblk0 = yb * dpb;
-    const int ws = a.wstride;
-    const int npw = a.ring_npw;                       // 1 KiB DMA pieces per window
-    const int nbp = a.ring_nbp;                       // pieces of a chunk's offset block
-    const int umax = a.umax;
+    const int ws = P.ws;
+    const int npw = P.npw;                       // 1 KiB DMA pieces per window
+    const int nbp = P.nbp;                       // pieces of a chunk's offset block
+    const int umax = P.umax;
     const int slot_bytes = (2 * PPC * npw + nbp) * 1024;
     const int npair = a.nsub >> 1;
     const int tab_bytes = npair * kPairTab * 4;
@@ -944,14 +949,14 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, const int32_
     const uint32_t ring0 = (uint32_t)tab_bytes;
     const uint32_t exp0 = ring0 + (uint32_t)(NS * slot_bytes);
     const uint32_t lane_byte = exp0 + (uint32_t)lane * 8u;   // host offsets are relative to exp0
-    const int16_t* sub = (const int16_t*)a.sub;
+    const int16_t* sub = (const int16_t*)P.sub;
     const int32_t* bo_g = boff + (int64_t)yb * npair * dpb;
     const int nchunk = npair / PPC;
 
-    for (int i = threadIdx.x; i < npair * kPairTab; i += nthr) ltab[i] = a.ptab[(int64_t)yb * npair * kPairTab + i];
+    for (int i = threadIdx.x; i < npair * kPairTab; i += nthr) ltab[i] = P.ptab[(int64_t)yb * npair * kPairTab + i];
     __syncthreads();
 
-    int maxabs = *a.maxabs;
+    int maxabs = *P.maxabs;
     maxabs = maxabs < 1 ? 1 : maxabs;
     // pairs per packed-16-bit group: signed halves hold |sum| <= 32767; with subbands known
     // non-negative (host) the halves are unsigned and hold sums <= 65535 (twice the group)
@@ -1014,7 +1019,7 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, const int32_
             const int s = 2 * pr + (sl & 1);
             const int b = __builtin_amdgcn_readfirstlane(ltab[pr * kPairTab + (sl & 1)]);   // base0 | b1
             const int64_t e0 = t0 + b - (b & 1);
-            const char* src = (const char*)(sub + (int64_t)s * a.sub_stride + e0) + pc * 1024;
+            const char* src = (const char*)(sub + (int64_t)s * P.sub_stride + e0) + pc * 1024;
             dma16s(src, (uint32_t)lane * 16u, slot + (uint32_t)((sl * npw + pc) * 1024));
         } else {
             const int bp = wave - 2 * PPC * npw;
@@ -1074,7 +1079,7 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, const int32_
             for (int r = 0; r < R; r++) {
                 const int64_t tl = t0 + 256 * r + 4 * lane;
                 if (dv && !(a.probe & 4)) {
-                    float* o = a.out + (int64_t)d * a.out_stride + tl;
+                    float* o = P.out + (int64_t)d * a.out_stride + tl;
                     if (tl + 3 < a.nvalid) {
                         *(float4*)o = make_float4((float)acc32[q][r][0], (float)acc32[q][r][1], (float)acc32[q][r][2],
                                                   (float)acc32[q][r][3]);
@@ -1089,10 +1094,10 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, const int32_
                     }
                 }
             }
-            if (dv && a.partial) {
+            if (dv && P.partial) {
     #pragma unroll
                 for (int m = 32; m >= 1; m >>= 1) part += __shfl_xor(part, m, 64);
-                if (lane == 0) a.partial[(int64_t)d * a.ntiles + tile] = (double)part;
+                if (lane == 0) P.partial[(int64_t)d * a.ntiles + tile] = (double)part;
             }
         }
         gcount = 0;
@@ -1174,7 +1179,7 @@ size_t stage2_pair_lds_bytes(int wstride, int npw, int nbp, int nsub, int umax, 
 }
 
 template <int Q, int R, int PPC, bool NN>
-static hipError_t launch_pair_qrpn(const Stage2Args& a, int nyblk, hipStream_t st)
+static hipError_t launch_pair_qrpn(const Stage2Args& a, const S2Multi& m, int nyblk, hipStream_t st)
 {
     {
         const hipError_t e = set_max_lds((const void*)k_stage2_pair<Q, R, PPC, NN>, 160 * 1024);
@@ -1184,18 +1189,23 @@ static hipError_t launch_pair_qrpn(const Stage2Args& a, int nyblk, hipStream_t s
     const unsigned nx = a.nwg > 0 && (unsigned)a.nwg < ntiles ? (unsigned)a.nwg : ntiles;
     Stage2Args b = a;
     if (nx == ntiles) b.nwg = 0;
-    hipLaunchKernelGGL((k_stage2_pair<Q, R, PPC, NN>), dim3(nx, (unsigned)nyblk), dim3(1024),
-                       stage2_pair_lds_bytes(a.wstride, a.ring_npw, a.ring_nbp, a.nsub, a.umax, PPC), st, b, a.off);
+    size_t lds = 0;
+    for (int i = 0; i < m.npass; i++)
+        lds = std::max(lds, stage2_pair_lds_bytes(m.p[i].ws, m.p[i].npw, m.p[i].nbp, a.nsub, m.p[i].umax, PPC));
+    S2Multi mm = m;
+    mm.nyblk = nyblk;
+    hipLaunchKernelGGL((k_stage2_pair<Q, R, PPC, NN>), dim3(nx, (unsigned)(nyblk * m.npass)), dim3(1024), lds, st, b,
+                       mm);
     return hipGetLastError();
 }
 
 // non-negative subbands (host-known): unsigned packed halves, twice the group (probe 64 keeps
 // the signed kernel for A/B)
 template <int Q, int R, int PPC>
-static hipError_t launch_pair_qrp(const Stage2Args& a, int nyblk, hipStream_t st)
+static hipError_t launch_pair_qrp(const Stage2Args& a, const S2Multi& m, int nyblk, hipStream_t st)
 {
-    if (a.nonneg && !(a.probe & 64)) return launch_pair_qrpn<Q, R, PPC, true>(a, nyblk, st);
-    return launch_pair_qrpn<Q, R, PPC, false>(a, nyblk, st);
+    if (a.nonneg && !(a.probe & 64)) return launch_pair_qrpn<Q, R, PPC, true>(a, m, nyblk, st);
+    return launch_pair_qrpn<Q, R, PPC, false>(a, m, nyblk, st);
 }
 
 // Two workgroups per CU: 8 waves x Q DMs (<= 40) per workgroup, one LDS window buffer, no
@@ -1429,14 +1439,40 @@ hipError_t launch_stage2_ring(const Stage2Args& a, int q, int r, hipStream_t st)
     return hipErrorInvalidValue;
 }
 
+S2Pass stage2_pass_of(const Stage2Args& a)
+{
+    S2Pass p{};
+    p.sub = a.sub;
+    p.ptab = a.ptab;
+    p.off = a.off;
+    p.maxabs = a.maxabs;
+    p.out = a.out;
+    p.partial = a.partial;
+    p.sub_stride = a.sub_stride;
+    p.ws = a.wstride;
+    p.npw = a.ring_npw;
+    p.nbp = a.ring_nbp;
+    p.umax = a.umax;
+    return p;
+}
+
 hipError_t launch_stage2_pair(const Stage2Args& a, int q, int r, int ppc, hipStream_t st)
 {
-    if (a.nvalid <= 0) return hipSuccess;
+    S2Multi m{};
+    m.npass = 1;
+    m.p[0] = stage2_pass_of(a);
+    return launch_stage2_pair_multi(a, m, q, r, ppc, st);
+}
+
+hipError_t launch_stage2_pair_multi(const Stage2Args& a, const S2Multi& m, int q, int r, int ppc, hipStream_t st)
+{
+    if (a.nvalid <= 0 || m.npass <= 0) return hipSuccess;
     if (ppc != 1 && ppc != 2) return hipErrorInvalidValue;
+    if (m.npass > kS2MaxPass) return hipErrorInvalidValue;
     const int nyblk = (a.numdms + a.dms_per_blk - 1) / a.dms_per_blk;
 #define HD_PL(QQ, RR)                                                                             \
     if (q == QQ && r == RR)                                                                       \
-        return ppc == 2 ? launch_pair_qrp<QQ, RR, 2>(a, nyblk, st) : launch_pair_qrp<QQ, RR, 1>(a, nyblk, st);
+        return ppc == 2 ? launch_pair_qrp<QQ, RR, 2>(a, m, nyblk, st) : launch_pair_qrp<QQ, RR, 1>(a, m, nyblk, st);
     HD_RING_QR(HD_PL)
 #undef HD_PL
     return hipErrorInvalidValue;

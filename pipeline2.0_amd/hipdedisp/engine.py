@@ -354,6 +354,12 @@ class Engine:
         self._chk(self._L.hd_run_subband_multi(arr, len(plans)),
                   "prepsubband -sub (x%d passes)" % len(plans))
 
+    def run_dedisp_multi(self, plans):
+        """Stage 2 of several passes, series left on the device (hd_run_dedisp_multi): the
+        passes of one DDplan stage share one pair-kernel launch."""
+        arr = (ctypes.c_void_p * len(plans))(*[p._p.value for p in plans])
+        self._chk(self._L.hd_run_dedisp_multi(arr, len(plans)), "prepsubband (x%d passes)" % len(plans))
+
 
 class Plan:
     """One DDplan pass on a context (hd_plan)."""
@@ -473,6 +479,13 @@ class Plan:
         buf = ctypes.create_string_buffer(64)
         self.eng._chk(self.eng._L.hd_plan_kernel(self._p, buf, 64), "hd_plan_kernel")
         return buf.value.decode()
+
+    def launch_passes(self):
+        """Passes the last stage-2 launch this plan led carried (hd_plan_launch_passes): 1
+        for run_dedisp, n for the first plan of a shared launch, 0 for the others."""
+        n = ctypes.c_int32()
+        self.eng._chk(self.eng._L.hd_plan_launch_passes(self._p, ctypes.byref(n)), "hd_plan_launch_passes")
+        return n.value
 
     def last_ms(self):
         a, b = ctypes.c_float(), ctypes.c_float()

@@ -68,8 +68,7 @@ def test_c2_stage_windows_bitexact(engine, c2, stage):
     plans = [engine.plan(pp) for pp in pps]
     try:
         engine.run_subband_multi(plans)
-        for p in plans:
-            p.run_dedisp(to_host=False)
+        engine.run_dedisp_multi(plans)                       # the bench's path: one launch per stage
         for pp, p in zip(pps, plans):
             idd, off = p.delays()
             nds = N // pp.ds

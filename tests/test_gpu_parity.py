@@ -540,6 +540,71 @@ def test_stage2_own_stream_overlap_matches(engine):
                 p.destroy()
 
 
+def test_stage2_multipass_launch_matches(engine):
+    """hd_run_dedisp_multi: the passes of a DDplan stage share one pair-kernel launch (per-pass
+    subbands, tables, outputs and padding sums from the launch's pass table).  Passes of three
+    stages given in mixed order over a ragged beam with more tiles than CUs, masked: every
+    series equals its own one-pass launch (which the oracle pins, checked here for one pass
+    per stage), over repeated beams of alternating raw contents and with stage 2 on two
+    streams before; the first plan of each shared launch reports its pass count, the others 0."""
+    obs = palfa_obs(N=(1 << 19) + 777, nbits=8)
+    engine.set_obs(obs, Opts())
+    synths = [palfa_synth(beam=0), palfa_synth(beam=1)]
+    pts = 2048
+    mask, pad = synth_mask(obs, synths[0], pts)
+    engine.set_mask(mask, pts, pad)
+    plans, pps = [], []
+    for st, idx in ((0, (0, 3, 7, 27)), (1, (1, 2, 11)), (3, (0, 8))):
+        d = plan.ddplans_for("pdev")[st]
+        for i in idx:
+            pp = PassParams(subdm=float(d.subdmlist[i]), lodm=float(d.lodm_arg(i)), dmstep=float(d.dmstep_arg()),
+                            numdms=d.dmsperpass, nsub=d.numsub, ds=d.sub_downsamp,
+                            numout=plan.choose_N(obs.N / d.downsamp))
+            pps.append(pp)
+            plans.append(engine.plan(pp))
+    order = [0, 4, 7, 1, 5, 2, 8, 3, 6]                      # stages interleaved
+    try:
+        want = []
+        for k in range(2):
+            engine.synth_device(synths[k])
+            engine.run_subband_multi(plans[0:4])
+            engine.run_subband_multi(plans[4:7])
+            engine.run_subband_multi(plans[7:9])
+            want.append([p.run_dedisp() for p in plans])
+            if k == 0:
+                raw = host_spectra(obs, synths[0])
+                for j in (0, 4, 7):
+                    _, w = OR.run_pass(obs, Opts(), raw, pps[j], mask=mask, ptsperint=pts, padvals=pad, omp=True)
+                    assert_series(want[0][j], w, obs.N // pps[j].ds)
+        for it in range(4):
+            k = it % 2
+            engine.synth_device(synths[k])
+            engine.run_subband_multi(plans[0:4])
+            engine.run_subband_multi(plans[4:7])
+            engine.run_subband_multi(plans[7:9])
+            if it == 2:
+                engine.set_streams(2)
+                for p in plans[:3]:
+                    p.run_dedisp(to_host=False)              # alternating streams, then the shared launch
+            engine.run_dedisp_multi([plans[i] for i in order])
+            engine.set_streams(1)
+            for j, p in enumerate(plans):
+                assert np.array_equal(p.get_series(0, None, 0, p.numout), want[k][j]), (it, j)
+            n = [p.launch_passes() for p in plans]
+            assert sum(n) == len(plans)
+            assert n[0] >= 1 and n[4] >= 1 and n[7] >= 1, n
+        engine.sync()
+        with pytest.raises(PrestoError):
+            engine.run_dedisp_multi([])
+        with pytest.raises(PrestoError):
+            engine.run_dedisp_multi([plans[0], plans[0]])
+    finally:
+        engine.set_streams(1)
+        engine.set_mask()
+        for p in plans:
+            p.destroy()
+
+
 def test_stage1_channel_major_fill(engine):
     """The 8-bit stage-1 kernel fills its LDS tile from a channel-major copy of the raw block
     (built once per raw block): results equal the row-major fill (probe bit 2) and the oracle,
