@@ -766,15 +766,26 @@ __device__ __forceinline__ float fix8_fold(const Stage1Multi& a, const uint8_t* 
             zb |= (uint32_t)zap[lc0 + cc] << cc;
             zb |= (uint32_t)zap[G + lc0 + cc] << (16 + cc);
         }
-#pragma unroll
-        for (int k = 0; k < ds; k++) {
-            float sk = 0.0f;
+        // branch-free: every step's flag and raw byte are loaded unconditionally (the window
+        // holds every row an output reads) and the pad is a register select, so one step's
+        // LDS reads issue together instead of two dependent round trips per channel
+#pragma unroll 1
+        for (int k = 0; k < ds; k++) {                      // (unrolled, ds 5-10 took 200-280 VGPRs)
+            uint32_t fb[CPS], rb[CPS];
+            float pv[CPS];
 #pragma unroll
             for (int cc = 0; cc < CPS; cc++) {
                 const int lr = d[cc] + k;
-                const int part = lr >= bndrel;
-                const bool rep = flg[lr] | ((zb >> (16 * part + cc)) & 1u);
-                const float x = rep ? pad[part * G + lc0 + cc] : (float)lraw[(lc0 + cc) * Wp + lr];
+                fb[cc] = flg[lr];
+                rb[cc] = lraw[(lc0 + cc) * Wp + lr];
+                pv[cc] = pad[(lr >= bndrel ? G : 0) + lc0 + cc];
+            }
+            float sk = 0.0f;
+#pragma unroll
+            for (int cc = 0; cc < CPS; cc++) {
+                const int part = d[cc] + k >= bndrel ? 16 : 0;
+                const bool rep = (fb[cc] | ((zb >> (part + cc)) & 1u)) != 0;
+                const float x = rep ? pv[cc] : (float)rb[cc];
                 sk += x;
             }
             acc += sk;
@@ -815,6 +826,16 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
     int* cnt_s = lo_s + npass * SG;
     __shared__ int amax_s[kMaxPass];
     __shared__ int needany;
+    // per-pass output rows staged once: indexing the kernel argument arrays with a per-lane
+    // pass made every task wait for two global loads of the argument block before its store
+    __shared__ char* outp_s[kMaxPass];
+    __shared__ int64_t ostr_s[kMaxPass];
+    if (threadIdx.x < npass) {
+        outp_s[threadIdx.x] = (char*)a.out[threadIdx.x];
+        ostr_s[threadIdx.x] = a.ostride[threadIdx.x];
+    }
+    const int fprobe = boundaries >> 8;                   // HD_FIX8_PROBE (profiling): 1 no folds, 2 no window
+    boundaries &= 1;
     const int nev = *nevents;
     const int nbound = boundaries ? a.rd.nblk - 1 : 0;
     const int nitems = nev + nbound;
@@ -869,7 +890,7 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
             if (!needany) continue;                       // uniform
         }
         // the window: raw bytes of the chunk's channels (16-byte runs), replaced-row flags
-        {
+        if (!(fprobe & 2)) {
             const int nq = Wp >> 4;
             for (int i = threadIdx.x; i < G * nq; i += blockDim.x) {
                 const int lc = i / nq, q = i - lc * nq;
@@ -884,7 +905,8 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
             }
         }
         __syncthreads();
-        if (clip_ev) {
+        if (fprobe & 1) {
+        } else if (clip_ev) {
             // task (p, lc): the output channel lc maps r to, unless an earlier channel of its
             // subband maps r to the same output
             for (int i = threadIdx.x; i < npass * G; i += blockDim.x) {
@@ -906,11 +928,11 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
                 const int s = (c0 + lc0) / cps;
                 if (a.sub_dtype == 0) {
                     const int16_t q = to_i16(acc, a.sub_round);
-                    ((int16_t*)a.out[p])[(int64_t)s * a.ostride[p] + j] = q;
+                    if (!(fprobe & 4)) ((int16_t*)outp_s[p])[(int64_t)s * ostr_s[p] + j] = q;
                     const int aq = q < 0 ? -(int)q : (int)q;
-                    if (aq > 0) atomicMax(&amax_s[p], aq);
+                    if (aq > 0 && !(fprobe & 8)) atomicMax(&amax_s[p], aq);
                 } else {
-                    ((float*)a.out[p])[(int64_t)s * a.ostride[p] + j] = acc;
+                    ((float*)outp_s[p])[(int64_t)s * ostr_s[p] + j] = acc;
                 }
             }
         } else {
@@ -924,11 +946,11 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
                 const int s = chunk * SG + sl;
                 if (a.sub_dtype == 0) {
                     const int16_t q = to_i16(acc, a.sub_round);
-                    ((int16_t*)a.out[p])[(int64_t)s * a.ostride[p] + j] = q;
+                    if (!(fprobe & 4)) ((int16_t*)outp_s[p])[(int64_t)s * ostr_s[p] + j] = q;
                     const int aq = q < 0 ? -(int)q : (int)q;
-                    if (aq > 0) atomicMax(&amax_s[p], aq);
+                    if (aq > 0 && !(fprobe & 8)) atomicMax(&amax_s[p], aq);
                 } else {
-                    ((float*)a.out[p])[(int64_t)s * a.ostride[p] + j] = acc;
+                    ((float*)outp_s[p])[(int64_t)s * ostr_s[p] + j] = acc;
                 }
             }
         }
@@ -1002,6 +1024,7 @@ hipError_t launch_stage1_fixup(const Stage1Multi& a, const int32_t* events, cons
             const hipError_t e = set_max_lds(fn, (int)lb);
             if (e != hipSuccess) return e;
         }
+        if (getenv("HD_FIX8_PROBE")) boundaries |= atoi(getenv("HD_FIX8_PROBE")) << 8;
         void* args[] = {(void*)&a, (void*)&g, (void*)&events, (void*)&nevents, (void*)&boundaries};
         return hipLaunchKernel(fn, dim3(grid), dim3(256), args, lb, st);
     }
