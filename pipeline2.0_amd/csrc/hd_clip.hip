@@ -746,63 +746,63 @@ struct Fix8Geom {
     int nchunk, jmax;         // chunks per item; boundary outputs per (pass, subband) at most
 };
 
-// The oracle's fold of one output (k outer, channel inner, from 0.0f) over the LDS window.
-// CPS / DS > 0 are compile-time (the channel loop unrolls; each channel's delay and its two
-// blocks' zap flags are read once, not once per k); 0 = runtime values.
+// The oracle's fold of one output (k outer, channel inner, from 0.0f) over the LDS window,
+// for compile-time CPS / DS (the channel loop unrolls): the subband's raw delays dr[] and zap
+// bits zb come in registers (the callers load them with the task's other LDS reads), and
+// every step's flag, raw byte and pad read issue together, so a task waits for two LDS round
+// trips -- delays, then window bytes -- instead of two per channel (branches around the loads).
+template <int CPS, int DS>
+__device__ __forceinline__ float fix8_fold_pre(const Stage1Multi& a, const uint8_t* lraw, const uint8_t* flg,
+                                               const float* pad, int Wp, int G, int lc0, const int (&dr)[CPS],
+                                               uint32_t zb, int trel, int bndrel)
+{
+    const int ds = DS ? DS : a.ds;
+    float acc = 0.0f;
+#pragma unroll 1
+    for (int k = 0; k < ds; k++) {
+        uint32_t fb[CPS], rb[CPS];
+        float pv[CPS];
+#pragma unroll
+        for (int cc = 0; cc < CPS; cc++) {
+            const int lr = trel + dr[cc] + k;
+            fb[cc] = flg[lr];
+            rb[cc] = lraw[(lc0 + cc) * Wp + lr];
+            pv[cc] = pad[(lr >= bndrel ? G : 0) + lc0 + cc];
+        }
+        float sk = 0.0f;
+#pragma unroll
+        for (int cc = 0; cc < CPS; cc++) {
+            const int part = trel + dr[cc] + k >= bndrel ? 16 : 0;
+            const bool rep = (fb[cc] | ((zb >> (part + cc)) & 1u)) != 0;
+            const float x = rep ? pv[cc] : (float)rb[cc];
+            sk += x;
+        }
+        acc += sk;
+    }
+    if (a.ds_mode == 1) acc = acc / (float)ds;
+    return acc;
+}
+
 template <int CPS, int DS>
 __device__ __forceinline__ float fix8_fold(const Stage1Multi& a, const uint8_t* lraw, const uint8_t* flg,
                                            const uint8_t* zap, const float* pad, const int16_t* dl, int Wp, int G,
                                            int lc0, int trel, int bndrel)
 {
-    // trel = j*ds - wlo: window row of (k = 0, delay 0); dl: this pass's delays of the chunk
+    // runtime cps / ds (the templated cases take fix8_fold_pre); trel = j*ds - wlo: window row
+    // of (k = 0, delay 0); dl: this pass's delays of the chunk
     const int ds = DS ? DS : a.ds, cps = CPS ? CPS : a.cps;
     float acc = 0.0f;
-    if constexpr (CPS > 0) {
-        int d[CPS];
-        uint32_t zb = 0;                                   // bit cc: zapped in block slot 0; 16 + cc: slot 1
-#pragma unroll
-        for (int cc = 0; cc < CPS; cc++) {
-            d[cc] = trel + dl[lc0 + cc];
-            zb |= (uint32_t)zap[lc0 + cc] << cc;
-            zb |= (uint32_t)zap[G + lc0 + cc] << (16 + cc);
+    for (int k = 0; k < ds; k++) {
+        float sk = 0.0f;
+        for (int cc = 0; cc < cps; cc++) {
+            const int lc = lc0 + cc;
+            const int lr = trel + k + dl[lc];
+            const int part = lr >= bndrel;
+            const bool rep = flg[lr] | zap[part * G + lc];
+            const float x = rep ? pad[part * G + lc] : (float)lraw[lc * Wp + lr];
+            sk += x;
         }
-        // branch-free: every step's flag and raw byte are loaded unconditionally (the window
-        // holds every row an output reads) and the pad is a register select, so one step's
-        // LDS reads issue together instead of two dependent round trips per channel
-#pragma unroll 1
-        for (int k = 0; k < ds; k++) {                      // (unrolled, ds 5-10 took 200-280 VGPRs)
-            uint32_t fb[CPS], rb[CPS];
-            float pv[CPS];
-#pragma unroll
-            for (int cc = 0; cc < CPS; cc++) {
-                const int lr = d[cc] + k;
-                fb[cc] = flg[lr];
-                rb[cc] = lraw[(lc0 + cc) * Wp + lr];
-                pv[cc] = pad[(lr >= bndrel ? G : 0) + lc0 + cc];
-            }
-            float sk = 0.0f;
-#pragma unroll
-            for (int cc = 0; cc < CPS; cc++) {
-                const int part = d[cc] + k >= bndrel ? 16 : 0;
-                const bool rep = (fb[cc] | ((zb >> (part + cc)) & 1u)) != 0;
-                const float x = rep ? pv[cc] : (float)rb[cc];
-                sk += x;
-            }
-            acc += sk;
-        }
-    } else {
-        for (int k = 0; k < ds; k++) {
-            float sk = 0.0f;
-            for (int cc = 0; cc < cps; cc++) {
-                const int lc = lc0 + cc;
-                const int lr = trel + k + dl[lc];
-                const int part = lr >= bndrel;
-                const bool rep = flg[lr] | zap[part * G + lc];
-                const float x = rep ? pad[part * G + lc] : (float)lraw[lc * Wp + lr];
-                sk += x;
-            }
-            acc += sk;
-        }
+        acc += sk;
     }
     if (a.ds_mode == 1) acc = acc / (float)ds;
     return acc;
@@ -826,6 +826,7 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
     int* cnt_s = lo_s + npass * SG;
     __shared__ int amax_s[kMaxPass];
     __shared__ int needany;
+    __shared__ uint32_t zbm_s[CPS > 0 ? 1024 / (CPS > 0 ? CPS : 1) : 1];   // per subband: zap bits of both blocks
     // per-pass output rows staged once: indexing the kernel argument arrays with a per-lane
     // pass made every task wait for two global loads of the argument block before its store
     __shared__ char* outp_s[kMaxPass];
@@ -904,6 +905,15 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
                 flg[i] = t >= N ? 1 : (a.rd.clipped ? a.rd.clipped[t] : 0);
             }
         }
+        if constexpr (CPS > 0) {
+            for (int i = threadIdx.x; i < SG; i += blockDim.x) {
+                uint32_t zb = 0;                          // bit cc: zapped in block slot 0; 16 + cc: slot 1
+#pragma unroll
+                for (int cc = 0; cc < CPS; cc++)
+                    zb |= ((uint32_t)zap[i * CPS + cc] << cc) | ((uint32_t)zap[G + i * CPS + cc] << (16 + cc));
+                zbm_s[i] = zb;
+            }
+        }
         __syncthreads();
         if (fprobe & 1) {
         } else if (clip_ev) {
@@ -912,19 +922,45 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
             for (int i = threadIdx.x; i < npass * G; i += blockDim.x) {
                 const int p = i / G, lc = i - p * G;
                 const int16_t* dl = dly + p * G;
-                const int jn = r - dl[lc];
-                if (jn < 0) continue;
-                const int j = jn / ds;
-                if (j >= nds) continue;
                 const int lc0 = lc - lc % cps;
-                // delays fall with frequency within a subband, so the outputs its channels map
-                // r to rise with the channel and equal ones are adjacent: only channel lc - 1
-                // can name j first
-                if (lc > lc0) {
-                    const int jn2 = r - dl[lc - 1];
-                    if (jn2 >= 0 && jn2 / ds == j) continue;
+                int j;
+                float acc;
+                if constexpr (CPS > 0) {
+                    // the subband's delays and zap bits with the task's own delay (one round)
+                    int dr[CPS];
+#pragma unroll
+                    for (int cc = 0; cc < CPS; cc++) dr[cc] = dl[lc0 + cc];
+                    const uint32_t zb = zbm_s[lc0 / CPS];
+                    const int ci = lc - lc0;
+                    int dlc = dr[0], dpv = dr[0];
+#pragma unroll
+                    for (int cc = 1; cc < CPS; cc++) {
+                        dlc = cc == ci ? dr[cc] : dlc;
+                        dpv = cc == ci - 1 ? dr[cc] : dpv;
+                    }
+                    const int jn = r - dlc;
+                    if (jn < 0) continue;
+                    j = jn / ds;
+                    if (j >= nds) continue;
+                    // delays fall with frequency within a subband, so the outputs its channels
+                    // map r to rise with the channel and equal ones are adjacent: only channel
+                    // lc - 1 can name j first
+                    if (ci > 0) {
+                        const int jn2 = r - dpv;
+                        if (jn2 >= 0 && jn2 / ds == j) continue;
+                    }
+                    acc = fix8_fold_pre<CPS, DS>(a, lraw, flg, pad, Wp, G, lc0, dr, zb, j * ds - wlo, bndrel);
+                } else {
+                    const int jn = r - dl[lc];
+                    if (jn < 0) continue;
+                    j = jn / ds;
+                    if (j >= nds) continue;
+                    if (lc > lc0) {
+                        const int jn2 = r - dl[lc - 1];
+                        if (jn2 >= 0 && jn2 / ds == j) continue;
+                    }
+                    acc = fix8_fold<CPS, DS>(a, lraw, flg, zap, pad, dl, Wp, G, lc0, j * ds - wlo, bndrel);
                 }
-                const float acc = fix8_fold<CPS, DS>(a, lraw, flg, zap, pad, dl, Wp, G, lc0, j * ds - wlo, bndrel);
                 const int s = (c0 + lc0) / cps;
                 if (a.sub_dtype == 0) {
                     const int16_t q = to_i16(acc, a.sub_round);
@@ -942,7 +978,15 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
                 const int p = ps / SG, sl = ps - p * SG;
                 const int j = lo_s[ps] + jj;
                 const int16_t* dl = dly + p * G;
-                const float acc = fix8_fold<CPS, DS>(a, lraw, flg, zap, pad, dl, Wp, G, sl * cps, j * ds - wlo, bndrel);
+                float acc;
+                if constexpr (CPS > 0) {
+                    int dr[CPS];
+#pragma unroll
+                    for (int cc = 0; cc < CPS; cc++) dr[cc] = dl[sl * CPS + cc];
+                    acc = fix8_fold_pre<CPS, DS>(a, lraw, flg, pad, Wp, G, sl * CPS, dr, zbm_s[sl], j * ds - wlo, bndrel);
+                } else {
+                    acc = fix8_fold<CPS, DS>(a, lraw, flg, zap, pad, dl, Wp, G, sl * cps, j * ds - wlo, bndrel);
+                }
                 const int s = chunk * SG + sl;
                 if (a.sub_dtype == 0) {
                     const int16_t q = to_i16(acc, a.sub_round);
