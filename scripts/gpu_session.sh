@@ -17,4 +17,8 @@ if [ "${PROF:-1}" = 1 ]; then
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --e2e-beams 0 --sp-beams 0 --fft-beams 0 --rfi-beams 0 --stream-beams 0 > gpurun_out/prof.log 2>&1 || { echo prof failed; exit 1; }
   python3 scripts/kstats.py "$(find gpurun_out/prof -name '*.db' | head -1)" gpurun_out/kstats.csv
 fi
+if [ "${PROF_SP:-1}" = 1 ]; then   # kernel times of the single-pulse leg (one beam)
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sp -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu --e2e-beams 0 --sp-beams 1 --fft-beams 0 --rfi-beams 0 --stream-beams 0 > gpurun_out/prof_sp.log 2>&1 || { echo prof_sp failed; exit 1; }
+  python3 scripts/kstats.py "$(find gpurun_out/prof_sp -name '*.db' | head -1)" gpurun_out/kstats_sp.csv
+fi
 echo "session done"
