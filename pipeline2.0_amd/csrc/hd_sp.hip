@@ -42,7 +42,8 @@ constexpr int kSpHalo = 224;                 // >= max downfact / 2 + 1 (a boxca
 constexpr int kSpSeg = 33;                   // prefix-sum segment per thread
 constexpr int kSpWin = 256 * kSpSeg;         // kSpChunk + 2 * kSpHalo = 8448
 constexpr int kSpWords = kSpChunk / 32;      // hit bitmask words per (chunk, width)
-constexpr int kSpRound = 8;                  // widths per round (bitmask LDS: 8 KB), walked by lanes 0-1 of each wave
+constexpr int kSpRound = 4;                  // widths per round: one wave walks each
+constexpr int kSpSegW = 4;                   // bitmask words (128 bins) per lane segment of a walk
 
 __device__ __forceinline__ double wave_sum_f64(double v)
 {
@@ -204,17 +205,6 @@ __global__ __launch_bounds__(1024) void k_sp_robust(double* __restrict__ coef, i
 // Normalised sample i: 0 outside [0, ls) and in bad blocks, else
 // y = (float)((double)d / std), d = (float)(x - (mean + slope * (t - 499.5))), t = i mod 1000
 // (std 0: y = 0).
-__device__ __forceinline__ float sp_norm(const float* xs, const double* cf, int64_t i, int64_t ls)
-{
-    if (i < 0 || i >= ls) return 0.0f;
-    const int64_t b = i / kSpBlock;
-    const double* c = cf + b * 4;
-    if (c[3] != 0.0 || c[2] == 0.0) return 0.0f;
-    const double t = (double)(i - b * kSpBlock) - 499.5;
-    const float d = (float)((double)xs[i] - (c[0] + c[1] * t));
-    return (float)((double)d / c[2]);
-}
-
 struct SpArgs {
     const float* x;
     int64_t stride;
@@ -248,8 +238,19 @@ __device__ __forceinline__ void sp_emit(const SpArgs& a, int dm, int64_t bin, in
 __global__ __launch_bounds__(256) void k_sp_hits(SpArgs a)
 {
     __shared__ double P[kSpWin + 1];
-    __shared__ double tot[257];
     __shared__ uint32_t bits[kSpRound][kSpWords];
+    // the walk's per-width state (its space also holds the segment totals of the prefix sum):
+    // spec[w]: pivots of the lanes' speculative walks; emt[w]: pivots whose next pivot is a gap
+    // (or none) -- the walk emits them when they are on the true path -- and the true path's
+    // pivots off the speculative walks; exit / merge / hit-count prefix per lane segment
+    struct WalkLds {
+        uint32_t spec[kSpRound][kSpWords];
+        uint32_t emt[kSpRound][kSpWords];
+        int16_t exitb[kSpRound][64], merge[kSpRound][64], hpre[kSpRound][65];
+    };
+    __shared__ __attribute__((aligned(16))) char wl_raw[sizeof(WalkLds) > 257 * 8 ? sizeof(WalkLds) : 257 * 8];
+    double* tot = (double*)wl_raw;
+    WalkLds& W = *(WalkLds*)wl_raw;
     const int dm = blockIdx.x / a.nchunks, ch = blockIdx.x - dm * a.nchunks;
     const float* xs = a.x + (int64_t)dm * a.stride;
     const double* cf = a.coef + (int64_t)dm * a.nblocks * 4;
@@ -259,19 +260,50 @@ __global__ __launch_bounds__(256) void k_sp_hits(SpArgs a)
     const int wv = tid >> 6, ln = tid & 63;
     double loc[kSpSeg];
     double run = 0.0;
+    // the normalised samples of the window in per-thread segments (detrended by the block's
+    // line, over its std; 0 in bad blocks and past the searched length); width 1
+    // is tested on the spot: every value above threshold outside the bad blocks is a hit (no
+    // prune_related1), so the chunk's samples are not read and normalised a second time
 #pragma unroll
     for (int j = 0; j < kSpSeg; j++) {
-        run += (double)sp_norm(xs, cf, w0 + tid * kSpSeg + j, a.ls);
+        const int e = tid * kSpSeg + j;
+        const int64_t i = w0 + e;
+        float v = 0.0f;
+        bool isbad = false;
+        if (i >= 0 && i < a.ls) {
+            const int64_t b = i / kSpBlock;
+            const double* c = cf + b * 4;
+            isbad = c[3] != 0.0;
+            if (!isbad && c[2] != 0.0) {
+                const double t = (double)(i - b * kSpBlock) - 499.5;
+                const float d = (float)((double)xs[i] - (c[0] + c[1] * t));
+                v = (float)((double)d / c[2]);
+            }
+        }
+        run += (double)v;
         loc[j] = run;
+        const int o = e - kSpHalo;
+        if (o >= 0 && o < kSpChunk && !isbad && !(a.probe & 2) && (double)v > a.threshold)
+            sp_emit(a, dm, c0 + o, 0, (double)v);
     }
     tot[tid] = run;
     __syncthreads();
     if (tid == 0) {                                           // exclusive scan of the segment totals
+        // (in order, as before; the totals are read 16 at a time so the chain waits only
+        // on its double adds, not on an LDS round trip per segment)
         double base = 0.0;
-        for (int t = 0; t < 256; t++) {
-            const double nb = base + tot[t];
-            tot[t] = base;
-            base = nb;
+        for (int t0 = 0; t0 < 256; t0 += 16) {
+            double v[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++) v[k] = tot[t0 + k];
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const double nb = base + v[k];
+                v[k] = base;
+                base = nb;
+            }
+#pragma unroll
+            for (int k = 0; k < 16; k++) tot[t0 + k] = v[k];
         }
         P[0] = 0.0;
     }
@@ -288,12 +320,6 @@ __global__ __launch_bounds__(256) void k_sp_hits(SpArgs a)
         return (P[hi] - P[lo]) * a.rsw[wi];
     };
     auto bad = [&](int o) { return cf[((c0 + o) / kSpBlock) * 4 + 3] != 0.0; };
-    // width 1: every value above threshold outside the bad blocks (no prune_related1)
-    for (int o = tid; o < kSpChunk && !(a.probe & 2); o += 256) {
-        if (bad(o)) continue;
-        const double s = (double)sp_norm(xs, cf, c0 + o, a.ls);
-        if (s > a.threshold) sp_emit(a, dm, c0 + o, 0, s);
-    }
     for (int r0 = 1; r0 < a.nwidths; r0 += kSpRound) {
         const int nr = min(kSpRound, a.nwidths - r0);
         // the above-threshold bins of widths r0 .. r0+nr-1 (bad blocks included: the script
@@ -309,59 +335,200 @@ __global__ __launch_bounds__(256) void k_sp_hits(SpArgs a)
             }
         }
         __syncthreads();
-        // prune_related1: width r0 + j walked by lane j >> 2 of wave j & 3
-        const int j = wv + 4 * ln;
-        if (ln < 2 && j < nr && !(a.probe & 1)) {
-            const int wi = r0 + j;
-            const int h = a.widths[wi] / 2;
-            const uint32_t* bm = bits[j];
-            int lpb = 0, zw = 0;
-            double lpx = 0.0;
-            bool have = false;
-            uint32_t zm = bm[0];
-            auto survivor = [&](int b, double x) {
-                while (zm == 0) zm = bm[++zw];                // the m-th unpruned hit (m <= current)
-                const int hb = 32 * zw + __builtin_ctz(zm);
-                zm &= zm - 1;
-                if (!bad(hb)) sp_emit(a, dm, c0 + b, wi, x);
-            };
-            // the hits in bin order, their boxcar values read kSpLook hits ahead of the walk
-            // (a dense run is thousands of hits: the walk must not wait for each value's LDS
-            // reads in turn)
-            int rw = 0;
-            uint32_t rm = bm[0];
-            auto next_bit = [&]() -> int {
-                while (!rm && rw < kSpWords - 1) rm = bm[++rw];
-                if (!rm) return -1;
-                const int b = 32 * rw + __builtin_ctz(rm);
-                rm &= rm - 1;
-                return b;
-            };
-            constexpr int kSpLook = 4;
-            int qb[kSpLook];
-            double qx[kSpLook];
-#pragma unroll
-            for (int k = 0; k < kSpLook; k++) {
-                qb[k] = next_bit();
-                qx[k] = qb[k] >= 0 ? boxcar(wi, qb[k]) : 0.0;
-            }
-            while (qb[0] >= 0) {
-                const int b = qb[0];
-                const double x = qx[0];
-#pragma unroll
-                for (int k = 0; k + 1 < kSpLook; k++) {
-                    qb[k] = qb[k + 1];
-                    qx[k] = qx[k + 1];
+        // prune_related1 of width r0 + wv, by wave wv.  The script's walk is a chain through a
+        // function of the pivot alone: next(p) = the first hit q > p with q - p > h or
+        // x_q >= x_p (hits between are dropped), and p is kept when that step is a gap (or p is
+        // the last pivot).  Each lane walks its 128-bin segment speculatively from the
+        // segment's first hit; one lane then follows the true chain, which coincides with a
+        // segment's speculative chain from the first pivot they share (merge), walking only the
+        // pivots before it; the kept pivots are emitted in order, paired with the hits of the
+        // unpruned list at the same index (the script's zip quirk) for the bad-block test.
+        const int jw = wv;
+        const bool walk = jw < nr && !(a.probe & 1);
+        const int wi = r0 + jw;
+        const int h = walk ? a.widths[wi] / 2 : 0;
+        const uint32_t* bm = bits[walk ? jw : 0];
+        uint64_t segmask = 0;                                 // lane segments holding hits (spec phase)
+        auto nexthit = [&](int b) -> int {                    // first hit bin > b, or -1
+            int w = (b + 1) >> 5;
+            if (w >= kSpWords) return -1;
+            const uint32_t m = bm[w] & (~0u << ((b + 1) & 31));
+            if (m) return 32 * w + __builtin_ctz(m);
+            const int sg = w / kSpSegW;
+            for (int ww = w + 1; ww < min(kSpSegW * (sg + 1), kSpWords); ww++)
+                if (bm[ww]) return 32 * ww + __builtin_ctz(bm[ww]);
+            const uint64_t rest = sg + 1 < 64 ? segmask >> (sg + 1) : 0ull;   // empty segments skipped
+            if (!rest) return -1;
+            for (int ww = kSpSegW * (sg + 1 + __builtin_ctzll(rest));; ww++)
+                if (bm[ww]) return 32 * ww + __builtin_ctz(bm[ww]);
+        };
+        auto nextword = [&](int w) -> int {                   // first word > w holding hits, or -1
+            const int sg = w / kSpSegW;
+            for (int ww = w + 1; ww < min(kSpSegW * (sg + 1), kSpWords); ww++)
+                if (bm[ww]) return ww;
+            const uint64_t rest = sg + 1 < 64 ? segmask >> (sg + 1) : 0ull;
+            if (!rest) return -1;
+            for (int ww = kSpSegW * (sg + 1 + __builtin_ctzll(rest));; ww++)
+                if (bm[ww]) return ww;
+        };
+        // next(p) and its value: the hits after p in batches of 8 from the word masks (their
+        // boxcar reads issue together; a dense run is thousands of hits)
+        auto nextpivot = [&](int p, double px, double& qx) -> int {
+            int w = (p + 1) >> 5;
+            if (w >= kSpWords) return -1;
+            uint32_t m = bm[w] & (~0u << ((p + 1) & 31));
+            while (true) {
+                if (!m) {
+                    w = nextword(w);
+                    if (w < 0) return -1;
+                    m = bm[w];
                 }
-                qb[kSpLook - 1] = next_bit();
-                qx[kSpLook - 1] = qb[kSpLook - 1] >= 0 ? boxcar(wi, qb[kSpLook - 1]) : 0.0;
-                if (have && b - lpb <= h && lpx > x) continue;         // removed by the last pivot
-                if (have && b - lpb > h) survivor(lpb, lpx);           // else the new pivot removes it
-                lpb = b;
-                lpx = x;
-                have = true;
+                int qq[8];
+                double xv[8];
+                int n = 0;
+#pragma unroll
+                for (int k = 0; k < 8; k++)
+                    if (m) {
+                        qq[k] = 32 * w + __builtin_ctz(m);
+                        m &= m - 1;
+                        n = k + 1;
+                    }
+#pragma unroll
+                for (int k = 0; k < 8; k++)
+                    if (k < n) xv[k] = boxcar(wi, qq[k]);
+#pragma unroll
+                for (int k = 0; k < 8; k++)
+                    if (k < n && (qq[k] - p > h || xv[k] >= px)) {
+                        qx = xv[k];
+                        return qq[k];
+                    }
             }
-            if (have) survivor(lpb, lpx);
+        };
+        const int sw0 = ln * kSpSegW;                             // this lane's words
+        if (walk) {
+            uint32_t sp[kSpSegW] = {0, 0, 0, 0}, em[kSpSegW] = {0, 0, 0, 0};
+            int ex = -1, nh = 0;
+            int p = -1;
+#pragma unroll
+            for (int k = 0; k < kSpSegW; k++) {
+                const uint32_t m = sw0 + k < kSpWords ? bm[sw0 + k] : 0u;
+                nh += __builtin_popcount(m);
+                if (p < 0 && m) p = 32 * (sw0 + k) + __builtin_ctz(m);
+            }
+            const int segend = 32 * (sw0 + kSpSegW);
+            segmask = __ballot(nh > 0);
+            if (p >= 0) {
+                double px = boxcar(wi, p);
+                while (true) {
+                    const int k = (p >> 5) - sw0;
+                    sp[k] |= 1u << (p & 31);
+                    double qx = 0.0;
+                    const int q = nextpivot(p, px, qx);
+                    if (q < 0 || q - p > h) em[k] |= 1u << (p & 31);
+                    if (q < 0) break;
+                    p = q;
+                    px = qx;
+                    if (p >= segend) {
+                        ex = p;
+                        break;
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < kSpSegW; k++)
+                if (sw0 + k < kSpWords) {
+                    W.spec[jw][sw0 + k] = sp[k];
+                    W.emt[jw][sw0 + k] = em[k];
+                }
+            W.exitb[jw][ln] = (int16_t)ex;
+            W.merge[jw][ln] = (int16_t)32767;
+            // exclusive prefix of the segments' hit counts (the zip quirk's rank lookup)
+            int inc = nh;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int t = __shfl_up(inc, o, 64);
+                if (ln >= o) inc += t;
+            }
+            W.hpre[jw][ln + 1] = (int16_t)inc;
+            if (ln == 0) W.hpre[jw][0] = 0;
+        }
+        __syncthreads();
+        // the true chain from the chunk's first hit (one lane)
+        if (walk && ln == 0 && !(a.probe & 8)) {                 // (probe 8: profiling only)
+            int p = nexthit(-1);
+            double px = p >= 0 ? boxcar(wi, p) : 0.0;
+            while (p >= 0) {
+                const int sg = p >> 7;
+                if ((W.spec[jw][p >> 5] >> (p & 31)) & 1u) {      // on the segment's chain from here
+                    W.merge[jw][sg] = (int16_t)p;
+                    p = W.exitb[jw][sg];
+                    if (p >= 0) px = boxcar(wi, p);
+                    continue;
+                }
+                double qx = 0.0;
+                const int q = nextpivot(p, px, qx);
+                if (q < 0 || q - p > h) W.emt[jw][p >> 5] |= 1u << (p & 31);   // not in spec: kept pivot
+                p = q;
+                px = qx;
+            }
+        }
+        __syncthreads();
+        // emit the kept pivots of this lane's segment in bin order, with their ordinals
+        if (walk) {
+            const int mg = W.merge[jw][ln];
+            uint32_t kv[kSpSegW];
+            int nk = 0;
+#pragma unroll
+            for (int k = 0; k < kSpSegW; k++) {
+                const int w = sw0 + k;
+                uint32_t v = 0;
+                if (w < kSpWords) {
+                    const uint32_t spw = W.spec[jw][w], emw = W.emt[jw][w];
+                    // spec pivots at or after the merge bin; plus true pivots off the spec chain
+                    const int lo = mg - 32 * w;
+                    const uint32_t ge = lo <= 0 ? ~0u : lo >= 32 ? 0u : (~0u << lo);
+                    v = (emw & spw & ge) | (emw & ~spw);
+                }
+                kv[k] = v;
+                nk += __builtin_popcount(v);
+            }
+            int inc = nk;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int t = __shfl_up(inc, o, 64);
+                if (ln >= o) inc += t;
+            }
+            int m = inc - nk;                                     // ordinal of this lane's first kept pivot
+            const int16_t* hp = W.hpre[jw];
+#pragma unroll
+            for (int k = 0; k < kSpSegW; k++) {
+                uint32_t v = kv[k];
+                while (v) {
+                    const int b = 32 * (sw0 + k) + __builtin_ctz(v);
+                    v &= v - 1;
+                    // the m-th hit of the unpruned list: its segment, then its bit
+                    int lo = 0, hi = 63;
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (hp[mid] <= m) lo = mid;
+                        else hi = mid - 1;
+                    }
+                    int r = m - hp[lo], hb = -1;
+                    for (int kk = 0; kk < kSpSegW && hb < 0; kk++) {
+                        const int w = lo * kSpSegW + kk;
+                        uint32_t mw = w < kSpWords ? bm[w] : 0u;
+                        const int c = __builtin_popcount(mw);
+                        if (r >= c) {
+                            r -= c;
+                            continue;
+                        }
+                        for (; r > 0; r--) mw &= mw - 1;
+                        hb = 32 * w + __builtin_ctz(mw);
+                    }
+                    if (!bad(hb)) sp_emit(a, dm, c0 + b, wi, boxcar(wi, b));
+                    m++;
+                }
+            }
         }
         __syncthreads();
     }
