@@ -2521,6 +2521,36 @@ extern "C" int hd_sp_widths(double dt, double maxwidth, int32_t* widths, int32_t
     return HD_OK;
 }
 
+// Wall time of hd_single_pulse's phases (device search + count, copies, host pruning),
+// summed over the process and printed at exit when HD_SP_TIMING is set (profiling only).
+struct SpTimer {
+    static double acc[3];
+    static int calls;
+    bool on;
+    std::chrono::steady_clock::time_point t;
+    SpTimer() : on(getenv("HD_SP_TIMING") != nullptr), t(std::chrono::steady_clock::now())
+    {
+        static bool reg = false;
+        if (on && !reg) {
+            reg = true;
+            atexit([] {
+                fprintf(stderr, "hd_single_pulse: %d calls, device+count %.1f ms, copies %.1f ms, prune %.1f ms\n",
+                        calls, acc[0], acc[1], acc[2]);
+            });
+        }
+        if (on) calls++;
+    }
+    void mark(int k)
+    {
+        if (!on) return;
+        const auto n = std::chrono::steady_clock::now();
+        acc[k] += std::chrono::duration<double, std::milli>(n - t).count();
+        t = n;
+    }
+};
+double SpTimer::acc[3] = {0, 0, 0};
+int SpTimer::calls = 0;
+
 extern "C" int hd_single_pulse(hd_plan* p, double dt, double maxwidth, double threshold, hd_sp_hit* hits,
                                int64_t cap, int64_t* nhits, uint8_t* bad_blocks, int64_t* nblocks_out)
 {
@@ -2539,6 +2569,7 @@ extern "C" int hd_single_pulse(hd_plan* p, double dt, double maxwidth, double th
         return fail(c, HD_E_INVAL, "hd_single_pulse: %lld blocks > %d", (long long)nblocks, hd::sp_max_blocks());
     const int64_t ls = nblocks * 1000 / 8000 * 8000;           // numchunks * chunklen
     HIPCHK(c, hipSetDevice(c->device));
+    SpTimer tm;                                                // HD_SP_TIMING=1 (profiling)
     hipStream_t st = p->dd_stream ? p->dd_stream : c->stream;
     const size_t cbytes = sizeof(double) * 4 * (size_t)std::max<int64_t>(1, (int64_t)ndm * nblocks);
     if (c->sp_coef_bytes < cbytes) {
@@ -2567,6 +2598,7 @@ extern "C" int hd_single_pulse(hd_plan* p, double dt, double maxwidth, double th
     }
     unsigned long long cnt = 0;
     HIPCHK(c, d2h(&cnt, c->d_sp_count, sizeof(cnt), st));
+    tm.mark(0);
     if ((int64_t)cnt > c->sp_hits_cap) {
         // the device list overflowed: grow it to the count and search again (once per size)
         HIPCHK(c, hipStreamSynchronize(st));
@@ -2617,6 +2649,7 @@ extern "C" int hd_single_pulse(hd_plan* p, double dt, double maxwidth, double th
     HIPCHK(c, hipMemcpyAsync(c->sp_pin, c->d_sp_hits, hbytes, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipStreamSynchronize(st));
     memcpy(hits, c->sp_pin, hbytes);
+    tm.mark(1);
     // per DM (in parallel): the script's dm_candlist order -- by bin, widths in increasing
     // order among equal bins (width-1 hits appended first, every downfactor's bisect.insort
     // after equals) -- then prune_related2 (its greedy walk, literally) and prune_border_cases
@@ -2683,6 +2716,7 @@ extern "C" int hd_single_pulse(hd_plan* p, double dt, double maxwidth, double th
         out += kept[(size_t)d];
     }
     *nhits = out;
+    tm.mark(2);
     return HD_OK;
 }
 
