@@ -195,3 +195,71 @@ def test_prune_related1_walks_agree():
         assert pivot_walk(bins, vals, w) == want, (trial, w)
     # the advisor's example: 10, 9, 8 at consecutive bins with downfact 2 keeps bins 0 and 2
     assert greedy_walk([0, 1, 2], [10.0, 9.0, 8.0], 2) == [0, 2] == pivot_walk([0, 1, 2], [10.0, 9.0, 8.0], 2)
+
+
+def segment_walk(bins, vals, downfact, seg=128):
+    """The parallel form of k_sp_hits's walk (csrc/hd_sp.hip): next(p) = the first hit q > p
+    with q - p > h or x_q >= x_p; p is kept when that step is a gap or p is last.  Each
+    segment of `seg` bins walks its own chain from its first hit (spec pivots, keep flags,
+    exit = first pivot past the segment); the true chain from the first hit jumps to a
+    segment's exit as soon as it reaches one of that segment's spec pivots (merge) and walks
+    only the pivots before.  Kept = spec pivots at or after the merge with the keep flag,
+    plus the kept pivots the true chain walked itself."""
+    h = downfact // 2
+    n = len(bins)
+    pos = {b: k for k, b in enumerate(bins)}
+
+    def nxt(k):
+        for j in range(k + 1, n):
+            if bins[j] - bins[k] > h or vals[j] >= vals[k]:
+                return j
+        return -1
+
+    nseg = (bins[-1] // seg + 1) if n else 0
+    spec, keepf, exitp = set(), set(), {}
+    for sg in range(nseg):
+        members = [k for k in range(n) if bins[k] // seg == sg]
+        if not members:
+            continue
+        k = members[0]
+        exitp[sg] = -1
+        while True:
+            spec.add(k)
+            q = nxt(k)
+            if q < 0 or bins[q] - bins[k] > h:
+                keepf.add(k)
+            if q < 0:
+                break
+            k = q
+            if bins[k] // seg != sg:
+                exitp[sg] = k
+                break
+    merge, extra = {}, set()
+    k = 0 if n else -1
+    while k >= 0:
+        sg = bins[k] // seg
+        if k in spec:
+            merge[sg] = bins[k]
+            k = exitp[sg]
+            continue
+        q = nxt(k)
+        if q < 0 or bins[q] - bins[k] > h:
+            extra.add(k)
+        k = q
+    kept = {k for k in spec & keepf if bins[k] >= merge.get(bins[k] // seg, 1 << 30)} | extra
+    assert all(bins[k] in pos for k in kept)
+    return [bins[k] for k in sorted(kept)]
+
+
+def test_prune_related1_segment_form_agrees():
+    """The segmented, merge-based walk of the device kernel keeps the same hits as the
+    script's greedy walk: random lists, monotone chains (where the true and speculative chains
+    run in step without meeting), humps, ties and pulse trains, at 128-bin segments and at
+    tiny segments (many merges), over every downfactor."""
+    rng = np.random.default_rng(11)
+    for trial in range(400):
+        w = int(rng.choice([2, 3, 4, 6, 9, 14, 20, 30, 45, 70, 100, 150, 220, 300]))
+        bins, vals = _hit_lists(rng)
+        want = greedy_walk(bins, vals, w)
+        for seg in (128, 8):
+            assert segment_walk(bins, vals, w, seg) == want, (trial, w, seg)
