@@ -319,7 +319,8 @@ __global__ __launch_bounds__(256) void k_sp_hits(SpArgs a)
         const int lo = k - w / 2, hi = k + ((w & 1) ? w / 2 : w / 2 - 1) + 1;
         return (P[hi] - P[lo]) * a.rsw[wi];
     };
-    auto bad = [&](int o) { return cf[((c0 + o) / kSpBlock) * 4 + 3] != 0.0; };
+    // the bad flags of the chunk's 8 blocks, one bit each (every wave, once)
+    const uint64_t badm = __ballot(ln < kSpChunk / kSpBlock && cf[(c0 / kSpBlock + ln) * 4 + 3] != 0.0);
     for (int r0 = 1; r0 < a.nwidths; r0 += kSpRound) {
         const int nr = min(kSpRound, a.nwidths - r0);
         // the above-threshold bins of widths r0 .. r0+nr-1 (bad blocks included: the script
@@ -498,37 +499,71 @@ __global__ __launch_bounds__(256) void k_sp_hits(SpArgs a)
                 const int t = __shfl_up(inc, o, 64);
                 if (ln >= o) inc += t;
             }
-            int m = inc - nk;                                     // ordinal of this lane's first kept pivot
             const int16_t* hp = W.hpre[jw];
-#pragma unroll
-            for (int k = 0; k < kSpSegW; k++) {
-                uint32_t v = kv[k];
-                while (v) {
-                    const int b = 32 * (sw0 + k) + __builtin_ctz(v);
-                    v &= v - 1;
-                    // the m-th hit of the unpruned list: its segment, then its bit
-                    int lo = 0, hi = 63;
-                    while (lo < hi) {
-                        const int mid = (lo + hi + 1) >> 1;
-                        if (hp[mid] <= m) lo = mid;
-                        else hi = mid - 1;
-                    }
-                    int r = m - hp[lo], hb = -1;
-                    for (int kk = 0; kk < kSpSegW && hb < 0; kk++) {
-                        const int w = lo * kSpSegW + kk;
-                        uint32_t mw = w < kSpWords ? bm[w] : 0u;
-                        const int c = __builtin_popcount(mw);
-                        if (r >= c) {
-                            r -= c;
-                            continue;
-                        }
-                        for (; r > 0; r--) mw &= mw - 1;
-                        hb = 32 * w + __builtin_ctz(mw);
-                    }
-                    if (!bad(hb)) sp_emit(a, dm, c0 + b, wi, boxcar(wi, b));
-                    m++;
+            // the m-th hit of the unpruned list (its segment by the prefix counts, then its bit)
+            auto hitrank = [&](int m) -> int {
+                int lo = 0, hi = 63;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (hp[mid] <= m) lo = mid;
+                    else hi = mid - 1;
                 }
+                int r = m - hp[lo];
+                for (int kk = 0; kk < kSpSegW; kk++) {
+                    const int w = lo * kSpSegW + kk;
+                    uint32_t mw = w < kSpWords ? bm[w] : 0u;
+                    const int c = __builtin_popcount(mw);
+                    if (r >= c) {
+                        r -= c;
+                        continue;
+                    }
+                    for (; r > 0; r--) mw &= mw - 1;
+                    return 32 * w + __builtin_ctz(mw);
+                }
+                return 0;
+            };
+            // kept pivots whose zip-quirk partner lies outside the bad blocks: counted, one
+            // atomic per wave reserves their slots, then written in bin order
+            const int m0 = inc - nk;                              // ordinal of this lane's first kept pivot
+            int ng = 0;
+            {
+                int m = m0;
+#pragma unroll
+                for (int k = 0; k < kSpSegW; k++)
+                    for (uint32_t v = kv[k]; v; v &= v - 1) {
+                        const int hb = hitrank(m++);
+                        ng += !((badm >> (hb / kSpBlock)) & 1ull);
+                    }
             }
+            int incg = ng;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int t = __shfl_up(incg, o, 64);
+                if (ln >= o) incg += t;
+            }
+            const int totg = __shfl(incg, 63, 64);
+            unsigned long long base = 0;
+            if (ln == 0 && totg > 0) base = atomicAdd(a.count, (unsigned long long)totg);
+            base = __shfl(base, 0, 64);
+            unsigned long long slot = base + (unsigned long long)(incg - ng);
+            int m = m0;
+#pragma unroll
+            for (int k = 0; k < kSpSegW; k++)
+                for (uint32_t v = kv[k]; v; v &= v - 1) {
+                    const int b = 32 * (sw0 + k) + __builtin_ctz(v);
+                    const int hb = hitrank(m++);
+                    if ((badm >> (hb / kSpBlock)) & 1ull) continue;
+                    if ((int64_t)slot < a.cap) {
+                        hd_sp_hit r;
+                        r.dm = dm;
+                        r.bin = (int32_t)(c0 + b);
+                        r.widx = wi;
+                        r.pad = 0;
+                        r.sigma = boxcar(wi, b);
+                        a.hits[slot] = r;
+                    }
+                    slot++;
+                }
         }
         __syncthreads();
     }

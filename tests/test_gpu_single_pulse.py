@@ -87,6 +87,22 @@ def test_single_pulse_downsampled_and_padded(engine, beam, tmp_path, ds, numout_
         p.destroy()
 
 
+@pytest.mark.parametrize("lodm,threshold", [(380.0, 5.0), (380.0, 3.0), (250.0, 3.0)])
+def test_single_pulse_dense_runs(engine, beam, tmp_path, lodm, threshold):
+    """ds-2 passes at DM 250-420, where the C2 beam's wide boxcars give dense, slowly varying
+    runs of hits: the walk's true chain and the lanes' speculative chains run in step there
+    without meeting for long stretches (csrc/hd_sp.hip), so most kept pivots come from the
+    serial part -- lists identical to the oracle's, thresholds 5 and 3."""
+    obs, s = beam
+    ds = 2
+    p, series = run(engine, obs, subdm=lodm + 10.0, lodm=lodm, dmstep=0.3, ds=ds)
+    try:
+        dm_strs = ["%.2f" % (lodm + 0.3 * k) for k in range(76)]
+        check_pass(p, series, dm_strs, tmp_path, threshold=threshold)
+    finally:
+        p.destroy()
+
+
 def test_single_pulse_many_hits_and_short_series(engine, beam, tmp_path):
     """A low threshold (many candidates, the 4.6-ms pulsar's train at DM 71) and a series
     shorter than one 8000-sample chunk (no candidates)."""
