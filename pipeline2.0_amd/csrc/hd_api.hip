@@ -2648,19 +2648,19 @@ extern "C" int hd_single_pulse(hd_plan* p, double dt, double maxwidth, double th
     if (!cnt) return HD_OK;
     HIPCHK(c, hipMemcpyAsync(c->sp_pin, c->d_sp_hits, hbytes, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipStreamSynchronize(st));
-    memcpy(hits, c->sp_pin, hbytes);
+    const hd_sp_hit* src = (const hd_sp_hit*)c->sp_pin;
     tm.mark(1);
     // per DM (in parallel): the script's dm_candlist order -- by bin, widths in increasing
     // order among equal bins (width-1 hits appended first, every downfactor's bisect.insort
     // after equals) -- then prune_related2 (its greedy walk, literally) and prune_border_cases
     // (padded series: data ends at nds - 1, padding runs to numout - 1 -- the .inf on/off pair)
+    // grouped by DM straight from the pinned block into the caller's buffer (one pass)
     std::vector<int64_t> dstart((size_t)ndm + 1, 0);
-    for (unsigned long long i = 0; i < cnt; i++) dstart[(size_t)hits[i].dm + 1]++;
+    for (unsigned long long i = 0; i < cnt; i++) dstart[(size_t)src[i].dm + 1]++;
     for (int d = 0; d < ndm; d++) dstart[d + 1] += dstart[d];
     {
-        std::vector<hd_sp_hit> tmp(hits, hits + cnt);
         std::vector<int64_t> pos(dstart.begin(), dstart.end() - 1);
-        for (const hd_sp_hit& h : tmp) hits[pos[(size_t)h.dm]++] = h;
+        for (unsigned long long i = 0; i < cnt; i++) hits[pos[(size_t)src[i].dm]++] = src[i];
     }
     const int reach = nw > 1 ? widths[nw - 1] / 2 : 0;
     const bool padded = p->numout > p->nds;
