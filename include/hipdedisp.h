@@ -406,6 +406,13 @@ HD_API int hd_sp_widths(double dt, double maxwidth, int32_t* widths, int32_t* n)
  * HD_E_NOMEM is returned (call again with room).  bad_blocks[numdms * nblocks] (may be
  * NULL): 1 = block not searched; *nblocks (may be NULL) = floor(numout / 1000).  A series
  * of fewer than 8000 samples gives no candidates.                                        */
+/* The host half of hd_single_pulse on caller-supplied hits (any order, n of them, DMs
+ * 0..ndm-1, widths[nw] of hd_sp_widths): grouped by DM, each DM's list in bin order (widths
+ * ascending among equal bins), prune_related2 and -- when numout > nds -- the border cases
+ * of single_pulse_search.py; the kept hits are compacted to the front, *nkept of them.
+ * Host only (no device).                                                                  */
+HD_API int hd_sp_prune(hd_sp_hit* hits, int64_t n, int32_t ndm, const int32_t* widths, int32_t nw, int64_t nds,
+                       int64_t numout, int64_t* nkept);
 HD_API int hd_single_pulse(hd_plan* plan, double dt, double maxwidth, double threshold, hd_sp_hit* hits,
                            int64_t cap, int64_t* nhits, uint8_t* bad_blocks, int64_t* nblocks);
 

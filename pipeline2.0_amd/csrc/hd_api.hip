@@ -2551,6 +2551,109 @@ struct SpTimer {
 double SpTimer::acc[3] = {0, 0, 0};
 int SpTimer::calls = 0;
 
+// prune_related2 (the script's greedy walk across widths) and, for padded series,
+// prune_border_cases, on one DM's hits sorted by (bin, width) in place; returns the kept count.
+// The walk's inner loop visits, for pivot i, every later hit within max(downfact)/2 bins; a
+// pair acts only when its gap is <= max(w_i/2, w_j/2, 1), and for a fixed i the pairs act
+// independently (each sets gone[j] or gone[i], and the loop reads only gone[j]), so the
+// relevant j are taken as the contiguous run within max(w_i/2, 1) plus, per wider width
+// class k, that class's hits within widths[k]/2 -- the same set, fewer visits.
+static int64_t sp_prune_dm(hd_sp_hit* h, int64_t n, const int32_t* widths, int nw, int64_t nds, int64_t numout)
+{
+    std::sort(h, h + n, [](const hd_sp_hit& x, const hd_sp_hit& y) {
+        return x.bin != y.bin ? x.bin < y.bin : x.widx < y.widx;
+    });
+    std::vector<char> gone((size_t)n, 0);
+    const int reach = nw > 1 ? widths[nw - 1] / 2 : 0;
+    std::vector<std::vector<int32_t>> cls((size_t)nw);
+    for (int64_t i = 0; i < n; i++) cls[(size_t)h[i].widx].push_back((int32_t)i);
+    auto act = [&](int64_t i, int64_t j) {
+        if (gone[j]) return;
+        if (h[i].sigma > h[j].sigma) gone[j] = 1;
+        else gone[i] = 1;
+    };
+    for (int64_t i = 0; i + 1 < n; i++) {
+        if (gone[i]) continue;
+        const int bi = h[i].bin;
+        const int own = std::max(widths[h[i].widx] / 2, 1);
+        const int run = std::min(own, reach);
+        int64_t j = i + 1;
+        for (; j < n && h[j].bin - bi <= run; j++) act(i, j);
+        for (int k = 0; k < nw; k++) {
+            const int lim = std::min(widths[k] / 2, reach);
+            if (lim <= run) continue;
+            const std::vector<int32_t>& L = cls[(size_t)k];
+            auto it = std::upper_bound(L.begin(), L.end(), bi + run,
+                                       [&](int v, int32_t idx) { return v < h[idx].bin; });
+            for (; it != L.end() && h[*it].bin - bi <= lim; ++it) act(i, *it);
+        }
+    }
+    if (numout > nds) {
+        const int64_t off = nds - 1, on = numout - 1;
+        for (int64_t i = n - 1; i >= 0; i--) {
+            if (gone[i]) continue;                        // the script walks the pruned list
+            const int64_t lo = h[i].bin - widths[h[i].widx] / 2, hi = h[i].bin + widths[h[i].widx] / 2;
+            if (hi < off) break;
+            if (hi > off && lo < on) gone[i] = 1;
+        }
+    }
+    int64_t k = 0;
+    for (int64_t i = 0; i < n; i++)
+        if (!gone[i]) h[k++] = h[i];
+    return k;
+}
+
+// Every DM's group [dstart[d], dstart[d+1]) pruned (DMs over up to 16 host threads), the
+// kept hits compacted to the front in DM order; returns their count.
+static int64_t sp_prune_groups(hd_sp_hit* hits, const std::vector<int64_t>& dstart, int ndm, const int32_t* widths,
+                               int nw, int64_t nds, int64_t numout)
+{
+    std::vector<int64_t> kept((size_t)ndm, 0);
+    auto one = [&](int d) {
+        kept[(size_t)d] = sp_prune_dm(hits + dstart[d], dstart[d + 1] - dstart[d], widths, nw, nds, numout);
+    };
+    const unsigned nth = std::max(1u, std::min({16u, std::thread::hardware_concurrency(), (unsigned)ndm}));
+    if (nth <= 1 || dstart[ndm] < 4096) {
+        for (int d = 0; d < ndm; d++) one(d);
+    } else {
+        std::vector<std::thread> th;
+        std::atomic<int> next{0};
+        for (unsigned t = 0; t < nth; t++)
+            th.emplace_back([&]() {
+                for (int d = next++; d < ndm; d = next++) one(d);
+            });
+        for (auto& t : th) t.join();
+    }
+    int64_t out = 0;
+    for (int d = 0; d < ndm; d++) {
+        if (out != dstart[d]) memmove(hits + out, hits + dstart[d], sizeof(hd_sp_hit) * (size_t)kept[(size_t)d]);
+        out += kept[(size_t)d];
+    }
+    return out;
+}
+
+extern "C" int hd_sp_prune(hd_sp_hit* hits, int64_t n, int32_t ndm, const int32_t* widths, int32_t nw, int64_t nds,
+                           int64_t numout, int64_t* nkept)
+{
+    if ((n > 0 && !hits) || !widths || !nkept || nw < 1 || nw > 16 || ndm < 1 || n < 0)
+        return fail(nullptr, HD_E_INVAL, "hd_sp_prune: bad argument");
+    std::vector<int64_t> dstart((size_t)ndm + 1, 0);
+    for (int64_t i = 0; i < n; i++) {
+        if (hits[i].dm < 0 || hits[i].dm >= ndm || hits[i].widx < 0 || hits[i].widx >= nw)
+            return fail(nullptr, HD_E_INVAL, "hd_sp_prune: hit %lld has dm %d / widx %d out of range", (long long)i,
+                        (int)hits[i].dm, (int)hits[i].widx);
+        dstart[(size_t)hits[i].dm + 1]++;
+    }
+    for (int d = 0; d < ndm; d++) dstart[d + 1] += dstart[d];
+    {
+        std::vector<hd_sp_hit> tmp(hits, hits + n);
+        std::vector<int64_t> pos(dstart.begin(), dstart.end() - 1);
+        for (const hd_sp_hit& h : tmp) hits[pos[(size_t)h.dm]++] = h;
+    }
+    *nkept = sp_prune_groups(hits, dstart, ndm, widths, nw, nds, numout);
+    return HD_OK;
+}
+
 extern "C" int hd_single_pulse(hd_plan* p, double dt, double maxwidth, double threshold, hd_sp_hit* hits,
                                int64_t cap, int64_t* nhits, uint8_t* bad_blocks, int64_t* nblocks_out)
 {
@@ -2662,59 +2765,7 @@ extern "C" int hd_single_pulse(hd_plan* p, double dt, double maxwidth, double th
         std::vector<int64_t> pos(dstart.begin(), dstart.end() - 1);
         for (unsigned long long i = 0; i < cnt; i++) hits[pos[(size_t)src[i].dm]++] = src[i];
     }
-    const int reach = nw > 1 ? widths[nw - 1] / 2 : 0;
-    const bool padded = p->numout > p->nds;
-    std::vector<int64_t> kept((size_t)ndm, 0);
-    auto prune_dm = [&](int d) {
-        hd_sp_hit* h = hits + dstart[d];
-        const int64_t n = dstart[d + 1] - dstart[d];
-        std::sort(h, h + n, [](const hd_sp_hit& x, const hd_sp_hit& y) {
-            return x.bin != y.bin ? x.bin < y.bin : x.widx < y.widx;
-        });
-        std::vector<char> gone((size_t)n, 0);
-        for (int64_t i = 0; i + 1 < n; i++) {
-            if (gone[i]) continue;
-            for (int64_t j = i + 1; j < n; j++) {
-                const int gap = std::abs(h[j].bin - h[i].bin);
-                if (gap > reach) break;
-                if (gone[j]) continue;
-                const int prox = std::max(std::max(widths[h[i].widx] / 2, widths[h[j].widx] / 2), 1);
-                if (gap <= prox) {
-                    if (h[i].sigma > h[j].sigma) gone[j] = 1;
-                    else gone[i] = 1;
-                }
-            }
-        }
-        if (padded) {
-            const int64_t off = p->nds - 1, on = p->numout - 1;
-            for (int64_t i = n - 1; i >= 0; i--) {
-                const int64_t lo = h[i].bin - widths[h[i].widx] / 2, hi = h[i].bin + widths[h[i].widx] / 2;
-                if (hi < off) break;
-                if (hi > off && lo < on) gone[i] = 1;
-            }
-        }
-        int64_t k = 0;
-        for (int64_t i = 0; i < n; i++)
-            if (!gone[i]) h[k++] = h[i];
-        kept[(size_t)d] = k;
-    };
-    const unsigned nth = std::max(1u, std::min({16u, std::thread::hardware_concurrency(), (unsigned)ndm}));
-    if (nth <= 1 || cnt < 4096) {
-        for (int d = 0; d < ndm; d++) prune_dm(d);
-    } else {
-        std::vector<std::thread> th;
-        std::atomic<int> next{0};
-        for (unsigned t = 0; t < nth; t++)
-            th.emplace_back([&]() {
-                for (int d = next++; d < ndm; d = next++) prune_dm(d);
-            });
-        for (auto& t : th) t.join();
-    }
-    int64_t out = 0;
-    for (int d = 0; d < ndm; d++) {
-        if (out != dstart[d]) memmove(hits + out, hits + dstart[d], sizeof(hd_sp_hit) * (size_t)kept[(size_t)d]);
-        out += kept[(size_t)d];
-    }
+    const int64_t out = sp_prune_groups(hits, dstart, ndm, widths, nw, p->nds, p->numout);
     *nhits = out;
     tm.mark(2);
     return HD_OK;

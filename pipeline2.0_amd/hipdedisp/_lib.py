@@ -42,7 +42,7 @@ EXPORTED = [
     "hd_sp_widths", "hd_single_pulse", "hd_rfifind_stats",
     "hd_push_raw_file_band", "hd_fill_raw",
     "hd_realfft", "hd_zap_ranges", "hd_zapbirds", "hd_rednoise_blocks", "hd_rednoise", "hd_get_fft",
-    "hd_bary_diffbins", "hd_plan_set_bary", "hd_run_dedisp_multi", "hd_plan_launch_passes",
+    "hd_bary_diffbins", "hd_plan_set_bary", "hd_run_dedisp_multi", "hd_plan_launch_passes", "hd_sp_prune",
     "hd_prefetch_raw_file", "hd_prefetch_raw_file_band", "hd_prefetch_fill", "hd_swap_raw",
 ]
 
@@ -145,6 +145,7 @@ def load():
         "hd_set_subbands": (ctypes.c_int, [vp, vp]),
         "hd_run_dedisp": (ctypes.c_int, [vp, f32p]),
         "hd_run_dedisp_multi": (ctypes.c_int, [P(vp), i32]),
+        "hd_sp_prune": (ctypes.c_int, [vp, i64, i32, P(i32), i32, i64, i64, P(i64)]),
         "hd_plan_launch_passes": (ctypes.c_int, [vp, P(i32)]),
         "hd_plan_last_ms": (ctypes.c_int, [vp, f32p, f32p]),
         "hd_plan_kernel": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int32]),

@@ -263,3 +263,48 @@ def test_prune_related1_segment_form_agrees():
         want = greedy_walk(bins, vals, w)
         for seg in (128, 8):
             assert segment_walk(bins, vals, w, seg) == want, (trial, w, seg)
+
+
+@pytest.mark.parametrize("padded", [False, True])
+def test_host_prune_matches_script(padded):
+    """hd_sp_prune (the host half of hd_single_pulse: grouping by DM, bin order, prune_related2
+    visiting only the pairs that can act, border cases) keeps exactly the script's candidates
+    (oracle._prune_related2 / _prune_border_cases) on dense and sparse multi-width hit sets
+    with ties and equal bins.  Host only: no device is touched."""
+    import ctypes
+    from hipdedisp import _lib
+    from hipdedisp.single_pulse import HIT
+    L = _lib.load()
+    widths = [1, 2, 3, 4, 6, 9, 14, 20, 30, 45, 70, 100, 150, 220, 300]
+    rng = np.random.default_rng(3 + padded)
+    for trial in range(40):
+        ndm = int(rng.integers(1, 5))
+        nds = 20000
+        numout = nds + 3000 if padded else nds
+        n = int(rng.integers(0, 4000))
+        h = np.zeros(n, HIT)
+        h["dm"] = rng.integers(0, ndm, n)
+        dense = rng.integers(0, 2)
+        h["bin"] = rng.integers(0, 600 if dense else nds, n) + (nds - 600 if padded and dense else 0)
+        h["widx"] = rng.integers(0, len(widths), n)
+        h["sigma"] = rng.normal(7.0, 1.0, n).round(int(rng.integers(0, 3)))   # ties
+        # the device emits each (dm, bin, width) once
+        _, first = np.unique(h[["dm", "bin", "widx"]], return_index=True)
+        h = h[np.sort(first)]
+        want = []
+        for d in range(ndm):
+            hd = h[h["dm"] == d]
+            hd = hd[np.lexsort((hd["widx"], hd["bin"]))]
+            cl = [OR.SpCand(float(d), float(r["sigma"]), float(r["bin"]), int(r["bin"]), widths[r["widx"]]) for r in hd]
+            cl = OR._prune_related2(cl, widths[1:])
+            if padded and cl:
+                cl = OR._prune_border_cases(cl, [(nds - 1, numout - 1)])
+            want += [(d, c.bin, c.downfact, c.sigma) for c in cl]
+        a = np.ascontiguousarray(h)
+        w = (ctypes.c_int32 * len(widths))(*widths)
+        nk = ctypes.c_int64()
+        rc = L.hd_sp_prune(a.ctypes.data_as(ctypes.c_void_p), len(a), ndm, w, len(widths), nds, numout,
+                           ctypes.byref(nk))
+        assert rc == 0
+        got = [(int(r["dm"]), int(r["bin"]), widths[r["widx"]], float(r["sigma"])) for r in a[:nk.value]]
+        assert got == want, trial
