@@ -2551,6 +2551,50 @@ struct SpTimer {
 double SpTimer::acc[3] = {0, 0, 0};
 int SpTimer::calls = 0;
 
+// Hits grouped by DM (src -> dst, any order within a DM): per-thread counts, offsets, then
+// per-thread scatters over up to 16 host threads; dstart[ndm + 1] receives the group starts.
+static void sp_group_by_dm(const hd_sp_hit* src, int64_t n, int ndm, hd_sp_hit* dst, std::vector<int64_t>& dstart)
+{
+    const int nth = n < 65536 ? 1 : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<int64_t> cnt((size_t)nth * ndm, 0);
+    auto range = [&](int t, int64_t& a, int64_t& b) {
+        a = n * t / nth;
+        b = n * (t + 1) / nth;
+    };
+    auto par = [&](auto&& fn) {
+        if (nth == 1) {
+            fn(0);
+            return;
+        }
+        std::vector<std::thread> th;
+        for (int t = 0; t < nth; t++) th.emplace_back(fn, t);
+        for (auto& x : th) x.join();
+    };
+    par([&](int t) {
+        int64_t a, b;
+        range(t, a, b);
+        int64_t* c = cnt.data() + (size_t)t * ndm;
+        for (int64_t i = a; i < b; i++) c[src[i].dm]++;
+    });
+    dstart.assign((size_t)ndm + 1, 0);
+    int64_t run = 0;
+    for (int d = 0; d < ndm; d++) {
+        dstart[(size_t)d] = run;
+        for (int t = 0; t < nth; t++) {
+            const int64_t k = cnt[(size_t)t * ndm + d];
+            cnt[(size_t)t * ndm + d] = run;
+            run += k;
+        }
+    }
+    dstart[(size_t)ndm] = run;
+    par([&](int t) {
+        int64_t a, b;
+        range(t, a, b);
+        int64_t* o = cnt.data() + (size_t)t * ndm;
+        for (int64_t i = a; i < b; i++) dst[o[src[i].dm]++] = src[i];
+    });
+}
+
 // prune_related2 (the script's greedy walk across widths) and, for padded series,
 // prune_border_cases, on one DM's hits sorted by (bin, width) in place; returns the kept count.
 // The walk's inner loop visits, for pivot i, every later hit within max(downfact)/2 bins; a
@@ -2637,18 +2681,14 @@ extern "C" int hd_sp_prune(hd_sp_hit* hits, int64_t n, int32_t ndm, const int32_
 {
     if ((n > 0 && !hits) || !widths || !nkept || nw < 1 || nw > 16 || ndm < 1 || n < 0)
         return fail(nullptr, HD_E_INVAL, "hd_sp_prune: bad argument");
-    std::vector<int64_t> dstart((size_t)ndm + 1, 0);
-    for (int64_t i = 0; i < n; i++) {
+    for (int64_t i = 0; i < n; i++)
         if (hits[i].dm < 0 || hits[i].dm >= ndm || hits[i].widx < 0 || hits[i].widx >= nw)
             return fail(nullptr, HD_E_INVAL, "hd_sp_prune: hit %lld has dm %d / widx %d out of range", (long long)i,
                         (int)hits[i].dm, (int)hits[i].widx);
-        dstart[(size_t)hits[i].dm + 1]++;
-    }
-    for (int d = 0; d < ndm; d++) dstart[d + 1] += dstart[d];
+    std::vector<int64_t> dstart;
     {
         std::vector<hd_sp_hit> tmp(hits, hits + n);
-        std::vector<int64_t> pos(dstart.begin(), dstart.end() - 1);
-        for (const hd_sp_hit& h : tmp) hits[pos[(size_t)h.dm]++] = h;
+        sp_group_by_dm(tmp.data(), n, ndm, hits, dstart);
     }
     *nkept = sp_prune_groups(hits, dstart, ndm, widths, nw, nds, numout);
     return HD_OK;
@@ -2757,14 +2797,9 @@ extern "C" int hd_single_pulse(hd_plan* p, double dt, double maxwidth, double th
     // order among equal bins (width-1 hits appended first, every downfactor's bisect.insort
     // after equals) -- then prune_related2 (its greedy walk, literally) and prune_border_cases
     // (padded series: data ends at nds - 1, padding runs to numout - 1 -- the .inf on/off pair)
-    // grouped by DM straight from the pinned block into the caller's buffer (one pass)
-    std::vector<int64_t> dstart((size_t)ndm + 1, 0);
-    for (unsigned long long i = 0; i < cnt; i++) dstart[(size_t)src[i].dm + 1]++;
-    for (int d = 0; d < ndm; d++) dstart[d + 1] += dstart[d];
-    {
-        std::vector<int64_t> pos(dstart.begin(), dstart.end() - 1);
-        for (unsigned long long i = 0; i < cnt; i++) hits[pos[(size_t)src[i].dm]++] = src[i];
-    }
+    // grouped by DM straight from the pinned block into the caller's buffer
+    std::vector<int64_t> dstart;
+    sp_group_by_dm(src, (int64_t)cnt, ndm, hits, dstart);
     const int64_t out = sp_prune_groups(hits, dstart, ndm, widths, nw, p->nds, p->numout);
     *nhits = out;
     tm.mark(2);

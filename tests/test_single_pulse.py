@@ -277,11 +277,11 @@ def test_host_prune_matches_script(padded):
     L = _lib.load()
     widths = [1, 2, 3, 4, 6, 9, 14, 20, 30, 45, 70, 100, 150, 220, 300]
     rng = np.random.default_rng(3 + padded)
-    for trial in range(40):
+    for trial in range(42):
         ndm = int(rng.integers(1, 5))
-        nds = 20000
+        nds = 20000 if trial < 40 else 4_000_000             # the last two: > 64 Ki hits (threaded grouping)
         numout = nds + 3000 if padded else nds
-        n = int(rng.integers(0, 4000))
+        n = int(rng.integers(0, 4000)) if trial < 40 else 150_000
         h = np.zeros(n, HIT)
         h["dm"] = rng.integers(0, ndm, n)
         dense = rng.integers(0, 2)
