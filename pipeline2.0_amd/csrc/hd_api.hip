@@ -2602,11 +2602,41 @@ static void sp_group_by_dm(const hd_sp_hit* src, int64_t n, int ndm, hd_sp_hit* 
 // independently (each sets gone[j] or gone[i], and the loop reads only gone[j]), so the
 // relevant j are taken as the contiguous run within max(w_i/2, 1) plus, per wider width
 // class k, that class's hits within widths[k]/2 -- the same set, fewer visits.
+// One DM's hits in (bin, width) order: an LSD radix sort on bin << 4 | widx (8-bit digits,
+// passes up to the key's highest digit) for larger lists, std::sort for short or odd ones.
+static void sp_sort_hits(hd_sp_hit* h, int64_t n)
+{
+    auto cmp = [](const hd_sp_hit& x, const hd_sp_hit& y) { return x.bin != y.bin ? x.bin < y.bin : x.widx < y.widx; };
+    uint32_t kmax = 0;
+    bool ok = n >= 512;
+    for (int64_t i = 0; i < n && ok; i++) {
+        ok = h[i].bin >= 0 && h[i].bin < (1 << 27) && h[i].widx >= 0 && h[i].widx < 16;
+        kmax = std::max(kmax, ((uint32_t)h[i].bin << 4) | (uint32_t)h[i].widx);
+    }
+    if (!ok) {
+        std::sort(h, h + n, cmp);
+        return;
+    }
+    std::vector<hd_sp_hit> tmp((size_t)n);
+    hd_sp_hit *a = h, *b = tmp.data();
+    for (int shift = 0; shift < 32 && (kmax >> shift) != 0; shift += 8) {
+        int64_t pos[256] = {0};
+        for (int64_t i = 0; i < n; i++) pos[((((uint32_t)a[i].bin << 4) | (uint32_t)a[i].widx) >> shift) & 255]++;
+        int64_t run = 0;
+        for (int d = 0; d < 256; d++) {
+            const int64_t c = pos[d];
+            pos[d] = run;
+            run += c;
+        }
+        for (int64_t i = 0; i < n; i++) b[pos[((((uint32_t)a[i].bin << 4) | (uint32_t)a[i].widx) >> shift) & 255]++] = a[i];
+        std::swap(a, b);
+    }
+    if (a != h) std::copy(a, a + n, h);
+}
+
 static int64_t sp_prune_dm(hd_sp_hit* h, int64_t n, const int32_t* widths, int nw, int64_t nds, int64_t numout)
 {
-    std::sort(h, h + n, [](const hd_sp_hit& x, const hd_sp_hit& y) {
-        return x.bin != y.bin ? x.bin < y.bin : x.widx < y.widx;
-    });
+    sp_sort_hits(h, n);
     std::vector<char> gone((size_t)n, 0);
     const int reach = nw > 1 ? widths[nw - 1] / 2 : 0;
     std::vector<std::vector<int32_t>> cls((size_t)nw);
