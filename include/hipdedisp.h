@@ -330,10 +330,16 @@ HD_API int hd_series_fill(hd_plan* plan, int64_t t0, float value);
  * no device); *ndiff receives the count (HD_E_INVAL when it exceeds cap, diffbins holding the
  * first cap).  hd_plan_set_bary makes the plan's stage 2 write the barycentred series
  * (numout samples; added bins and the tail take the plan's padding value, hd_opts.pad_mode);
- * ndiff = 0 (or diffbins NULL) turns it off.  Not for time-sliced plans (HD_E_INVAL).   */
+ * ndiff = 0 (or diffbins NULL) turns it off.  Not for time-sliced plans (HD_E_INVAL).
+ * Setting the list the plan already holds returns at once (no wait on queued work).
+ * hd_plan_data_end: the samples of real data at the head of the output -- min(N/ds, numout),
+ * or, barycentred, where the last data segment ends (prepsubband's datawrote after the
+ * added and removed bins): the .inf on/off pair is [0, n-1], [numout-1, numout-1] when
+ * n < numout, and hd_single_pulse's border-case prune uses the same boundary.            */
 HD_API int hd_bary_diffbins(const double* topo, const double* bary, int32_t n, double tdt, double dsdt,
                             int32_t* diffbins, int32_t cap, int32_t* ndiff);
 HD_API int hd_plan_set_bary(hd_plan* plan, const int32_t* diffbins, int32_t ndiff);
+HD_API int hd_plan_data_end(const hd_plan* plan, int64_t* n);
 /* The .dat output path (replaces the files prepsubband leaves in the tempdir,
  * PALFA2_presto_search.py:514-520, 532-537): queue the device-resident series of the last
  * hd_run_dedisp of this plan to paths[numdms] -- raw little-endian float32, numout samples,
@@ -349,7 +355,8 @@ HD_API int hd_wait_writes(hd_ctx* ctx, double* write_seconds, int64_t* bytes);
 /* Device-time of the last hd_run_subband / hd_run_dedisp of this plan, ms.           */
 HD_API int hd_plan_last_ms(const hd_plan* plan, float* ms_subband, float* ms_dedisp);
 /* Name of the stage-2 kernel the last hd_run_dedisp of this plan launched, as rocprofv3
- * prints it without namespace and arguments (e.g. "k_stage2_pair<5, 3, 2>"): lets a
+ * prints it without namespace and arguments (e.g. "k_stage2_pair<5, 3, 2, true>": every
+ * template argument, the last one the non-negative-subband flag of the pair kernel): lets a
  * benchmark key its roofline and PMC counters by kernel.  NUL-terminated in name[cap].   */
 HD_API int hd_plan_kernel(const hd_plan* plan, char* name, int32_t cap);
 /* Kernel variants: (s1 << 8) | s2.  s2: 0 auto, 1 direct, 2 LDS-tiled (4 waves x 256 samples),

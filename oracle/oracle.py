@@ -340,6 +340,29 @@ def bary_series(topo, nvalid, numout, diffbins, padv):
     return out
 
 
+def bary_data_end(nvalid, numout, diffbins):
+    """Samples of real data at the head of a barycentred series (prepsubband's datawrote, the
+    .inf on/off boundary): one past the output index of the last topocentric sample
+    bary_series writes, counting the bins added before it."""
+    n, k, end = 0, 0, 0
+    for t in range(nvalid):
+        skip = False
+        while k < len(diffbins) and abs(int(diffbins[k])) == t:
+            if diffbins[k] > 0:
+                n += 1
+            else:
+                skip = True
+            k += 1
+        if n >= numout:
+            break
+        if not skip:
+            n += 1
+            end = n
+        if n >= numout:
+            break
+    return end
+
+
 def stats_padvals(dataavg):
     """determine_padvals from rfifind .stats interval averages [numint][numchan]."""
     a = np.ascontiguousarray(dataavg, np.float32)

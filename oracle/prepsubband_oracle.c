@@ -396,8 +396,12 @@ static void zero_dm(const float* rawdata, int ptsperblk, int numchan, float* zer
  * global read blocks [b0, b0 + nrows), row r = {avg, std, numgood, chansum[nchan]} (zeros for
  * a block whose every channel is masked).  raw holds the observation's spectra from
  * t0 = b0 * blk on (a time slice's own rows); obs->N is the whole observation's length.   */
-int or_clip_rows(const or_obs* obs, const or_opts* opts, const uint8_t* raw, const float* scl, const float* offs,
-                 const float* wts, const uint8_t* allzap, int blk, int64_t b0, int64_t nrows, double* rows)
+/* The rows, and (zdm_out != NULL) each block's zero-DM series into zdm_out[(b - b0) * blk + i]
+ * from the same decode: the whole-beam path keeps it, so every block is decoded once, as
+ * prepsubband's read loop does. */
+static int clip_rows_z(const or_obs* obs, const or_opts* opts, const uint8_t* raw, const float* scl,
+                       const float* offs, const float* wts, const uint8_t* allzap, int blk, int64_t b0,
+                       int64_t nrows, double* rows, float* zdm_out)
 {
     const int nchan = obs->nchan;
     const int64_t nblk = (obs->N + blk - 1) / blk;
@@ -422,6 +426,7 @@ int or_clip_rows(const or_obs* obs, const or_opts* opts, const uint8_t* raw, con
             row[0] = bs.avg;
             row[1] = bs.std;
             row[2] = (double)bs.numgood;
+            if (zdm_out) memcpy(zdm_out + r * blk, zdm, sizeof(float) * (size_t)nb);
         }
         free(zdm);
         free(X);
@@ -429,13 +434,22 @@ int or_clip_rows(const or_obs* obs, const or_opts* opts, const uint8_t* raw, con
     return 0;
 }
 
+int or_clip_rows(const or_obs* obs, const or_opts* opts, const uint8_t* raw, const float* scl, const float* offs,
+                 const float* wts, const uint8_t* allzap, int blk, int64_t b0, int64_t nrows, double* rows)
+{
+    return clip_rows_z(obs, opts, raw, scl, offs, wts, allzap, blk, b0, nrows, rows, NULL);
+}
+
 /* clip_times' block-order recurrence over the exchange rows table[nblk][nchan + 3] of the
  * whole observation: pad[nblk][nchan] (the channel levels in force per block) and the
  * clipped flags of spectra [t0, t0 + n) of raw (which holds those spectra; t0 a multiple of
  * blk).  Returns the number of clipped spectra among them.                                */
-int64_t or_clip_finish(const or_obs* obs, const or_opts* opts, const uint8_t* raw, const float* scl,
-                       const float* offs, const float* wts, const uint8_t* allzap, const float* padvals0, int blk,
-                       int nblk, const double* table, int64_t t0, int64_t n, float* pad, uint8_t* clipped)
+/* zdm_all != NULL: the zero-DM series of spectra [t0, t0 + n) already computed (the rows'
+ * decode); else each of those blocks is decoded here (a time slice's restatement). */
+static int64_t clip_finish_z(const or_obs* obs, const or_opts* opts, const uint8_t* raw, const float* scl,
+                             const float* offs, const float* wts, const uint8_t* allzap, const float* padvals0,
+                             int blk, int nblk, const double* table, int64_t t0, int64_t n, float* pad,
+                             uint8_t* clipped, const float* zdm_all)
 {
     const int nchan = obs->nchan;
     if (blk <= 0 || nblk != (int)((obs->N + blk - 1) / blk) || t0 % blk || t0 < 0 || t0 + n > obs->N) return -1;
@@ -444,7 +458,7 @@ int64_t or_clip_finish(const or_obs* obs, const or_opts* opts, const uint8_t* ra
     if (padvals0) memcpy(padvals, padvals0, sizeof(float) * nchan);
     const int clip = opts->clip_sigma > 0.0f;
     const int64_t rowbytes = (int64_t)nchan * obs->nbits / 8;
-    float* X = (float*)malloc(sizeof(float) * (size_t)blk * nchan);
+    float* X = zdm_all ? NULL : (float*)malloc(sizeof(float) * (size_t)blk * nchan);
     float* zdm = (float*)malloc(sizeof(float) * (size_t)blk);
     uint8_t* scratch = (uint8_t*)malloc((size_t)blk);
     double* cat = (double*)malloc(sizeof(double) * nchan);
@@ -459,16 +473,21 @@ int64_t or_clip_finish(const or_obs* obs, const or_opts* opts, const uint8_t* ra
             blockstat bs = {(int)row[2], row[0], row[1]};
             for (int jj = 0; jj < nchan; jj++) cat[jj] = bs.numgood >= 1 ? row[3 + jj] / bs.numgood : row[3 + jj];
             uint8_t* flags = scratch;
+            const float* z = zdm;
             memset(scratch, 0, (size_t)blk);
             if (mine) {
-                for (int ii = 0; ii < nb; ii++)
-                    decode_row(obs, opts, raw + (s0 - t0 + ii) * rowbytes, scl, offs, wts, X + (int64_t)ii * nchan);
-                zero_dm(X, nb, nchan, zdm);
+                if (zdm_all) {
+                    z = zdm_all + (s0 - t0);
+                } else {
+                    for (int ii = 0; ii < nb; ii++)
+                        decode_row(obs, opts, raw + (s0 - t0 + ii) * rowbytes, scl, offs, wts, X + (int64_t)ii * nchan);
+                    zero_dm(X, nb, nchan, zdm);
+                }
                 flags = clipped + (s0 - t0);
             } else {
                 for (int ii = 0; ii < nb; ii++) zdm[ii] = st.running_avg;   /* flags of other slices: unused */
             }
-            const int k = clip_update(zdm, nb, nchan, opts->clip_sigma, &bs, cat, padvals, &st, flags);
+            const int k = clip_update(z, nb, nchan, opts->clip_sigma, &bs, cat, padvals, &st, flags);
             if (mine) total += k;
         }
         memcpy(pad + (int64_t)b * nchan, padvals, sizeof(float) * nchan);
@@ -482,21 +501,33 @@ int64_t or_clip_finish(const or_obs* obs, const or_opts* opts, const uint8_t* ra
     return total;
 }
 
+int64_t or_clip_finish(const or_obs* obs, const or_opts* opts, const uint8_t* raw, const float* scl,
+                       const float* offs, const float* wts, const uint8_t* allzap, const float* padvals0, int blk,
+                       int nblk, const double* table, int64_t t0, int64_t n, float* pad, uint8_t* clipped)
+{
+    return clip_finish_z(obs, opts, raw, scl, offs, wts, allzap, padvals0, blk, nblk, table, t0, n, pad, clipped,
+                         NULL);
+}
+
 int64_t or_clip_prepare(const or_obs* obs, const or_opts* opts, const uint8_t* raw,
                         const float* scl, const float* offs, const float* wts,
                         const uint8_t* allzap, const float* padvals0, int blk, int nblk,
                         float* pad, uint8_t* clipped)
 {
     /* the reference's -sub command leaves prepsubband's default clip on; a block whose
-     * every channel is masked is neither clipped nor counted (read_psrdata) */
+     * every channel is masked is neither clipped nor counted (read_psrdata).  The whole beam:
+     * one decode per block (the rows' pass keeps the zero-DM series for the recurrence). */
     if (blk <= 0 || nblk != (int)((obs->N + blk - 1) / blk)) return -1;
     double* table = NULL;
+    float* zdm = NULL;
     if (opts->clip_sigma > 0.0f) {
         table = (double*)malloc(sizeof(double) * (size_t)nblk * (obs->nchan + 3));
-        or_clip_rows(obs, opts, raw, scl, offs, wts, allzap, blk, 0, nblk, table);
+        zdm = (float*)malloc(sizeof(float) * (size_t)nblk * blk);
+        clip_rows_z(obs, opts, raw, scl, offs, wts, allzap, blk, 0, nblk, table, zdm);
     }
-    const int64_t total = or_clip_finish(obs, opts, raw, scl, offs, wts, allzap, padvals0, blk, nblk, table, 0,
-                                         obs->N, pad, clipped);
+    const int64_t total = clip_finish_z(obs, opts, raw, scl, offs, wts, allzap, padvals0, blk, nblk, table, 0,
+                                        obs->N, pad, clipped, zdm);
+    free(zdm);
     free(table);
     return total;
 }

@@ -250,6 +250,9 @@ struct hd_plan {
     // len}; d_padv [numdms] the padding values
     int32_t nbseg = 0;
     bool bary_adds = false;         // some bin is added (the padding value is needed)
+    int64_t data_end = -1;          // samples of real data in the output (-1: nvalid; barycentred:
+                                    // the end of the last data segment, PRESTO's datawrote)
+    std::vector<int32_t> bary_diff; // the diffbins the segments were built from
     int32_t* d_bseg = nullptr;
     float* d_topo = nullptr;
     float* d_padv = nullptr;
@@ -2595,13 +2598,6 @@ static void sp_group_by_dm(const hd_sp_hit* src, int64_t n, int ndm, hd_sp_hit* 
     });
 }
 
-// prune_related2 (the script's greedy walk across widths) and, for padded series,
-// prune_border_cases, on one DM's hits sorted by (bin, width) in place; returns the kept count.
-// The walk's inner loop visits, for pivot i, every later hit within max(downfact)/2 bins; a
-// pair acts only when its gap is <= max(w_i/2, w_j/2, 1), and for a fixed i the pairs act
-// independently (each sets gone[j] or gone[i], and the loop reads only gone[j]), so the
-// relevant j are taken as the contiguous run within max(w_i/2, 1) plus, per wider width
-// class k, that class's hits within widths[k]/2 -- the same set, fewer visits.
 // One DM's hits in (bin, width) order: an LSD radix sort on bin << 4 | widx (8-bit digits,
 // passes up to the key's highest digit) for larger lists, std::sort for short or odd ones.
 static void sp_sort_hits(hd_sp_hit* h, int64_t n)
@@ -2634,6 +2630,13 @@ static void sp_sort_hits(hd_sp_hit* h, int64_t n)
     if (a != h) std::copy(a, a + n, h);
 }
 
+// prune_related2 (the script's greedy walk across widths) and, for padded series,
+// prune_border_cases, on one DM's hits sorted by (bin, width) in place; returns the kept count.
+// The walk's inner loop visits, for pivot i, every later hit within max(downfact)/2 bins; a
+// pair acts only when its gap is <= max(w_i/2, w_j/2, 1), and for a fixed i the pairs act
+// independently (each sets gone[j] or gone[i], and the loop reads only gone[j]), so the
+// relevant j are taken as the contiguous run within max(w_i/2, 1) plus, per wider width
+// class k, that class's hits within widths[k]/2 -- the same set, fewer visits.
 static int64_t sp_prune_dm(hd_sp_hit* h, int64_t n, const int32_t* widths, int nw, int64_t nds, int64_t numout)
 {
     sp_sort_hits(h, n);
@@ -2826,11 +2829,13 @@ extern "C" int hd_single_pulse(hd_plan* p, double dt, double maxwidth, double th
     // per DM (in parallel): the script's dm_candlist order -- by bin, widths in increasing
     // order among equal bins (width-1 hits appended first, every downfactor's bisect.insort
     // after equals) -- then prune_related2 (its greedy walk, literally) and prune_border_cases
-    // (padded series: data ends at nds - 1, padding runs to numout - 1 -- the .inf on/off pair)
+    // (padded series: data ends at dend - 1, padding runs to numout - 1 -- the .inf on/off pair)
     // grouped by DM straight from the pinned block into the caller's buffer
     std::vector<int64_t> dstart;
     sp_group_by_dm(src, (int64_t)cnt, ndm, hits, dstart);
-    const int64_t out = sp_prune_groups(hits, dstart, ndm, widths, nw, p->nds, p->numout);
+    // barycentred series: the data end where the last data segment ends (hd_plan_data_end)
+    const int64_t dend = p->data_end >= 0 ? p->data_end : p->nvalid;
+    const int64_t out = sp_prune_groups(hits, dstart, ndm, widths, nw, dend, p->numout);
     *nhits = out;
     tm.mark(2);
     return HD_OK;
@@ -2957,14 +2962,16 @@ extern "C" int hd_bary_diffbins(const double* topo, const double* bary, int32_t 
 // topocentric samples [0, nvalid) are written: the samples before |v|, then one padding sample
 // (v > 0) or sample |v| skipped (v < 0); the rest, then padding to numout.
 static void bary_segments(const int32_t* dv, int32_t nd, int64_t nvalid, int64_t numout, std::vector<int32_t>& seg,
-                          bool& adds)
+                          bool& adds, int64_t& data_end)
 {
     seg.clear();
     adds = false;
+    data_end = 0;
     int64_t out = 0, src = 0;
     auto put = [&](int64_t s, int64_t len) {
         len = std::min<int64_t>(len, numout - out);
         if (len <= 0) return;
+        if (s >= 0) data_end = out + len;                     // end of the last data segment
         const size_t k = seg.size();
         if (s < 0 && k >= 3 && seg[k - 2] < 0) {              // merge padding runs
             seg[k - 1] += (int32_t)len;
@@ -2992,30 +2999,52 @@ extern "C" int hd_plan_set_bary(hd_plan* p, const int32_t* diffbins, int32_t ndi
 {
     if (!p) return fail(nullptr, HD_E_INVAL, "hd_plan_set_bary: NULL plan");
     hd_ctx* c = p->ctx;
+    if (ndiff < 0 || (ndiff > 0 && !diffbins)) return fail(c, HD_E_INVAL, "hd_plan_set_bary: bad diffbins");
+    // unchanged settings (the same list, or topocentric again): nothing to do, and no wait
+    // on the plan's queued work (run_pass sets the table on every pass)
+    if (ndiff == (int32_t)p->bary_diff.size() && (ndiff == 0 ? p->nbseg == 0 : p->nbseg > 0) &&
+        std::equal(p->bary_diff.begin(), p->bary_diff.end(), diffbins ? diffbins : p->bary_diff.data()))
+        return HD_OK;
+    if (ndiff > 0) {
+        if (c->slice_total > 0) return fail(c, HD_E_INVAL, "hd_plan_set_bary: not for a time-sliced context");
+        for (int32_t i = 1; i < ndiff; i++)
+            if (std::abs((int64_t)diffbins[i]) < std::abs((int64_t)diffbins[i - 1]))
+                return fail(c, HD_E_INVAL, "hd_plan_set_bary: |diffbins| must not decrease (entry %d)", (int)i);
+        if (p->numout >= ((int64_t)1 << 31)) return fail(c, HD_E_INVAL, "hd_plan_set_bary: numout >= 2^31");
+    }
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, sync_all(c));
+    // the old segment table may still be read by this plan's queued stage 2 / k_bary, and its
+    // series by the writer: wait for exactly those (ev[3] ends the plan's last hd_run_dedisp)
+    if (p->ran_dd && p->ev[3]) HIPCHK(c, hipEventSynchronize(p->ev[3]));
     if (p->copy_pending && c->writer) HIPCHK(c, hipEventSynchronize(p->ev_copy));
     dfree(p->d_bseg);
     p->d_bseg = nullptr;
     p->nbseg = 0;
-    if (!diffbins || ndiff <= 0) {
+    p->bary_diff.clear();
+    p->data_end = -1;
+    p->ran_dd = false;                 // the device series no longer match the settings
+    if (ndiff == 0) {
         dfree(p->d_topo);
         p->d_topo = nullptr;
         return HD_OK;
     }
-    if (c->slice_total > 0) return fail(c, HD_E_INVAL, "hd_plan_set_bary: not for a time-sliced context");
-    for (int32_t i = 1; i < ndiff; i++)
-        if (std::abs((int64_t)diffbins[i]) < std::abs((int64_t)diffbins[i - 1]))
-            return fail(c, HD_E_INVAL, "hd_plan_set_bary: |diffbins| must not decrease (entry %d)", (int)i);
-    if (p->numout >= ((int64_t)1 << 31)) return fail(c, HD_E_INVAL, "hd_plan_set_bary: numout >= 2^31");
     std::vector<int32_t> seg;
-    bary_segments(diffbins, ndiff, p->nvalid, p->numout, seg, p->bary_adds);
+    bary_segments(diffbins, ndiff, p->nvalid, p->numout, seg, p->bary_adds, p->data_end);
     const size_t bytes = sizeof(int32_t) * seg.size();
     HIPCHK(c, hipMalloc(&p->d_bseg, std::max<size_t>(bytes, 16)));
-    if (bytes) HIPCHK(c, hipMemcpy(p->d_bseg, seg.data(), bytes, hipMemcpyHostToDevice));
+    // a pageable source: the copy has completed when the call returns, so seg may go
+    if (bytes) HIPCHK(c, hipMemcpyAsync(p->d_bseg, seg.data(), bytes, hipMemcpyHostToDevice, c->stream));
+    if (bytes) HIPCHK(c, hipStreamSynchronize(c->stream));
     p->nbseg = (int32_t)(seg.size() / 3);
+    p->bary_diff.assign(diffbins, diffbins + ndiff);
     if (!p->d_padv) HIPCHK(c, hipMalloc(&p->d_padv, sizeof(float) * (size_t)std::max(p->pass.numdms, 1)));
-    p->ran_dd = false;                 // the device series no longer match the settings
+    return HD_OK;
+}
+
+extern "C" int hd_plan_data_end(const hd_plan* p, int64_t* n)
+{
+    if (!p || !n) return fail(p ? p->ctx : nullptr, HD_E_INVAL, "hd_plan_data_end: NULL argument");
+    *n = p->data_end >= 0 ? p->data_end : p->nvalid;
     return HD_OK;
 }
 

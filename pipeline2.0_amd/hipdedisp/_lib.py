@@ -42,7 +42,7 @@ EXPORTED = [
     "hd_sp_widths", "hd_single_pulse", "hd_rfifind_stats",
     "hd_push_raw_file_band", "hd_fill_raw",
     "hd_realfft", "hd_zap_ranges", "hd_zapbirds", "hd_rednoise_blocks", "hd_rednoise", "hd_get_fft",
-    "hd_bary_diffbins", "hd_plan_set_bary", "hd_run_dedisp_multi", "hd_plan_launch_passes", "hd_sp_prune",
+    "hd_bary_diffbins", "hd_plan_set_bary", "hd_plan_data_end", "hd_run_dedisp_multi", "hd_plan_launch_passes", "hd_sp_prune",
     "hd_prefetch_raw_file", "hd_prefetch_raw_file_band", "hd_prefetch_fill", "hd_swap_raw",
 ]
 
@@ -176,6 +176,7 @@ def load():
         "hd_bary_diffbins": (ctypes.c_int, [P(ctypes.c_double), P(ctypes.c_double), i32, ctypes.c_double,
                                             ctypes.c_double, P(ctypes.c_int32), i32, P(ctypes.c_int32)]),
         "hd_plan_set_bary": (ctypes.c_int, [vp, P(ctypes.c_int32), i32]),
+        "hd_plan_data_end": (ctypes.c_int, [vp, P(ctypes.c_int64)]),
         "hd_prefetch_raw_file": (ctypes.c_int, [vp, ctypes.c_char_p, P(hd_rows_src), i64]),
         "hd_prefetch_raw_file_band": (ctypes.c_int, [vp, ctypes.c_char_p, P(hd_rows_src), i64, i64, i64, i64, i64]),
         "hd_prefetch_fill": (ctypes.c_int, [vp, i64, i64, i32]),

@@ -410,6 +410,13 @@ class Plan:
         self.eng._chk(self.eng._L.hd_plan_set_bary(self._p, d.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), len(d)),
                       "hd_plan_set_bary")
 
+    def data_end(self):
+        """Samples of real data at the head of the output (hd_plan_data_end): min(nds,
+        numout), or where the barycentred data ends; the .inf on/off boundary."""
+        n = ctypes.c_int64()
+        self.eng._chk(self.eng._L.hd_plan_data_end(self._p, ctypes.byref(n)), "hd_plan_data_end")
+        return n.value
+
     def run_subband(self):
         self.eng._chk(self.eng._L.hd_run_subband(self._p), "prepsubband -sub -subdm %.2f" % self.pp.subdm)
 

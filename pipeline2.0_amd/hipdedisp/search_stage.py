@@ -212,7 +212,7 @@ def run_pass(job, ddplan, passnum, maskfilenm, tempdir, single_pulse=None, fft=N
         job.set_bary(plan)
         plan.run_dedisp(to_host=False)
         info = job.info_template(pp.nsub, plan.sub_lofreq, plan.sub_chanwid, plan.sub_dt, series=True)
-        write_dats_device(plan, os.path.join(tempdir, job.basefilenm), ddplan.dmlist[passnum], info, plan.nds)
+        write_dats_device(plan, os.path.join(tempdir, job.basefilenm), ddplan.dmlist[passnum], info, plan.data_end())
         t_dd = time.time() - t0
         if single_pulse is not None:
             _single_pulse(job, plan, ddplan, passnum, tempdir, single_pulse)
@@ -239,7 +239,7 @@ def _run_pass_nosub(job, ddplan, passnum, maskfilenm, tempdir, single_pulse=None
         job.set_bary(plan)
         plan.run_dedisp(to_host=False)
         info = job.info_template(pp.nsub, plan.sub_lofreq, plan.sub_chanwid, plan.sub_dt, series=True)
-        write_dats_device(plan, os.path.join(tempdir, job.basefilenm), ddplan.dmlist[passnum], info, plan.nds)
+        write_dats_device(plan, os.path.join(tempdir, job.basefilenm), ddplan.dmlist[passnum], info, plan.data_end())
         t_dd = time.time() - t0
         if single_pulse is not None:
             _single_pulse(job, plan, ddplan, passnum, tempdir, single_pulse)

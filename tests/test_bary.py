@@ -74,6 +74,12 @@ def test_bary_series_oracle_properties():
     assert got.tolist() == want
     got = OR.bary_series(topo, 20, 25, np.array([-0, 19, 25], np.int32), pv)[0]
     assert got.tolist() == list(range(1, 19)) + [-1, 19] + [-1] * 5
+    # the data end: one past the last topocentric sample written
+    assert OR.bary_data_end(20, 22, np.array([3, 3, -7, 12], np.int32)) == 22
+    assert OR.bary_data_end(20, 25, np.array([-0, 19, 25], np.int32)) == 20
+    assert OR.bary_data_end(20, 30, np.array([-2, -5, -9], np.int32)) == 17
+    assert OR.bary_data_end(20, 20, np.array([-2, 19], np.int32)) == 20
+    assert OR.bary_data_end(20, 19, np.array([-2, 19], np.int32)) == 18
 
 
 @pytest.mark.gpu
@@ -106,7 +112,55 @@ def test_gpu_bary_series(engine, numout_kind, k):
         padv = OR.pad_values(topo, nds, Opts().pad_mode)
         want = OR.bary_series(topo, nvalid, numout, db, padv)
         assert np.array_equal(got, want)
+        assert p.data_end() == OR.bary_data_end(nvalid, numout, db)
+        p.set_bary(db)                                     # the same list again: a no-op
+        assert p.data_end() == OR.bary_data_end(nvalid, numout, db)
         p.set_bary(None)                                   # back to topocentric
+        assert p.data_end() == nvalid
         assert np.array_equal(p.run_dedisp(to_host=True), topo)
+    finally:
+        p.destroy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [1, 2])
+def test_gpu_bary_inf_and_single_pulse_border(engine, tmp_path, k):
+    """A barycentred, padded pass: the .inf on/off pair ends the data at hd_plan_data_end - 1
+    (the barycentred count, not N/ds - 1), and hd_single_pulse's border-case prune uses the same
+    boundary -- candidates identical to the oracle's with nds = that data end."""
+    from hipdedisp import single_pulse as SP
+    from hipdedisp.formats import inf as INF
+    from hipdedisp.formats.series import write_dats_device
+    from hipdedisp.synth import palfa_obs, palfa_synth
+    obs = palfa_obs(N=1 << 18, nbits=8)
+    engine.set_obs(obs, Opts())
+    engine.synth_device(palfa_synth())
+    nds = obs.N
+    numout = nds + 2000
+    pp = PassParams(subdm=30.0, lodm=25.0, dmstep=0.5, numdms=76, nsub=96, ds=1, numout=numout)
+    p = engine.plan(pp)
+    try:
+        p.run_subband()
+        topo = p.run_dedisp(to_host=True)
+        top, bar = tempo_table(obs.N * obs.dt, 1.0, **[dict(v=3e-3), dict(v=-2e-3), dict(v=1e-3, amp=2e-3, per=5.0)][k])
+        db = bary_diffbins(top, bar, 1.0, obs.dt)
+        p.set_bary(db)
+        series = p.run_dedisp(to_host=True)
+        dend = OR.bary_data_end(nds, numout, db)
+        assert p.data_end() == dend and dend != nds
+        dms = ["%.2f" % (25.0 + 0.5 * i) for i in range(76)]
+        info = INF.InfoData(name="beam", dt=obs.dt, num_chan=96)
+        write_dats_device(p, str(tmp_path / "beam"), dms[:76], info, p.data_end())
+        d = INF.read_inf(str(tmp_path / ("beam_DM%s.inf" % dms[0])))
+        assert d.onoff == [0.0, float(dend - 1), float(numout - 1), float(numout - 1)]
+        wl = SP.widths(obs.dt, 0.1)
+        got, bad = SP.device_candidates(p, obs.dt, 0.1, 3.0)
+        raw, wbad = OR.sp_hits(series, wl, 3.0)
+        assert np.array_equal(bad, wbad)
+        ref = OR.sp_candidates(raw, wbad, wl, [float(x) for x in dms], obs.dt, dend, numout,
+                               ls=numout // 1000 * 1000 // 8000 * 8000)
+        want = [(d_, c.bin, c.downfact, c.sigma) for d_, cl in enumerate(ref) for c in cl]
+        have = [(r[0], r[1], wl[r[2]], r[4]) for r in got.tolist()]
+        assert have == want
     finally:
         p.destroy()
