@@ -63,6 +63,14 @@ def parse():
                          "time slices, every rank runs all 57 passes on its slice (strong, configs[2]; RCCL carries "
                          "only the clip statistics and padding sums); shard: ONE beam's passes LPT-sharded after "
                          "an RCCL broadcast of the raw block (strong, the round-1 design, kept for comparison)")
+    ap.add_argument("--check-union", action="store_true",
+                    help="--mode slices: after the timed steps, gather every rank's exact per-DM sums of its owned "
+                         "series (and the last rank's padding values) and check, on rank 0, that their union equals a "
+                         "whole-beam one-context run of the same beam")
+    ap.add_argument("--sim-slice", default=None, metavar="R/G",
+                    help="--mode slices on ONE process: run only rank R's slice of a G-way cut (no collectives; the "
+                         "other ranks' clip statistics are absent, so only the timing is meaningful) -- the per-rank "
+                         "compute time behind the multi-GPU prediction, not a scaling measurement")
     return ap.parse_args()
 
 
@@ -179,16 +187,21 @@ def fft_leg(eng, stages, beams):
         eng.sync()
 
     t = time.perf_counter()
-    beam()                                        # hipFFT plans (rocFFT kernel builds) + spectra buffers
+    for plans in stages:                          # hipFFT plans (rocFFT kernel builds), one per geometry
+        if plans:
+            FS.prepare(plans[0])
+    prep = time.perf_counter() - t
+    t = time.perf_counter()
+    beam()
     first = time.perf_counter() - t
     t = time.perf_counter()
     for _ in range(beams):
         beam()
     s = (time.perf_counter() - t) / beams
-    return {"s_per_beam": s, "first_beam_s": first,
+    return {"s_per_beam": s, "first_beam_s": first, "plan_build_s": prep,
             "note": "hd_realfft + hd_zapbirds (the 221 PALFA.zaplist birdies) + hd_rednoise over the 57 passes' series in HBM "
-                    "(spectra stay on the device); wall time with the plans' FFT state built (first_beam_s: "
-                    "including the hipFFT plan builds and buffer allocation)"}
+                    "(spectra stay on the device); wall time with the plans' FFT state built (plan_build_s: the six "
+                    "hipFFT plans built ahead by hd_fft_prepare; first_beam_s: the first beam after that)"}
 
 
 def rfifind_leg(eng, obs, beams):
@@ -355,8 +368,7 @@ def run_slice_step(eng, ts, rank, stages, dist, torch):
         if not st:
             continue
         eng.run_subband_multi(st)
-        for p in st:
-            p.run_dedisp(to_host=False)
+        run_dedisp_stage(eng, st)
         plans += st
     sums = ts.pass_sums(rank, plans)
     if dist is not None:
@@ -367,6 +379,54 @@ def run_slice_step(eng, ts, rank, stages, dist, torch):
         sums = t.cpu().numpy().astype(np.float64)
     ts.pad_passes(rank, plans, sums)
     eng.sync()
+
+
+def slice_checksums(ts, rank, stages):
+    """Per pass of this rank's slice: the exact double sum of every DM's owned output samples
+    (hd_series_sum; the series are integer-valued, so the sums over ranks add exactly) and,
+    on the last rank, the padding value of the padded tail (NaN elsewhere)."""
+    import numpy as np
+    out = []
+    for st in stages:
+        for p in st:
+            nj = ts.out_range(rank, p.pp.ds)[1]
+            sums = np.array([p.series_sum(d, 0, nj) for d in range(p.pp.numdms)], np.float64)
+            padv = float(p.get_series(0, 1, nj, 1)[0, 0]) if p.numout > nj else float("nan")
+            out.append((sums, padv))
+    return out
+
+
+def union_check(eng_factory, obs, synth, ddplans, mask, pts, pad, gathered):
+    """Rank 0: the union of the ranks' slice checksums against one whole-beam context."""
+    import numpy as np
+    from hipdedisp import Opts
+    eng = eng_factory()
+    try:
+        eng.set_obs(obs, Opts())
+        eng.synth_device(synth)
+        eng.set_mask(mask, pts, pad)
+        stages = build_plans(eng, obs, ddplans, 0)
+        run_step(eng, stages)
+        k, bad, ndm = 0, [], 0
+        for st in stages:
+            for p in st:
+                want = np.array([p.series_sum(d, 0, p.nds) for d in range(p.pp.numdms)], np.float64)
+                got = sum(g[k][0] for g in gathered)
+                ndm += p.pp.numdms
+                if not np.array_equal(got, want):
+                    bad.append((k, "sums", int(np.sum(got != want))))
+                if p.numout > p.nds:
+                    wpad = float(p.get_series(0, 1, p.nds, 1)[0, 0])
+                    gpad = gathered[-1][k][1]
+                    if wpad != gpad:
+                        bad.append((k, "pad", wpad, gpad))
+                k += 1
+                p.destroy()
+    finally:
+        eng.close()
+    return {"passes": k, "dm_trials": ndm, "ranks": len(gathered), "equal": not bad, "mismatches": bad[:8],
+            "note": "per DM: sum over ranks of hd_series_sum of the owned samples == the whole-beam run's sum over "
+                    "[0, N/ds), exact; last rank's padding value == the whole-beam padding value, exact"}
 
 
 def broadcast_beam(eng, obs, rank, dist, torch):
@@ -459,11 +519,17 @@ def main():
         synth = palfa_synth(beam=0, nbits=args.nbits)       # one beam for the whole node
     eng = Engine(local)
     ts = None
+    srank = rank                                     # slices: this process's slice
     if slices:
         from hipdedisp.sharding import TimeSlices
-        ts = TimeSlices(obs, ddplans, world)
-        eng.set_obs(ts.local_obs(rank), Opts())
-        eng.set_slice(ts.slice(rank)[0], obs.N)
+        sworld = world
+        if args.sim_slice:
+            if world != 1:
+                sys.exit("--sim-slice runs one process")
+            srank, sworld = (int(x) for x in args.sim_slice.split("/"))
+        ts = TimeSlices(obs, ddplans, sworld)
+        eng.set_obs(ts.local_obs(srank), Opts())
+        eng.set_slice(ts.slice(srank)[0], obs.N)
     else:
         eng.set_obs(obs, Opts())
     eng.set_streams(args.streams)
@@ -475,12 +541,12 @@ def main():
     if shard:
         stages = shard_stages(eng, obs, ddplans, rank, world, args.variant)
     elif slices:
-        stages = slice_stages(eng, ts, rank, args.variant)
+        stages = slice_stages(eng, ts, srank, args.variant)
     else:
         stages = build_plans(eng, obs, ddplans, args.variant)
     plans = [p for st in stages for p in st]
     if slices:                                                      # this rank's owned samples
-        out_per_step = sum(p.pp.numdms * ts.out_range(rank, p.pp.ds)[1] for p in plans)
+        out_per_step = sum(p.pp.numdms * ts.out_range(srank, p.pp.ds)[1] for p in plans)
     else:
         out_per_step = sum(p.pp.numdms * p.nds for p in plans)
     if shard and world > 1:
@@ -490,7 +556,7 @@ def main():
 
     def step():
         if slices:
-            run_slice_step(eng, ts, rank, stages, dist, torch)
+            run_slice_step(eng, ts, srank, stages, dist, torch)
         else:
             run_step(eng, stages)
 
@@ -526,8 +592,8 @@ def main():
         k = per_kernel.setdefault(p.kernel(), {"ms": 0.0, "launches": 0, "units": 0})
         k["ms"] += b
         k["launches"] += 1 if p.launch_passes() > 0 else 0      # passes sharing a launch count once
-        k["units"] += p.pp.numdms * (ts.out_range(rank, p.pp.ds)[1] if slices else p.nds)
-    raw_bytes = (ts.slice(rank)[1] if slices else obs.N) * obs.rowbytes
+        k["units"] += p.pp.numdms * (ts.out_range(srank, p.pp.ds)[1] if slices else p.nds)
+    raw_bytes = (ts.slice(srank)[1] if slices else obs.N) * obs.rowbytes
     adds2 = sum(p.pp.numdms * p.nds * p.pp.nsub for p in plans)
     # algorithmic bytes per output sample (SURVEY §8d compulsory model): raw once + 4 B out
     b_unit = (raw_bytes + 4.0 * out_per_step) / out_per_step
@@ -569,7 +635,9 @@ def main():
                    "out_samples_per_beam": sum(d.numpasses * d.dmsperpass * (obs.N // d.sub_downsamp) for d in ddplans),
                    "parallelism": ("1 beam, passes LPT-sharded x%d, RCCL raw broadcast" % world) if shard
                    else ("1 beam, time slices x%d (halo %d spectra), RCCL clip-stats + padding all-reduce"
-                         % (world, ts.halo)) if slices
+                         % (world, ts.halo)) if slices and not args.sim_slice
+                   else ("ONE rank's time slice (%s, halo %d spectra) alone, no collectives: per-rank compute time, "
+                         "a prediction input, not a scaling measurement" % (args.sim_slice, ts.halo)) if slices
                    else "beam-per-GPU x%d" % world},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -613,6 +681,20 @@ def main():
         st = stream_leg(eng, stages, obs, [synth, palfa_synth(beam=rank + 8, nbits=args.nbits)], args.stream_beams)
         if st:
             line["stream_beams"] = st
+    if slices and args.check_union:
+        mine = slice_checksums(ts, srank, stages)
+        gathered = [None] * world
+        if dist is not None:
+            dist.all_gather_object(gathered, mine)
+        else:
+            gathered = [mine]
+        if rank == 0:
+            for p in plans:
+                p.destroy()
+            plans = []
+            eng.close()
+            line["union_check"] = union_check(lambda: Engine(local), obs, synth, ddplans, mask, pts, pad, gathered)
+        barrier(dist, torch)
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(obs, synth, ddplans, args.cpu_seconds, mask, pts, pad, omp=False)
         line["cpu_baseline_openmp"] = cpu_baseline(obs, synth, ddplans, args.cpu_seconds, mask, pts, pad, omp=True)
@@ -621,6 +703,8 @@ def main():
     for p in plans:
         p.destroy()
     eng.close()
+    if "union_check" in line and not line["union_check"]["equal"]:
+        sys.exit("union check failed: %s" % line["union_check"]["mismatches"])
     if dist is not None:
         dist.destroy_process_group()
 

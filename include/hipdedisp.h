@@ -434,6 +434,10 @@ HD_API int hd_single_pulse(hd_plan* plan, double dt, double maxwidth, double thr
  * reuse them: a later hd_realfft of another plan of the same geometry takes the buffer over,
  * and hd_zapbirds / hd_rednoise / hd_get_fft of the earlier plan then fail with HD_E_STATE. */
 HD_API int hd_realfft(hd_plan* plan);
+/* Build the hipFFT plan and spectra buffer of this plan's geometry now (no transform; the
+ * plan need not have run): rocFFT compiles its kernels for a new size, seconds per geometry,
+ * which a caller moves off its timed path by preparing each DDplan stage's geometry once.  */
+HD_API int hd_fft_prepare(hd_plan* plan);
 /* Bin ranges [lo, hi) zapped for birdies lobins[i] .. hibins[i] (frequency * T, the
  * zaplist's freq -+ width/2): lo = floor(lobin), hi = ceil(hibin), clamped to
  * [1, numbins), empty ones dropped, sorted and merged where they overlap or touch; the

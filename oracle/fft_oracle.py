@@ -27,6 +27,14 @@ def realfft(x):
     return out
 
 
+def birdie_bins(birds, T, baryv=0.0):
+    """zapbirds' bin ranges of zaplist entries (freq, width, barycentric) for T seconds:
+    (f -/+ w/2) * T, a barycentric frequency divided by (1 + baryv) first."""
+    lo = np.array([((f / (1.0 + baryv)) if b else f) * T - 0.5 * w * T for f, w, b in birds], np.float64)
+    hi = np.array([((f / (1.0 + baryv)) if b else f) * T + 0.5 * w * T for f, w, b in birds], np.float64)
+    return lo, hi
+
+
 def zap_ranges(lobins, hibins, numbins):
     r = []
     for a, b in zip(lobins, hibins):

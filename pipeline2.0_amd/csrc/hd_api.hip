@@ -3458,6 +3458,21 @@ extern "C" int hd_realfft(hd_plan* p)
     return HD_OK;
 }
 
+extern "C" int hd_fft_prepare(hd_plan* p)
+{
+    if (!p) return fail(nullptr, HD_E_INVAL, "hd_fft_prepare: NULL plan");
+    hd_ctx* c = p->ctx;
+    if (p->numout < 4 || p->numout % 2) return fail(c, HD_E_INVAL, "hd_fft_prepare: numout %lld must be even, >= 4",
+                                                    (long long)p->numout);
+    if (p->out_stride > INT32_MAX) return fail(c, HD_E_INVAL, "hd_fft_prepare: series stride beyond 2^31");
+    HIPCHK(c, hipSetDevice(c->device));
+    const auto key = std::make_tuple(p->numout, p->pass.numdms, p->out_stride);
+    hd::FftState*& st_fft = c->fft_cache[key];
+    if (!st_fft) st_fft = hd::fft_state_new();
+    HIPCHK(c, hd::fft_prepare(st_fft, p->out_stride, p->numout, p->pass.numdms));
+    return HD_OK;
+}
+
 extern "C" int hd_zap_ranges(const double* lobins, const double* hibins, int32_t n, int64_t numbins, int32_t* rng4,
                              int32_t cap, int32_t* nr)
 {

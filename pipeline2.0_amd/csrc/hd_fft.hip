@@ -220,6 +220,35 @@ hipError_t fft_end(FftState* s, hipStream_t st)
     return e;
 }
 
+// the hipFFT plan and spectra buffer of a geometry (rocFFT builds its kernels here: seconds
+// for a new size, so hd_fft_prepare can run it ahead of the timed path)
+hipError_t fft_prepare(FftState* s, int64_t xstride, int64_t n, int ndm)
+{
+    if (n < 4 || (n & 1) || ndm < 1) return hipErrorInvalidValue;
+    if (s->n == n && s->ndm == ndm && s->d_fft) return hipSuccess;
+    if (s->pending) {
+        const hipError_t e = hipEventSynchronize(s->done);
+        if (e != hipSuccess) return e;
+        s->pending = false;
+    }
+    const int64_t fs = n / 2 + 1;
+    if (s->have_plan) hipfftDestroy(s->plan);
+    s->have_plan = false;
+    (void)hipFree(s->d_fft);
+    s->d_fft = nullptr;
+    hipError_t e = hipMalloc(&s->d_fft, sizeof(float2) * (size_t)fs * ndm);
+    if (e != hipSuccess) return e;
+    int nn = (int)n;
+    int inembed = (int)xstride, onembed = (int)fs;
+    if (hipfftPlanMany(&s->plan, 1, &nn, &inembed, 1, (int)xstride, &onembed, 1, (int)fs, HIPFFT_R2C, ndm) !=
+        HIPFFT_SUCCESS)
+        return hipErrorUnknown;
+    s->have_plan = true;
+    s->n = n;
+    s->ndm = ndm;
+    return hipSuccess;
+}
+
 hipError_t fft_series(FftState* s, const float* x, int64_t xstride, int64_t n, int ndm, hipStream_t st)
 {
     if (n < 4 || (n & 1) || ndm < 1) return hipErrorInvalidValue;
@@ -228,21 +257,9 @@ hipError_t fft_series(FftState* s, const float* x, int64_t xstride, int64_t n, i
         if (e != hipSuccess) return e;
     }
     const int64_t fs = n / 2 + 1;
-    if (s->n != n || s->ndm != ndm || !s->d_fft) {
-        if (s->have_plan) hipfftDestroy(s->plan);
-        s->have_plan = false;
-        (void)hipFree(s->d_fft);
-        s->d_fft = nullptr;
-        hipError_t e = hipMalloc(&s->d_fft, sizeof(float2) * (size_t)fs * ndm);
+    {
+        hipError_t e = fft_prepare(s, xstride, n, ndm);
         if (e != hipSuccess) return e;
-        int nn = (int)n;
-        int inembed = (int)xstride, onembed = (int)fs;
-        if (hipfftPlanMany(&s->plan, 1, &nn, &inembed, 1, (int)xstride, &onembed, 1, (int)fs, HIPFFT_R2C, ndm) !=
-            HIPFFT_SUCCESS)
-            return hipErrorUnknown;
-        s->have_plan = true;
-        s->n = n;
-        s->ndm = ndm;
     }
     if (hipfftSetStream(s->plan, st) != HIPFFT_SUCCESS ||
         hipfftExecR2C(s->plan, (hipfftReal*)x, (hipfftComplex*)s->d_fft) != HIPFFT_SUCCESS)

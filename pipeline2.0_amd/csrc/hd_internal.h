@@ -216,6 +216,7 @@ hipError_t fft_end(FftState* s, hipStream_t st);
 float2* fft_buffer(FftState* s);
 const void* fft_owner(const FftState* s);
 void fft_set_owner(FftState* s, const void* owner);
+hipError_t fft_prepare(FftState* s, int64_t xstride, int64_t n, int ndm);
 hipError_t fft_series(FftState* s, const float* x, int64_t xstride, int64_t n, int ndm, hipStream_t st);
 hipError_t fft_zap(FftState* s, const int32_t* rng4, int nr, hipStream_t st);
 hipError_t fft_rednoise(FftState* s, const int32_t* boff, const double* cen, int nblk, hipStream_t st);

@@ -41,7 +41,7 @@ EXPORTED = [
     "hd_set_slice", "hd_clip_stats", "hd_clip_set_stats", "hd_series_sum", "hd_series_fill",
     "hd_sp_widths", "hd_single_pulse", "hd_rfifind_stats",
     "hd_push_raw_file_band", "hd_fill_raw",
-    "hd_realfft", "hd_zap_ranges", "hd_zapbirds", "hd_rednoise_blocks", "hd_rednoise", "hd_get_fft",
+    "hd_realfft", "hd_fft_prepare", "hd_zap_ranges", "hd_zapbirds", "hd_rednoise_blocks", "hd_rednoise", "hd_get_fft",
     "hd_bary_diffbins", "hd_plan_set_bary", "hd_plan_data_end", "hd_run_dedisp_multi", "hd_plan_launch_passes", "hd_sp_prune",
     "hd_prefetch_raw_file", "hd_prefetch_raw_file_band", "hd_prefetch_fill", "hd_swap_raw",
 ]
@@ -166,6 +166,7 @@ def load():
         "hd_series_fill": (ctypes.c_int, [vp, i64, ctypes.c_float]),
         "hd_rfifind_stats": (ctypes.c_int, [vp, i32, f32p, f32p, f32p]),
         "hd_realfft": (ctypes.c_int, [vp]),
+        "hd_fft_prepare": (ctypes.c_int, [vp]),
         "hd_zap_ranges": (ctypes.c_int, [P(ctypes.c_double), P(ctypes.c_double), i32, i64, P(ctypes.c_int32), i32,
                                          P(ctypes.c_int32)]),
         "hd_zapbirds": (ctypes.c_int, [vp, P(ctypes.c_double), P(ctypes.c_double), i32]),

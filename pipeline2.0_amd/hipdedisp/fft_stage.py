@@ -89,6 +89,12 @@ def rednoise_blocks(numbins, T, startwidth=RED_STARTWIDTH, endwidth=RED_ENDWIDTH
     return out
 
 
+def prepare(plan):
+    """hd_fft_prepare: the hipFFT plan + spectra buffer of the plan's series geometry built
+    now (rocFFT's kernel builds, seconds per new size), so a later realfft only transforms."""
+    plan.eng._chk(plan.eng._L.hd_fft_prepare(plan._p), "fft prepare")
+
+
 def realfft(plan):
     plan.eng._chk(plan.eng._L.hd_realfft(plan._p), "realfft")
 

@@ -37,7 +37,7 @@ class DedispJob:
     """The part of obs_info (PALFA2_presto_search.py:231-294) the dedispersion stage uses."""
 
     def __init__(self, filenms, resultsdir=".", tmpdir_base=None, device=0, opts=None,
-                 use_subbands=True, keep_subbands=False, backend=None, voverc=0.0, bary_table=None):
+                 use_subbands=True, keep_subbands=False, backend=None, voverc=0.0, bary_table=None, workdir=None):
         self.filenms = list(filenms)
         self.filenmstr = " ".join(self.filenms)
         self.outputdir = resultsdir
@@ -81,7 +81,9 @@ class DedispJob:
         self.ddplans = P.ddplans_for(self.backend)
         self.tempdir = tempfile.mkdtemp(suffix="_tmp", prefix=self.basefilenm,
                                         dir=tmpdir_base or ("/dev/shm" if os.path.isdir("/dev/shm") else None))
-        self.workdir = os.getcwd()
+        # where the reference runs (search_job chdirs there, :416): the per-pass .subout /
+        # .prepout logs go here
+        self.workdir = workdir or os.getcwd()
         # without subbands prepsubband dedisperses the channels themselves (nsub = nchan
         # [PRESTO-ext]) and no .sub int16 file is written, so they stay float32 (:522-529)
         self.opts = opts or (Opts() if use_subbands else Opts(sub_dtype=1))
@@ -166,6 +168,36 @@ def pass_params(job, ddplan, passnum):
                       ds=ddplan.sub_downsamp, numout=numout)
 
 
+def command_lines(job, ddplan, passnum, maskfilenm, tempdir):
+    """The two prepsubband command strings of the pass (PALFA2_presto_search.py:506-509,
+    514-518) -- or the one of :522-527 without subbands -- as the reference formats them."""
+    numout = P.choose_N(job.orig_N / ddplan.downsamp)
+    lodm = ddplan.lodm + passnum * ddplan.sub_dmstep
+    flag = "-psrfits"
+    if not job.use_subbands:
+        return ["prepsubband -mask %s -lodm %.2f -dmstep %.2f -numdms %d -downsamp %d -numout %d -o %s/%s %s"
+                % (maskfilenm, lodm, ddplan.dmstep, ddplan.dmsperpass, ddplan.dd_downsamp * ddplan.sub_downsamp,
+                   numout, tempdir, job.basefilenm, job.filenmstr)]
+    subbasenm = "%s_DM%s" % (job.basefilenm, ddplan.subdmlist[passnum])
+    return ["prepsubband %s -sub -subdm %s -downsamp %d -nsub %d -mask %s -o %s/subbands/%s %s"
+            % (flag, ddplan.subdmlist[passnum], ddplan.sub_downsamp, ddplan.numsub, maskfilenm, tempdir,
+               job.basefilenm, job.filenmstr),
+            "prepsubband -lodm %.2f -dmstep %.2f -numdms %d -downsamp %d -nsub %d -numout %d -o %s/%s "
+            "%s/subbands/%s.sub[0-9]*" % (lodm, ddplan.dmstep, ddplan.dmsperpass, ddplan.dd_downsamp, ddplan.numsub,
+                                          numout, tempdir, job.basefilenm, tempdir, subbasenm)]
+
+
+def _write_log(path, cmd, lines):
+    """The per-pass stdout capture the reference keeps (<subbasenm>.subout / .prepout,
+    :511,520, in the working directory): the command it stands for, then what ran."""
+    from . import _lib
+    with open(path, "w") as f:
+        f.write("'%s'\n\n" % cmd)
+        f.write("hipdedisp %s (libhipdedisp, MI355X gfx950)\n" % _lib.load().hd_version().decode())
+        for ln in lines:
+            f.write(ln + "\n")
+
+
 def _single_pulse(job, plan, ddplan, passnum, tempdir, sp):
     """:539-546 for the pass's DMs on the device-resident series (hipdedisp.single_pulse):
     <base>_DM<dm>.singlepulse in sp['workdir'] (or tempdir); adds to job.singlepulse_time."""
@@ -214,6 +246,14 @@ def run_pass(job, ddplan, passnum, maskfilenm, tempdir, single_pulse=None, fft=N
         info = job.info_template(pp.nsub, plan.sub_lofreq, plan.sub_chanwid, plan.sub_dt, series=True)
         write_dats_device(plan, os.path.join(tempdir, job.basefilenm), ddplan.dmlist[passnum], info, plan.data_end())
         t_dd = time.time() - t0
+        ms_sub, ms_dd = plan.last_ms()
+        cmds = command_lines(job, ddplan, passnum, maskfilenm, tempdir)
+        _write_log(os.path.join(job.workdir, subbasenm + ".subout"), cmds[0],
+                   ["stage 1: %d subbands x %d samples (downsamp %d, subDM %s), %.3f ms on the device, %.3f s wall"
+                    % (pp.nsub, plan.nds, pp.ds, ddplan.subdmlist[passnum], ms_sub, t_sub)])
+        _write_log(os.path.join(job.workdir, subbasenm + ".prepout"), cmds[1],
+                   ["stage 2: %d DMs x %d samples (%s), %.3f ms on the device, %.3f s wall with the .dat writes"
+                    % (pp.numdms, plan.numout, plan.kernel(), ms_dd, t_dd)])
         if single_pulse is not None:
             _single_pulse(job, plan, ddplan, passnum, tempdir, single_pulse)
         if fft is not None:
@@ -251,10 +291,28 @@ def _run_pass_nosub(job, ddplan, passnum, maskfilenm, tempdir, single_pulse=None
     return 0.0, t_dd
 
 
+def prepare_fft(job):
+    """The FFT stage's hipFFT plans, one per DDplan stage's series geometry, built before the
+    passes (hd_fft_prepare): rocFFT's kernel builds stay out of job.FFT_time."""
+    from .fft_stage import prepare
+    eng = job.open_engine()
+    for ddplan in job.ddplans:
+        if ddplan.numpasses < 1:
+            continue
+        p = eng.plan(pass_params(job, ddplan, 0))
+        try:
+            if p.numout >= 4 and p.numout % 2 == 0:
+                prepare(p)
+        finally:
+            p.destroy()
+
+
 def dedisperse_job(job, maskfilenm=None, per_dm=None, remove_dat=False, single_pulse=None, fft=None):
     """The loop of PALFA2_presto_search.py:494-537: every pass of every DDplan stage (with
     the device single-pulse search of :539-546 when single_pulse is given), then
     `per_dm(job, dmstr, basenm)` for each new DM (the reference's downstream tools)."""
+    if fft is not None:
+        prepare_fft(job)
     dmstrs = []
     for ddplan in job.ddplans:
         for passnum in range(ddplan.numpasses):

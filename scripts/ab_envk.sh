@@ -13,6 +13,7 @@ for e in "$@"; do
       --no-cpu --e2e-beams 0 --sp-beams 0 --fft-beams 0 --rfi-beams 0 --stream-beams 0 > $d.log 2>&1 \
       || { echo "setting [$e] failed"; exit 1; }
   python3 scripts/kstats.py "$(find $d -name '*.db' | head -1)" $d.csv
-  echo "== [$e] $(tail -1 $d.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print("%.2f ms/step" % d["ms_per_step"])')"
+  s=$(python3 scripts/benchline.py $d.log ms) || { echo "no bench line [$e]"; exit 1; }
+  echo "== [$e] $s"
   python3 scripts/kstats_grep.py $d.csv ${WORDS:-fix8}
 done

@@ -64,3 +64,42 @@ def fft_candidates(series, n=10, numharm=(1, 2, 4, 8)):
             top = np.argsort(s)[::-1][:n]
             out.extend((d, h, int(b), round(float(s[b]), 4)) for b in sorted(top))
     return out
+
+
+HARM_THRESH = {1: 20.0, 2: 24.0, 4: 32.0, 8: 48.0}
+
+
+def spectrum_candidates(F, thresh=HARM_THRESH):
+    """accelsearch's zero-acceleration candidates from de-reddened packed spectra
+    [ndm][nb] (complex, the rednoise output: unit mean noise power): per DM and harmonic
+    count h, every fundamental bin b >= 1 whose incoherently summed power
+    sum_{k=1..h} |F[k*b]|^2 exceeds thresh[h]; {(dm, h, b): summed power}."""
+    out = {}
+    F = np.asarray(F)
+    for d in range(F.shape[0]):
+        p = F[d].real.astype(np.float64) ** 2 + F[d].imag.astype(np.float64) ** 2
+        p[0] = 0.0
+        for h, thr in thresh.items():
+            m = len(p) // h
+            s = np.zeros(m)
+            for k in range(1, h + 1):
+                s += p[: m * k: k][:m]
+            for b in np.nonzero(s > thr)[0]:
+                if b >= 1:
+                    out[(d, h, int(b))] = float(s[b])
+    return out
+
+
+def candidate_mismatch(a, b, thresh=HARM_THRESH, rel=1e-3):
+    """Entries of one list missing from the other that are NOT explained by a power within
+    `rel` of the threshold (float32 vs float64 FFT rounding can move such a bin across it),
+    plus entries in both whose powers differ by more than `rel`."""
+    bad = []
+    for key in set(a) ^ set(b):
+        v = a.get(key, b.get(key))
+        if v > thresh[key[1]] * (1.0 + rel):
+            bad.append((key, a.get(key), b.get(key)))
+    for key in set(a) & set(b):
+        if abs(a[key] - b[key]) > rel * max(a[key], b[key]):
+            bad.append((key, a[key], b[key]))
+    return sorted(bad)

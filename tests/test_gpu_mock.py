@@ -48,7 +48,8 @@ def test_gap_zero_filled_on_device(engine, tmp_path):
 
 def test_dedisp_job_on_mock_halves(engine, tmp_path):
     paths, _ = halves(tmp_path, 4, True, nrows=23, nsblk=512, seed=5)
-    job = DedispJob(paths, resultsdir=str(tmp_path), tmpdir_base=str(tmp_path), device=0, backend="pdev")
+    job = DedispJob(paths, resultsdir=str(tmp_path), tmpdir_base=str(tmp_path), device=0, backend="pdev",
+                    workdir=str(tmp_path))
     d = copy.copy(job.ddplans[0])
     d.numpasses = 1
     job.ddplans = [d]

@@ -646,7 +646,7 @@ def test_search_stage_dedisperse_job(engine, tmp_path, use_subbands):
     fn = str(tmp_path / "beam.fits")
     psrfits.write_psrfits(fn, spectra, obs)
     job = DedispJob([fn], resultsdir=str(tmp_path), tmpdir_base=str(tmp_path), device=0,
-                    use_subbands=use_subbands, backend="pdev")
+                    use_subbands=use_subbands, backend="pdev", workdir=str(tmp_path))
     ddplans = []
     for st in (0, 3):
         d = copy.copy(job.ddplans[st])
@@ -660,6 +660,16 @@ def test_search_stage_dedisperse_job(engine, tmp_path, use_subbands):
                                 fft=dict(zaplist=None, baryv=0.0, write=True))
         assert len(dmstrs) == sum(d.dmsperpass for d in ddplans)
         assert job.singlepulse_time > 0 and job.FFT_time > 0
+        from hipdedisp.search_stage import command_lines
+        for d in ddplans:                       # the per-pass stdout logs of :511,520
+            sub = tmp_path / ("%s_DM%s.subout" % (job.basefilenm, d.subdmlist[0]))
+            prep = tmp_path / ("%s_DM%s.prepout" % (job.basefilenm, d.subdmlist[0]))
+            if use_subbands:
+                cmds = command_lines(job, d, 0, None, job.tempdir)
+                assert sub.read_text().startswith("'%s'" % cmds[0]) and "-sub -subdm" in cmds[0]
+                assert prep.read_text().startswith("'%s'" % cmds[1]) and "-numout" in cmds[1]
+            else:
+                assert not sub.exists() and not prep.exists()
         sobs = job.specinfo.obs_params(0.0)
         for d in ddplans:
             pp = pass_params(job, d, 0)
@@ -835,7 +845,7 @@ def test_reference_pass_loop_control_flow(engine, tmp_path, fold_rawdata):
     psrfits.write_psrfits(fn, host_spectra(obs, palfa_synth()), obs)
     workdir = tmp_path / "work"
     (workdir / "subbands").mkdir(parents=True)
-    job = DedispJob([fn], resultsdir=str(workdir), tmpdir_base=str(tmp_path), device=0,
+    job = DedispJob([fn], resultsdir=str(workdir), tmpdir_base=str(tmp_path), device=0, workdir=str(tmp_path),
                     backend="pdev", keep_subbands=not fold_rawdata)
     try:
         d = copy.copy(job.ddplans[0])

@@ -110,3 +110,64 @@ def test_time_slices_union_equals_whole_beam(engine, world):
                 p.destroy()
         for e in engs:
             e.close()
+
+
+def _hip():
+    """The HIP runtime libhipdedisp.so is linked against (already loaded: same handle)."""
+    import ctypes
+    h = ctypes.CDLL("libamdhip64.so.7")
+    h.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+    h.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    h.hipMemset.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t]
+    h.hipFree.argtypes = [ctypes.c_void_p]
+    return h
+
+
+def test_clip_stats_device_pointer_path(engine):
+    """hd_clip_stats / hd_clip_set_stats with a DEVICE table (the RCCL path of bench.py
+    --mode slices, where the all-reduce runs in HBM): every rank's rows and the finished clip
+    state bit-identical to the host-table path of the same ranks."""
+    import ctypes
+    world = 2
+    obs = palfa_obs(N=(1 << 18) + 2 * 30720 + 99, nbits=8, nsblk=2048)
+    synth = spiky()
+    pts = 16384
+    mask, pad = synth_mask(obs, synth, pts, frac=0.03)
+    ts = S.TimeSlices(obs, small_plan(), world)
+    hip = _hip()
+    nbytes = ts.stats_table().nbytes
+    dtab = ctypes.c_void_p()
+    assert hip.hipMalloc(ctypes.byref(dtab), nbytes) == 0
+    engs = []
+    try:
+        host_sum = ts.stats_table()
+        dev_sum = ts.stats_table()
+        for r in range(world):
+            e = Engine(0)
+            engs.append(e)
+            t0, own, nloc = ts.slice(r)
+            e.set_obs(ts.local_obs(r), Opts())
+            e.set_slice(t0, obs.N)
+            e.synth_device(synth)
+            e.set_mask(mask, pts, pad)
+            mine = ts.stats_table()
+            ts.contribute_clip_stats(e, r, mine)                     # host table
+            assert hip.hipMemset(dtab, 0, nbytes) == 0
+            ts.contribute_clip_stats(e, r, int(dtab.value))          # device table
+            back = ts.stats_table()
+            assert hip.hipMemcpy(back.ctypes.data, dtab, nbytes, 2) == 0      # hipMemcpyDeviceToHost
+            assert np.array_equal(back.view(np.uint64), mine.view(np.uint64)), r
+            host_sum += mine
+            dev_sum += back
+        assert hip.hipMemcpy(dtab, dev_sum.ctypes.data, nbytes, 1) == 0      # hipMemcpyHostToDevice
+        for r, e in enumerate(engs):
+            e.clip_set_stats(int(dtab.value))
+            dpad, dclip, dzap, dn = e.get_clean()
+            e.clip_set_stats(host_sum)
+            hpad, hclip, hzap, hn = e.get_clean()
+            assert dn == hn and np.array_equal(dclip, hclip) and np.array_equal(dzap, hzap)
+            assert np.array_equal(dpad.view(np.uint32), hpad.view(np.uint32)), r
+    finally:
+        for e in engs:
+            e.close()
+        hip.hipFree(dtab)

@@ -88,7 +88,7 @@ def test_rejects(tmp_path):
 
 def test_dedisp_job_uses_merged_beam(tmp_path):
     paths, _ = halves(tmp_path, 4, True)
-    job = DedispJob(paths, resultsdir=str(tmp_path), tmpdir_base=str(tmp_path), backend="pdev")
+    job = DedispJob(paths, resultsdir=str(tmp_path), tmpdir_base=str(tmp_path), backend="pdev", workdir=str(tmp_path))
     try:
         assert isinstance(job.specinfo, mock.MockBeam)
         assert job.basefilenm == "p2030.20120314.G34.5+0.1.b3.00123"
