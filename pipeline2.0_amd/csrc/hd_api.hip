@@ -224,9 +224,10 @@ struct hd_plan {
         int32_t umax = 0;               // [3] only: largest pattern count of a subband pair
         int32_t* d_omin = nullptr;      // [3]: the pair table (kPairTab ints per y-block and pair)
         int32_t* d_boff = nullptr;
-    } wide[5];                      // [2]: k_stage2_ring (16 waves, LDS-DMA staging ring);
+    } wide[6];                      // [2]: k_stage2_ring (16 waves, LDS-DMA staging ring);
                                     // [3]: k_stage2_pair (the ring over subband-pair partials),
-                                    // [4]: the same with two pairs per chunk (half the chunks)
+                                    // [4]: the same with two pairs per chunk (half the chunks),
+                                    // [5]: k_stage2_rw (register windows, one copy, 2 WGs per CU)
     bool sub_nonneg = false;        // every subband value >= 0 (known on the host with sub_bound)
     int32_t sub_bound = -1;         // bound on |subband| known on the host (-1: none), set when
                                     // the subbands are formed or uploaded (pair variant gate)
@@ -1592,6 +1593,105 @@ static void pair_tables(hd_plan* p, bool i16, int ppc, hd_plan::Wide& w, std::ve
     w.umax = umax;
 }
 
+// Tables of the register-window pair kernel (k_stage2_rw): y-blocks of 8 waves x Q DMs, two
+// pairs per chunk, 768-sample tiles (lane l: samples 12l .. 12l+11).  Per (y-block, pair) the
+// pair kernel's {base0, b1, U, k1[U]} over the block's DMs.  Per (y-block, chunk) one block of
+// kRwBlock ints: [pair k][DM slot] the jump code 12 + 100 * shift of the DM's 12 values in
+// its wave's current window, then [pair k][wave] {reload mask, window byte offsets}: a wave
+// loads a window (24 elements per lane, 8-byte aligned) at its first DM and again at each DM
+// of the mask whose pattern buffer or offset leaves the current one (> 10 elements on).
+// Window offsets are LDS bytes from the expanded area: buffer ((chunk & 1) * 2 + k) x umax
+// patterns x ws elements; element i of pattern u = P_u[i], tile sample 0 at offset base0.
+static void rw_tables(hd_plan* p, bool i16, hd_plan::Wide& w, std::vector<int32_t>& ptab, std::vector<int32_t>& blk)
+{
+    w = hd_plan::Wide{};
+    constexpr int NW = hd::kRwWaves, PPC = 2;
+    const int nsub = p->pass.nsub, numdms = p->pass.numdms;
+    if (!i16 || nsub % (4 * PPC) || numdms < 1) return;
+    int nyb = (numdms + 5 * NW - 1) / (5 * NW);
+    const int per = (numdms + nyb - 1) / nyb;
+    const int Q = (per + NW - 1) / NW;                    // 1..5
+    const int dpb = NW * Q;
+    nyb = (numdms + dpb - 1) / dpb;
+    const int npair = nsub / 2, nchunk = npair / PPC;
+    if (PPC * dpb + PPC * NW * 4 > hd::kRwBlock) return;
+    auto dmof = [&](int yb, int k) { return std::min(yb * dpb + k, numdms - 1); };
+    ptab.assign((size_t)nyb * npair * hd::kPairTab, 0);
+    std::vector<std::vector<int32_t>> rs((size_t)nyb * npair);
+    int32_t span0 = 0, k1max = 0;
+    int umax = 0;
+    for (int yb = 0; yb < nyb; yb++)
+        for (int c = 0; c < npair; c++) {
+            int32_t lo = INT32_MAX, hi = INT32_MIN;
+            std::vector<int32_t>& r = rs[(size_t)yb * npair + c];
+            for (int k = 0; k < dpb; k++) {
+                const int dm = dmof(yb, k);
+                const int32_t o0 = p->off[(size_t)dm * nsub + 2 * c], o1 = p->off[(size_t)dm * nsub + 2 * c + 1];
+                lo = std::min(lo, o0);
+                hi = std::max(hi, o0);
+                r.push_back(o1 - o0);
+            }
+            std::sort(r.begin(), r.end());
+            r.erase(std::unique(r.begin(), r.end()), r.end());
+            if ((int)r.size() > hd::kPairUMax) return;
+            const int32_t b1 = lo + r[0];
+            int32_t* t = &ptab[((size_t)yb * npair + c) * hd::kPairTab];
+            t[0] = lo;
+            t[1] = b1;
+            t[2] = (int32_t)r.size();
+            for (size_t u = 0; u < r.size(); u++) {
+                t[3 + u] = r[u] - r[0] + (b1 & 1);
+                k1max = std::max(k1max, t[3 + u]);
+            }
+            span0 = std::max(span0, hi - lo);
+            umax = std::max(umax, (int)r.size());
+        }
+    // a lane's window reaches element (o & ~3) + 12 * 63 + 23 <= span0 + 779; 8-element items
+    const int ws = (int)round_up((size_t)span0 + 780, 8);
+    // the expand's 8-element loads read the staging window up to element k1 + ws + 1
+    const int npw = (int)((((size_t)ws + 16 + k1max) * 2 + 1023) / 1024);
+    if (hd::stage2_rw_lds_bytes(ws, npw, nsub, umax) > 80 * 1024) return;
+    blk.assign((size_t)nyb * nchunk * hd::kRwBlock, 0);
+    for (int yb = 0; yb < nyb; yb++)
+        for (int ch = 0; ch < nchunk; ch++) {
+            int32_t* b = &blk[((size_t)yb * nchunk + ch) * hd::kRwBlock];
+            for (int k = 0; k < PPC; k++) {
+                const int c = PPC * ch + k;
+                const std::vector<int32_t>& r = rs[(size_t)yb * npair + c];
+                const int32_t base0 = ptab[((size_t)yb * npair + c) * hd::kPairTab];
+                const int buf = (ch & 1) * PPC + k;
+                for (int wv = 0; wv < NW; wv++) {
+                    int32_t* rec = b + PPC * dpb + (k * NW + wv) * 4;
+                    int64_t wb = -1;
+                    int nwin = 0;
+                    for (int q = 0; q < Q; q++) {
+                        const int dm = dmof(yb, wv * Q + q);
+                        const int32_t o0 = p->off[(size_t)dm * nsub + 2 * c], o1 = p->off[(size_t)dm * nsub + 2 * c + 1];
+                        const int u = (int)(std::lower_bound(r.begin(), r.end(), o1 - o0) - r.begin());
+                        const int64_t a = 2 * ((int64_t)(buf * umax + u) * ws + (o0 - base0));
+                        if (q == 0 || a < wb || a - wb > 20) {
+                            if (nwin == hd::kRwMaxWin) return;    // (a wave spanning more windows: not this kernel)
+                            wb = a & ~(int64_t)7;
+                            if (q > 0) rec[0] |= 1 << q;
+                            rec[1 + nwin++] = (int32_t)wb;
+                        }
+                        b[k * dpb + wv * Q + q] = 12 + 100 * (int32_t)((a - wb) / 2);
+                    }
+                }
+            }
+        }
+    w.ok = true;
+    w.q = Q;
+    w.r = 3;                       // 256 * r = the 768-sample tile (ntiles / partial sums)
+    w.nw = NW;
+    w.dpb = dpb;
+    w.ws = ws;
+    w.sc = 2;
+    w.npw = npw;
+    w.nbp = 1;
+    w.umax = umax;
+}
+
 // Subbands formed by stage 1 on the device are >= 0 when the samples are unsigned integers
 // (<= 8 bits, no calibration) and every pad value is >= 0: mask pads from the .stats file
 // (h_padvals) and clip_times' running channel means (means of unsigned samples).
@@ -1680,15 +1780,16 @@ extern "C" int hd_plan_create(hd_ctx* c, const hd_pass* ps, hd_plan** out)
                 boff[((size_t)yb * nsub + s) * p->dpb + k] = ((sl * 4 + (o2 & 3)) * p->wstride + (o2 & ~3)) * 2;
             }
 
-    std::vector<int32_t> womin[5], wboff[5];
+    std::vector<int32_t> womin[6], wboff[6];
     for (int k = 0; k < 3; k++)
         wide_tables(p, k == 1 ? 8 : 16, k != 1, c->opts.sub_dtype == HD_SUB_I16, p->wide[k], womin[k], wboff[k], k == 2);
     pair_tables(p, c->opts.sub_dtype == HD_SUB_I16, 1, p->wide[3], womin[3], wboff[3]);
     pair_tables(p, c->opts.sub_dtype == HD_SUB_I16, 2, p->wide[4], womin[4], wboff[4]);
+    rw_tables(p, c->opts.sub_dtype == HD_SUB_I16, p->wide[5], womin[5], wboff[5]);
 
     int rc = HD_OK;
     hipError_t e = hipSetDevice(c->device);
-    for (int k = 0; k < 5 && e == hipSuccess; k++) {
+    for (int k = 0; k < 6 && e == hipSuccess; k++) {
         hd_plan::Wide& w = p->wide[k];
         if (!w.ok) continue;
         e = hipMalloc(&w.d_omin, sizeof(int32_t) * womin[k].size());
@@ -1756,11 +1857,11 @@ extern "C" int hd_plan_set_variant(hd_plan* p, int32_t v)
     p->probe = (v >> 16) & 0xFF;     // profiling only (results invalid): see hipdedisp.h
     p->pair_persist = (v >> 24) & 0x3;   // pair kernel: 0/1 persistent workgroups (default), 2 one per tile
     v &= 0xFF;
-    if (v < 0 || v > 7 || v1 > 3) return fail(p->ctx, HD_E_INVAL, "variant must be (s1<<8)|s2 with s1 in 0..3, s2 in 0..7");
+    if (v < 0 || v > 8 || v1 > 3) return fail(p->ctx, HD_E_INVAL, "variant must be (s1<<8)|s2 with s1 in 0..3, s2 in 0..8");
     p->s1_variant = v1;
     if (v == 2 && !p->lds_ok) return fail(p->ctx, HD_E_INVAL, "LDS variant unavailable for this plan (needs int16 subbands and a window that fits 64 KiB)");
     if ((v == 3 && !p->wide[0].ok) || (v == 4 && !p->wide[1].ok) || (v == 5 && !p->wide[2].ok) ||
-        (v == 6 && !p->wide[3].ok) || (v == 7 && !p->wide[4].ok))
+        (v == 6 && !p->wide[3].ok) || (v == 7 && !p->wide[4].ok) || (v == 8 && !p->wide[5].ok))
         return fail(p->ctx, HD_E_INVAL, "wide-tile variant unavailable for this plan (needs int16 subbands and a window that fits LDS)");
     p->variant = v;
     return HD_OK;
@@ -3087,7 +3188,8 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
     // pair partials need |sub[s0] + sub[s1]| <= 32767 (packed int16), known on the host
     const bool pair_bound = p->sub_bound >= 0 && 2 * p->sub_bound <= 32767;
     const bool pair_ok = p->wide[3].ok && pair_bound;
-    if ((p->variant == 6 && !pair_ok) || (p->variant == 7 && !(p->wide[4].ok && pair_bound)))
+    if ((p->variant == 6 && !pair_ok) || (p->variant == 7 && !(p->wide[4].ok && pair_bound)) ||
+        (p->variant == 8 && !(p->wide[5].ok && pair_bound)))
         return fail(c, HD_E_INVAL, "hd_run_dedisp: pair variant needs 2 * max|subband| <= 32767 known on the host "
                     "(bound %d)", (int)p->sub_bound);
     int wk = -1;                       // wide variant in use (index into p->wide), or -1
@@ -3101,7 +3203,10 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         // stage (profiles/r02_stage2_variants.txt: 1.10 / 0.56 / 0.42 / 0.27 / 0.22 / 0.17 ms
         // vs the ring's 1.42 / 0.60 / 0.53 / 0.33 / 0.27 / 0.20)
         const bool pair2_auto = p->wide[4].ok && pair_bound;
-        wk = pair2_auto ? 4 : pair_auto ? 3 : p->wide[2].ok ? 2 : p->wide[0].ok ? 0 : (p->wide[1].ok ? 1 : -1);
+        // register windows over one-copy pair partials, two workgroups per CU: first choice
+        // wherever its tables apply (a wave's DMs within 3 windows of a pair)
+        const bool rw_auto = p->wide[5].ok && pair_bound;
+        wk = rw_auto ? 5 : pair2_auto ? 4 : pair_auto ? 3 : p->wide[2].ok ? 2 : p->wide[0].ok ? 0 : (p->wide[1].ok ? 1 : -1);
     }
     const bool use_wide = wk >= 0;
     const bool use_lds = !use_wide && (p->variant == 2 || (p->variant == 0 && p->lds_ok));
@@ -3157,11 +3262,17 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         if (wk == 0) HIPCHK(c, hd::launch_stage2_wide(a, w.q, w.r, w.nw, st));
         else if (wk == 1) HIPCHK(c, hd::launch_stage2_wide2(a, w.q, w.r, w.nw, st));
         else if (wk == 2) HIPCHK(c, hd::launch_stage2_ring(a, w.q, w.r, st));
-        else HIPCHK(c, hd::launch_stage2_pair(a, w.q, w.r, wk == 4 ? 2 : 1, st));
+        else if (wk == 5) {
+            hd::S2Multi m{};
+            m.npass = 1;
+            m.p[0] = hd::stage2_pass_of(a);
+            HIPCHK(c, hd::launch_stage2_rw_multi(a, m, w.q, st));
+        } else HIPCHK(c, hd::launch_stage2_pair(a, w.q, w.r, wk == 4 ? 2 : 1, st));
         // the names rocprofv3 prints (template arguments as the compiler spells them)
         if (wk == 0) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_wide<%d, %d, %d>", w.q, w.r, w.sc);
         else if (wk == 1) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_wide2<%d, %d, %d>", w.q, w.r, w.sc);
         else if (wk == 2) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_ring<%d, %d>", w.q, w.r);
+        else if (wk == 5) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_rw<%d>", w.q);
         else snprintf(p->s2name, sizeof(p->s2name), "k_stage2_pair<%d, %d, %d, %s>", w.q, w.r, wk == 4 ? 2 : 1,
                       a.nonneg && !(p->probe & 64) ? "true" : "false");
     } else if (use_lds) {
@@ -3198,16 +3309,24 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
 // A plan joins a multi-pass launch when it takes the two-pairs-per-chunk pair kernel (auto or
 // variant 7) on the topocentric grid; plans with the same kernel and geometry (one DDplan
 // stage) share a launch of at most kS2MaxPass passes, the rest run one by one.
-static bool dedisp_multi_ok(const hd_plan* p)
+// The kernel a plan takes in a shared launch: 5 (k_stage2_rw: auto or variant 8), 4 (the
+// two-pairs-per-chunk pair kernel: auto without rw tables, or variant 7), or -1 (alone).
+static int dedisp_multi_kernel(const hd_plan* p)
 {
     const bool pair_bound = p->sub_bound >= 0 && 2 * p->sub_bound <= 32767;
-    return p->sub_valid && (p->variant == 0 || p->variant == 7) && p->wide[4].ok && pair_bound && p->nbseg == 0 &&
-           p->pair_persist != 2;
+    if (!p->sub_valid || !pair_bound || p->nbseg != 0 || p->pair_persist == 2) return -1;
+    if ((p->variant == 0 || p->variant == 8) && p->wide[5].ok) return 5;
+    if ((p->variant == 0 || p->variant == 7) && p->wide[4].ok) return 4;
+    return -1;
 }
+
+static bool dedisp_multi_ok(const hd_plan* p) { return dedisp_multi_kernel(p) >= 0; }
 
 static bool dedisp_same_group(const hd_plan* a, const hd_plan* b)
 {
-    const hd_plan::Wide &x = a->wide[4], &y = b->wide[4];
+    const int ka = dedisp_multi_kernel(a);
+    if (ka != dedisp_multi_kernel(b)) return false;
+    const hd_plan::Wide &x = a->wide[ka], &y = b->wide[ka];
     return a->ctx == b->ctx && x.q == y.q && x.r == y.r && x.dpb == y.dpb && a->pass.numdms == b->pass.numdms &&
            a->pass.nsub == b->pass.nsub && a->nds == b->nds && a->nvalid == b->nvalid && a->numout == b->numout &&
            a->out_stride == b->out_stride && a->sub_nonneg == b->sub_nonneg && a->probe == b->probe;
@@ -3216,7 +3335,8 @@ static bool dedisp_same_group(const hd_plan* a, const hd_plan* b)
 static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
 {
     hd_plan* p0 = g[0];
-    const hd_plan::Wide& w0 = p0->wide[4];
+    const int wk = dedisp_multi_kernel(p0);
+    const hd_plan::Wide& w0 = p0->wide[wk];
     // hd_set_streams(2 or 3): the shared launch runs on stream2, so the main stream goes on
     // to the next DDplan stage's stage 1 (other plans' subbands) beside it
     const bool alt = c->dual;
@@ -3291,7 +3411,7 @@ static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
     m.npass = n;
     for (int i = 0; i < n; i++) {
         const hd_plan* p = g[i];
-        const hd_plan::Wide& w = p->wide[4];
+        const hd_plan::Wide& w = p->wide[wk];
         hd::S2Pass& q = m.p[i];
         q.sub = p->d_sub;
         q.ptab = w.d_omin;
@@ -3306,7 +3426,8 @@ static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
         q.umax = w.umax;
     }
     HIPCHK(c, hipEventRecord(p0->ev[2], st));
-    HIPCHK(c, hd::launch_stage2_pair_multi(a, m, w0.q, w0.r, 2, st));
+    if (wk == 5) HIPCHK(c, hd::launch_stage2_rw_multi(a, m, w0.q, st));
+    else HIPCHK(c, hd::launch_stage2_pair_multi(a, m, w0.q, w0.r, 2, st));
     if (pad)
         for (int i = 0; i < n; i++)
             HIPCHK(c, hd::launch_pad(g[i]->d_out, g[i]->out_stride, g[i]->pass.numdms, g[i]->nds, g[i]->numout,
@@ -3318,8 +3439,9 @@ static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
         p->ran_dd = true;
         p->dd_stream = st;
         p->s2passes = i == 0 ? n : 0;
-        snprintf(p->s2name, sizeof(p->s2name), "k_stage2_pair<%d, %d, 2, %s>", w0.q, w0.r,
-                 a.nonneg && !(a.probe & 64) ? "true" : "false");
+        if (wk == 5) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_rw<%d>", w0.q);
+        else snprintf(p->s2name, sizeof(p->s2name), "k_stage2_pair<%d, %d, 2, %s>", w0.q, w0.r,
+                      a.nonneg && !(a.probe & 64) ? "true" : "false");
     }
     if (alt) {
         HIPCHK(c, hipEventRecord(c->ev_join, st));

@@ -1171,6 +1171,441 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, S2Multi m)
 
 }
 
+
+// ---- register-window pair kernel ---------------------------------------------------------
+// acc[i] += element (k + i) of the lane's 24-element window w (12 dwords, 2 int16 each),
+// i = 0..11, for a wave-uniform shift k = 0..10: a jump into one of 11 straight-line cases
+// of 12 SDWA adds (word selects fixed per case), so the accumulators and the window stay in
+// fixed registers and nothing is moved.  The words are sign-extended (sext): the partials
+// are int16 (|P| <= 32767 by the host's bound), negative for signed subbands.  jc = the case's byte offset from Lpc: 12 + 100 * k
+// (the three instructions after s_getpc_b64 are 12 bytes; a case is 12 x 8-byte SDWA adds +
+// a 4-byte s_branch).  The host table carries jc; the kernel clamps k before it gets here.
+__device__ __forceinline__ void rw_add12(int (&A)[12], const uint32_t (&w)[12], uint32_t jc)
+{
+    asm volatile(
+        "s_getpc_b64 s[98:99]\n"
+        "Lpc_%=:\n\t"
+        "s_add_u32 s98, s98, %24\n\t"
+        "s_addc_u32 s99, s99, 0\n\t"
+        "s_setpc_b64 s[98:99]\n"
+        "L0_%=:\n\t"
+        "v_add_u32_sdwa %0, %0, sext(%12) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %1, %1, sext(%12) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %2, %2, sext(%13) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %3, %3, sext(%13) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %4, %4, sext(%14) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %5, %5, sext(%14) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %6, %6, sext(%15) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %7, %7, sext(%15) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %8, %8, sext(%16) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %9, %9, sext(%16) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %10, %10, sext(%17) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %11, %11, sext(%17) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "s_branch Lend_%=\n\t"
+        "L1_%=:\n\t"
+        "v_add_u32_sdwa %0, %0, sext(%12) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %1, %1, sext(%13) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %2, %2, sext(%13) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %3, %3, sext(%14) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %4, %4, sext(%14) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %5, %5, sext(%15) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %6, %6, sext(%15) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %7, %7, sext(%16) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %8, %8, sext(%16) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %9, %9, sext(%17) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %10, %10, sext(%17) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %11, %11, sext(%18) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "s_branch Lend_%=\n\t"
+        "L2_%=:\n\t"
+        "v_add_u32_sdwa %0, %0, sext(%13) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %1, %1, sext(%13) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %2, %2, sext(%14) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %3, %3, sext(%14) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %4, %4, sext(%15) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %5, %5, sext(%15) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %6, %6, sext(%16) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %7, %7, sext(%16) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %8, %8, sext(%17) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %9, %9, sext(%17) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %10, %10, sext(%18) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %11, %11, sext(%18) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "s_branch Lend_%=\n\t"
+        "L3_%=:\n\t"
+        "v_add_u32_sdwa %0, %0, sext(%13) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %1, %1, sext(%14) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %2, %2, sext(%14) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %3, %3, sext(%15) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %4, %4, sext(%15) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %5, %5, sext(%16) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %6, %6, sext(%16) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %7, %7, sext(%17) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %8, %8, sext(%17) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %9, %9, sext(%18) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %10, %10, sext(%18) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %11, %11, sext(%19) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "s_branch Lend_%=\n\t"
+        "L4_%=:\n\t"
+        "v_add_u32_sdwa %0, %0, sext(%14) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %1, %1, sext(%14) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %2, %2, sext(%15) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %3, %3, sext(%15) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %4, %4, sext(%16) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %5, %5, sext(%16) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %6, %6, sext(%17) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %7, %7, sext(%17) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %8, %8, sext(%18) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %9, %9, sext(%18) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %10, %10, sext(%19) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %11, %11, sext(%19) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "s_branch Lend_%=\n\t"
+        "L5_%=:\n\t"
+        "v_add_u32_sdwa %0, %0, sext(%14) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %1, %1, sext(%15) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %2, %2, sext(%15) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %3, %3, sext(%16) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %4, %4, sext(%16) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %5, %5, sext(%17) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %6, %6, sext(%17) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %7, %7, sext(%18) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %8, %8, sext(%18) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %9, %9, sext(%19) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %10, %10, sext(%19) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %11, %11, sext(%20) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "s_branch Lend_%=\n\t"
+        "L6_%=:\n\t"
+        "v_add_u32_sdwa %0, %0, sext(%15) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %1, %1, sext(%15) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %2, %2, sext(%16) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %3, %3, sext(%16) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %4, %4, sext(%17) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %5, %5, sext(%17) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %6, %6, sext(%18) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %7, %7, sext(%18) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %8, %8, sext(%19) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %9, %9, sext(%19) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %10, %10, sext(%20) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %11, %11, sext(%20) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "s_branch Lend_%=\n\t"
+        "L7_%=:\n\t"
+        "v_add_u32_sdwa %0, %0, sext(%15) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %1, %1, sext(%16) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %2, %2, sext(%16) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %3, %3, sext(%17) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %4, %4, sext(%17) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %5, %5, sext(%18) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %6, %6, sext(%18) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %7, %7, sext(%19) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %8, %8, sext(%19) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %9, %9, sext(%20) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %10, %10, sext(%20) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %11, %11, sext(%21) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "s_branch Lend_%=\n\t"
+        "L8_%=:\n\t"
+        "v_add_u32_sdwa %0, %0, sext(%16) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %1, %1, sext(%16) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %2, %2, sext(%17) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %3, %3, sext(%17) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %4, %4, sext(%18) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %5, %5, sext(%18) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %6, %6, sext(%19) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %7, %7, sext(%19) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %8, %8, sext(%20) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %9, %9, sext(%20) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %10, %10, sext(%21) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %11, %11, sext(%21) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "s_branch Lend_%=\n\t"
+        "L9_%=:\n\t"
+        "v_add_u32_sdwa %0, %0, sext(%16) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %1, %1, sext(%17) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %2, %2, sext(%17) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %3, %3, sext(%18) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %4, %4, sext(%18) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %5, %5, sext(%19) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %6, %6, sext(%19) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %7, %7, sext(%20) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %8, %8, sext(%20) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %9, %9, sext(%21) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %10, %10, sext(%21) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %11, %11, sext(%22) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "s_branch Lend_%=\n\t"
+        "L10_%=:\n\t"
+        "v_add_u32_sdwa %0, %0, sext(%17) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %1, %1, sext(%17) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %2, %2, sext(%18) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %3, %3, sext(%18) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %4, %4, sext(%19) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %5, %5, sext(%19) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %6, %6, sext(%20) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %7, %7, sext(%20) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %8, %8, sext(%21) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %9, %9, sext(%21) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_add_u32_sdwa %10, %10, sext(%22) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_add_u32_sdwa %11, %11, sext(%22) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "s_branch Lend_%=\n\t"
+        "Lend_%=:"
+        : "+v"(A[0]), "+v"(A[1]), "+v"(A[2]), "+v"(A[3]), "+v"(A[4]), "+v"(A[5]), "+v"(A[6]), "+v"(A[7]),
+          "+v"(A[8]), "+v"(A[9]), "+v"(A[10]), "+v"(A[11])
+        : "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]), "v"(w[6]), "v"(w[7]), "v"(w[8]),
+          "v"(w[9]), "v"(w[10]), "v"(w[11]), "s"(jc)
+        : "s98", "s99", "scc");
+}
+
+// Register-window pair kernel (k_stage2_rw).  The pair partials P_u of each subband pair are
+// formed once per tile in ONE copy (not four shifted ones), and each wave reads, per pair, a
+// 24-element window per lane that serves all of its Q DMs: lane l owns the 12 contiguous
+// output samples 12l .. 12l+11 of a 768-sample tile, so a DM whose pattern offset lies
+// within 10 elements of the window base takes its 12 values out of the lane's registers
+// (rw_add12: a jump to the case of its shift, 12 SDWA adds) instead of three LDS reads of its
+// own.  One window load (6 ds_read_b64) serves ~4 DMs; the expand writes a quarter of the
+// bytes.  8 waves x Q DMs per workgroup, <= 80 KiB of LDS and <= 128 VGPRs, so two
+// workgroups share a CU and one's barriers and DMA waits overlap the other's work.
+// Host tables (rw_tables): per (y-block, pair) {base0, b1, U, k1[U]} as the pair kernel;
+// per (y-block, chunk) a 256-int block DMA'd with the chunk: [pair k][DM] jump codes
+// 12 + 100 * shift, then [pair k][wave] {reload mask, window byte offsets (<= 3)}.
+constexpr int kRwNW = 8, kRwNS = 4, kRwPPC = 2, kRwT = 768, kRwBlk = 256;
+
+__device__ __forceinline__ void rw_load_win(uint32_t (&w)[12], uint32_t addr)
+{
+    uint64_t b[6];
+#pragma unroll
+    for (int j = 0; j < 6; j++) asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(b[j]) : "v"(addr), "i"(8 * j));
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]), "+v"(b[4]), "+v"(b[5]));
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+        w[2 * j] = (uint32_t)b[j];
+        w[2 * j + 1] = (uint32_t)(b[j] >> 32);
+    }
+}
+
+// Wait until only this wave's pieces of the most recent chunk (mine per chunk) may still be
+// in flight: the chunk before it has landed (and every store issued before).
+__device__ __forceinline__ void rw_wait_vm(int mine)
+{
+    if (mine >= 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else if (mine == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if (mine == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int Q>
+__global__ __launch_bounds__(512, 4) void k_stage2_rw(Stage2Args a, S2Multi m)
+{
+    extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+    constexpr int NS = kRwNS, PPC = kRwPPC, T = kRwT, NW = kRwNW;
+    const int pi = (int)blockIdx.y / m.nyblk;
+    const S2Pass& P = m.p[pi];
+    int tb, ntl;
+    if (a.nwg == 0) {
+        tb = xcd_remap(blockIdx.x, gridDim.x);
+        ntl = 1;
+    } else {
+        const int nt = (int)((a.nvalid + T - 1) / T);
+        tb = (int)((int64_t)blockIdx.x * nt / gridDim.x);
+        ntl = (int)((int64_t)(blockIdx.x + 1) * nt / gridDim.x) - tb;
+    }
+    const int yb = (int)blockIdx.y - pi * m.nyblk;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    constexpr int nthr = 64 * NW;
+    constexpr int dpb = NW * Q;
+    const int dblk0 = yb * dpb;
+    const int ws = P.ws;
+    const int npw = P.npw;
+    const int umax = P.umax;
+    const int nwin = 2 * PPC * npw;                       // window pieces of a chunk
+    const int slot_bytes = (nwin + 1) * 1024;
+    const int npair = a.nsub >> 1;
+    const int nchunk = npair / PPC;
+    int32_t* ltab = (int32_t*)lds_raw;
+    const uint32_t ring0 = (uint32_t)(npair * kPairTab * 4);
+    const uint32_t exp0 = ring0 + (uint32_t)(NS * slot_bytes);
+    const int16_t* sub = (const int16_t*)P.sub;
+    const int32_t* bo_g = P.off + (int64_t)yb * nchunk * kRwBlk;
+
+    for (int i = threadIdx.x; i < npair * kPairTab; i += nthr) ltab[i] = P.ptab[(int64_t)yb * npair * kPairTab + i];
+    __syncthreads();
+
+    int acc[Q][12];
+#pragma unroll
+    for (int q = 0; q < Q; q++)
+#pragma unroll
+        for (int i = 0; i < 12; i++) acc[q][i] = 0;
+
+    const int ntot = ntl * nchunk;
+    int dchunk = 0, dtile = 0, dcount = 0;
+    auto dma = [&](int cc) {
+        const int c2 = dchunk;
+        const int64_t t0 = (int64_t)(tb + dtile) * T;
+        if (dcount + 1 < ntot) {
+            dcount++;
+            if (++dchunk == nchunk) { dchunk = 0; dtile++; }
+        }
+        const uint32_t slot = ring0 + (uint32_t)((cc % NS) * slot_bytes);
+        for (int pc = wave; pc <= nwin; pc += NW) {
+            if (pc < nwin) {
+                const int sl = pc / npw, pw = pc - sl * npw;      // window sl: pair sl / 2, side sl % 2
+                const int pr = PPC * c2 + (sl >> 1);
+                const int s = 2 * pr + (sl & 1);
+                const int b = __builtin_amdgcn_readfirstlane(ltab[pr * kPairTab + (sl & 1)]);
+                const int64_t e0 = t0 + b - (b & 1);
+                const char* src = (const char*)(sub + (int64_t)s * P.sub_stride + e0) + pw * 1024;
+                dma16s(src, (uint32_t)lane * 16u, slot + (uint32_t)(pc * 1024));
+            } else {
+                dma16s((const char*)(bo_g + (int64_t)c2 * kRwBlk), (uint32_t)lane * 16u, slot + (uint32_t)(pc * 1024));
+            }
+        }
+    };
+    // staging slot of chunk cc -> one copy of each pattern partial of its pairs, buffers
+    // ((cc & 1) * PPC + k) x umax patterns x ws elements
+    auto expand = [&](int cc, int chk) {
+        const char* slot = lds_raw + ring0 + (cc % NS) * slot_bytes;
+#pragma unroll
+        for (int k = 0; k < PPC; k++) {
+            const uint32_t* S0 = (const uint32_t*)(slot + (2 * k) * npw * 1024);
+            const uint32_t* S1 = (const uint32_t*)(slot + (2 * k + 1) * npw * 1024);
+            const int32_t* pt = ltab + (PPC * chk + k) * kPairTab;
+            const int k0 = pt[0] & 1;
+            const int U = pt[2];
+            int16_t* buf = (int16_t*)(lds_raw + exp0) + ((cc & 1) * PPC + k) * (umax * ws);
+            const int up8 = ws >> 3;
+            for (int idx = threadIdx.x; idx < U * up8; idx += nthr) {
+                int u = 0, uu = idx;
+#pragma unroll
+                for (int mm = 1; mm < kPairUMax; mm++)
+                    if (uu >= up8) { uu -= up8; u++; }
+                uint32_t A[4], B[4];
+                load8_shift64(S0, k0 + 8 * uu, A);
+                load8_shift64(S1, pt[3 + u] + 8 * uu, B);
+                uint32_t Pv[4];
+#pragma unroll
+                for (int mm = 0; mm < 4; mm++)
+                    Pv[mm] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(short2v, A[mm]) + __builtin_bit_cast(short2v, B[mm]));
+                *(uint4*)(buf + u * ws + 8 * uu) = make_uint4(Pv[0], Pv[1], Pv[2], Pv[3]);
+            }
+        }
+    };
+    auto flush = [&](int tile) {
+        const int64_t t0 = (int64_t)tile * T;
+#pragma unroll
+        for (int q = 0; q < Q; q++) {
+            const int dl = wave * Q + q;
+            const int d = dblk0 + dl;
+            const bool dv = d < a.numdms;
+            int64_t part = 0;
+            if (dv && !(a.probe & 4)) {
+#pragma unroll
+                for (int j = 0; j < 3; j++) {
+                    const int64_t tl = t0 + 12 * lane + 4 * j;
+                    float* o = P.out + (int64_t)d * a.out_stride + tl;
+                    if (tl + 3 < a.nvalid) {
+                        *(float4*)o = make_float4((float)acc[q][4 * j], (float)acc[q][4 * j + 1], (float)acc[q][4 * j + 2],
+                                                  (float)acc[q][4 * j + 3]);
+                        part += (int64_t)acc[q][4 * j] + acc[q][4 * j + 1] + acc[q][4 * j + 2] + acc[q][4 * j + 3];
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < 4; i++)
+                            if (tl + i < a.nvalid) {
+                                o[i] = (float)acc[q][4 * j + i];
+                                part += acc[q][4 * j + i];
+                            }
+                    }
+                }
+            }
+            if (dv && P.partial) {
+#pragma unroll
+                for (int mm = 32; mm >= 1; mm >>= 1) part += __shfl_xor(part, mm, 64);
+                if (lane == 0) P.partial[(int64_t)d * a.ntiles + tile] = (double)part;
+            }
+#pragma unroll
+            for (int i = 0; i < 12; i++) acc[q][i] = 0;
+        }
+    };
+
+    // this wave's DMA pieces per chunk (nwin + 1 pieces over NW waves)
+    const int mine = wave <= nwin ? (nwin - wave) / NW + 1 : 0;
+#pragma unroll
+    for (int cc = 0; cc < NS - 1; cc++) dma(cc);
+    rw_wait_vm(mine);
+    ring_barrier();
+    expand(0, 0);
+    ring_barrier();
+
+    int chk = 0, ktile = 0;
+    for (int c = 0; c < ntot; c++) {
+        if (!(a.probe & 2)) dma(c + NS - 1);
+        const int chn = chk + 1 == nchunk ? 0 : chk + 1;
+        if (c + 1 < ntot && !(a.probe & 8)) expand(c + 1, chn);
+        if (!(a.probe & 1)) {
+            const int32_t* sb = (const int32_t*)(lds_raw + ring0 + (c % NS) * slot_bytes + nwin * 1024);
+#pragma unroll
+            for (int k = 0; k < PPC; k++) {
+                const int jcv = lane < Q ? sb[k * dpb + wave * Q + lane] : 0;
+                const int rec = lane < 4 ? sb[PPC * dpb + (k * NW + wave) * 4 + lane] : 0;
+                const uint32_t mask = (uint32_t)__builtin_amdgcn_readlane(rec, 0);
+                uint32_t w[12];
+                rw_load_win(w, exp0 + (uint32_t)__builtin_amdgcn_readlane(rec, 1) + 24u * (uint32_t)lane);
+                int nwn = 2;
+#pragma unroll
+                for (int q = 0; q < Q; q++) {
+                    if (q > 0 && ((mask >> q) & 1u)) {
+                        rw_load_win(w, exp0 + (uint32_t)__builtin_amdgcn_readlane(rec, nwn) + 24u * (uint32_t)lane);
+                        nwn = nwn < 3 ? nwn + 1 : 3;
+                    }
+                    const uint32_t jc = min((uint32_t)__builtin_amdgcn_readlane(jcv, q), 1012u);
+                    rw_add12(acc[q], w, jc);
+                }
+            }
+        }
+        rw_wait_vm(a.probe & 2 ? 0 : mine);
+        ring_barrier();
+        if (chk == nchunk - 1) flush(tb + ktile++);
+        chk = chn;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+size_t stage2_rw_lds_bytes(int ws, int npw, int nsub, int umax)
+{
+    return (size_t)(nsub / 2) * kPairTab * 4 + (size_t)kRwNS * (2 * kRwPPC * npw + 1) * 1024 +
+           (size_t)2 * kRwPPC * umax * ws * 2;
+}
+
+template <int Q>
+static hipError_t launch_rw_q(const Stage2Args& a, const S2Multi& m, int nyblk, hipStream_t st)
+{
+    {
+        const hipError_t e = set_max_lds((const void*)k_stage2_rw<Q>, 80 * 1024);
+        if (e != hipSuccess) return e;
+    }
+    const unsigned ntiles = (unsigned)((a.nvalid + kRwT - 1) / kRwT);
+    const unsigned nx = a.nwg > 0 && (unsigned)a.nwg < ntiles ? (unsigned)a.nwg : ntiles;
+    Stage2Args b = a;
+    if (nx == ntiles) b.nwg = 0;
+    size_t lds = 0;
+    for (int i = 0; i < m.npass; i++)
+        lds = std::max(lds, stage2_rw_lds_bytes(m.p[i].ws, m.p[i].npw, a.nsub, m.p[i].umax));
+    if (lds > 80 * 1024) return hipErrorInvalidValue;
+    S2Multi mm = m;
+    mm.nyblk = nyblk;
+    hipLaunchKernelGGL((k_stage2_rw<Q>), dim3(nx, (unsigned)(nyblk * m.npass)), dim3(64 * kRwNW), lds, st, b, mm);
+    return hipGetLastError();
+}
+
+hipError_t launch_stage2_rw_multi(const Stage2Args& a, const S2Multi& m, int q, hipStream_t st)
+{
+    if (a.nvalid <= 0 || m.npass <= 0) return hipSuccess;
+    if (m.npass > kS2MaxPass || a.dms_per_blk != kRwNW * q) return hipErrorInvalidValue;
+    const int nyblk = (a.numdms + a.dms_per_blk - 1) / a.dms_per_blk;
+    switch (q) {
+    case 1: return launch_rw_q<1>(a, m, nyblk, st);
+    case 2: return launch_rw_q<2>(a, m, nyblk, st);
+    case 3: return launch_rw_q<3>(a, m, nyblk, st);
+    case 4: return launch_rw_q<4>(a, m, nyblk, st);
+    case 5: return launch_rw_q<5>(a, m, nyblk, st);
+    default: return hipErrorInvalidValue;
+    }
+}
+
 size_t stage2_pair_lds_bytes(int wstride, int npw, int nbp, int nsub, int umax, int ppc)
 {
     const int ns = ppc == 2 ? 4 : kRingNS;
