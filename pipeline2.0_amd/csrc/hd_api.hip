@@ -1597,7 +1597,7 @@ static void pair_tables(hd_plan* p, bool i16, int ppc, hd_plan::Wide& w, std::ve
 // pairs per chunk, 768-sample tiles (lane l: samples 12l .. 12l+11).  Per (y-block, pair) the
 // pair kernel's {base0, b1, U, k1[U]} over the block's DMs.  Per (y-block, chunk) one block of
 // kRwBlock ints: [pair k][DM slot] the jump code 12 + 100 * shift of the DM's 12 values in
-// its wave's current window, then [pair k][wave] {reload mask, window byte offsets}: a wave
+// its wave's current window, then [pair k][wave] {reload mask, window byte offsets} (8 ints): a wave
 // loads a window (24 elements per lane, 8-byte aligned) at its first DM and again at each DM
 // of the mask whose pattern buffer or offset leaves the current one (> 10 elements on).
 // Window offsets are LDS bytes from the expanded area: buffer ((chunk & 1) * 2 + k) x umax
@@ -1614,7 +1614,7 @@ static void rw_tables(hd_plan* p, bool i16, hd_plan::Wide& w, std::vector<int32_
     const int dpb = NW * Q;
     nyb = (numdms + dpb - 1) / dpb;
     const int npair = nsub / 2, nchunk = npair / PPC;
-    if (PPC * dpb + PPC * NW * 4 > hd::kRwBlock) return;
+    if (PPC * dpb + PPC * NW * 8 > hd::kRwBlock) return;
     auto dmof = [&](int yb, int k) { return std::min(yb * dpb + k, numdms - 1); };
     ptab.assign((size_t)nyb * npair * hd::kPairTab, 0);
     std::vector<std::vector<int32_t>> rs((size_t)nyb * npair);
@@ -1661,7 +1661,7 @@ static void rw_tables(hd_plan* p, bool i16, hd_plan::Wide& w, std::vector<int32_
                 const int32_t base0 = ptab[((size_t)yb * npair + c) * hd::kPairTab];
                 const int buf = (ch & 1) * PPC + k;
                 for (int wv = 0; wv < NW; wv++) {
-                    int32_t* rec = b + PPC * dpb + (k * NW + wv) * 4;
+                    int32_t* rec = b + PPC * dpb + (k * NW + wv) * 8;
                     int64_t wb = -1;
                     int nwin = 0;
                     for (int q = 0; q < Q; q++) {
@@ -3203,10 +3203,9 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         // stage (profiles/r02_stage2_variants.txt: 1.10 / 0.56 / 0.42 / 0.27 / 0.22 / 0.17 ms
         // vs the ring's 1.42 / 0.60 / 0.53 / 0.33 / 0.27 / 0.20)
         const bool pair2_auto = p->wide[4].ok && pair_bound;
-        // register windows over one-copy pair partials, two workgroups per CU: first choice
-        // wherever its tables apply (a wave's DMs within 3 windows of a pair)
-        const bool rw_auto = p->wide[5].ok && pair_bound;
-        wk = rw_auto ? 5 : pair2_auto ? 4 : pair_auto ? 3 : p->wide[2].ok ? 2 : p->wide[0].ok ? 0 : (p->wide[1].ok ? 1 : -1);
+        // (the register-window kernel, variant 8, measured slower at every DDplan stage: 1.63 vs
+        // 1.07 ms per stage-0 pass, profiles/r04_stage2_rw_probe.txt -- not an auto choice)
+        wk = pair2_auto ? 4 : pair_auto ? 3 : p->wide[2].ok ? 2 : p->wide[0].ok ? 0 : (p->wide[1].ok ? 1 : -1);
     }
     const bool use_wide = wk >= 0;
     const bool use_lds = !use_wide && (p->variant == 2 || (p->variant == 0 && p->lds_ok));
@@ -3309,13 +3308,13 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
 // A plan joins a multi-pass launch when it takes the two-pairs-per-chunk pair kernel (auto or
 // variant 7) on the topocentric grid; plans with the same kernel and geometry (one DDplan
 // stage) share a launch of at most kS2MaxPass passes, the rest run one by one.
-// The kernel a plan takes in a shared launch: 5 (k_stage2_rw: auto or variant 8), 4 (the
-// two-pairs-per-chunk pair kernel: auto without rw tables, or variant 7), or -1 (alone).
+// The kernel a plan takes in a shared launch: 5 (k_stage2_rw: variant 8), 4 (the
+// two-pairs-per-chunk pair kernel: auto or variant 7), or -1 (alone).
 static int dedisp_multi_kernel(const hd_plan* p)
 {
     const bool pair_bound = p->sub_bound >= 0 && 2 * p->sub_bound <= 32767;
     if (!p->sub_valid || !pair_bound || p->nbseg != 0 || p->pair_persist == 2) return -1;
-    if ((p->variant == 0 || p->variant == 8) && p->wide[5].ok) return 5;
+    if (p->variant == 8 && p->wide[5].ok) return 5;
     if ((p->variant == 0 || p->variant == 7) && p->wide[4].ok) return 4;
     return -1;
 }

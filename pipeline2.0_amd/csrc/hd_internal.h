@@ -148,7 +148,7 @@ S2Pass stage2_pass_of(const Stage2Args& a);
 hipError_t launch_stage2_pair(const Stage2Args& a, int q, int r, int ppc, hipStream_t st);
 // register-window pair kernel (k_stage2_rw): 8 waves x q DMs per workgroup, 768-sample tiles,
 // two workgroups per CU; per-chunk table blocks of kRwBlock ints
-constexpr int kRwWaves = 8, kRwBlock = 256, kRwTile = 768, kRwMaxWin = 3;
+constexpr int kRwWaves = 8, kRwBlock = 256, kRwTile = 768, kRwMaxWin = 5;
 size_t stage2_rw_lds_bytes(int ws, int npw, int nsub, int umax);
 hipError_t launch_stage2_rw_multi(const Stage2Args& a, const S2Multi& m, int q, hipStream_t st);
 hipError_t launch_stage2_pair_multi(const Stage2Args& a, const S2Multi& m, int q, int r, int ppc, hipStream_t st);

@@ -1361,7 +1361,7 @@ __device__ __forceinline__ void rw_add12(int (&A)[12], const uint32_t (&w)[12], 
 // workgroups share a CU and one's barriers and DMA waits overlap the other's work.
 // Host tables (rw_tables): per (y-block, pair) {base0, b1, U, k1[U]} as the pair kernel;
 // per (y-block, chunk) a 256-int block DMA'd with the chunk: [pair k][DM] jump codes
-// 12 + 100 * shift, then [pair k][wave] {reload mask, window byte offsets (<= 3)}.
+// 12 + 100 * shift, then [pair k][wave] {reload mask, window byte offsets (<= 5)} (8 ints).
 constexpr int kRwNW = 8, kRwNS = 4, kRwPPC = 2, kRwT = 768, kRwBlk = 256;
 
 __device__ __forceinline__ void rw_load_win(uint32_t (&w)[12], uint32_t addr)
@@ -1540,7 +1540,7 @@ __global__ __launch_bounds__(512, 4) void k_stage2_rw(Stage2Args a, S2Multi m)
 #pragma unroll
             for (int k = 0; k < PPC; k++) {
                 const int jcv = lane < Q ? sb[k * dpb + wave * Q + lane] : 0;
-                const int rec = lane < 4 ? sb[PPC * dpb + (k * NW + wave) * 4 + lane] : 0;
+                const int rec = lane < 8 ? sb[PPC * dpb + (k * NW + wave) * 8 + lane] : 0;
                 const uint32_t mask = (uint32_t)__builtin_amdgcn_readlane(rec, 0);
                 uint32_t w[12];
                 rw_load_win(w, exp0 + (uint32_t)__builtin_amdgcn_readlane(rec, 1) + 24u * (uint32_t)lane);
@@ -1549,7 +1549,7 @@ __global__ __launch_bounds__(512, 4) void k_stage2_rw(Stage2Args a, S2Multi m)
                 for (int q = 0; q < Q; q++) {
                     if (q > 0 && ((mask >> q) & 1u)) {
                         rw_load_win(w, exp0 + (uint32_t)__builtin_amdgcn_readlane(rec, nwn) + 24u * (uint32_t)lane);
-                        nwn = nwn < 3 ? nwn + 1 : 3;
+                        nwn = nwn < 5 ? nwn + 1 : 5;
                     }
                     const uint32_t jc = min((uint32_t)__builtin_amdgcn_readlane(jcv, q), 1012u);
                     rw_add12(acc[q], w, jc);
