@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--dd-single", action="store_true",
                     help="stage 2 as one launch per pass (hd_run_dedisp) instead of one launch per DDplan stage "
                          "(hd_run_dedisp_multi)")
+    ap.add_argument("--s1-per-stage", action="store_true",
+                    help="stage 1 as one hd_run_subband_multi call per DDplan stage instead of one for every "
+                         "stage with ds >= 2 (the fused k_stage1_q8m launch)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU work for the baseline sample")
     # the legs after the timed steps characterise one GPU: by default (-1) they run at world
     # size 1 only (8 ranks each writing a beam's 47 GB of .dat files, or two 4 GB PSRFITS
@@ -127,15 +130,27 @@ def run_step(eng, stages):
     stage-2 sweep of each pass.  Every step is a new beam for the engine (hd_touch_raw), so
     the per-beam channel-major copy of the raw block is rebuilt and timed in each step."""
     eng.touch_raw()
-    for plans in stages:
-        if not plans:
-            continue
-        eng.run_subband_multi(plans)
-        run_dedisp_stage(eng, plans)
+    for grp in subband_groups(stages):
+        eng.run_subband_multi([p for st in grp for p in st])
+        for plans in grp:
+            run_dedisp_stage(eng, plans)
     eng.sync()
 
 
 DD_MULTI = True
+S1_FUSE = True
+
+
+def subband_groups(stages):
+    """The beam's stage-1 calls: the ds = 1 stage alone, then every stage with ds >= 2 in one
+    hd_run_subband_multi call (one k_stage1_q8m launch reads the channel-major copy once for
+    all of them); with --s1-per-stage one call per DDplan stage."""
+    live = [st for st in stages if st]
+    if not S1_FUSE:
+        return [[st] for st in live]
+    lone = [[st] for st in live if st[0].pp.ds < 2]
+    multi = [st for st in live if st[0].pp.ds >= 2]
+    return lone + ([multi] if multi else [])
 
 
 def run_dedisp_stage(eng, plans):
@@ -157,14 +172,13 @@ def single_pulse_leg(eng, stages, beams):
     t = time.perf_counter()
     ncand = 0
     for _ in range(beams):
-        for plans in stages:
-            for p in plans:
-                hits, _ = SP.device_candidates(p, p.sub_dt, 0.1, 5.0)
-                ncand += len(hits)
+        for _, hits, _ in SP.device_candidates_many([p for plans in stages for p in plans], 0.1, 5.0):
+            ncand += len(hits)
     s = (time.perf_counter() - t) / beams
     return {"s_per_beam": s, "candidates_per_beam": ncand // beams,
             "note": "hd_single_pulse over the 57 passes' series in HBM (-m 0.1 -t 5.0): detrend, block stds, "
-                    "boxcars, prune_related1 on the GPU; prune_related2 + border cases on the host; wall time"}
+                    "boxcars, prune_related1 on the GPU; prune_related2 + border cases on the host, the device "
+                    "searches of the next 4 passes queued meanwhile (hd_single_pulse_launch/_collect); wall time"}
 
 
 def fft_leg(eng, stages, beams):
@@ -293,20 +307,19 @@ def end_to_end(eng, stages, obs, outdir):
     eng.sync()
     t = time.perf_counter()
     eng.touch_raw()
-    for plans in stages:
-        if not plans:
-            continue
-        eng.run_subband_multi(plans)
-        run_dedisp_stage(eng, plans)
-        for p in plans:
-            info.dt, info.freq, info.chan_wid, info.num_chan = p.sub_dt, p.sub_lofreq, p.sub_chanwid, p.pp.nsub
-            info.freqband = p.pp.nsub * p.sub_chanwid
-            write_dats_device(p, base, p.dmstrs, info, p.nds, wait=False)
-        eng.wait_writes()
-        elapsed += time.perf_counter() - t
-        for f in os.listdir(outdir):
-            os.remove(os.path.join(outdir, f))
-        t = time.perf_counter()
+    for grp in subband_groups(stages):
+        eng.run_subband_multi([p for st in grp for p in st])
+        for plans in grp:
+            run_dedisp_stage(eng, plans)
+            for p in plans:
+                info.dt, info.freq, info.chan_wid, info.num_chan = p.sub_dt, p.sub_lofreq, p.sub_chanwid, p.pp.nsub
+                info.freqband = p.pp.nsub * p.sub_chanwid
+                write_dats_device(p, base, p.dmstrs, info, p.nds, wait=False)
+            eng.wait_writes()
+            elapsed += time.perf_counter() - t
+            for f in os.listdir(outdir):
+                os.remove(os.path.join(outdir, f))
+            t = time.perf_counter()
     w1, b1 = eng.wait_writes()
     return elapsed, b1 - b0, w1 - w0
 
@@ -364,12 +377,11 @@ def run_slice_step(eng, ts, rank, stages, dist, torch):
                 dist.all_reduce(t)
             eng.clip_set_stats(table)
     plans = []
-    for st in stages:
-        if not st:
-            continue
-        eng.run_subband_multi(st)
-        run_dedisp_stage(eng, st)
-        plans += st
+    for grp in subband_groups(stages):
+        eng.run_subband_multi([p for st in grp for p in st])
+        for st in grp:
+            run_dedisp_stage(eng, st)
+            plans += st
     sums = ts.pass_sums(rank, plans)
     if dist is not None:
         t = torch.from_numpy(sums)
@@ -501,8 +513,9 @@ def cpu_baseline(obs, synth, ddplans, target_s, mask, pts, pad, omp):
 
 def main():
     args = parse()
-    global DD_MULTI
+    global DD_MULTI, S1_FUSE
     DD_MULTI = not args.dd_single
+    S1_FUSE = not args.s1_per_stage
     world, rank, local, dist, torch = dist_setup(args)
     for leg, n1 in (("e2e_beams", 1), ("sp_beams", 1), ("fft_beams", 1), ("rfi_beams", 1), ("stream_beams", 3)):
         if getattr(args, leg) < 0:
@@ -649,6 +662,8 @@ def main():
                            for k, v in sorted(per_kernel.items(), key=lambda kv: -kv[1]["ms"])},
         "stage2_streams": args.streams,
         "stage2_launch": "one per pass" if args.dd_single else "one per DDplan stage (hd_run_dedisp_multi)",
+        "stage1_launch": "one per DDplan stage" if args.s1_per_stage else
+                         "ds=1 stage alone, the ds>=2 stages in one hd_run_subband_multi call (k_stage1_q8m)",
         "step_compulsory_hbm_frac": (raw_bytes + 4.0 * out_per_step) / step_s / (HBM_PEAK_GBS * 1e9),
         "stage2_valu_frac": adds2 / (ms2 * 1e-3) / VALU_ADD_PEAK if ms2 > 0 else None,
     }

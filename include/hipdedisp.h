@@ -413,6 +413,17 @@ HD_API int hd_sp_widths(double dt, double maxwidth, int32_t* widths, int32_t* n)
  * HD_E_NOMEM is returned (call again with room).  bad_blocks[numdms * nblocks] (may be
  * NULL): 1 = block not searched; *nblocks (may be NULL) = floor(numout / 1000).  A series
  * of fewer than 8000 samples gives no candidates.                                        */
+HD_API int hd_single_pulse(hd_plan* plan, double dt, double maxwidth, double threshold, hd_sp_hit* hits,
+                           int64_t cap, int64_t* nhits, uint8_t* bad_blocks, int64_t* nblocks);
+/* hd_single_pulse in two halves, so the device search of later plans runs while the host
+ * prunes this one's hits: _launch queues the device half on the plan's stream (its series
+ * must stay unchanged until the collect) and returns; _collect waits for that plan's device
+ * half only (copies on a context stream of their own) and then behaves as hd_single_pulse,
+ * HD_E_NOMEM included (the search stays collectable: call again with room).  A launch again
+ * before the collect replaces the pending search.  hd_single_pulse = _launch + _collect.   */
+HD_API int hd_single_pulse_launch(hd_plan* plan, double dt, double maxwidth, double threshold);
+HD_API int hd_single_pulse_collect(hd_plan* plan, hd_sp_hit* hits, int64_t cap, int64_t* nhits, uint8_t* bad_blocks,
+                                   int64_t* nblocks);
 /* The host half of hd_single_pulse on caller-supplied hits (any order, n of them, DMs
  * 0..ndm-1, widths[nw] of hd_sp_widths): grouped by DM, each DM's list in bin order (widths
  * ascending among equal bins), prune_related2 and -- when numout > nds -- the border cases
@@ -420,8 +431,6 @@ HD_API int hd_sp_widths(double dt, double maxwidth, int32_t* widths, int32_t* n)
  * Host only (no device).                                                                  */
 HD_API int hd_sp_prune(hd_sp_hit* hits, int64_t n, int32_t ndm, const int32_t* widths, int32_t nw, int64_t nds,
                        int64_t numout, int64_t* nkept);
-HD_API int hd_single_pulse(hd_plan* plan, double dt, double maxwidth, double threshold, hd_sp_hit* hits,
-                           int64_t cap, int64_t* nhits, uint8_t* bad_blocks, int64_t* nblocks);
 
 /* ---- realfft, zapbirds, rednoise on the device-resident series -----------------------
  * Replace `realfft <dat>; zapbirds -zap -zapfile <zaplist> -baryv <v> <fft>; rednoise <fft>`

@@ -109,16 +109,12 @@ struct hd_ctx {
     std::vector<SpecialList> special_cache;
     double* d_partial = nullptr;    // shared per-tile partial sums
     size_t partial_bytes = 0;
-    // single-pulse search scratch: per-block coefficients, hit list, hit counter
-    double* d_sp_coef = nullptr;
-    size_t sp_coef_bytes = 0;
-    hd_sp_hit* d_sp_hits = nullptr;
-    int64_t sp_hits_cap = 0;
-    unsigned long long* d_sp_count = nullptr;
-    uint8_t* d_sp_bad = nullptr;    // bad-block flags as bytes
-    size_t sp_bad_bytes = 0;
-    void* sp_pin = nullptr;         // pinned staging of the hits / flags D2H
+    // single-pulse search: the host half's copy stream, pinned staging of the hits / flags
+    // D2H, and the largest device hit count seen (the next plans' first list size)
+    hipStream_t ssp = nullptr;
+    void* sp_pin = nullptr;
     size_t sp_pin_bytes = 0;
+    int64_t sp_cap_hint = 1 << 16;
     double* d_sum_parts = nullptr;  // hd_series_sum partials
     // streaming ingest (hd_push_raw_file): pinned host blocks of the reader threads
     PinSet pins;
@@ -257,6 +253,29 @@ struct hd_plan {
     int32_t* d_bseg = nullptr;
     float* d_topo = nullptr;
     float* d_padv = nullptr;
+    struct SpPlan* sp = nullptr;    // single-pulse search state (hd_single_pulse_launch / _collect)
+};
+
+// A plan's single-pulse search in flight: the device half (block statistics, boxcar hits,
+// prune_related1, bad flags) launched on the plan's stream and marked by ev; the host half
+// (copies, prune_related2, border cases) waits for ev only, on the context's ssp stream, so
+// the device half of later plans keeps running while this plan's hits are pruned.
+struct SpPlan {
+    double* d_coef = nullptr;
+    size_t coef_bytes = 0;
+    hd_sp_hit* d_hits = nullptr;
+    int64_t cap = 0;
+    unsigned long long* d_count = nullptr;
+    uint8_t* d_bad = nullptr;
+    size_t bad_bytes = 0;
+    hipEvent_t ev = nullptr;
+    hipStream_t st = nullptr;
+    bool pending = false;
+    int32_t widths[16] = {0};
+    double rsw[16] = {0};
+    int32_t nw = 0;
+    double threshold = 0;
+    int64_t nblocks = 0, ls = 0;
 };
 
 static thread_local std::string g_err;
@@ -431,11 +450,8 @@ extern "C" int hd_close(hd_ctx* c)
     free_obs_buffers(c);
     dfree(c->d_partial);
     dfree(c->d_partial2);
-    dfree(c->d_sp_coef);
-    dfree(c->d_sp_hits);
-    dfree(c->d_sp_count);
-    dfree(c->d_sp_bad);
     if (c->sp_pin) (void)hipHostFree(c->sp_pin);
+    if (c->ssp) (void)hipStreamDestroy(c->ssp);
     dfree(c->d_sum_parts);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_aux0) (void)hipEventDestroy(c->ev_aux0);
@@ -1350,6 +1366,15 @@ static void plan_free(hd_plan* p)
     for (auto& e : p->ev)
         if (e) (void)hipEventDestroy(e);
     if (p->ev_copy) (void)hipEventDestroy(p->ev_copy);
+    if (p->sp) {
+        dfree(p->sp->d_coef);
+        dfree(p->sp->d_hits);
+        dfree(p->sp->d_count);
+        dfree(p->sp->d_bad);
+        if (p->sp->ev) (void)hipEventDestroy(p->sp->ev);
+        delete p->sp;
+        p->sp = nullptr;
+    }
 }
 
 struct Tables {
@@ -2497,6 +2522,141 @@ static int run_subband_chunk(hd_ctx* c, hd_plan** plans, int n)
     return HD_OK;
 }
 
+// tie_eps of the 8-bit integer path at downsampling ds (stage1_q8_tiling's bound)
+static double q8_tie_eps(const hd_ctx* c, int cps, int ds)
+{
+    double maxpad = 255.0;
+    for (float v : c->h_padvals) maxpad = std::max(maxpad, (double)fabsf(v));
+    const double smax = cps * maxpad, amax = ds * smax;
+    auto ulp2 = [](double x) { return ldexp(1.0, (int)floor(log2(x)) - 22); };
+    double e = ds * cps * 0.5 * ulp2(smax) + ds * 0.5 * ulp2(amax);
+    if (c->opts.ds_mode == HD_DS_MEAN) e += ds * 0.5 * ulp2(smax);
+    return e;
+}
+
+// Whether these plans (several DDplan stages, ds >= 2) can share one k_stage1_q8m launch.
+static bool q8m_ok(const hd_ctx* c, hd_plan* const* plans, int n)
+{
+    if (n < 2 || n > hd::kMaxPass || (getenv("HD_Q8M") && atoi(getenv("HD_Q8M")) == 0)) return false;
+    if ((c->obs.nbits != 8 && c->obs.nbits != 4) || c->d_scl || c->d_offs || c->d_wts) return false;
+    if (getenv("HD_QFIX") && atoi(getenv("HD_QFIX")) != 0) return false;
+    const int nsub = plans[0]->pass.nsub, cps = c->obs.nchan / nsub;
+    int nds = 0, ds0 = plans[0]->pass.ds;
+    for (int i = 0; i < n; i++) {
+        const hd_plan* p = plans[i];
+        if (p->pass.nsub != nsub || (p->s1_variant != 0 && p->s1_variant != 3) || p->probe) return false;
+        if (!hd::stage1_q8m_supports_ds(p->pass.ds) || !hd::stage1_q8_supports(cps, p->pass.ds)) return false;
+        if (p->pass.ds != ds0) nds = 1;
+    }
+    return nds > 0 && (cps == 8 || cps == 10 || cps == 16);
+}
+
+// Stage 1 of several DDplan stages in one launch (k_stage1_q8m), then per stage its special
+// tiles (float kernel) and fixups, as run_subband_chunk does for one stage.  Returns 1 when
+// the fused tile does not fit (the caller then runs the stages one by one).
+static int run_subband_fused(hd_ctx* c, hd_plan** plans, int n)
+{
+    hd_plan* p0 = plans[0];
+    const int nsub = p0->pass.nsub, cps = c->obs.nchan / nsub;
+    int dmax = 0;
+    for (int i = 0; i < n; i++) dmax = std::max(dmax, plans[i]->maxdelay);
+    const int S = hd::stage1_q8m_quarter_rows();
+    hd::Stage1Multi m{};
+    m.sg = 1;
+    m.W = S + ((dmax + 15) & ~15);
+    m.cps = cps;
+    if (hd::stage1_q8m_lds_bytes(m) > 160 * 1024) return 1;     // 1: does not apply (per-stage launches)
+    if (c->obs.nbits != 8 && !alloc_rawT(c, dmax)) return 1;
+    int rc0 = ensure_blocks(c);
+    if (rc0) return rc0;
+    for (int i = 0; i < n; i++) HIPCHK(c, hipMemsetAsync(plans[i]->d_maxabs, 0, sizeof(int32_t), c->stream));
+    HIPCHK(c, hipEventRecord(p0->ev[0], c->stream));
+    const bool clip_runs = c->opts.clip_sigma > 0.0f && !c->clip_valid;
+    const bool fork_clip = clip_runs && !c->rawT_valid && alloc_rawT(c, dmax);
+    const uint8_t* rawT = !fork_clip ? ensure_rawT(c, dmax, true) : nullptr;
+    rc0 = ensure_clip(c, fork_clip ? c->ev_aux0 : nullptr);
+    if (fork_clip && !rc0) rawT = ensure_rawT(c, dmax, true, true);
+    const hipError_t ej = join_aux(c);
+    if (rc0) return rc0;
+    HIPCHK(c, ej);
+    if (!rawT) return fail(c, HD_E_HIP, "stage 1: channel-major copy failed");
+    const bool clip = c->opts.clip_sigma > 0.0f;
+    m.rd = raw_desc(c);
+    m.rawT = rawT;
+    m.tstride = c->rawT_stride;
+    m.npass = n;
+    m.nsub = nsub;
+    m.cps = cps;
+    m.ds = 1;                                     // tiles of 4 * S raw rows (special-tile list)
+    m.to = 4 * S;
+    m.ds_mode = c->opts.ds_mode;
+    m.sub_dtype = c->opts.sub_dtype;
+    m.sub_round = c->opts.sub_round;
+    m.dmax = dmax;
+    m.two_ok = 2;
+    m.ngroups = nsub;
+    m.ntiles = (int)((c->obs.N + 4 * S - 1) / (4 * S));
+    m.nds = c->obs.N;
+    m.out_stride = p0->sub_stride;
+    for (int i = 0; i < n; i++) {
+        m.dly[i] = plans[i]->d_idispdt;
+        m.out[i] = plans[i]->d_sub;
+        m.maxabs[i] = plans[i]->d_maxabs;
+        m.ostride[i] = plans[i]->sub_stride;
+        m.pds[i] = plans[i]->pass.ds;
+        m.ptie[i] = q8_tie_eps(c, cps, plans[i]->pass.ds);
+    }
+    int nsp = 0, *d_sp = nullptr;
+    int rc = special_tiles(c, m, &d_sp, &nsp);
+    if (rc) return rc;
+    HIPCHK(c, hd::launch_stage1_q8m(m, c->stream));
+    // per DDplan stage (ds): the special tiles on the float kernel, then the fixups
+    for (int i0 = 0; i0 < n;) {
+        int i1 = i0;
+        while (i1 < n && plans[i1]->pass.ds == plans[i0]->pass.ds) i1++;
+        hd::Stage1Multi g = m;
+        const int ds = plans[i0]->pass.ds;
+        g.ds = ds;
+        g.npass = i1 - i0;
+        g.nds = plans[i0]->nds;
+        g.out_stride = plans[i0]->sub_stride;
+        g.dmax = 0;
+        for (int i = i0; i < i1; i++) {
+            const int k = i - i0;
+            g.dly[k] = plans[i]->d_idispdt;
+            g.out[k] = plans[i]->d_sub;
+            g.maxabs[k] = plans[i]->d_maxabs;
+            g.ostride[k] = plans[i]->sub_stride;
+            g.dmax = std::max(g.dmax, plans[i]->maxdelay);
+        }
+        if (nsp) {
+            hd::Stage1Multi f = g;
+            int fvw = 4;
+            f.dmax = dmax;                            // the fused tiles' rows: 4 S + dmax
+            if (!stage1_tiling_fixed(c, nsub, ds, dmax, 4 * S / ds, f, fvw))
+                return fail(c, HD_E_INVAL, "stage 1: no float tiling for the fused launch's special tiles (ds %d)", ds);
+            f.ntiles = m.ntiles;
+            const size_t flds = hd::stage1_tiled_lds_bytes(f);
+            if (flds > c->lds_attr_set) {
+                HIPCHK(c, hd::stage1_tiled_set_lds_limit(flds));
+                c->lds_attr_set = flds;
+            }
+            HIPCHK(c, hd::launch_stage1_tiled(f, fvw, d_sp, nsp, true, c->stream));
+        }
+        if (clip)
+            HIPCHK(c, hd::launch_stage1_fixup(g, c->clip.events, c->clip.nevents, g.rd.zidx != nullptr, c->stream));
+        i0 = i1;
+    }
+    HIPCHK(c, hipEventRecord(p0->ev[1], c->stream));
+    for (int i = 0; i < n; i++) {
+        plans[i]->sub_valid = true;
+        plans[i]->sub_bound = stage1_sub_bound(c, plans[i]);
+        plans[i]->sub_nonneg = plans[i]->sub_bound >= 0 && stage1_sub_nonneg(c);
+        plans[i]->ran_sub = (i == 0);
+    }
+    return HD_OK;
+}
+
 extern "C" int hd_run_subband_multi(hd_plan** plans, int32_t n)
 {
     if (!plans || n < 1 || !plans[0]) return fail(nullptr, HD_E_INVAL, "hd_run_subband_multi: no plans");
@@ -2505,8 +2665,8 @@ extern "C" int hd_run_subband_multi(hd_plan** plans, int32_t n)
         hd_plan* p = plans[i];
         if (!p) return fail(c, HD_E_INVAL, "hd_run_subband_multi: plan %d is NULL", i);
         if (p->ctx != c) return fail(c, HD_E_INVAL, "hd_run_subband_multi: plans from different contexts");
-        if (p->pass.nsub != plans[0]->pass.nsub || p->pass.ds != plans[0]->pass.ds)
-            return fail(c, HD_E_INVAL, "hd_run_subband_multi: plans must share nsub and ds");
+        if (p->pass.nsub != plans[0]->pass.nsub)
+            return fail(c, HD_E_INVAL, "hd_run_subband_multi: plans must share nsub");
         if (p->pass.flags & HD_PASS_SUB_INPUT)
             return fail(c, HD_E_STATE, "hd_run_subband: a HD_PASS_SUB_INPUT plan takes hd_set_subbands");
     }
@@ -2526,9 +2686,27 @@ extern "C" int hd_run_subband_multi(hd_plan** plans, int32_t n)
         int rc = ensure_sub(c, plans[i]);
         if (rc) return rc;
     }
-    for (int i0 = 0; i0 < n; i0 += hd::kMaxPass) {
-        int rc = run_subband_chunk(c, plans + i0, std::min(hd::kMaxPass, n - i0));
+    // plans ordered by ds (stable): the stages of a mixed call run in ascending ds
+    std::vector<hd_plan*> v(plans, plans + n);
+    std::stable_sort(v.begin(), v.end(), [](const hd_plan* x, const hd_plan* y) { return x->pass.ds < y->pass.ds; });
+    // the passes of several DDplan stages with ds >= 2: one fused launch when they qualify
+    const int cps = c->obs.nchan / plans[0]->pass.nsub;
+    std::vector<hd_plan*> fz, rest;
+    for (hd_plan* p : v)
+        (hd::stage1_q8m_supports_ds(p->pass.ds) && hd::stage1_q8_supports(cps, p->pass.ds) ? fz : rest).push_back(p);
+    if (q8m_ok(c, fz.data(), (int)fz.size())) {
+        const int rc = run_subband_fused(c, fz.data(), (int)fz.size());
+        if (rc < 0) return rc;
+        if (rc == HD_OK) fz.clear();
+    }
+    rest.insert(rest.end(), fz.begin(), fz.end());
+    std::stable_sort(rest.begin(), rest.end(), [](const hd_plan* x, const hd_plan* y) { return x->pass.ds < y->pass.ds; });
+    for (int a0 = 0; a0 < (int)rest.size();) {
+        int a1 = a0;
+        while (a1 < (int)rest.size() && rest[a1]->pass.ds == rest[a0]->pass.ds && a1 - a0 < hd::kMaxPass) a1++;
+        int rc = run_subband_chunk(c, rest.data() + a0, a1 - a0);
         if (rc) return rc;
+        a0 = a1;
     }
     return HD_OK;
 }
@@ -2828,103 +3006,141 @@ extern "C" int hd_sp_prune(hd_sp_hit* hits, int64_t n, int32_t ndm, const int32_
     return HD_OK;
 }
 
-extern "C" int hd_single_pulse(hd_plan* p, double dt, double maxwidth, double threshold, hd_sp_hit* hits,
-                               int64_t cap, int64_t* nhits, uint8_t* bad_blocks, int64_t* nblocks_out)
+// The device half into the plan's SpPlan buffers (hit list sized cap), marked by sp->ev.
+static int sp_launch_device(hd_ctx* c, hd_plan* p, SpPlan* sp, int64_t cap)
 {
-    if (!p || !nhits || (cap > 0 && !hits)) return fail(p ? p->ctx : nullptr, HD_E_INVAL, "hd_single_pulse: NULL argument");
+    const int ndm = p->pass.numdms;
+    if (sp->cap < cap) {
+        HIPCHK(c, hipStreamSynchronize(sp->st));
+        dfree(sp->d_hits);
+        sp->d_hits = nullptr;
+        sp->cap = 0;
+        HIPCHK(c, hipMalloc(&sp->d_hits, sizeof(hd_sp_hit) * (size_t)cap));
+        sp->cap = cap;
+    }
+    HIPCHK(c, hipMemsetAsync(sp->d_count, 0, sizeof(unsigned long long), sp->st));
+    if (sp->nblocks > 0) {
+        HIPCHK(c, hd::launch_sp_blocks(p->d_out, p->out_stride, ndm, (int)sp->nblocks, sp->d_coef, sp->st));
+        HIPCHK(c, hd::launch_sp_hits(p->d_out, p->out_stride, ndm, (int)sp->nblocks, sp->d_coef, sp->ls, sp->widths,
+                                     sp->rsw, sp->nw, sp->threshold, sp->d_hits, sp->d_count, sp->cap, sp->st));
+        HIPCHK(c, hd::launch_sp_badflags(sp->d_coef, (int64_t)ndm * sp->nblocks, sp->d_bad, sp->st));
+    }
+    HIPCHK(c, hipEventRecord(sp->ev, sp->st));
+    return HD_OK;
+}
+
+extern "C" int hd_single_pulse_launch(hd_plan* p, double dt, double maxwidth, double threshold)
+{
+    if (!p) return fail(nullptr, HD_E_INVAL, "hd_single_pulse_launch: NULL plan");
     hd_ctx* c = p->ctx;
     if (!p->ran_dd || !p->d_out) return fail(c, HD_E_STATE, "hd_single_pulse: run hd_run_dedisp first");
     int32_t widths[16], nw = 0;
     int rc = hd_sp_widths(dt, maxwidth, widths, &nw);
     if (rc) return fail(c, rc, "hd_single_pulse: dt must be > 0");
-    double rsw[16];
-    for (int i = 0; i < nw; i++) rsw[i] = 1.0 / std::sqrt((double)widths[i]);
     const int ndm = p->pass.numdms;
     const int64_t nblocks = p->numout / 1000;                  // roundN / detrendlen
-    if (nblocks_out) *nblocks_out = nblocks;
     if (nblocks > hd::sp_max_blocks())
         return fail(c, HD_E_INVAL, "hd_single_pulse: %lld blocks > %d", (long long)nblocks, hd::sp_max_blocks());
-    const int64_t ls = nblocks * 1000 / 8000 * 8000;           // numchunks * chunklen
+    HIPCHK(c, hipSetDevice(c->device));
+    if (!p->sp) p->sp = new SpPlan();
+    SpPlan* sp = p->sp;
+    if (!sp->ev) {
+        HIPCHK(c, hipEventCreateWithFlags(&sp->ev, hipEventDisableTiming));
+        HIPCHK(c, hipMalloc(&sp->d_count, sizeof(unsigned long long)));
+    }
+    if (!c->ssp) HIPCHK(c, hipStreamCreateWithFlags(&c->ssp, hipStreamNonBlocking));
+    if (sp->pending) HIPCHK(c, hipEventSynchronize(sp->ev));   // a relaunch before its collect
+    sp->st = p->dd_stream ? p->dd_stream : c->stream;
+    sp->nw = nw;
+    for (int i = 0; i < nw; i++) {
+        sp->widths[i] = widths[i];
+        sp->rsw[i] = 1.0 / std::sqrt((double)widths[i]);
+    }
+    sp->threshold = threshold;
+    sp->nblocks = nblocks;
+    sp->ls = nblocks * 1000 / 8000 * 8000;                     // numchunks * chunklen
+    const size_t cbytes = sizeof(double) * 4 * (size_t)std::max<int64_t>(1, (int64_t)ndm * nblocks);
+    const size_t bbytes = (size_t)std::max<int64_t>(1, (int64_t)ndm * nblocks);
+    if (sp->coef_bytes < cbytes || sp->bad_bytes < bbytes) {
+        HIPCHK(c, hipStreamSynchronize(sp->st));
+        dfree(sp->d_coef);
+        dfree(sp->d_bad);
+        sp->d_coef = nullptr;
+        sp->d_bad = nullptr;
+        sp->coef_bytes = sp->bad_bytes = 0;
+        HIPCHK(c, hipMalloc(&sp->d_coef, cbytes));
+        HIPCHK(c, hipMalloc(&sp->d_bad, bbytes));
+        sp->coef_bytes = cbytes;
+        sp->bad_bytes = bbytes;
+    }
+    rc = sp_launch_device(c, p, sp, std::max(sp->cap, c->sp_cap_hint));
+    if (rc) return rc;
+    sp->pending = true;
+    return HD_OK;
+}
+
+// pinned staging of at least `need` bytes (the host half runs one plan at a time)
+static int sp_pin(hd_ctx* c, size_t need)
+{
+    if (need <= c->sp_pin_bytes) return HD_OK;
+    if (c->sp_pin) HIPCHK(c, hipHostFree(c->sp_pin));
+    c->sp_pin = nullptr;
+    c->sp_pin_bytes = 0;
+    HIPCHK(c, hipHostMalloc(&c->sp_pin, need + need / 4, hipHostMallocDefault));
+    c->sp_pin_bytes = need + need / 4;
+    return HD_OK;
+}
+
+extern "C" int hd_single_pulse_collect(hd_plan* p, hd_sp_hit* hits, int64_t cap, int64_t* nhits, uint8_t* bad_blocks,
+                                       int64_t* nblocks_out)
+{
+    if (!p || !nhits || (cap > 0 && !hits)) return fail(p ? p->ctx : nullptr, HD_E_INVAL, "hd_single_pulse: NULL argument");
+    hd_ctx* c = p->ctx;
+    SpPlan* sp = p->sp;
+    if (!sp || !sp->pending) return fail(c, HD_E_STATE, "hd_single_pulse_collect: no search launched on this plan");
     HIPCHK(c, hipSetDevice(c->device));
     SpTimer tm;                                                // HD_SP_TIMING=1 (profiling)
-    hipStream_t st = p->dd_stream ? p->dd_stream : c->stream;
-    const size_t cbytes = sizeof(double) * 4 * (size_t)std::max<int64_t>(1, (int64_t)ndm * nblocks);
-    if (c->sp_coef_bytes < cbytes) {
-        HIPCHK(c, hipStreamSynchronize(st));
-        dfree(c->d_sp_coef);
-        c->d_sp_coef = nullptr;
-        c->sp_coef_bytes = 0;
-        HIPCHK(c, hipMalloc(&c->d_sp_coef, cbytes));
-        c->sp_coef_bytes = cbytes;
-    }
-    const int64_t dcap = std::max<int64_t>(cap, 1 << 16);
-    if (c->sp_hits_cap < dcap) {
-        HIPCHK(c, hipStreamSynchronize(st));
-        dfree(c->d_sp_hits);
-        c->d_sp_hits = nullptr;
-        c->sp_hits_cap = 0;
-        HIPCHK(c, hipMalloc(&c->d_sp_hits, sizeof(hd_sp_hit) * (size_t)dcap));
-        c->sp_hits_cap = dcap;
-    }
-    if (!c->d_sp_count) HIPCHK(c, hipMalloc(&c->d_sp_count, sizeof(unsigned long long)));
-    HIPCHK(c, hipMemsetAsync(c->d_sp_count, 0, sizeof(unsigned long long), st));
-    if (nblocks > 0) {
-        HIPCHK(c, hd::launch_sp_blocks(p->d_out, p->out_stride, ndm, (int)nblocks, c->d_sp_coef, st));
-        HIPCHK(c, hd::launch_sp_hits(p->d_out, p->out_stride, ndm, (int)nblocks, c->d_sp_coef, ls, widths, rsw, nw,
-                                     threshold, c->d_sp_hits, c->d_sp_count, c->sp_hits_cap, st));
-    }
-    unsigned long long cnt = 0;
-    HIPCHK(c, d2h(&cnt, c->d_sp_count, sizeof(cnt), st));
+    const int ndm = p->pass.numdms;
+    if (nblocks_out) *nblocks_out = sp->nblocks;
+    int rc = sp_pin(c, 64);
+    if (rc) return rc;
+    // the count, on the copy stream after the plan's device half only
+    HIPCHK(c, hipStreamWaitEvent(c->ssp, sp->ev, 0));
+    HIPCHK(c, hipMemcpyAsync(c->sp_pin, sp->d_count, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->ssp));
+    HIPCHK(c, hipStreamSynchronize(c->ssp));
+    unsigned long long cnt = *(const unsigned long long*)c->sp_pin;
     tm.mark(0);
-    if ((int64_t)cnt > c->sp_hits_cap) {
+    if ((int64_t)cnt > sp->cap) {
         // the device list overflowed: grow it to the count and search again (once per size)
-        HIPCHK(c, hipStreamSynchronize(st));
-        dfree(c->d_sp_hits);
-        c->d_sp_hits = nullptr;
-        c->sp_hits_cap = 0;
         const int64_t ncap = (int64_t)cnt + (int64_t)cnt / 4;
-        HIPCHK(c, hipMalloc(&c->d_sp_hits, sizeof(hd_sp_hit) * (size_t)ncap));
-        c->sp_hits_cap = ncap;
-        HIPCHK(c, hipMemsetAsync(c->d_sp_count, 0, sizeof(unsigned long long), st));
-        HIPCHK(c, hd::launch_sp_hits(p->d_out, p->out_stride, ndm, (int)nblocks, c->d_sp_coef, ls, widths, rsw, nw,
-                                     threshold, c->d_sp_hits, c->d_sp_count, c->sp_hits_cap, st));
-        HIPCHK(c, d2h(&cnt, c->d_sp_count, sizeof(cnt), st));
+        c->sp_cap_hint = std::max(c->sp_cap_hint, ncap);
+        rc = sp_launch_device(c, p, sp, ncap);
+        if (rc) return rc;
+        HIPCHK(c, hipStreamWaitEvent(c->ssp, sp->ev, 0));
+        HIPCHK(c, hipMemcpyAsync(c->sp_pin, sp->d_count, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->ssp));
+        HIPCHK(c, hipStreamSynchronize(c->ssp));
+        cnt = *(const unsigned long long*)c->sp_pin;
     }
-    // the bad-block flags as bytes (device-packed), and the hits, through the context's pinned
-    // staging block (pageable copies of a few MB cost milliseconds per pass)
-    const size_t nbad = bad_blocks && nblocks > 0 ? (size_t)ndm * nblocks : 0;
+    // the bad-block flags as bytes (device-packed), and the hits, through the pinned block
+    // (pageable copies of a few MB cost milliseconds per pass)
+    const size_t nbad = bad_blocks && sp->nblocks > 0 ? (size_t)ndm * sp->nblocks : 0;
     *nhits = (int64_t)cnt;
     const bool fits = (int64_t)cnt <= cap;
     const size_t hbytes = fits ? sizeof(hd_sp_hit) * cnt : 0;
-    const size_t need = std::max(hbytes, nbad);
-    if (need > c->sp_pin_bytes) {
-        HIPCHK(c, hipStreamSynchronize(st));
-        if (c->sp_pin) HIPCHK(c, hipHostFree(c->sp_pin));
-        c->sp_pin = nullptr;
-        c->sp_pin_bytes = 0;
-        HIPCHK(c, hipHostMalloc(&c->sp_pin, need + need / 4, hipHostMallocDefault));
-        c->sp_pin_bytes = need + need / 4;
-    }
+    rc = sp_pin(c, std::max(hbytes, nbad));
+    if (rc) return rc;
     if (nbad) {
-        if (c->sp_bad_bytes < nbad) {
-            HIPCHK(c, hipStreamSynchronize(st));
-            dfree(c->d_sp_bad);
-            c->d_sp_bad = nullptr;
-            c->sp_bad_bytes = 0;
-            HIPCHK(c, hipMalloc(&c->d_sp_bad, nbad));
-            c->sp_bad_bytes = nbad;
-        }
-        HIPCHK(c, hd::launch_sp_badflags(c->d_sp_coef, (int64_t)nbad, c->d_sp_bad, st));
-        HIPCHK(c, hipMemcpyAsync(c->sp_pin, c->d_sp_bad, nbad, hipMemcpyDeviceToHost, st));
-        HIPCHK(c, hipStreamSynchronize(st));
+        HIPCHK(c, hipMemcpyAsync(c->sp_pin, sp->d_bad, nbad, hipMemcpyDeviceToHost, c->ssp));
+        HIPCHK(c, hipStreamSynchronize(c->ssp));
         memcpy(bad_blocks, c->sp_pin, nbad);
     }
-    if (!fits)
+    if (!fits)                                                 // (still pending: call again with room)
         return fail(c, HD_E_NOMEM, "hd_single_pulse: %llu hits > capacity %lld (call again with room)", cnt,
                     (long long)cap);
+    sp->pending = false;
     if (!cnt) return HD_OK;
-    HIPCHK(c, hipMemcpyAsync(c->sp_pin, c->d_sp_hits, hbytes, hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipStreamSynchronize(st));
+    HIPCHK(c, hipMemcpyAsync(c->sp_pin, sp->d_hits, hbytes, hipMemcpyDeviceToHost, c->ssp));
+    HIPCHK(c, hipStreamSynchronize(c->ssp));
     const hd_sp_hit* src = (const hd_sp_hit*)c->sp_pin;
     tm.mark(1);
     // per DM (in parallel): the script's dm_candlist order -- by bin, widths in increasing
@@ -2936,10 +3152,19 @@ extern "C" int hd_single_pulse(hd_plan* p, double dt, double maxwidth, double th
     sp_group_by_dm(src, (int64_t)cnt, ndm, hits, dstart);
     // barycentred series: the data end where the last data segment ends (hd_plan_data_end)
     const int64_t dend = p->data_end >= 0 ? p->data_end : p->nvalid;
-    const int64_t out = sp_prune_groups(hits, dstart, ndm, widths, nw, dend, p->numout);
+    const int64_t out = sp_prune_groups(hits, dstart, ndm, sp->widths, sp->nw, dend, p->numout);
     *nhits = out;
     tm.mark(2);
     return HD_OK;
+}
+
+extern "C" int hd_single_pulse(hd_plan* p, double dt, double maxwidth, double threshold, hd_sp_hit* hits,
+                               int64_t cap, int64_t* nhits, uint8_t* bad_blocks, int64_t* nblocks_out)
+{
+    if (!p || !nhits || (cap > 0 && !hits)) return fail(p ? p->ctx : nullptr, HD_E_INVAL, "hd_single_pulse: NULL argument");
+    const int rc = hd_single_pulse_launch(p, dt, maxwidth, threshold);
+    if (rc) return rc;
+    return hd_single_pulse_collect(p, hits, cap, nhits, bad_blocks, nblocks_out);
 }
 
 extern "C" int hd_series_sum(hd_plan* p, int32_t dm, int64_t t0, int64_t count, double* sum)

@@ -83,6 +83,20 @@ __device__ __forceinline__ int16_t to_i16(float x, int sub_round)
 
 // Blocks b, b+8, b+16, ... share an XCD (round-robin dispatch; speed only, never
 // correctness): give each XCD a contiguous range of logical block ids (bijective).
+// A tile is "special" when it is the last one (reads past the end of the data) or its
+// rows straddle a masked read-block boundary.  The hot kernel (SPECIAL = false) skips those
+// tiles and runs only the CLEAN / FAST paths, which keeps its register footprint at two
+// 8-wave workgroups per CU; the few special tiles (host-built list) get a second launch.
+__device__ __host__ __forceinline__ bool s1_special(const Stage1Multi& a, int64_t tR0, int rows)
+{
+    if (tR0 + rows > a.rd.N) return true;
+    if (a.rd.zidx) {
+        const int64_t b0 = tR0 / a.rd.blk, b1 = (tR0 + rows - 1) / a.rd.blk;
+        if (b1 > b0 + a.two_ok) return true;   // the integer path takes two- (ds >= 10: three-) block tiles
+    }
+    return false;
+}
+
 __device__ __forceinline__ int xcd_remap(int b, int nb)
 {
     const int xcd = b & 7, q = nb >> 3, r = nb & 7;

@@ -62,6 +62,8 @@ struct Stage1Multi {
     double tie_eps;           // 8-bit integer path: margin the rounding of a masked subband's pad
                               // constant needs (float-fold error, plus the /ds rounding in mean mode)
     int32_t ntiles, ngroups;
+    int32_t pds[kMaxPass];          // k_stage1_q8m: per-pass downsampling
+    double ptie[kMaxPass];          // k_stage1_q8m: per-pass tie_eps (its ds)
     const int32_t* dly[kMaxPass];   // per-pass idispdt [nchan]
     void* out[kMaxPass];            // per-pass subbands [nsub][out_stride]
     int32_t* maxabs[kMaxPass];      // per-pass max |subband|
@@ -109,6 +111,11 @@ size_t stage1_q8_lds_bytes(const Stage1Multi& a);
 hipError_t stage1_q8_set_lds_limit(size_t bytes);
 hipError_t launch_stage1_q8(const Stage1Multi& a, int vb, hipStream_t st);
 bool stage1_tiled_supports_cps(int cps);
+// several DDplan stages' passes in one launch (hd_q8m.hip): quarter rows 960, ds | 960
+bool stage1_q8m_supports_ds(int ds);
+int stage1_q8m_quarter_rows();
+size_t stage1_q8m_lds_bytes(const Stage1Multi& a);
+hipError_t launch_stage1_q8m(const Stage1Multi& a, hipStream_t st);
 hipError_t stage1_tiled_set_lds_limit(size_t bytes);
 // wide stage-2 tiles: at most kSC2 subbands staged per chunk, kUMax prefetched fill units
 // per thread per chunk, at most kWideWaves waves per workgroup

@@ -212,20 +212,6 @@ __device__ __forceinline__ void form_outputs(const Stage1Multi& a, const uint8_t
     }
 }
 
-// A tile is "special" when it is the last one (reads past the end of the data) or its
-// rows straddle a masked read-block boundary.  The hot kernel (SPECIAL = false) skips those
-// tiles and runs only the CLEAN / FAST paths, which keeps its register footprint at two
-// 8-wave workgroups per CU; the few special tiles (host-built list) get a second launch.
-__device__ __host__ __forceinline__ bool s1_special(const Stage1Multi& a, int64_t tR0, int rows)
-{
-    if (tR0 + rows > a.rd.N) return true;
-    if (a.rd.zidx) {
-        const int64_t b0 = tR0 / a.rd.blk, b1 = (tR0 + rows - 1) / a.rd.blk;
-        if (b1 > b0 + a.two_ok) return true;   // the integer path takes two- (ds >= 10: three-) block tiles
-    }
-    return false;
-}
-
 template <int NBITS, int CPS, bool CALIB, int VW, bool SPECIAL>
 __global__ __launch_bounds__(512, SPECIAL ? 1 : 4)   // hot: 2 x 8-wave WGs per CU -> <= 128 VGPRs
 void k_stage1_tiled(Stage1Multi a, const int* __restrict__ special_tiles)

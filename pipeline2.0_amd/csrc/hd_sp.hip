@@ -42,7 +42,8 @@ constexpr int kSpHalo = 224;                 // >= max downfact / 2 + 1 (a boxca
 constexpr int kSpSeg = 33;                   // prefix-sum segment per thread
 constexpr int kSpWin = 256 * kSpSeg;         // kSpChunk + 2 * kSpHalo = 8448
 constexpr int kSpWords = kSpChunk / 32;      // hit bitmask words per (chunk, width)
-constexpr int kSpRound = 4;                  // widths per round: one wave walks each
+// widths per round = waves per workgroup (one wave walks each): 16 waves take the 14
+// widths > 1 of the 0.1-s downfactors in one round (4 waves: four rounds)
 constexpr int kSpSegW = 4;                   // bitmask words (128 bins) per lane segment of a walk
 
 __device__ __forceinline__ double wave_sum_f64(double v)
@@ -235,8 +236,10 @@ __device__ __forceinline__ void sp_emit(const SpArgs& a, int dm, int64_t bin, in
     }
 }
 
-__global__ __launch_bounds__(256) void k_sp_hits(SpArgs a)
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
 {
+    constexpr int kSpRound = NW;
     __shared__ double P[kSpWin + 1];
     __shared__ uint32_t bits[kSpRound][kSpWords];
     // the walk's per-width state (its space also holds the segment totals of the prefix sum):
@@ -258,15 +261,11 @@ __global__ __launch_bounds__(256) void k_sp_hits(SpArgs a)
     const int64_t c0 = (int64_t)ch * kSpChunk;               // first bin of the chunk
     const int tid = threadIdx.x;
     const int wv = tid >> 6, ln = tid & 63;
-    double loc[kSpSeg];
-    double run = 0.0;
-    // the normalised samples of the window in per-thread segments (detrended by the block's
-    // line, over its std; 0 in bad blocks and past the searched length); width 1
-    // is tested on the spot: every value above threshold outside the bad blocks is a hit (no
+    // the normalised samples of the window (detrended by the block's line, over its std; 0 in
+    // bad blocks and past the searched length), staged as doubles in P[e + 1]; width 1 is
+    // tested on the spot: every value above threshold outside the bad blocks is a hit (no
     // prune_related1), so the chunk's samples are not read and normalised a second time
-#pragma unroll
-    for (int j = 0; j < kSpSeg; j++) {
-        const int e = tid * kSpSeg + j;
+    for (int e = tid; e < kSpWin; e += NW * 64) {
         const int64_t i = w0 + e;
         float v = 0.0f;
         bool isbad = false;
@@ -280,13 +279,22 @@ __global__ __launch_bounds__(256) void k_sp_hits(SpArgs a)
                 v = (float)((double)d / c[2]);
             }
         }
-        run += (double)v;
-        loc[j] = run;
+        P[e + 1] = (double)v;
         const int o = e - kSpHalo;
         if (o >= 0 && o < kSpChunk && !isbad && !(a.probe & 2) && (double)v > a.threshold)
             sp_emit(a, dm, c0 + o, 0, (double)v);
     }
-    tot[tid] = run;
+    __syncthreads();
+    // running sums over 256 segments of kSpSeg samples (the oracle's order), in place
+    if (tid < 256) {
+        double run = 0.0;
+#pragma unroll
+        for (int j = 0; j < kSpSeg; j++) {
+            run += P[tid * kSpSeg + j + 1];
+            P[tid * kSpSeg + j + 1] = run;
+        }
+        tot[tid] = run;
+    }
     __syncthreads();
     if (tid == 0) {                                           // exclusive scan of the segment totals
         // (in order, as before; the totals are read 16 at a time so the chain waits only
@@ -308,9 +316,11 @@ __global__ __launch_bounds__(256) void k_sp_hits(SpArgs a)
         P[0] = 0.0;
     }
     __syncthreads();
-    const double base = tot[tid];
+    if (tid < 256) {
+        const double base = tot[tid];
 #pragma unroll
-    for (int j = 0; j < kSpSeg; j++) P[tid * kSpSeg + j + 1] = base + loc[j];
+        for (int j = 0; j < kSpSeg; j++) P[tid * kSpSeg + j + 1] = base + P[tid * kSpSeg + j + 1];
+    }
     __syncthreads();
     // boxcar value (width index wi > 0) at chunk bin o
     auto boxcar = [&](int wi, int o) -> double {
@@ -326,7 +336,7 @@ __global__ __launch_bounds__(256) void k_sp_hits(SpArgs a)
         // the above-threshold bins of widths r0 .. r0+nr-1 (bad blocks included: the script
         // prunes before it looks at blocks): lane = bin, one ballot per 64 bins (consecutive
         // lanes read consecutive P entries: no bank conflicts)
-        for (int t = wv; t < nr * (kSpChunk / 64); t += 4) {
+        for (int t = wv; t < nr * (kSpChunk / 64); t += NW) {
             const int j = t / (kSpChunk / 64), q = t - j * (kSpChunk / 64);
             const bool hit = !(a.probe & 4) && boxcar(r0 + j, 64 * q + ln) > a.threshold;
             const uint64_t m = __ballot(hit);
@@ -622,7 +632,11 @@ hipError_t launch_sp_hits(const float* x, int64_t stride, int ndm, int nblocks, 
     a.cap = cap;
     a.probe = getenv("HD_SP_PROBE") ? atoi(getenv("HD_SP_PROBE")) : 0;
     if (a.nchunks <= 0 || ndm <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_sp_hits, dim3((unsigned)(ndm * a.nchunks)), dim3(256), 0, st, a);
+    // HD_SP_NW=4 (profiling): the 4-wave workgroup, four rounds of widths
+    if (getenv("HD_SP_NW") && atoi(getenv("HD_SP_NW")) == 4)
+        hipLaunchKernelGGL(k_sp_hits<4>, dim3((unsigned)(ndm * a.nchunks)), dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL(k_sp_hits<16>, dim3((unsigned)(ndm * a.nchunks)), dim3(1024), 0, st, a);
     return hipGetLastError();
 }
 

@@ -39,7 +39,7 @@ EXPORTED = [
     "hd_push_raw_file", "hd_set_streams", "hd_touch_raw", "hd_stats_padvals", "hd_get_clean",
     "hd_get_subbands_window", "hd_get_series", "hd_write_series", "hd_wait_writes",
     "hd_set_slice", "hd_clip_stats", "hd_clip_set_stats", "hd_series_sum", "hd_series_fill",
-    "hd_sp_widths", "hd_single_pulse", "hd_rfifind_stats",
+    "hd_sp_widths", "hd_single_pulse", "hd_single_pulse_launch", "hd_single_pulse_collect", "hd_rfifind_stats",
     "hd_push_raw_file_band", "hd_fill_raw",
     "hd_realfft", "hd_fft_prepare", "hd_zap_ranges", "hd_zapbirds", "hd_rednoise_blocks", "hd_rednoise", "hd_get_fft",
     "hd_bary_diffbins", "hd_plan_set_bary", "hd_plan_data_end", "hd_run_dedisp_multi", "hd_plan_launch_passes", "hd_sp_prune",
@@ -185,6 +185,8 @@ def load():
         "hd_sp_widths": (ctypes.c_int, [ctypes.c_double, ctypes.c_double, P(ctypes.c_int32), P(ctypes.c_int32)]),
         "hd_single_pulse": (ctypes.c_int, [vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp, i64, P(i64),
                                            P(ctypes.c_uint8), P(i64)]),
+        "hd_single_pulse_launch": (ctypes.c_int, [vp, ctypes.c_double, ctypes.c_double, ctypes.c_double]),
+        "hd_single_pulse_collect": (ctypes.c_int, [vp, vp, i64, P(i64), P(ctypes.c_uint8), P(i64)]),
         "hd_plan_tables": (ctypes.c_int, [P(hd_obs), P(hd_opts), P(hd_pass), P(ctypes.c_int32),
                                           P(ctypes.c_int32), P(ctypes.c_double), P(ctypes.c_double),
                                           P(ctypes.c_double)]),

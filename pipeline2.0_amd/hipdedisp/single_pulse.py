@@ -52,9 +52,9 @@ def widths(dt, maxwidth):
     return [int(w[i]) for i in range(n.value)]
 
 
-def device_candidates(plan, dt, maxwidth=0.1, threshold=5.0):
-    """(candidates sorted by (dm, bin, widx) as HIT records, bad[numdms][nblocks]) of the
-    plan's series (hd_single_pulse)."""
+def _collect(plan):
+    """hd_single_pulse_collect of the plan's launched search: (HIT records sorted by (dm, bin,
+    widx), bad[numdms][nblocks])."""
     eng = plan.eng
     nb = plan.numout // 1000
     bad = np.zeros((plan.pp.numdms, max(nb, 1)), np.uint8)
@@ -62,15 +62,41 @@ def device_candidates(plan, dt, maxwidth=0.1, threshold=5.0):
     while True:
         hits = np.empty(cap, HIT)
         n, nbk = ctypes.c_int64(), ctypes.c_int64()
-        rc = eng._L.hd_single_pulse(plan._p, float(dt), float(maxwidth), float(threshold),
-                                    hits.ctypes.data_as(ctypes.c_void_p), cap, ctypes.byref(n),
-                                    bad.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), ctypes.byref(nbk))
+        rc = eng._L.hd_single_pulse_collect(plan._p, hits.ctypes.data_as(ctypes.c_void_p), cap, ctypes.byref(n),
+                                            bad.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), ctypes.byref(nbk))
         if rc == _lib.HD_E_NOMEM and n.value > cap:           # room for every device hit
             cap = int(n.value) + int(n.value) // 4
             eng._sp_cap = cap
             continue
         eng._chk(rc, "single_pulse_search.py")
         return hits[:n.value], bad[:, :nb]
+
+
+def _launch(plan, dt, maxwidth, threshold):
+    plan.eng._chk(plan.eng._L.hd_single_pulse_launch(plan._p, float(dt), float(maxwidth), float(threshold)),
+                  "single_pulse_search.py")
+
+
+def device_candidates(plan, dt, maxwidth=0.1, threshold=5.0):
+    """(candidates sorted by (dm, bin, widx) as HIT records, bad[numdms][nblocks]) of the
+    plan's series (hd_single_pulse)."""
+    _launch(plan, dt, maxwidth, threshold)
+    return _collect(plan)
+
+
+def device_candidates_many(plans, maxwidth=0.1, threshold=5.0, depth=4):
+    """device_candidates of several plans (each at its own sub_dt), yielded in order as
+    (plan, hits, bad): the device searches of the next `depth` plans are queued before a
+    plan's hits are pruned on the host, so both halves run at once."""
+    plans = list(plans)
+    for k in range(min(depth, len(plans))):
+        _launch(plans[k], plans[k].sub_dt, maxwidth, threshold)
+    for i, p in enumerate(plans):
+        if i + depth < len(plans):
+            q = plans[i + depth]
+            _launch(q, q.sub_dt, maxwidth, threshold)
+        hits, bad = _collect(p)
+        yield p, hits, bad
 
 
 def candidates(hits, wlist, dm_values, dt):

@@ -163,3 +163,47 @@ def test_candidate_lists_end_to_end_clip_vs_noclip(engine):
     assert lists[6.0] != lists[0.0]
     assert low[0.0] > 10 * max(low[6.0], 1) and len(lists[0.0]) > 5 * len(lists[6.0])
     engine.set_obs(obs, Opts())
+
+
+def test_single_pulse_launch_collect_pipelined(engine, beam):
+    """hd_single_pulse_launch / _collect: the device searches of several passes queued before
+    any host pruning (device_candidates_many) give each pass's one-shot candidates and bad
+    blocks; a launch again before the collect replaces the pending search; a collect with
+    too little room returns HD_E_NOMEM and stays collectable; a collect with nothing
+    launched is refused."""
+    import ctypes
+    from hipdedisp import _lib
+    from hipdedisp.engine import PrestoError
+    obs, s = beam
+    specs = [(350.0, 346.2, 0.1, 1, 0), (220.0, 210.0, 0.6, 2, 0), (390.0, 380.0, 0.6, 2, 0),
+             (71.0, 67.2, 0.1, 1, 0), (220.0, 210.0, 3.0, 10, (1 << 18) // 10 + 1234)]
+    plans = []
+    try:
+        for subdm, lodm, dmstep, ds, numout in specs:
+            p, _ = run(engine, obs, subdm, lodm, dmstep, ds, numout)
+            plans.append(p)
+        want = [SP.device_candidates(p, p.sub_dt, 0.1, 5.0) for p in plans]
+        assert sum(len(w[0]) for w in want) > 100
+        for depth in (1, 4, 8):
+            got = list(SP.device_candidates_many(plans, 0.1, 5.0, depth=depth))
+            assert [g[0] for g in got] == plans
+            for (_, h, b), (wh, wb) in zip(got, want):
+                assert np.array_equal(h, wh) and np.array_equal(b, wb)
+        p = plans[0]
+        SP._launch(p, p.sub_dt, 0.1, 3.0)                     # replaced before its collect
+        SP._launch(p, p.sub_dt, 0.1, 5.0)
+        h, b = SP._collect(p)
+        assert np.array_equal(h, want[0][0]) and np.array_equal(b, want[0][1])
+        SP._launch(p, p.sub_dt, 0.1, 5.0)
+        small = np.empty(1, SP.HIT)
+        n, nbk = ctypes.c_int64(), ctypes.c_int64()
+        rc = engine._L.hd_single_pulse_collect(p._p, small.ctypes.data_as(ctypes.c_void_p), 1, ctypes.byref(n),
+                                               None, ctypes.byref(nbk))
+        assert rc == _lib.HD_E_NOMEM and n.value > 1
+        h, b = SP._collect(p)                                   # still pending
+        assert np.array_equal(h, want[0][0])
+        with pytest.raises(PrestoError, match="no search launched"):
+            SP._collect(p)
+    finally:
+        for p in plans:
+            p.destroy()
