@@ -317,6 +317,10 @@ HD_API int hd_get_series(hd_plan* plan, int32_t dm0, int32_t ndm, int64_t t0, in
  * [t0, numout) of every DM with value -- the padding of a time-sliced pass, whose value
  * (prepsubband's first-DM mean) is the observation's, not the slice's.                 */
 HD_API int hd_series_sum(hd_plan* plan, int32_t dm, int64_t t0, int64_t count, double* sum);
+/* hd_series_sum of n plans (one context) at once: sums[i] = the sum over samples
+ * [t0[i], t0[i]+count[i]) of DM dm of plans[i] -- the same doubles, one device wait.     */
+HD_API int hd_series_sum_multi(hd_plan* const* plans, int32_t n, int32_t dm, const int64_t* t0, const int64_t* count,
+                               double* sums);
 HD_API int hd_series_fill(hd_plan* plan, int64_t t0, float value);
 
 /* ---- barycentric output (prepsubband without -nobary) ---------------------------------

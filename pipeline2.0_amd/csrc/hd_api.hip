@@ -116,6 +116,8 @@ struct hd_ctx {
     size_t sp_pin_bytes = 0;
     int64_t sp_cap_hint = 1 << 16;
     double* d_sum_parts = nullptr;  // hd_series_sum partials
+    double* d_sum_parts_multi = nullptr;   // hd_series_sum_multi partials [n][512]
+    size_t sum_parts_bytes = 0;
     // streaming ingest (hd_push_raw_file): pinned host blocks of the reader threads
     PinSet pins;
     // stage 2 alternates between the main stream and stream2, so one pass's last tiles and
@@ -280,6 +282,7 @@ struct SpPlan {
 
 static thread_local std::string g_err;
 static void clear_special_cache(hd_ctx* c);
+static int s2_swait();
 
 static int fail(hd_ctx* ctx, int code, const char* fmt, ...)
 {
@@ -453,6 +456,7 @@ extern "C" int hd_close(hd_ctx* c)
     if (c->sp_pin) (void)hipHostFree(c->sp_pin);
     if (c->ssp) (void)hipStreamDestroy(c->ssp);
     dfree(c->d_sum_parts);
+    dfree(c->d_sum_parts_multi);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_aux0) (void)hipEventDestroy(c->ev_aux0);
     if (c->ev_aux1) (void)hipEventDestroy(c->ev_aux1);
@@ -2566,7 +2570,7 @@ static int run_subband_fused(hd_ctx* c, hd_plan** plans, int n)
     m.W = S + ((dmax + 15) & ~15);
     m.cps = cps;
     if (hd::stage1_q8m_lds_bytes(m) > 160 * 1024) return 1;     // 1: does not apply (per-stage launches)
-    if (c->obs.nbits != 8 && !alloc_rawT(c, dmax)) return 1;
+    if (!alloc_rawT(c, dmax)) return 1;                          // (the fill reads the channel-major copy)
     int rc0 = ensure_blocks(c);
     if (rc0) return rc0;
     for (int i = 0; i < n; i++) HIPCHK(c, hipMemsetAsync(plans[i]->d_maxabs, 0, sizeof(int32_t), c->stream));
@@ -2610,7 +2614,8 @@ static int run_subband_fused(hd_ctx* c, hd_plan** plans, int n)
     int rc = special_tiles(c, m, &d_sp, &nsp);
     if (rc) return rc;
     HIPCHK(c, hd::launch_stage1_q8m(m, c->stream));
-    // per DDplan stage (ds): the special tiles on the float kernel, then the fixups
+    // per DDplan stage (ds): the special tiles on the float kernel
+    std::vector<hd::Stage1Multi> groups;
     for (int i0 = 0; i0 < n;) {
         int i1 = i0;
         while (i1 < n && plans[i1]->pass.ds == plans[i0]->pass.ds) i1++;
@@ -2633,6 +2638,7 @@ static int run_subband_fused(hd_ctx* c, hd_plan** plans, int n)
             hd::Stage1Multi f = g;
             int fvw = 4;
             f.dmax = dmax;                            // the fused tiles' rows: 4 S + dmax
+            f.to = 4 * S / ds;                        // (tile t: outputs from t * to, raw rows from t * 4 S)
             if (!stage1_tiling_fixed(c, nsub, ds, dmax, 4 * S / ds, f, fvw))
                 return fail(c, HD_E_INVAL, "stage 1: no float tiling for the fused launch's special tiles (ds %d)", ds);
             f.ntiles = m.ntiles;
@@ -2643,9 +2649,27 @@ static int run_subband_fused(hd_ctx* c, hd_plan** plans, int n)
             }
             HIPCHK(c, hd::launch_stage1_tiled(f, fvw, d_sp, nsp, true, c->stream));
         }
-        if (clip)
-            HIPCHK(c, hd::launch_stage1_fixup(g, c->clip.events, c->clip.nevents, g.rd.zidx != nullptr, c->stream));
+        groups.push_back(g);
         i0 = i1;
+    }
+    // the clipped-spectrum and block-boundary outputs of every pass in one k_stage1_fix8 launch
+    // (per-pass ds: one raw window per item for all the stages), else per DDplan stage
+    if (clip) {
+        hd::Stage1Multi fx = m;
+        fx.ds = 0;
+        for (int i = 0; i < n; i++) fx.ds = std::max(fx.ds, (int)m.pds[i]);
+        fx.pass_ds = 1;
+        fx.nds = c->obs.N / fx.ds;
+        const bool env_off = getenv("HD_FIX8M") && atoi(getenv("HD_FIX8M")) == 0;
+        const hipError_t e = env_off ? hipErrorNotSupported
+                                     : hd::launch_stage1_fixup(fx, c->clip.events, c->clip.nevents, fx.rd.zidx != nullptr,
+                                                               c->stream);
+        if (e == hipErrorNotSupported) {
+            for (const auto& g : groups)
+                HIPCHK(c, hd::launch_stage1_fixup(g, c->clip.events, c->clip.nevents, g.rd.zidx != nullptr, c->stream));
+        } else {
+            HIPCHK(c, e);
+        }
     }
     HIPCHK(c, hipEventRecord(p0->ev[1], c->stream));
     for (int i = 0; i < n; i++) {
@@ -3194,6 +3218,53 @@ extern "C" int hd_series_sum(hd_plan* p, int32_t dm, int64_t t0, int64_t count, 
     return HD_OK;
 }
 
+extern "C" int hd_series_sum_multi(hd_plan* const* plans, int32_t n, int32_t dm, const int64_t* t0, const int64_t* count,
+                                   double* sums)
+{
+    if (n < 0 || (n > 0 && (!plans || !t0 || !count || !sums)))
+        return fail(nullptr, HD_E_INVAL, "hd_series_sum_multi: bad argument");
+    if (n == 0) return HD_OK;
+    hd_ctx* c = plans[0] ? plans[0]->ctx : nullptr;
+    for (int i = 0; i < n; i++) {
+        const hd_plan* p = plans[i];
+        if (!p || p->ctx != c) return fail(c, HD_E_INVAL, "hd_series_sum_multi: plan %d is NULL or of another context", i);
+        if (!p->ran_dd || !p->d_out) return fail(c, HD_E_STATE, "hd_series_sum_multi: plan %d: run hd_run_dedisp first", i);
+        if (dm < 0 || dm >= p->pass.numdms || t0[i] < 0 || count[i] < 0 || t0[i] + count[i] > p->numout)
+            return fail(c, HD_E_INVAL, "hd_series_sum_multi: plan %d: window outside [%d DMs] x [0, %lld)", i,
+                        p->pass.numdms, (long long)p->numout);
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    // hd_series_sum's partials (512 per series, summed on the host in index order: the same
+    // doubles), every series' kernel queued on the main stream behind that plan's stage 2,
+    // then one copy and one wait for all of them
+    constexpr int kParts = 512;
+    const size_t need = (size_t)n * kParts * sizeof(double);
+    if (c->sum_parts_bytes < need) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        dfree(c->d_sum_parts_multi);
+        c->d_sum_parts_multi = nullptr;
+        c->sum_parts_bytes = 0;
+        HIPCHK(c, hipMalloc(&c->d_sum_parts_multi, need));
+        c->sum_parts_bytes = need;
+    }
+    HIPCHK(c, hipMemsetAsync(c->d_sum_parts_multi, 0, need, c->stream));
+    for (int i = 0; i < n; i++) {
+        hd_plan* p = plans[i];
+        if (count[i] == 0) continue;
+        if (p->dd_stream && p->dd_stream != c->stream) HIPCHK(c, hipStreamWaitEvent(c->stream, p->ev[3], 0));
+        HIPCHK(c, hd::launch_series_sum(p->d_out + (size_t)dm * p->out_stride + t0[i], count[i],
+                                        c->d_sum_parts_multi + (size_t)i * kParts, kParts, c->stream));
+    }
+    std::vector<double> h((size_t)n * kParts);
+    HIPCHK(c, d2h(h.data(), c->d_sum_parts_multi, need, c->stream));
+    for (int i = 0; i < n; i++) {
+        double acc = 0.0;
+        for (int k = 0; k < kParts; k++) acc += h[(size_t)i * kParts + k];
+        sums[i] = count[i] ? acc : 0.0;
+    }
+    return HD_OK;
+}
+
 extern "C" int hd_series_fill(hd_plan* p, int64_t t0, float value)
 {
     if (!p) return fail(nullptr, HD_E_INVAL, "hd_series_fill: NULL plan");
@@ -3477,6 +3548,7 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         a.dms_per_blk = w.dpb;
         a.sc = w.sc;
         a.probe = p->probe;
+        a.swait = s2_swait();
         a.ring_npw = w.npw;
         a.ring_nbp = w.nbp;
         a.ptab = w.d_omin;
@@ -3535,6 +3607,13 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
 // stage) share a launch of at most kS2MaxPass passes, the rest run one by one.
 // The kernel a plan takes in a shared launch: 5 (k_stage2_rw: variant 8), 4 (the
 // two-pairs-per-chunk pair kernel: auto or variant 7), or -1 (alone).
+// k_stage2_pair's relaxed store wait (Stage2Args::swait); HD_S2_SWAIT=0 restores the full wait
+static int s2_swait()
+{
+    static const int v = getenv("HD_S2_SWAIT") ? (atoi(getenv("HD_S2_SWAIT")) != 0) : 1;
+    return v;
+}
+
 static int dedisp_multi_kernel(const hd_plan* p)
 {
     const bool pair_bound = p->sub_bound >= 0 && 2 * p->sub_bound <= 32767;
@@ -3625,6 +3704,7 @@ static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
     a.dms_per_blk = w0.dpb;
     a.sc = w0.sc;
     a.probe = p0->probe;
+    a.swait = s2_swait();
     a.ring_npw = w0.npw;
     a.ring_nbp = w0.nbp;
     a.ptab = w0.d_omin;

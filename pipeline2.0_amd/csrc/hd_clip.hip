@@ -754,9 +754,9 @@ struct Fix8Geom {
 template <int CPS, int DS>
 __device__ __forceinline__ float fix8_fold_pre(const Stage1Multi& a, const uint8_t* lraw, const uint8_t* flg,
                                                const float* pad, int Wp, int G, int lc0, const int (&dr)[CPS],
-                                               uint32_t zb, int trel, int bndrel)
+                                               uint32_t zb, int trel, int bndrel, int dsr)
 {
-    const int ds = DS ? DS : a.ds;
+    const int ds = DS ? DS : dsr;
     float acc = 0.0f;
 #pragma unroll 1
     for (int k = 0; k < ds; k++) {
@@ -786,11 +786,11 @@ __device__ __forceinline__ float fix8_fold_pre(const Stage1Multi& a, const uint8
 template <int CPS, int DS>
 __device__ __forceinline__ float fix8_fold(const Stage1Multi& a, const uint8_t* lraw, const uint8_t* flg,
                                            const uint8_t* zap, const float* pad, const int16_t* dl, int Wp, int G,
-                                           int lc0, int trel, int bndrel)
+                                           int lc0, int trel, int bndrel, int dsr)
 {
     // runtime cps / ds (the templated cases take fix8_fold_pre); trel = j*ds - wlo: window row
     // of (k = 0, delay 0); dl: this pass's delays of the chunk
-    const int ds = DS ? DS : a.ds, cps = CPS ? CPS : a.cps;
+    const int ds = DS ? DS : dsr, cps = CPS ? CPS : a.cps;
     float acc = 0.0f;
     for (int k = 0; k < ds; k++) {
         float sk = 0.0f;
@@ -808,6 +808,8 @@ __device__ __forceinline__ float fix8_fold(const Stage1Multi& a, const uint8_t* 
     return acc;
 }
 
+// DS > 0: compile-time ds; 0: a.ds; -1: per pass (a.pds[p], the fused k_stage1_q8m launch's
+// passes of several DDplan stages: one window per item, of the widest stage)
 template <int CPS, int DS>
 __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm, const int32_t* __restrict__ events,
                                                     const int32_t* __restrict__ nevents, int boundaries)
@@ -816,7 +818,7 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
     //              | lo, cnt [npass][SG] (boundary items)
     extern __shared__ __attribute__((aligned(16))) char fsm[];
     const int G = gm.G, Wp = gm.Wp, SG = gm.SG, npass = a.npass;
-    const int cps = CPS ? CPS : a.cps, ds = DS ? DS : a.ds;
+    const int cps = CPS ? CPS : a.cps, ds = DS > 0 ? DS : a.ds;   // (DS -1: the largest pass ds)
     uint8_t* lraw = (uint8_t*)fsm;
     uint8_t* flg = lraw + G * Wp;
     float* pad = (float*)(flg + Wp);                      // Wp is a multiple of 16
@@ -831,10 +833,14 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
     // pass made every task wait for two global loads of the argument block before its store
     __shared__ char* outp_s[kMaxPass];
     __shared__ int64_t ostr_s[kMaxPass];
+    __shared__ int pds_s[kMaxPass];
     if (threadIdx.x < npass) {
         outp_s[threadIdx.x] = (char*)a.out[threadIdx.x];
         ostr_s[threadIdx.x] = a.ostride[threadIdx.x];
+        pds_s[threadIdx.x] = DS < 0 ? a.pds[threadIdx.x] : ds;
     }
+    // a pass's ds and output count
+    auto pds = [&](int p) { return DS > 0 ? DS : DS == 0 ? ds : pds_s[p]; };
     const int fprobe = boundaries >> 8;                   // HD_FIX8_PROBE (profiling): 1 no folds, 2 no window
     boundaries &= 1;
     const int nev = *nevents;
@@ -880,9 +886,10 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
                     maxd = max(maxd, d);
                     need |= zap[lc] && zap[G + lc] && pad[lc] != pad[G + lc];
                 }
-                int lo = r - (ds - 1) - maxd, hi = r - 1 - mind;
-                lo = lo <= 0 ? 0 : (lo + ds - 1) / ds;
-                hi = hi < 0 ? -1 : min(hi / ds, nds - 1);
+                const int dsp = pds(p), ndsp = DS < 0 ? N / dsp : nds;
+                int lo = r - (dsp - 1) - maxd, hi = r - 1 - mind;
+                lo = lo <= 0 ? 0 : (lo + dsp - 1) / dsp;
+                hi = hi < 0 ? -1 : min(hi / dsp, ndsp - 1);
                 lo_s[i] = lo;
                 cnt_s[i] = need && hi >= lo ? hi - lo + 1 : 0;
                 if (cnt_s[i]) needany = 1;
@@ -923,6 +930,7 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
                 const int p = i / G, lc = i - p * G;
                 const int16_t* dl = dly + p * G;
                 const int lc0 = lc - lc % cps;
+                const int dsp = pds(p), ndsp = DS < 0 ? N / dsp : nds;
                 int j;
                 float acc;
                 if constexpr (CPS > 0) {
@@ -940,26 +948,28 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
                     }
                     const int jn = r - dlc;
                     if (jn < 0) continue;
-                    j = jn / ds;
-                    if (j >= nds) continue;
+                    j = jn / dsp;
+                    if (j >= ndsp) continue;
                     // delays fall with frequency within a subband, so the outputs its channels
                     // map r to rise with the channel and equal ones are adjacent: only channel
                     // lc - 1 can name j first
                     if (ci > 0) {
                         const int jn2 = r - dpv;
-                        if (jn2 >= 0 && jn2 / ds == j) continue;
+                        if (jn2 >= 0 && jn2 / dsp == j) continue;
                     }
-                    acc = fix8_fold_pre<CPS, DS>(a, lraw, flg, pad, Wp, G, lc0, dr, zb, j * ds - wlo, bndrel);
+                    acc = fix8_fold_pre<CPS, (DS > 0 ? DS : 0)>(a, lraw, flg, pad, Wp, G, lc0, dr, zb, j * dsp - wlo,
+                                                               bndrel, dsp);
                 } else {
                     const int jn = r - dl[lc];
                     if (jn < 0) continue;
-                    j = jn / ds;
-                    if (j >= nds) continue;
+                    j = jn / dsp;
+                    if (j >= ndsp) continue;
                     if (lc > lc0) {
                         const int jn2 = r - dl[lc - 1];
-                        if (jn2 >= 0 && jn2 / ds == j) continue;
+                        if (jn2 >= 0 && jn2 / dsp == j) continue;
                     }
-                    acc = fix8_fold<CPS, DS>(a, lraw, flg, zap, pad, dl, Wp, G, lc0, j * ds - wlo, bndrel);
+                    acc = fix8_fold<CPS, (DS > 0 ? DS : 0)>(a, lraw, flg, zap, pad, dl, Wp, G, lc0, j * dsp - wlo, bndrel,
+                                                           dsp);
                 }
                 const int s = (c0 + lc0) / cps;
                 if (a.sub_dtype == 0) {
@@ -978,14 +988,17 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
                 const int p = ps / SG, sl = ps - p * SG;
                 const int j = lo_s[ps] + jj;
                 const int16_t* dl = dly + p * G;
+                const int dsp = pds(p);
                 float acc;
                 if constexpr (CPS > 0) {
                     int dr[CPS];
 #pragma unroll
                     for (int cc = 0; cc < CPS; cc++) dr[cc] = dl[sl * CPS + cc];
-                    acc = fix8_fold_pre<CPS, DS>(a, lraw, flg, pad, Wp, G, sl * CPS, dr, zbm_s[sl], j * ds - wlo, bndrel);
+                    acc = fix8_fold_pre<CPS, (DS > 0 ? DS : 0)>(a, lraw, flg, pad, Wp, G, sl * CPS, dr, zbm_s[sl],
+                                                               j * dsp - wlo, bndrel, dsp);
                 } else {
-                    acc = fix8_fold<CPS, DS>(a, lraw, flg, zap, pad, dl, Wp, G, sl * cps, j * ds - wlo, bndrel);
+                    acc = fix8_fold<CPS, (DS > 0 ? DS : 0)>(a, lraw, flg, zap, pad, dl, Wp, G, sl * cps, j * dsp - wlo,
+                                                           bndrel, dsp);
                 }
                 const int s = chunk * SG + sl;
                 if (a.sub_dtype == 0) {
@@ -1045,7 +1058,10 @@ static bool fix8_geom(const Stage1Multi& a, Fix8Geom& g)
     if (!g.SG) return false;
     g.G = g.SG * a.cps;
     g.nchunk = a.nsub / g.SG;
-    g.jmax = (a.dmax + a.ds - 1) / a.ds + 1;
+    int dsmin = a.ds;
+    if (a.pass_ds)
+        for (int p = 0; p < a.npass; p++) dsmin = std::min(dsmin, (int)a.pds[p]);
+    g.jmax = (a.dmax + dsmin - 1) / dsmin + 1;
     return true;
 }
 
@@ -1064,6 +1080,9 @@ hipError_t launch_stage1_fixup(const Stage1Multi& a, const int32_t* events, cons
         HD_F8(10, 1) HD_F8(10, 2) HD_F8(10, 3) HD_F8(10, 5) HD_F8(10, 6) HD_F8(10, 10)
         HD_F8(8, 1) HD_F8(16, 1)
 #undef HD_F8
+        if (a.pass_ds)                                    // several DDplan stages' passes
+            fn = a.cps == 10 ? (const void*)k_stage1_fix8<10, -1> : a.cps == 8 ? (const void*)k_stage1_fix8<8, -1>
+               : a.cps == 16 ? (const void*)k_stage1_fix8<16, -1> : (const void*)k_stage1_fix8<0, -1>;
         if (lb > 64 * 1024) {
             const hipError_t e = set_max_lds(fn, (int)lb);
             if (e != hipSuccess) return e;
@@ -1072,6 +1091,7 @@ hipError_t launch_stage1_fixup(const Stage1Multi& a, const int32_t* events, cons
         void* args[] = {(void*)&a, (void*)&g, (void*)&events, (void*)&nevents, (void*)&boundaries};
         return hipLaunchKernel(fn, dim3(grid), dim3(256), args, lb, st);
     }
+    if (a.pass_ds) return hipErrorNotSupported;       // (the caller launches per DDplan stage)
     // boundary items scan one subband per thread (nsub <= blockDim); clipped-spectrum items loop
     // over channels, so any nsub (e.g. the nsub = nchan no-subband pass) takes them
     if ((boundaries && a.nsub > 256) || a.rd.N >= ((int64_t)1 << 31) - (1 << 24)) return hipErrorInvalidValue;

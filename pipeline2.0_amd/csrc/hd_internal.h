@@ -62,7 +62,8 @@ struct Stage1Multi {
     double tie_eps;           // 8-bit integer path: margin the rounding of a masked subband's pad
                               // constant needs (float-fold error, plus the /ds rounding in mean mode)
     int32_t ntiles, ngroups;
-    int32_t pds[kMaxPass];          // k_stage1_q8m: per-pass downsampling
+    int32_t pass_ds;                // k_stage1_fix8: 1 = per-pass ds in pds[] (ds = their max)
+    int32_t pds[kMaxPass];          // k_stage1_q8m / pass_ds: per-pass downsampling
     double ptie[kMaxPass];          // k_stage1_q8m: per-pass tie_eps (its ds)
     const int32_t* dly[kMaxPass];   // per-pass idispdt [nchan]
     void* out[kMaxPass];            // per-pass subbands [nsub][out_stride]
@@ -93,6 +94,8 @@ struct Stage2Args {
     int32_t sc;               // wide variant: subbands per LDS chunk
     int32_t ring_npw, ring_nbp;   // ring variant: 1 KiB DMA pieces per window / per offset block
     int32_t probe;            // profiling only: bit0 skip accumulation, bit1 skip fill, bit2 skip stores
+    int32_t swait;            // k_stage2_pair: 1 = a tile's series stores may still be in flight at
+                              // the next chunk's DMA wait (only loader waves wait, past them)
     // pair variant: per (y-block, subband pair) {base0, b1, U, k1[0..U)} (kPairTab ints) and
     // the largest U of the plan (expanded copies per pair = 4*umax)
     const int32_t* ptab;

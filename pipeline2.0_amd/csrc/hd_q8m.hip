@@ -136,9 +136,13 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
                 const int t = (lane + 64 * m) * DS + k;    // quarter-relative raw row
                 uint32_t pe = 0, po = 0;
                 float sk[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
+                // (channel loop not unrolled: each channel's LDS row and delay re-derived)
+#pragma unroll 1
                 for (int cc = 0; cc < CPS; cc++) {
-                    const uint32_t x = lbase[lrb[cc] + dl[cc] + m * 64 * DS + k];
+                    const int lr = a.rd.flip ? a.sg * CPS - 1 - (cbase - (cbase / (a.sg * CPS)) * (a.sg * CPS) + cc)
+                                             : cbase - (cbase / (a.sg * CPS)) * (a.sg * CPS) + cc;
+                    const int dcc = a.dly[p][cbase + cc];
+                    const uint32_t x = lbase[lr * a.W + dcc + m * 64 * DS + k];
                     if (cc < fz) {
                         pe += x & 0x00FF00FFu;
                         po += __builtin_amdgcn_perm(0u, x, 0x0c030c01u);
@@ -152,7 +156,7 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
                         float v[4] = {(float)(x & 0xFFu), (float)((x >> 8) & 0xFFu), (float)((x >> 16) & 0xFFu),
                                       (float)(x >> 24)};
                         if (zany & (1u << cc)) {
-                            const int rr = t + dl[cc];
+                            const int rr = t + dcc;
                             const bool za = (z0 >> cc) & 1, zb = (z1 >> cc) & 1, zc = (z2 >> cc) & 1;
 #pragma unroll
                             for (int q = 0; q < 4; q++) {
@@ -187,7 +191,7 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
 }
 
 template <int CPS>
-__global__ __launch_bounds__(256, 2) void k_stage1_q8m(Stage1Multi a)
+__global__ __launch_bounds__(256, 3) void k_stage1_q8m(Stage1Multi a)
 {
     constexpr int S = kQ8mS;
     extern __shared__ __attribute__((aligned(16))) char smem[];

@@ -348,6 +348,16 @@ class Engine:
     def plan(self, pp: PassParams):
         return Plan(self, pp)
 
+    def series_sums(self, plans, dm, t0, count):
+        """hd_series_sum of several plans in one call (hd_series_sum_multi): float64 array."""
+        n = len(plans)
+        arr = (ctypes.c_void_p * max(n, 1))(*[p._p for p in plans])
+        a0 = (ctypes.c_int64 * max(n, 1))(*[int(x) for x in t0])
+        a1 = (ctypes.c_int64 * max(n, 1))(*[int(x) for x in count])
+        out = (ctypes.c_double * max(n, 1))()
+        self._chk(self._L.hd_series_sum_multi(arr, n, int(dm), a0, a1, out), "hd_series_sum_multi")
+        return np.array(out[:n], np.float64)
+
     def run_subband_multi(self, plans):
         """Stage 1 of several passes of one DDplan stage from one read of the raw block."""
         arr = (ctypes.c_void_p * len(plans))(*[p._p.value for p in plans])

@@ -260,7 +260,10 @@ class TimeSlices:
     def pass_sums(self, rank, plans):
         """Phase C: per plan, the exact sum of the first DM's owned output samples (the
         padding value of prepsubband is the observation's first-DM mean)."""
-        return np.array([p.series_sum(0, 0, self.out_range(rank, p.pp.ds)[1]) for p in plans], np.float64)
+        if not plans:
+            return np.zeros(0, np.float64)
+        return plans[0].eng.series_sums(plans, 0, [0] * len(plans),
+                                        [self.out_range(rank, p.pp.ds)[1] for p in plans])
 
     def pad_passes(self, rank, plans, sums):
         """Phase D (after summing pass_sums over the ranks): the last rank pads its series

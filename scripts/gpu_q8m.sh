@@ -10,6 +10,7 @@ rc=$?; echo "pytest rc=$rc" >> gpurun_out/q8m_tests.log
 [ $rc -eq 0 ] || { echo "pytest rc=$rc"; tail -60 gpurun_out/q8m_tests.log; exit 1; }
 tail -2 gpurun_out/q8m_tests.log
 bash scripts/ab_args.sh "" "--s1-per-stage" > gpurun_out/ab_q8m.txt 2>&1 || { echo "ab failed"; cat gpurun_out/ab_q8m.txt; exit 1; }
+bash scripts/ab_env.sh HD_FIX8M=0 >> gpurun_out/ab_q8m.txt 2>&1 || { echo "ab env failed"; cat gpurun_out/ab_q8m.txt; exit 1; }
 cat gpurun_out/ab_q8m.txt
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_q8m -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu \
     --e2e-beams 0 --sp-beams 0 --fft-beams 0 --rfi-beams 0 --stream-beams 0 > gpurun_out/prof_q8m.log 2>&1 || { echo "rocprof failed"; tail -20 gpurun_out/prof_q8m.log; exit 1; }

@@ -27,7 +27,7 @@ print("probe %s: %.3f s/beam, %d candidates/beam | %s" % (pr, line["single_pulse
 PY
 done
 cat gpurun_out/sp_split.txt
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sp -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_sp -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu \
     --e2e-beams 0 --fft-beams 0 --rfi-beams 0 --stream-beams 0 --sp-beams 1 > gpurun_out/prof_sp.log 2>&1 || { echo "rocprof failed"; tail -20 gpurun_out/prof_sp.log; exit 1; }
 for f in $(find gpurun_out/prof_sp -name "*kernel_stats.csv"); do cp "$f" gpurun_out/sp_kernel_stats.csv; done
 echo "sp done"

@@ -1,8 +1,9 @@
 """Stage 1 of several DDplan stages in one call (hd_run_subband_multi with mixed ds): the
 passes of every stage with ds in {2, 3, 5, 6, 10} share one k_stage1_q8m launch (tiles of
 4 x 960 raw rows, one channel-major fill for all of them), then per stage the float kernel's
-special tiles and the clipped-spectrum / block-boundary fixups.  Every pass must equal its
-own oracle run, and the per-stage launches (HD_Q8M=0) -- over 8/4-bit data, flipped bands,
+special tiles, and one k_stage1_fix8 launch (per-pass ds) for the clipped-spectrum /
+block-boundary outputs of all of them.  Every pass must equal its own oracle run, the
+per-stage fixups (HD_FIX8M=0) and the per-stage launches (HD_Q8M=0) -- over 8/4-bit data, flipped bands,
 int16 and float32 subbands, mean and sum downsampling, masks whose blocks a tile crosses
 (two- and three-block tiles, and wider ones on the special list), cps 8 / 10 / 16."""
 import numpy as np
@@ -34,15 +35,16 @@ def subband_launches(plans):
     return sum(1 for p in plans if p.last_ms()[0] > 0.0)
 
 
-@pytest.mark.parametrize("nbits,nsub,flip,sub_dtype,ds_mode,pts", [
-    (8, 96, False, 0, 1, 8192),        # the bench's case: mean, int16, mask blocks of 8192 rows
-    (8, 96, True, 0, 0, 2048),         # tiles across 3+ blocks: special list and 3-block tiles
-    (8, 120, False, 1, 1, 0),          # cps 8, float32 subbands, no mask
-    (8, 60, True, 1, 0, 4096),         # cps 16
-    (4, 96, False, 0, 1, 8192),        # 4-bit data through its unpacked channel-major copy
+@pytest.mark.parametrize("nbits,nsub,flip,sub_dtype,ds_mode,pts,extra", [
+    (8, 96, False, 0, 1, 8192, 776),   # the bench's case: mean, int16, mask blocks of 8192 rows
+    (8, 96, True, 0, 0, 2048, 776),    # tiles across 3+ blocks: special list and 3-block tiles
+    (8, 120, False, 1, 1, 0, 776),     # cps 8, float32 subbands, no mask
+    (8, 60, True, 1, 0, 4096, 776),    # cps 16 (ds 10 exceeds its packed sums: per-stage launch)
+    (4, 96, False, 0, 1, 8192, 776),   # 4-bit data through its unpacked channel-major copy
+    (8, 96, False, 0, 1, 8192, 777),   # N % 4 != 0: no channel-major copy, per-stage launches
 ])
-def test_fused_stage1_bitexact(engine, monkeypatch, nbits, nsub, flip, sub_dtype, ds_mode, pts):
-    N = (1 << 19) + 776 if nbits == 4 else (1 << 19) + 777
+def test_fused_stage1_bitexact(engine, monkeypatch, nbits, nsub, flip, sub_dtype, ds_mode, pts, extra):
+    N = (1 << 19) + extra
     obs = palfa_obs(N=N, nbits=nbits, flip=flip)
     opts = Opts(sub_dtype=sub_dtype, ds_mode=ds_mode)
     s = palfa_synth(nbits=nbits)
@@ -59,11 +61,17 @@ def test_fused_stage1_bitexact(engine, monkeypatch, nbits, nsub, flip, sub_dtype
         engine.run_subband_multi(plans)
         engine.sync()
         fused = [p.get_subbands() for p in plans]
-        assert subband_launches(plans) == 2             # ds 1 alone, then one launch for ds >= 2
+        # ds 1 alone, then one launch for the ds >= 2 stages the fused kernel takes
+        assert subband_launches(plans) == (6 if N % 4 else 3 if nsub == 60 else 2)
         cl = OR.prepare(obs, opts, raw, mask=mask, ptsperint=pts, padvals=pad, omp=True)
         for pp, g in zip(pps, fused):
             want = OR.stage1(obs, opts, raw, nsub, pp.ds, pp.subdm, clean=cl, omp=True)
             assert np.array_equal(g, want), (pp.ds, pp.subdm)
+        monkeypatch.setenv("HD_FIX8M", "0")                  # fixups per DDplan stage
+        engine.run_subband_multi(plans)
+        engine.sync()
+        for p, g in zip(plans, fused):
+            assert np.array_equal(p.get_subbands(), g)
         monkeypatch.setenv("HD_Q8M", "0")
         engine.run_subband_multi(plans)
         engine.sync()
@@ -80,7 +88,7 @@ def test_fused_stage1_bitexact(engine, monkeypatch, nbits, nsub, flip, sub_dtype
 def test_fused_stage1_then_stage2_repeated_beams(engine):
     """The bench's order (one fused stage-1 call, then every stage's stage-2 launch) over
     alternating beams: the series equal the per-stage schedule's."""
-    N = (1 << 19) + 777
+    N = (1 << 19) + 776
     obs = palfa_obs(N=N, nbits=8)
     engine.set_obs(obs, Opts())
     synths = [palfa_synth(beam=0), palfa_synth(beam=1)]

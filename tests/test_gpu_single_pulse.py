@@ -175,6 +175,8 @@ def test_single_pulse_launch_collect_pipelined(engine, beam):
     from hipdedisp import _lib
     from hipdedisp.engine import PrestoError
     obs, s = beam
+    engine.set_obs(obs, Opts())                   # (an earlier test may have replaced the beam)
+    engine.synth_device(s)
     specs = [(350.0, 346.2, 0.1, 1, 0), (220.0, 210.0, 0.6, 2, 0), (390.0, 380.0, 0.6, 2, 0),
              (71.0, 67.2, 0.1, 1, 0), (220.0, 210.0, 3.0, 10, (1 << 18) // 10 + 1234)]
     plans = []

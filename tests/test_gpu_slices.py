@@ -90,6 +90,12 @@ def test_time_slices_union_equals_whole_beam(engine, world):
                     p.run_dedisp(to_host=False)
                 mine += ps
             plans.append(mine)
+        for r in range(world):                                             # the batched sums (one wait)
+            one = [p.series_sum(0, 0, ts.out_range(r, p.pp.ds)[1]) for p in plans[r]]
+            assert list(ts.pass_sums(r, plans[r])) == one
+            mid = [p.numout // 3 for p in plans[r]]
+            assert list(plans[r][0].eng.series_sums(plans[r], 1, mid, mid)) == \
+                [p.series_sum(1, m, m) for p, m in zip(plans[r], mid)]
         sums = sum(ts.pass_sums(r, plans[r]) for r in range(world))      # phase C + all-reduce
         for r in range(world):
             ts.pad_passes(r, plans[r], sums)                               # phase D
