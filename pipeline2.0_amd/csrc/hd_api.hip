@@ -112,6 +112,7 @@ struct hd_ctx {
     // single-pulse search: the host half's copy stream, pinned staging of the hits / flags
     // D2H, and the largest device hit count seen (the next plans' first list size)
     hipStream_t ssp = nullptr;
+    std::vector<struct SpBufs*> sp_free, sp_all;   // search buffer sets (free / every one made)
     void* sp_pin = nullptr;
     size_t sp_pin_bytes = 0;
     int64_t sp_cap_hint = 1 << 16;
@@ -258,11 +259,10 @@ struct hd_plan {
     struct SpPlan* sp = nullptr;    // single-pulse search state (hd_single_pulse_launch / _collect)
 };
 
-// A plan's single-pulse search in flight: the device half (block statistics, boxcar hits,
-// prune_related1, bad flags) launched on the plan's stream and marked by ev; the host half
-// (copies, prune_related2, border cases) waits for ev only, on the context's ssp stream, so
-// the device half of later plans keeps running while this plan's hits are pruned.
-struct SpPlan {
+// Device buffers of one single-pulse search in flight (block coefficients, hit list, hit
+// count, bad flags) and the event after its device half: a context pool, taken by a launch
+// and given back by its collect, so a pipeline of k searches allocates k sets once.
+struct SpBufs {
     double* d_coef = nullptr;
     size_t coef_bytes = 0;
     hd_sp_hit* d_hits = nullptr;
@@ -271,6 +271,14 @@ struct SpPlan {
     uint8_t* d_bad = nullptr;
     size_t bad_bytes = 0;
     hipEvent_t ev = nullptr;
+};
+
+// A plan's single-pulse search in flight: the device half (block statistics, boxcar hits,
+// prune_related1, bad flags) launched on the plan's stream and marked by b->ev; the host half
+// (copies, prune_related2, border cases) waits for that event only, on the context's ssp
+// stream, so the device half of later plans keeps running while this plan's hits are pruned.
+struct SpPlan {
+    SpBufs* b = nullptr;
     hipStream_t st = nullptr;
     bool pending = false;
     int32_t widths[16] = {0};
@@ -282,7 +290,7 @@ struct SpPlan {
 
 static thread_local std::string g_err;
 static void clear_special_cache(hd_ctx* c);
-static int s2_swait();
+static void sp_bufs_free(SpBufs* b);
 
 static int fail(hd_ctx* ctx, int code, const char* fmt, ...)
 {
@@ -454,6 +462,9 @@ extern "C" int hd_close(hd_ctx* c)
     dfree(c->d_partial);
     dfree(c->d_partial2);
     if (c->sp_pin) (void)hipHostFree(c->sp_pin);
+    for (SpBufs* b : c->sp_all) sp_bufs_free(b);
+    c->sp_all.clear();
+    c->sp_free.clear();
     if (c->ssp) (void)hipStreamDestroy(c->ssp);
     dfree(c->d_sum_parts);
     dfree(c->d_sum_parts_multi);
@@ -1371,11 +1382,10 @@ static void plan_free(hd_plan* p)
         if (e) (void)hipEventDestroy(e);
     if (p->ev_copy) (void)hipEventDestroy(p->ev_copy);
     if (p->sp) {
-        dfree(p->sp->d_coef);
-        dfree(p->sp->d_hits);
-        dfree(p->sp->d_count);
-        dfree(p->sp->d_bad);
-        if (p->sp->ev) (void)hipEventDestroy(p->sp->ev);
+        if (p->sp->b) {                               // a search never collected: its buffers back
+            (void)hipEventSynchronize(p->sp->b->ev);
+            p->ctx->sp_free.push_back(p->sp->b);
+        }
         delete p->sp;
         p->sp = nullptr;
     }
@@ -3030,26 +3040,37 @@ extern "C" int hd_sp_prune(hd_sp_hit* hits, int64_t n, int32_t ndm, const int32_
     return HD_OK;
 }
 
-// The device half into the plan's SpPlan buffers (hit list sized cap), marked by sp->ev.
+static void sp_bufs_free(SpBufs* b)
+{
+    dfree(b->d_coef);
+    dfree(b->d_hits);
+    dfree(b->d_count);
+    dfree(b->d_bad);
+    if (b->ev) (void)hipEventDestroy(b->ev);
+    delete b;
+}
+
+// The device half into the search's buffers (hit list sized cap), marked by b->ev.
 static int sp_launch_device(hd_ctx* c, hd_plan* p, SpPlan* sp, int64_t cap)
 {
     const int ndm = p->pass.numdms;
-    if (sp->cap < cap) {
+    SpBufs* b = sp->b;
+    if (b->cap < cap) {
         HIPCHK(c, hipStreamSynchronize(sp->st));
-        dfree(sp->d_hits);
-        sp->d_hits = nullptr;
-        sp->cap = 0;
-        HIPCHK(c, hipMalloc(&sp->d_hits, sizeof(hd_sp_hit) * (size_t)cap));
-        sp->cap = cap;
+        dfree(b->d_hits);
+        b->d_hits = nullptr;
+        b->cap = 0;
+        HIPCHK(c, hipMalloc(&b->d_hits, sizeof(hd_sp_hit) * (size_t)cap));
+        b->cap = cap;
     }
-    HIPCHK(c, hipMemsetAsync(sp->d_count, 0, sizeof(unsigned long long), sp->st));
+    HIPCHK(c, hipMemsetAsync(b->d_count, 0, sizeof(unsigned long long), sp->st));
     if (sp->nblocks > 0) {
-        HIPCHK(c, hd::launch_sp_blocks(p->d_out, p->out_stride, ndm, (int)sp->nblocks, sp->d_coef, sp->st));
-        HIPCHK(c, hd::launch_sp_hits(p->d_out, p->out_stride, ndm, (int)sp->nblocks, sp->d_coef, sp->ls, sp->widths,
-                                     sp->rsw, sp->nw, sp->threshold, sp->d_hits, sp->d_count, sp->cap, sp->st));
-        HIPCHK(c, hd::launch_sp_badflags(sp->d_coef, (int64_t)ndm * sp->nblocks, sp->d_bad, sp->st));
+        HIPCHK(c, hd::launch_sp_blocks(p->d_out, p->out_stride, ndm, (int)sp->nblocks, b->d_coef, sp->st));
+        HIPCHK(c, hd::launch_sp_hits(p->d_out, p->out_stride, ndm, (int)sp->nblocks, b->d_coef, sp->ls, sp->widths,
+                                     sp->rsw, sp->nw, sp->threshold, b->d_hits, b->d_count, b->cap, sp->st));
+        HIPCHK(c, hd::launch_sp_badflags(b->d_coef, (int64_t)ndm * sp->nblocks, b->d_bad, sp->st));
     }
-    HIPCHK(c, hipEventRecord(sp->ev, sp->st));
+    HIPCHK(c, hipEventRecord(b->ev, sp->st));
     return HD_OK;
 }
 
@@ -3068,12 +3089,20 @@ extern "C" int hd_single_pulse_launch(hd_plan* p, double dt, double maxwidth, do
     HIPCHK(c, hipSetDevice(c->device));
     if (!p->sp) p->sp = new SpPlan();
     SpPlan* sp = p->sp;
-    if (!sp->ev) {
-        HIPCHK(c, hipEventCreateWithFlags(&sp->ev, hipEventDisableTiming));
-        HIPCHK(c, hipMalloc(&sp->d_count, sizeof(unsigned long long)));
-    }
     if (!c->ssp) HIPCHK(c, hipStreamCreateWithFlags(&c->ssp, hipStreamNonBlocking));
-    if (sp->pending) HIPCHK(c, hipEventSynchronize(sp->ev));   // a relaunch before its collect
+    if (sp->b) {
+        HIPCHK(c, hipEventSynchronize(sp->b->ev));            // a relaunch before its collect
+    } else if (!c->sp_free.empty()) {
+        sp->b = c->sp_free.back();
+        c->sp_free.pop_back();
+    } else {
+        SpBufs* b = new SpBufs();
+        c->sp_all.push_back(b);
+        sp->b = b;
+        HIPCHK(c, hipEventCreateWithFlags(&b->ev, hipEventDisableTiming));
+        HIPCHK(c, hipMalloc(&b->d_count, sizeof(unsigned long long)));
+    }
+    SpBufs* b = sp->b;
     sp->st = p->dd_stream ? p->dd_stream : c->stream;
     sp->nw = nw;
     for (int i = 0; i < nw; i++) {
@@ -3085,19 +3114,19 @@ extern "C" int hd_single_pulse_launch(hd_plan* p, double dt, double maxwidth, do
     sp->ls = nblocks * 1000 / 8000 * 8000;                     // numchunks * chunklen
     const size_t cbytes = sizeof(double) * 4 * (size_t)std::max<int64_t>(1, (int64_t)ndm * nblocks);
     const size_t bbytes = (size_t)std::max<int64_t>(1, (int64_t)ndm * nblocks);
-    if (sp->coef_bytes < cbytes || sp->bad_bytes < bbytes) {
+    if (b->coef_bytes < cbytes || b->bad_bytes < bbytes) {
         HIPCHK(c, hipStreamSynchronize(sp->st));
-        dfree(sp->d_coef);
-        dfree(sp->d_bad);
-        sp->d_coef = nullptr;
-        sp->d_bad = nullptr;
-        sp->coef_bytes = sp->bad_bytes = 0;
-        HIPCHK(c, hipMalloc(&sp->d_coef, cbytes));
-        HIPCHK(c, hipMalloc(&sp->d_bad, bbytes));
-        sp->coef_bytes = cbytes;
-        sp->bad_bytes = bbytes;
+        dfree(b->d_coef);
+        dfree(b->d_bad);
+        b->d_coef = nullptr;
+        b->d_bad = nullptr;
+        b->coef_bytes = b->bad_bytes = 0;
+        HIPCHK(c, hipMalloc(&b->d_coef, cbytes));
+        HIPCHK(c, hipMalloc(&b->d_bad, bbytes));
+        b->coef_bytes = cbytes;
+        b->bad_bytes = bbytes;
     }
-    rc = sp_launch_device(c, p, sp, std::max(sp->cap, c->sp_cap_hint));
+    rc = sp_launch_device(c, p, sp, std::max(b->cap, c->sp_cap_hint));
     if (rc) return rc;
     sp->pending = true;
     return HD_OK;
@@ -3121,7 +3150,8 @@ extern "C" int hd_single_pulse_collect(hd_plan* p, hd_sp_hit* hits, int64_t cap,
     if (!p || !nhits || (cap > 0 && !hits)) return fail(p ? p->ctx : nullptr, HD_E_INVAL, "hd_single_pulse: NULL argument");
     hd_ctx* c = p->ctx;
     SpPlan* sp = p->sp;
-    if (!sp || !sp->pending) return fail(c, HD_E_STATE, "hd_single_pulse_collect: no search launched on this plan");
+    if (!sp || !sp->pending || !sp->b) return fail(c, HD_E_STATE, "hd_single_pulse_collect: no search launched on this plan");
+    SpBufs* b = sp->b;
     HIPCHK(c, hipSetDevice(c->device));
     SpTimer tm;                                                // HD_SP_TIMING=1 (profiling)
     const int ndm = p->pass.numdms;
@@ -3129,19 +3159,19 @@ extern "C" int hd_single_pulse_collect(hd_plan* p, hd_sp_hit* hits, int64_t cap,
     int rc = sp_pin(c, 64);
     if (rc) return rc;
     // the count, on the copy stream after the plan's device half only
-    HIPCHK(c, hipStreamWaitEvent(c->ssp, sp->ev, 0));
-    HIPCHK(c, hipMemcpyAsync(c->sp_pin, sp->d_count, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->ssp));
+    HIPCHK(c, hipStreamWaitEvent(c->ssp, b->ev, 0));
+    HIPCHK(c, hipMemcpyAsync(c->sp_pin, b->d_count, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->ssp));
     HIPCHK(c, hipStreamSynchronize(c->ssp));
     unsigned long long cnt = *(const unsigned long long*)c->sp_pin;
     tm.mark(0);
-    if ((int64_t)cnt > sp->cap) {
+    if ((int64_t)cnt > b->cap) {
         // the device list overflowed: grow it to the count and search again (once per size)
         const int64_t ncap = (int64_t)cnt + (int64_t)cnt / 4;
         c->sp_cap_hint = std::max(c->sp_cap_hint, ncap);
         rc = sp_launch_device(c, p, sp, ncap);
         if (rc) return rc;
-        HIPCHK(c, hipStreamWaitEvent(c->ssp, sp->ev, 0));
-        HIPCHK(c, hipMemcpyAsync(c->sp_pin, sp->d_count, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->ssp));
+        HIPCHK(c, hipStreamWaitEvent(c->ssp, b->ev, 0));
+        HIPCHK(c, hipMemcpyAsync(c->sp_pin, b->d_count, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->ssp));
         HIPCHK(c, hipStreamSynchronize(c->ssp));
         cnt = *(const unsigned long long*)c->sp_pin;
     }
@@ -3154,17 +3184,21 @@ extern "C" int hd_single_pulse_collect(hd_plan* p, hd_sp_hit* hits, int64_t cap,
     rc = sp_pin(c, std::max(hbytes, nbad));
     if (rc) return rc;
     if (nbad) {
-        HIPCHK(c, hipMemcpyAsync(c->sp_pin, sp->d_bad, nbad, hipMemcpyDeviceToHost, c->ssp));
+        HIPCHK(c, hipMemcpyAsync(c->sp_pin, b->d_bad, nbad, hipMemcpyDeviceToHost, c->ssp));
         HIPCHK(c, hipStreamSynchronize(c->ssp));
         memcpy(bad_blocks, c->sp_pin, nbad);
     }
     if (!fits)                                                 // (still pending: call again with room)
         return fail(c, HD_E_NOMEM, "hd_single_pulse: %llu hits > capacity %lld (call again with room)", cnt,
                     (long long)cap);
-    sp->pending = false;
+    if (cnt) {
+        HIPCHK(c, hipMemcpyAsync(c->sp_pin, b->d_hits, hbytes, hipMemcpyDeviceToHost, c->ssp));
+        HIPCHK(c, hipStreamSynchronize(c->ssp));
+    }
+    sp->pending = false;                                       // the buffers go back to the pool
+    c->sp_free.push_back(b);
+    sp->b = nullptr;
     if (!cnt) return HD_OK;
-    HIPCHK(c, hipMemcpyAsync(c->sp_pin, sp->d_hits, hbytes, hipMemcpyDeviceToHost, c->ssp));
-    HIPCHK(c, hipStreamSynchronize(c->ssp));
     const hd_sp_hit* src = (const hd_sp_hit*)c->sp_pin;
     tm.mark(1);
     // per DM (in parallel): the script's dm_candlist order -- by bin, widths in increasing
@@ -3548,7 +3582,6 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         a.dms_per_blk = w.dpb;
         a.sc = w.sc;
         a.probe = p->probe;
-        a.swait = s2_swait();
         a.ring_npw = w.npw;
         a.ring_nbp = w.nbp;
         a.ptab = w.d_omin;
@@ -3607,13 +3640,6 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
 // stage) share a launch of at most kS2MaxPass passes, the rest run one by one.
 // The kernel a plan takes in a shared launch: 5 (k_stage2_rw: variant 8), 4 (the
 // two-pairs-per-chunk pair kernel: auto or variant 7), or -1 (alone).
-// k_stage2_pair's relaxed store wait (Stage2Args::swait); HD_S2_SWAIT=0 restores the full wait
-static int s2_swait()
-{
-    static const int v = getenv("HD_S2_SWAIT") ? (atoi(getenv("HD_S2_SWAIT")) != 0) : 1;
-    return v;
-}
-
 static int dedisp_multi_kernel(const hd_plan* p)
 {
     const bool pair_bound = p->sub_bound >= 0 && 2 * p->sub_bound <= 32767;
@@ -3704,7 +3730,6 @@ static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
     a.dms_per_blk = w0.dpb;
     a.sc = w0.sc;
     a.probe = p0->probe;
-    a.swait = s2_swait();
     a.ring_npw = w0.npw;
     a.ring_nbp = w0.nbp;
     a.ptab = w0.d_omin;

@@ -94,8 +94,6 @@ struct Stage2Args {
     int32_t sc;               // wide variant: subbands per LDS chunk
     int32_t ring_npw, ring_nbp;   // ring variant: 1 KiB DMA pieces per window / per offset block
     int32_t probe;            // profiling only: bit0 skip accumulation, bit1 skip fill, bit2 skip stores
-    int32_t swait;            // k_stage2_pair: 1 = a tile's series stores may still be in flight at
-                              // the next chunk's DMA wait (only loader waves wait, past them)
     // pair variant: per (y-block, subband pair) {base0, b1, U, k1[0..U)} (kPairTab ints) and
     // the largest U of the plan (expanded copies per pair = 4*umax)
     const int32_t* ptab;

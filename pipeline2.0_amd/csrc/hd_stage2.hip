@@ -1066,13 +1066,9 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, S2Multi m)
         }
     };
 
-    // vector-memory instructions the last flush issued (wave-uniform: every store below is
-    // issued by the whole wave or skipped by it)
-    int nst = 0;
     auto flush = [&](int tile) {
         const int64_t t0 = (int64_t)tile * T;
         widen();
-        nst = 0;
     #pragma unroll
         for (int q = 0; q < Q; q++) {
             const int dl = wave * Q + q;
@@ -1084,11 +1080,7 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, S2Multi m)
                 const int64_t tl = t0 + 256 * r + 4 * lane;
                 if (dv && !(a.probe & 4)) {
                     float* o = P.out + (int64_t)d * a.out_stride + tl;
-                    // (wave-uniform; the edge path's masked stores are not counted: an
-                    // undercount only makes the wait below stricter)
-                    const bool full = t0 + 256 * r + 256 <= a.nvalid;
-                    nst += full ? 1 : 0;
-                    if (full) {
+                    if (tl + 3 < a.nvalid) {
                         *(float4*)o = make_float4((float)acc32[q][r][0], (float)acc32[q][r][1], (float)acc32[q][r][2],
                                                   (float)acc32[q][r][3]);
                         part += (int64_t)acc32[q][r][0] + acc32[q][r][1] + acc32[q][r][2] + acc32[q][r][3];
@@ -1106,7 +1098,6 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, S2Multi m)
     #pragma unroll
                 for (int m = 32; m >= 1; m >>= 1) part += __shfl_xor(part, m, 64);
                 if (lane == 0) P.partial[(int64_t)d * a.ntiles + tile] = (double)part;
-                nst += 1;
             }
         }
         gcount = 0;
@@ -1170,19 +1161,7 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, S2Multi m)
                 }
             }
         }
-        // the DMA of chunk c + 2 must have landed.  In the chunk after a flush the tile's stores
-        // were issued after that DMA: a loader wave then waits with vmcnt past them (counts are
-        // retired in issue order), so the stores drain behind the next chunk's work; waves that
-        // issue no DMA need no wait at all (the barrier orders the slots)
-        if (!a.swait) {
-            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NS - 3) : "memory");
-        } else if (loader) {
-            if (nst >= 20) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NS - 3 + 20) : "memory");
-            else if (nst >= 15) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NS - 3 + 15) : "memory");
-            else if (nst >= 5) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NS - 3 + 5) : "memory");
-            else asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NS - 3) : "memory");
-        }
-        nst = 0;
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NS - 3) : "memory");
         ring_barrier();
         // tile done: its stores go out after this chunk's DMA wait, so they do not hold it up
         if (chk == nchunk - 1) flush(tb + ktile++);
