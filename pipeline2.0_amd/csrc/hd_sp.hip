@@ -222,14 +222,24 @@ struct SpArgs {
     int32_t probe;                               // profiling (HD_SP_PROBE): 1 no walk, 2 no width-1, 4 no bitmask
 };
 
-__device__ __forceinline__ void sp_emit(const SpArgs& a, int dm, int64_t bin, int wi, double s)
+// The width-1 hits of the active lanes: one counter atomic per wave (a bright pulse gives
+// thousands of hits per chunk; one global atomic each serialised the whole grid on one address)
+__device__ __forceinline__ void sp_emit_wave(const SpArgs& a, int dm, int64_t bin, bool hit, double s)
 {
-    const unsigned long long slot = atomicAdd(a.count, 1ull);
+    const uint64_t hm = __ballot(hit);
+    if (!hm) return;                                           // (uniform)
+    const int ln = threadIdx.x & 63;
+    const int leader = __ffsll((unsigned long long)__ballot(1)) - 1;
+    unsigned long long base = 0;
+    if (ln == leader) base = atomicAdd(a.count, (unsigned long long)__popcll(hm));
+    base = __shfl(base, leader, 64);
+    if (!hit) return;
+    const unsigned long long slot = base + (unsigned long long)__popcll(hm & ((1ull << ln) - 1ull));
     if ((int64_t)slot < a.cap) {
         hd_sp_hit h;
         h.dm = dm;
         h.bin = (int32_t)bin;
-        h.widx = wi;
+        h.widx = 0;
         h.pad = 0;
         h.sigma = s;
         a.hits[slot] = h;
@@ -281,8 +291,8 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
         }
         P[e + 1] = (double)v;
         const int o = e - kSpHalo;
-        if (o >= 0 && o < kSpChunk && !isbad && !(a.probe & 2) && (double)v > a.threshold)
-            sp_emit(a, dm, c0 + o, 0, (double)v);
+        sp_emit_wave(a, dm, c0 + o, o >= 0 && o < kSpChunk && !isbad && !(a.probe & 2) && (double)v > a.threshold,
+                     (double)v);
     }
     __syncthreads();
     // running sums over 256 segments of kSpSeg samples (the oracle's order), in place

@@ -1031,18 +1031,21 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, S2Multi m)
     // expanded buffers (cc & 1) * PPC + k
     auto expand = [&](int cc, int chk) {
         const char* slot = lds_raw + ring0 + (cc % NS) * slot_bytes;
-#pragma unroll
-        for (int k = 0; k < PPC; k++) {
+        // item = 8 elements of every copy (ws is a multiple of 8: 16-byte stores); the items of
+        // the chunk's PPC pairs form one index range over the workgroup's threads, so no thread
+        // does two while others idle (a pair has U * ws / 8 ~ 400 items for 1024 threads)
+        const int up8 = ws >> 3;
+        const int n0 = ltab[(PPC * chk) * kPairTab + 2] * up8;
+        const int nall = PPC == 2 ? n0 + ltab[(PPC * chk + 1) * kPairTab + 2] * up8 : n0;
+        for (int idx = threadIdx.x; idx < nall; idx += nthr) {
+            const int k = PPC == 2 && idx >= n0 ? 1 : 0;
             const uint32_t* S0 = (const uint32_t*)(slot + (2 * k) * npw * 1024);
             const uint32_t* S1 = (const uint32_t*)(slot + (2 * k + 1) * npw * 1024);
             const int32_t* pt = ltab + (PPC * chk + k) * kPairTab;
             const int k0 = pt[0] & 1;
-            const int U = pt[2];
             int16_t* buf = (int16_t*)(lds_raw + exp0) + ((cc & 1) * PPC + k) * (umax * 4 * ws);
-            // item = 8 elements of every copy (ws is a multiple of 8: 16-byte stores)
-            const int up8 = ws >> 3;
-            for (int idx = threadIdx.x; idx < U * up8; idx += nthr) {
-                int u = 0, uu = idx;
+            {
+                int u = 0, uu = idx - (k ? n0 : 0);
 #pragma unroll
                 for (int m = 1; m < kPairUMax; m++)
                     if (uu >= up8) { uu -= up8; u++; }
