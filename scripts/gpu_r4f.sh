@@ -18,5 +18,5 @@ HD_SP_TIMING=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-forma
 for f in $(find gpurun_out/prof_sp2 -name "*kernel_stats.csv"); do cp "$f" gpurun_out/sp2_kernel_stats.csv; done
 python3 scripts/benchline.py gpurun_out/prof_sp2.log || exit 1
 grep -h "hd_single_pulse:\|single_pulse" gpurun_out/prof_sp2.log | cut -c1-300
-COMMIT=$(cat gpurun_out/commit.txt 2>/dev/null || echo unknown) bash scripts/gpu_pmc.sh || exit 1
+bash scripts/gpu_pmc.sh || exit 1
 echo "r4f done"
