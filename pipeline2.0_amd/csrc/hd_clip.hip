@@ -751,11 +751,12 @@ struct Fix8Geom {
 // bits zb come in registers (the callers load them with the task's other LDS reads), and
 // every step's flag, raw byte and pad read issue together, so a task waits for two LDS round
 // trips -- delays, then window bytes -- instead of two per channel (branches around the loads).
-template <int CPS, int DS>
+template <int CPS, int DS, bool FLAGS = true>
 __device__ __forceinline__ float fix8_fold_pre(const Stage1Multi& a, const uint8_t* lraw, const uint8_t* flg,
                                                const float* pad, int Wp, int G, int lc0, const int (&dr)[CPS],
                                                uint32_t zb, int trel, int bndrel, int dsr)
 {
+    // FLAGS = false: no replaced row in the item's window (its flag reads skipped)
     const int ds = DS ? DS : dsr;
     float acc = 0.0f;
 #pragma unroll 1
@@ -765,7 +766,7 @@ __device__ __forceinline__ float fix8_fold_pre(const Stage1Multi& a, const uint8
 #pragma unroll
         for (int cc = 0; cc < CPS; cc++) {
             const int lr = trel + dr[cc] + k;
-            fb[cc] = flg[lr];
+            fb[cc] = FLAGS ? flg[lr] : 0u;
             rb[cc] = lraw[(lc0 + cc) * Wp + lr];
             pv[cc] = pad[(lr >= bndrel ? G : 0) + lc0 + cc];
         }
@@ -826,8 +827,11 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
     int16_t* dly = (int16_t*)(zap + ((2 * G + 15) & ~15));
     int* lo_s = (int*)(dly + ((npass * G + 7) & ~7));
     int* cnt_s = lo_s + npass * SG;
+    int* pre_s = cnt_s + npass * SG;                       // [npass * SG + 1] exclusive prefix of cnt_s
+    uint16_t* tlist = (uint16_t*)(pre_s + npass * SG + 1);   // [npass * G] clipped-spectrum tasks to fold
     __shared__ int amax_s[kMaxPass];
-    __shared__ int needany;
+    __shared__ int needany, anyflag, ntask_s;
+    __shared__ int wsum_s[8];
     __shared__ uint32_t zbm_s[CPS > 0 ? 1024 / (CPS > 0 ? CPS : 1) : 1];   // per subband: zap bits of both blocks
     // per-pass output rows staged once: indexing the kernel argument arrays with a per-lane
     // pass made every task wait for two global loads of the argument block before its store
@@ -864,7 +868,11 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
         const int bndrel = (b0 + 1) * a.rd.blk - wlo;
         __syncthreads();                                  // the previous item is done with LDS
         if (threadIdx.x < kMaxPass) amax_s[threadIdx.x] = 0;
-        if (threadIdx.x == 0) needany = clip_ev;
+        if (threadIdx.x == 0) {
+            needany = clip_ev;
+            anyflag = 0;
+            ntask_s = 0;
+        }
         for (int i = threadIdx.x; i < G; i += blockDim.x) {
             zap[i] = zap_at(a.rd, b0, c0 + i);
             zap[G + i] = zap_at(a.rd, b1, c0 + i);
@@ -907,10 +915,13 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
                 const uint4 v = *(const uint4*)(a.rawT + (int64_t)rc * a.tstride + wlo + 16 * q);
                 *(uint4*)(lraw + lc * Wp + 16 * q) = v;
             }
+            int fl = 0;
             for (int i = threadIdx.x; i < Wp; i += blockDim.x) {
                 const int t = wlo + i;
                 flg[i] = t >= N ? 1 : (a.rd.clipped ? a.rd.clipped[t] : 0);
+                fl |= flg[i];
             }
+            if (__ballot(fl != 0) && (threadIdx.x & 63) == 0) anyflag = 1;
         }
         if constexpr (CPS > 0) {
             for (int i = threadIdx.x; i < SG; i += blockDim.x) {
@@ -925,49 +936,58 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
         if (fprobe & 1) {
         } else if (clip_ev) {
             // task (p, lc): the output channel lc maps r to, unless an earlier channel of its
-            // subband maps r to the same output
-            for (int i = threadIdx.x; i < npass * G; i += blockDim.x) {
+            // subband maps r to the same output.  The tasks that fold are listed first (one LDS
+            // atomic per wave), so the folds run on dense lanes (~1 task in 6 folds)
+            auto task = [&](int i, int& j) -> bool {             // (p, lc) = task i; j: its output
                 const int p = i / G, lc = i - p * G;
                 const int16_t* dl = dly + p * G;
                 const int lc0 = lc - lc % cps;
                 const int dsp = pds(p), ndsp = DS < 0 ? N / dsp : nds;
-                int j;
+                const int jn = r - dl[lc];
+                if (jn < 0) return false;
+                j = jn / dsp;
+                if (j >= ndsp) return false;
+                // delays fall with frequency within a subband, so the outputs its channels map r
+                // to rise with the channel and equal ones are adjacent: only channel lc - 1 can
+                // name j first
+                if (lc > lc0) {
+                    const int jn2 = r - dl[lc - 1];
+                    if (jn2 >= 0 && jn2 / dsp == j) return false;
+                }
+                return true;
+            };
+            for (int i0 = 0; i0 < npass * G; i0 += blockDim.x) {
+                const int i = i0 + threadIdx.x;
+                int j = 0;
+                const bool keep = i < npass * G && task(i, j);
+                const uint64_t m = __ballot(keep);
+                if (m) {
+                    const int ln = threadIdx.x & 63;
+                    int base = 0;
+                    if (ln == 0) base = atomicAdd(&ntask_s, __popcll(m));
+                    base = __shfl(base, 0, 64);
+                    if (keep) tlist[base + __popcll(m & ((1ull << ln) - 1ull))] = (uint16_t)i;
+                }
+            }
+            __syncthreads();
+            const int ntask = ntask_s;
+            for (int t = threadIdx.x; t < ntask; t += blockDim.x) {
+                const int i = tlist[t];
+                int j = 0;
+                (void)task(i, j);
+                const int p = i / G, lc = i - p * G;
+                const int16_t* dl = dly + p * G;
+                const int lc0 = lc - lc % cps;
+                const int dsp = pds(p);
                 float acc;
                 if constexpr (CPS > 0) {
-                    // the subband's delays and zap bits with the task's own delay (one round)
                     int dr[CPS];
 #pragma unroll
                     for (int cc = 0; cc < CPS; cc++) dr[cc] = dl[lc0 + cc];
                     const uint32_t zb = zbm_s[lc0 / CPS];
-                    const int ci = lc - lc0;
-                    int dlc = dr[0], dpv = dr[0];
-#pragma unroll
-                    for (int cc = 1; cc < CPS; cc++) {
-                        dlc = cc == ci ? dr[cc] : dlc;
-                        dpv = cc == ci - 1 ? dr[cc] : dpv;
-                    }
-                    const int jn = r - dlc;
-                    if (jn < 0) continue;
-                    j = jn / dsp;
-                    if (j >= ndsp) continue;
-                    // delays fall with frequency within a subband, so the outputs its channels
-                    // map r to rise with the channel and equal ones are adjacent: only channel
-                    // lc - 1 can name j first
-                    if (ci > 0) {
-                        const int jn2 = r - dpv;
-                        if (jn2 >= 0 && jn2 / dsp == j) continue;
-                    }
                     acc = fix8_fold_pre<CPS, (DS > 0 ? DS : 0)>(a, lraw, flg, pad, Wp, G, lc0, dr, zb, j * dsp - wlo,
                                                                bndrel, dsp);
                 } else {
-                    const int jn = r - dl[lc];
-                    if (jn < 0) continue;
-                    j = jn / dsp;
-                    if (j >= ndsp) continue;
-                    if (lc > lc0) {
-                        const int jn2 = r - dl[lc - 1];
-                        if (jn2 >= 0 && jn2 / dsp == j) continue;
-                    }
                     acc = fix8_fold<CPS, (DS > 0 ? DS : 0)>(a, lraw, flg, zap, pad, dl, Wp, G, lc0, j * dsp - wlo, bndrel,
                                                            dsp);
                 }
@@ -982,9 +1002,46 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
                 }
             }
         } else {
-            for (int i = threadIdx.x; i < npass * SG * gm.jmax; i += blockDim.x) {
-                const int ps = i / gm.jmax, jj = i - ps * gm.jmax;
-                if (jj >= cnt_s[ps]) continue;
+            // the boundary outputs of every (pass, subband) as one dense task range (the
+            // (pass, subband, jmax) grid left ~3/4 of the lanes idle): an exclusive prefix of
+            // the counts, then each task finds its (pass, subband) by binary search
+            const int nps = npass * SG;
+            {
+                const int per = (nps + (int)blockDim.x - 1) / (int)blockDim.x;
+                const int i0 = threadIdx.x * per;
+                int sum = 0;
+                for (int k = 0; k < per; k++)
+                    if (i0 + k < nps) sum += cnt_s[i0 + k];
+                int incl = sum;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int t = __shfl_up(incl, o, 64);
+                    if ((threadIdx.x & 63) >= o) incl += t;
+                }
+                const int wv = threadIdx.x >> 6;
+                if ((threadIdx.x & 63) == 63) wsum_s[wv] = incl;
+                __syncthreads();
+                int base = 0;
+                for (int w = 0; w < wv; w++) base += wsum_s[w];
+                int run = base + incl - sum;
+                for (int k = 0; k < per; k++)
+                    if (i0 + k < nps) {
+                        pre_s[i0 + k] = run;
+                        run += cnt_s[i0 + k];
+                    }
+                if (threadIdx.x == blockDim.x - 1) pre_s[nps] = run;
+                __syncthreads();
+            }
+            const int total = pre_s[nps];
+            const bool flags = anyflag != 0;
+            for (int t = threadIdx.x; t < total; t += blockDim.x) {
+                int lo = 0, hi = nps - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (pre_s[mid] <= t) lo = mid;
+                    else hi = mid - 1;
+                }
+                const int ps = lo, jj = t - pre_s[ps];
                 const int p = ps / SG, sl = ps - p * SG;
                 const int j = lo_s[ps] + jj;
                 const int16_t* dl = dly + p * G;
@@ -994,8 +1051,10 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
                     int dr[CPS];
 #pragma unroll
                     for (int cc = 0; cc < CPS; cc++) dr[cc] = dl[sl * CPS + cc];
-                    acc = fix8_fold_pre<CPS, (DS > 0 ? DS : 0)>(a, lraw, flg, pad, Wp, G, sl * CPS, dr, zbm_s[sl],
-                                                               j * dsp - wlo, bndrel, dsp);
+                    acc = flags ? fix8_fold_pre<CPS, (DS > 0 ? DS : 0), true>(a, lraw, flg, pad, Wp, G, sl * CPS, dr,
+                                                                             zbm_s[sl], j * dsp - wlo, bndrel, dsp)
+                                : fix8_fold_pre<CPS, (DS > 0 ? DS : 0), false>(a, lraw, flg, pad, Wp, G, sl * CPS, dr,
+                                                                              zbm_s[sl], j * dsp - wlo, bndrel, dsp);
                 } else {
                     acc = fix8_fold<CPS, (DS > 0 ? DS : 0)>(a, lraw, flg, zap, pad, dl, Wp, G, sl * cps, j * dsp - wlo,
                                                            bndrel, dsp);
@@ -1019,7 +1078,7 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
 static size_t fix8_lds_bytes(const Stage1Multi& a, const Fix8Geom& g)
 {
     return (size_t)g.G * g.Wp + g.Wp + (size_t)2 * g.G * 4 + (size_t)((2 * g.G + 15) & ~15) +
-           (size_t)2 * ((a.npass * g.G + 7) & ~7) + (size_t)2 * a.npass * g.SG * 4;
+           (size_t)2 * ((a.npass * g.G + 7) & ~7) + (size_t)(3 * a.npass * g.SG + 1) * 4 + (size_t)2 * a.npass * g.G;
 }
 
 // LDS budget of one k_stage1_fix8 workgroup: smaller windows per workgroup mean more of
@@ -1057,6 +1116,7 @@ static bool fix8_geom(const Stage1Multi& a, Fix8Geom& g)
     }
     if (!g.SG) return false;
     g.G = g.SG * a.cps;
+    if ((int64_t)a.npass * g.G > 65535) return false;   // (task ids are 16-bit)
     g.nchunk = a.nsub / g.SG;
     int dsmin = a.ds;
     if (a.pass_ds)

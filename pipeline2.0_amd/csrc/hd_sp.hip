@@ -393,35 +393,72 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
                 if (bm[ww]) return ww;
         };
         // next(p) and its value: the hits after p in batches of 8 from the word masks (their
-        // boxcar reads issue together; a dense run is thousands of hits)
+        // boxcar reads issue together; a dense run is thousands of hits).  The batch is kept:
+        // when the chain asks again from the pivot just returned, the batch's later hits are
+        // tested first, so a dense rising run steps through all 8 per LDS round trip instead
+        // of one (cache: hits cq/cx with bits cm, after pivot clastp; loading resumes at word
+        // cw with bits cmk)
+        int cq[8];
+        double cx[8];
+        uint32_t cm = 0, cmk = 0;
+        int cw = 0, clastp = -2;
         auto nextpivot = [&](int p, double px, double& qx) -> int {
-            int w = (p + 1) >> 5;
-            if (w >= kSpWords) return -1;
-            uint32_t m = bm[w] & (~0u << ((p + 1) & 31));
+            int w;
+            uint32_t m;
+            if (p == clastp) {
+#pragma unroll
+                for (int k = 0; k < 8; k++)
+                    if ((cm >> k) & 1u) {
+                        cm &= ~(1u << k);
+                        if (cq[k] - p > h || cx[k] >= px) {
+                            qx = cx[k];
+                            clastp = cq[k];
+                            return cq[k];
+                        }
+                    }
+                w = cw;
+                m = cmk;
+            } else {
+                cm = 0;
+                w = (p + 1) >> 5;
+                if (w >= kSpWords) {
+                    clastp = -2;
+                    return -1;
+                }
+                m = bm[w] & (~0u << ((p + 1) & 31));
+            }
             while (true) {
                 if (!m) {
                     w = nextword(w);
-                    if (w < 0) return -1;
+                    if (w < 0) {
+                        clastp = -2;
+                        return -1;
+                    }
                     m = bm[w];
                 }
-                int qq[8];
-                double xv[8];
                 int n = 0;
 #pragma unroll
                 for (int k = 0; k < 8; k++)
                     if (m) {
-                        qq[k] = 32 * w + __builtin_ctz(m);
+                        cq[k] = 32 * w + __builtin_ctz(m);
                         m &= m - 1;
                         n = k + 1;
                     }
 #pragma unroll
                 for (int k = 0; k < 8; k++)
-                    if (k < n) xv[k] = boxcar(wi, qq[k]);
+                    if (k < n) cx[k] = boxcar(wi, cq[k]);
+                cm = (1u << n) - 1u;
 #pragma unroll
                 for (int k = 0; k < 8; k++)
-                    if (k < n && (qq[k] - p > h || xv[k] >= px)) {
-                        qx = xv[k];
-                        return qq[k];
+                    if (k < n) {
+                        cm &= ~(1u << k);
+                        if (cq[k] - p > h || cx[k] >= px) {
+                            qx = cx[k];
+                            clastp = cq[k];
+                            cw = w;
+                            cmk = m;
+                            return cq[k];
+                        }
                     }
             }
         };
@@ -476,6 +513,7 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
         __syncthreads();
         // the true chain from the chunk's first hit (one lane)
         if (walk && ln == 0 && !(a.probe & 8)) {                 // (probe 8: profiling only)
+            clastp = -2;                                          // (the lane's own walk's batch)
             int p = nexthit(-1);
             double px = p >= 0 ? boxcar(wi, p) : 0.0;
             while (p >= 0) {
