@@ -756,8 +756,15 @@ __device__ __forceinline__ float fix8_fold_pre(const Stage1Multi& a, const uint8
                                                const float* pad, int Wp, int G, int lc0, const int (&dr)[CPS],
                                                uint32_t zb, int trel, int bndrel, int dsr)
 {
-    // FLAGS = false: no replaced row in the item's window (its flag reads skipped)
+    // FLAGS = false: no replaced row in the item's window (its flag reads skipped).  The
+    // subband's pads of both blocks are read once, not once per step
     const int ds = DS ? DS : dsr;
+    float pa[CPS], pb[CPS];
+#pragma unroll
+    for (int cc = 0; cc < CPS; cc++) {
+        pa[cc] = pad[lc0 + cc];
+        pb[cc] = pad[G + lc0 + cc];
+    }
     float acc = 0.0f;
 #pragma unroll 1
     for (int k = 0; k < ds; k++) {
@@ -768,7 +775,7 @@ __device__ __forceinline__ float fix8_fold_pre(const Stage1Multi& a, const uint8
             const int lr = trel + dr[cc] + k;
             fb[cc] = FLAGS ? flg[lr] : 0u;
             rb[cc] = lraw[(lc0 + cc) * Wp + lr];
-            pv[cc] = pad[(lr >= bndrel ? G : 0) + lc0 + cc];
+            pv[cc] = lr >= bndrel ? pb[cc] : pa[cc];
         }
         float sk = 0.0f;
 #pragma unroll

@@ -511,22 +511,43 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
             if (ln == 0) W.hpre[jw][0] = 0;
         }
         __syncthreads();
-        // the true chain from the chunk's first hit (one lane)
-        if (walk && ln == 0 && !(a.probe & 8)) {                 // (probe 8: profiling only)
-            clastp = -2;                                          // (the lane's own walk's batch)
+        // the true chain from the chunk's first hit, walked by the whole wave: each step tests
+        // the 64 bins from the first hit after the pivot at once (lane l: bin start + l; the
+        // first qualifying hit by ballot), so a step that skips a dense stretch of h bins costs
+        // h / 64 LDS round trips instead of h / 8 (one lane's batches) -- in a dense falling
+        // run the chain hops by h + 1 and never meets the lanes' speculative chains
+        if (walk && !(a.probe & 8)) {                             // (probe 8: profiling only)
             int p = nexthit(-1);
             double px = p >= 0 ? boxcar(wi, p) : 0.0;
             while (p >= 0) {
                 const int sg = p >> 7;
                 if ((W.spec[jw][p >> 5] >> (p & 31)) & 1u) {      // on the segment's chain from here
-                    W.merge[jw][sg] = (int16_t)p;
+                    if (ln == 0) W.merge[jw][sg] = (int16_t)p;
                     p = W.exitb[jw][sg];
                     if (p >= 0) px = boxcar(wi, p);
                     continue;
                 }
+                int q = -1;
                 double qx = 0.0;
-                const int q = nextpivot(p, px, qx);
-                if (q < 0 || q - p > h) W.emt[jw][p >> 5] |= 1u << (p & 31);   // not in spec: kept pivot
+                for (int start = nexthit(p); start >= 0;) {
+                    const int b = start + ln;
+                    const bool ishit = b < kSpChunk && ((bm[b >> 5] >> (b & 31)) & 1u);
+                    double xb = 0.0;
+                    bool qual = false;
+                    if (ishit) {
+                        xb = boxcar(wi, b);
+                        qual = b - p > h || xb >= px;
+                    }
+                    const uint64_t qm = __ballot(qual);
+                    if (qm) {
+                        const int fl = __ffsll((unsigned long long)qm) - 1;
+                        q = start + fl;
+                        qx = __shfl(xb, fl, 64);
+                        break;
+                    }
+                    start = start + 63 < kSpChunk ? nexthit(start + 63) : -1;
+                }
+                if (ln == 0 && (q < 0 || q - p > h)) W.emt[jw][p >> 5] |= 1u << (p & 31);   // not in spec: kept pivot
                 p = q;
                 px = qx;
             }

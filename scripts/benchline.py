@@ -5,7 +5,7 @@ import json
 import sys
 
 log, mode = sys.argv[1], (sys.argv[2] if len(sys.argv) > 2 else "step")
-lines = [ln for ln in open(log, errors="replace").read().splitlines() if ln.strip()]
+lines = [ln for ln in open(log, errors="replace").read().splitlines() if ln.strip().startswith("{")]
 try:
     d = json.loads(lines[-1])
     if mode == "ms":
