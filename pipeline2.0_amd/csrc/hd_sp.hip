@@ -45,6 +45,11 @@ constexpr int kSpWords = kSpChunk / 32;      // hit bitmask words per (chunk, wi
 // widths per round = waves per workgroup (one wave walks each): 16 waves take the 14
 // widths > 1 of the 0.1-s downfactors in one round (4 waves: four rounds)
 constexpr int kSpSegW = 4;                   // bitmask words (128 bins) per lane segment of a walk
+// LDS slot of prefix entry i: one double of padding per 128 entries.  The walk's lanes read
+// P at the same offset into their 128-bin segments; unpadded, that is a 1 KiB stride -- one
+// bank for all 64 lanes (64-way conflicts on every boxcar of the speculative walks)
+__device__ __forceinline__ int pix(int i) { return i + (i >> 7); }
+constexpr int kSpPLen = kSpWin + 1 + ((kSpWin + 1) >> 7) + 1;
 
 __device__ __forceinline__ double wave_sum_f64(double v)
 {
@@ -250,7 +255,7 @@ template <int NW>
 __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
 {
     constexpr int kSpRound = NW;
-    __shared__ double P[kSpWin + 1];
+    __shared__ double P[kSpPLen];
     __shared__ uint32_t bits[kSpRound][kSpWords];
     // the walk's per-width state (its space also holds the segment totals of the prefix sum):
     // spec[w]: pivots of the lanes' speculative walks; emt[w]: pivots whose next pivot is a gap
@@ -289,7 +294,7 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
                 v = (float)((double)d / c[2]);
             }
         }
-        P[e + 1] = (double)v;
+        P[pix(e + 1)] = (double)v;
         const int o = e - kSpHalo;
         sp_emit_wave(a, dm, c0 + o, o >= 0 && o < kSpChunk && !isbad && !(a.probe & 2) && (double)v > a.threshold,
                      (double)v);
@@ -300,8 +305,8 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
         double run = 0.0;
 #pragma unroll
         for (int j = 0; j < kSpSeg; j++) {
-            run += P[tid * kSpSeg + j + 1];
-            P[tid * kSpSeg + j + 1] = run;
+            run += P[pix(tid * kSpSeg + j + 1)];
+            P[pix(tid * kSpSeg + j + 1)] = run;
         }
         tot[tid] = run;
     }
@@ -329,7 +334,7 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
     if (tid < 256) {
         const double base = tot[tid];
 #pragma unroll
-        for (int j = 0; j < kSpSeg; j++) P[tid * kSpSeg + j + 1] = base + P[tid * kSpSeg + j + 1];
+        for (int j = 0; j < kSpSeg; j++) P[pix(tid * kSpSeg + j + 1)] = base + P[pix(tid * kSpSeg + j + 1)];
     }
     __syncthreads();
     // boxcar value (width index wi > 0) at chunk bin o
@@ -337,7 +342,7 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
         const int w = a.widths[wi];
         const int k = o + kSpHalo;
         const int lo = k - w / 2, hi = k + ((w & 1) ? w / 2 : w / 2 - 1) + 1;
-        return (P[hi] - P[lo]) * a.rsw[wi];
+        return (P[pix(hi)] - P[pix(lo)]) * a.rsw[wi];
     };
     // the bad flags of the chunk's 8 blocks, one bit each (every wave, once)
     const uint64_t badm = __ballot(ln < kSpChunk / kSpBlock && cf[(c0 / kSpBlock + ln) * 4 + 3] != 0.0);
@@ -346,13 +351,26 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
         // the above-threshold bins of widths r0 .. r0+nr-1 (bad blocks included: the script
         // prunes before it looks at blocks): lane = bin, one ballot per 64 bins (consecutive
         // lanes read consecutive P entries: no bank conflicts)
-        for (int t = wv; t < nr * (kSpChunk / 64); t += NW) {
-            const int j = t / (kSpChunk / 64), q = t - j * (kSpChunk / 64);
-            const bool hit = !(a.probe & 4) && boxcar(r0 + j, 64 * q + ln) > a.threshold;
-            const uint64_t m = __ballot(hit);
-            if (ln == 0) {
-                bits[j][2 * q] = (uint32_t)m;
-                bits[j][2 * q + 1] = (uint32_t)(m >> 32);
+        // (four tasks per wave in flight: their boxcar reads issue together)
+        const int ntask = nr * (kSpChunk / 64);
+        for (int t0 = wv; t0 < ntask; t0 += 4 * NW) {
+            double xv[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int t = min(t0 + u * NW, ntask - 1);
+                const int j = t / (kSpChunk / 64), q = t - j * (kSpChunk / 64);
+                xv[u] = boxcar(r0 + j, 64 * q + ln);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int t = t0 + u * NW;
+                if (t >= ntask) break;                                    // (uniform)
+                const int j = t / (kSpChunk / 64), q = t - j * (kSpChunk / 64);
+                const uint64_t m = __ballot(!(a.probe & 4) && xv[u] > a.threshold);
+                if (ln == 0) {
+                    bits[j][2 * q] = (uint32_t)m;
+                    bits[j][2 * q + 1] = (uint32_t)(m >> 32);
+                }
             }
         }
         __syncthreads();
