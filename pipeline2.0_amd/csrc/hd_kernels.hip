@@ -918,6 +918,10 @@ __global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
                 int16_t* o = (int16_t*)a.out[p] + (int64_t)s * a.ostride[p] + tO0 + lane;
 #pragma unroll
                 for (int m = 0; m < M; m++) {
+                    if (a.probe & 8) {                        // (profiling: sums without the stores)
+                        mx = __builtin_elementwise_max(mx, __builtin_bit_cast(u16x2, ae[m] ^ ao[m]));
+                        continue;
+                    }
                     o[64 * m] = (int16_t)(ae[m] & 0xFFFFu);
                     o[64 * m + JQ] = (int16_t)(ao[m] & 0xFFFFu);
                     o[64 * m + 2 * JQ] = (int16_t)(ae[m] >> 16);

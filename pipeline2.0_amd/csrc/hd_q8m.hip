@@ -19,7 +19,7 @@ namespace hd {
 
 constexpr int kQ8mS = 960;                    // raw rows per quarter of the tile
 #ifndef Q8M_UNROLL
-#define Q8M_UNROLL 1
+#define Q8M_UNROLL 4
 #endif
 
 bool stage1_q8m_supports_ds(int ds) { return ds == 2 || ds == 3 || ds == 5 || ds == 6 || ds == 10; }
@@ -87,14 +87,10 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
 #pragma unroll
             for (int cc = 0; cc < CPS; cc++) {
                 const uint32_t keep = ((zall >> cc) & 1u) ? 0u : 0xFFFFFFFFu;
-                // even DS: odd lanes take the steps in rotated order (1 .. DS-1, then 0: exact
-                // integer sums, any order), so a wave's reads cover odd and even banks -- lanes
-                // DS dwords apart otherwise hit only the even ones (2-way conflicts)
-                const int par = (DS & 1) ? 0 : (lane & 1);
-                const uint32_t* b = lbase + lrb[cc] + dl[cc] + mo + par;
+                const uint32_t* b = lbase + lrb[cc] + dl[cc] + mo;
 #pragma unroll
                 for (int k = 0; k < DS; k++) {
-                    const uint32_t x = (k < DS - 1 ? b[k] : b[par ? -1 : DS - 1]) & keep;
+                    const uint32_t x = b[k] & keep;
                     ae += x & 0x00FF00FFu;
                     ao += __builtin_amdgcn_perm(0u, x, 0x0c030c01u);
                 }

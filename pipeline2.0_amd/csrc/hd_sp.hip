@@ -45,11 +45,6 @@ constexpr int kSpWords = kSpChunk / 32;      // hit bitmask words per (chunk, wi
 // widths per round = waves per workgroup (one wave walks each): 16 waves take the 14
 // widths > 1 of the 0.1-s downfactors in one round (4 waves: four rounds)
 constexpr int kSpSegW = 4;                   // bitmask words (128 bins) per lane segment of a walk
-// LDS slot of prefix entry i: one double of padding per 128 entries.  The walk's lanes read
-// P at the same offset into their 128-bin segments; unpadded, that is a 1 KiB stride -- one
-// bank for all 64 lanes (64-way conflicts on every boxcar of the speculative walks)
-__device__ __forceinline__ int pix(int i) { return i + (i >> 7); }
-constexpr int kSpPLen = kSpWin + 1 + ((kSpWin + 1) >> 7) + 1;
 
 __device__ __forceinline__ double wave_sum_f64(double v)
 {
@@ -224,7 +219,8 @@ struct SpArgs {
     hd_sp_hit* hits;
     unsigned long long* count;
     int64_t cap;
-    int32_t probe;                               // profiling (HD_SP_PROBE): 1 no walk, 2 no width-1, 4 no bitmask
+    int32_t probe;                               // profiling (HD_SP_PROBE): 1 no walk, 2 no width-1, 4 no bitmask,
+                                                 // 8 no true chain, 16 no emission of the walk's survivors
 };
 
 // The width-1 hits of the active lanes: one counter atomic per wave (a bright pulse gives
@@ -255,7 +251,7 @@ template <int NW>
 __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
 {
     constexpr int kSpRound = NW;
-    __shared__ double P[kSpPLen];
+    __shared__ double P[kSpWin + 1];
     __shared__ uint32_t bits[kSpRound][kSpWords];
     // the walk's per-width state (its space also holds the segment totals of the prefix sum):
     // spec[w]: pivots of the lanes' speculative walks; emt[w]: pivots whose next pivot is a gap
@@ -294,7 +290,7 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
                 v = (float)((double)d / c[2]);
             }
         }
-        P[pix(e + 1)] = (double)v;
+        P[e + 1] = (double)v;
         const int o = e - kSpHalo;
         sp_emit_wave(a, dm, c0 + o, o >= 0 && o < kSpChunk && !isbad && !(a.probe & 2) && (double)v > a.threshold,
                      (double)v);
@@ -305,8 +301,8 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
         double run = 0.0;
 #pragma unroll
         for (int j = 0; j < kSpSeg; j++) {
-            run += P[pix(tid * kSpSeg + j + 1)];
-            P[pix(tid * kSpSeg + j + 1)] = run;
+            run += P[tid * kSpSeg + j + 1];
+            P[tid * kSpSeg + j + 1] = run;
         }
         tot[tid] = run;
     }
@@ -334,7 +330,7 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
     if (tid < 256) {
         const double base = tot[tid];
 #pragma unroll
-        for (int j = 0; j < kSpSeg; j++) P[pix(tid * kSpSeg + j + 1)] = base + P[pix(tid * kSpSeg + j + 1)];
+        for (int j = 0; j < kSpSeg; j++) P[tid * kSpSeg + j + 1] = base + P[tid * kSpSeg + j + 1];
     }
     __syncthreads();
     // boxcar value (width index wi > 0) at chunk bin o
@@ -342,7 +338,7 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
         const int w = a.widths[wi];
         const int k = o + kSpHalo;
         const int lo = k - w / 2, hi = k + ((w & 1) ? w / 2 : w / 2 - 1) + 1;
-        return (P[pix(hi)] - P[pix(lo)]) * a.rsw[wi];
+        return (P[hi] - P[lo]) * a.rsw[wi];
     };
     // the bad flags of the chunk's 8 blocks, one bit each (every wave, once)
     const uint64_t badm = __ballot(ln < kSpChunk / kSpBlock && cf[(c0 / kSpBlock + ln) * 4 + 3] != 0.0);
@@ -351,26 +347,13 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
         // the above-threshold bins of widths r0 .. r0+nr-1 (bad blocks included: the script
         // prunes before it looks at blocks): lane = bin, one ballot per 64 bins (consecutive
         // lanes read consecutive P entries: no bank conflicts)
-        // (four tasks per wave in flight: their boxcar reads issue together)
-        const int ntask = nr * (kSpChunk / 64);
-        for (int t0 = wv; t0 < ntask; t0 += 4 * NW) {
-            double xv[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int t = min(t0 + u * NW, ntask - 1);
-                const int j = t / (kSpChunk / 64), q = t - j * (kSpChunk / 64);
-                xv[u] = boxcar(r0 + j, 64 * q + ln);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int t = t0 + u * NW;
-                if (t >= ntask) break;                                    // (uniform)
-                const int j = t / (kSpChunk / 64), q = t - j * (kSpChunk / 64);
-                const uint64_t m = __ballot(!(a.probe & 4) && xv[u] > a.threshold);
-                if (ln == 0) {
-                    bits[j][2 * q] = (uint32_t)m;
-                    bits[j][2 * q + 1] = (uint32_t)(m >> 32);
-                }
+        for (int t = wv; t < nr * (kSpChunk / 64); t += NW) {
+            const int j = t / (kSpChunk / 64), q = t - j * (kSpChunk / 64);
+            const bool hit = !(a.probe & 4) && boxcar(r0 + j, 64 * q + ln) > a.threshold;
+            const uint64_t m = __ballot(hit);
+            if (ln == 0) {
+                bits[j][2 * q] = (uint32_t)m;
+                bits[j][2 * q + 1] = (uint32_t)(m >> 32);
             }
         }
         __syncthreads();
@@ -572,7 +555,7 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
         }
         __syncthreads();
         // emit the kept pivots of this lane's segment in bin order, with their ordinals
-        if (walk) {
+        if (walk && !(a.probe & 16)) {                           // (probe 16: profiling only)
             const int mg = W.merge[jw][ln];
             uint32_t kv[kSpSegW];
             int nk = 0;
@@ -621,14 +604,16 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
             };
             // kept pivots whose zip-quirk partner lies outside the bad blocks: counted, one
             // atomic per wave reserves their slots, then written in bin order
+            // (the lane's kept pivots have consecutive ordinals, so their partners are
+            // consecutive hits: the first by rank, each next one the hit after the last)
             const int m0 = inc - nk;                              // ordinal of this lane's first kept pivot
             int ng = 0;
             {
-                int m = m0;
+                int hb = -1;
 #pragma unroll
                 for (int k = 0; k < kSpSegW; k++)
                     for (uint32_t v = kv[k]; v; v &= v - 1) {
-                        const int hb = hitrank(m++);
+                        hb = hb < 0 ? hitrank(m0) : nexthit(hb);
                         ng += !((badm >> (hb / kSpBlock)) & 1ull);
                     }
             }
@@ -643,12 +628,12 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
             if (ln == 0 && totg > 0) base = atomicAdd(a.count, (unsigned long long)totg);
             base = __shfl(base, 0, 64);
             unsigned long long slot = base + (unsigned long long)(incg - ng);
-            int m = m0;
+            int hb = -1;
 #pragma unroll
             for (int k = 0; k < kSpSegW; k++)
                 for (uint32_t v = kv[k]; v; v &= v - 1) {
                     const int b = 32 * (sw0 + k) + __builtin_ctz(v);
-                    const int hb = hitrank(m++);
+                    hb = hb < 0 ? hitrank(m0) : nexthit(hb);
                     if ((badm >> (hb / kSpBlock)) & 1ull) continue;
                     if ((int64_t)slot < a.cap) {
                         hd_sp_hit r;
