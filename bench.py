@@ -70,6 +70,10 @@ def parse():
                     help="--mode slices: after the timed steps, gather every rank's exact per-DM sums of its owned "
                          "series (and the last rank's padding values) and check, on rank 0, that their union equals a "
                          "whole-beam one-context run of the same beam")
+    ap.add_argument("--comm", choices=["torch", "hd"], default="torch",
+                    help="--mode slices: the two exchanges over torch.distributed (default) or over the library's own "
+                         "RCCL communicator (hd_comm_*: hd_slice_exchange_clip, hd_comm_allreduce_sum_f64), the path a "
+                         "C caller takes")
     ap.add_argument("--sim-slice", default=None, metavar="R/G",
                     help="--mode slices on ONE process: run only rank R's slice of a G-way cut (no collectives; the "
                          "other ranks' clip statistics are absent, so only the timing is meaningful) -- the per-rank "
@@ -356,14 +360,20 @@ def slice_stages(eng, ts, rank, variant):
     return stages
 
 
+SLICE_COMM = ["torch"]
+
+
 def run_slice_step(eng, ts, rank, stages, dist, torch):
     """One beam as time slices: clip statistics of the owned read blocks -> all-reduce ->
     clip_times finished on each slice; every pass; padding sums -> all-reduce -> last rank pads."""
     import numpy as np
     eng.touch_raw()
     on_gpu = dist is not None and dist.get_backend() == "nccl"
+    hdc = SLICE_COMM[0] == "hd"
     if eng.opts.clip_sigma > 0:
-        if on_gpu:
+        if hdc:
+            eng.slice_exchange_clip(ts.nown_blocks(rank), ts.nblk_total)
+        elif on_gpu:
             table = torch.zeros((ts.nblk_total, ts.obs.nchan + 3), dtype=torch.float64, device="cuda")
             ts.contribute_clip_stats(eng, rank, table.data_ptr())
             dist.all_reduce(table)
@@ -383,7 +393,9 @@ def run_slice_step(eng, ts, rank, stages, dist, torch):
             run_dedisp_stage(eng, st)
             plans += st
     sums = ts.pass_sums(rank, plans)
-    if dist is not None:
+    if hdc:
+        eng.comm_allreduce(sums)
+    elif dist is not None:
         t = torch.from_numpy(sums)
         if on_gpu:
             t = t.cuda()
@@ -564,6 +576,15 @@ def main():
         out_per_step = sum(p.pp.numdms * p.nds for p in plans)
     if shard and world > 1:
         broadcast_beam(eng, obs, rank, dist, torch)                 # untimed: makes warmup valid
+    if slices and args.comm == "hd" and not args.sim_slice:
+        # the library's communicator: rank 0's id reaches the others over the process group
+        uid = Engine.comm_unique_id() if rank == 0 else bytes(128)
+        if dist is not None:
+            t = torch.tensor(list(uid), dtype=torch.uint8, device="cuda" if dist.get_backend() == "nccl" else "cpu")
+            dist.broadcast(t, 0)
+            uid = bytes(t.cpu().tolist())
+        eng.comm_init(uid, rank, world)
+        SLICE_COMM[0] = "hd"
 
     bcast_s = 0.0
 
@@ -662,6 +683,8 @@ def main():
                            for k, v in sorted(per_kernel.items(), key=lambda kv: -kv[1]["ms"])},
         "stage2_streams": args.streams,
         "stage2_launch": "one per pass" if args.dd_single else "one per DDplan stage (hd_run_dedisp_multi)",
+        "slice_exchanges": (("library RCCL communicator (hd_comm_*)" if SLICE_COMM[0] == "hd" else "torch.distributed")
+                            if slices else None),
         "stage1_launch": "one per DDplan stage" if args.s1_per_stage else
                          "ds=1 stage alone, the ds>=2 stages in one hd_run_subband_multi call (k_stage1_q8m)",
         "step_compulsory_hbm_frac": (raw_bytes + 4.0 * out_per_step) / step_s / (HBM_PEAK_GBS * 1e9),

@@ -323,6 +323,20 @@ HD_API int hd_series_sum_multi(hd_plan* const* plans, int32_t n, int32_t dm, con
                                double* sums);
 HD_API int hd_series_fill(hd_plan* plan, int64_t t0, float value);
 
+/* ---- in-library collectives (RCCL over xGMI) for a time-sliced beam -------------------
+ * The two exchanges of hipdedisp.sharding.TimeSlices without torch.distributed, for a caller
+ * of the C ABI (librccl is loaded at run time on first use).  Rank 0 makes the 128-byte id,
+ * the caller hands it to every rank by any means (MPI, a file, a socket), every rank calls
+ * hd_comm_init with its own context (collective).  hd_slice_exchange_clip replaces the
+ * hd_clip_stats -> all-reduce -> hd_clip_set_stats sequence (nown = this slice's own read
+ * blocks, nblk_total = the beam's); hd_comm_allreduce_sum_f64 sums n doubles in place over
+ * the ranks (host or device memory) -- the padding sums of hd_series_sum_multi.           */
+HD_API int hd_comm_unique_id(uint8_t* id);
+HD_API int hd_comm_init(hd_ctx* ctx, const uint8_t* id, int32_t rank, int32_t world);
+HD_API int hd_comm_allreduce_sum_f64(hd_ctx* ctx, double* buf, int64_t n);
+HD_API int hd_slice_exchange_clip(hd_ctx* ctx, int64_t nown, int64_t nblk_total);
+HD_API int hd_comm_destroy(hd_ctx* ctx);
+
 /* ---- barycentric output (prepsubband without -nobary) ---------------------------------
  * The reference's stage-2 command passes no -nobary (PALFA2_presto_search.py:514-520), so
  * PRESTO resamples every DM series to the solar-system barycentre [PRESTO-ext]: from a TEMPO

@@ -3,6 +3,8 @@
 // Host side of the engine: observation/mask/calibration state, integer delay tables
 // (double precision, PRESTO NEAREST_LONG), device buffers, launch sequencing and
 // hipEvent timing.  One context = one device + one stream; plans are per DDplan pass.
+#include <dlfcn.h>
+#include <rccl/rccl.h>
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -111,6 +113,12 @@ struct hd_ctx {
     size_t partial_bytes = 0;
     // single-pulse search: the host half's copy stream, pinned staging of the hits / flags
     // D2H, and the largest device hit count seen (the next plans' first list size)
+    // in-library collectives (hd_comm_*): an RCCL communicator, its rank / size, a device
+    // scratch for host buffers and the slice clip-statistics table
+    void* comm = nullptr;
+    int32_t comm_rank = 0, comm_world = 0;
+    double* d_comm = nullptr;
+    size_t comm_bytes = 0;
     hipStream_t ssp = nullptr;
     std::vector<struct SpBufs*> sp_free, sp_all;   // search buffer sets (free / every one made)
     void* sp_pin = nullptr;
@@ -289,6 +297,7 @@ struct SpPlan {
 };
 
 static thread_local std::string g_err;
+extern "C" int hd_comm_destroy(hd_ctx* c);
 static void clear_special_cache(hd_ctx* c);
 static void sp_bufs_free(SpBufs* b);
 
@@ -461,6 +470,7 @@ extern "C" int hd_close(hd_ctx* c)
     free_obs_buffers(c);
     dfree(c->d_partial);
     dfree(c->d_partial2);
+    (void)hd_comm_destroy(c);
     if (c->sp_pin) (void)hipHostFree(c->sp_pin);
     for (SpBufs* b : c->sp_all) sp_bufs_free(b);
     c->sp_all.clear();
@@ -4037,5 +4047,149 @@ extern "C" int hd_get_fft(hd_plan* p, int32_t dm0, int32_t ndm, float* out)
     HIPCHK(c, d2h_2d(out, sizeof(float) * p->numout, hd::fft_buffer(p->fft) + (size_t)dm0 * fs,
                      sizeof(float2) * fs, sizeof(float) * p->numout, ndm, st));
     HIPCHK(c, hd::fft_end(p->fft, st));
+    return HD_OK;
+}
+
+// ---- in-library collectives: RCCL over xGMI, loaded at run time ------------------------
+// librccl is dlopen'ed on first use (a process that already holds one -- torch's -- gets that
+// one back by soname), so the library has no link-time RCCL dependency and a caller that
+// never makes a communicator never loads it.  The types come from the ROCm header.
+namespace {
+struct RcclApi {
+    bool ok = false;
+    std::string err;
+    ncclResult_t (*get_id)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*destroy)(ncclComm_t) = nullptr;
+    const char* (*errstr)(ncclResult_t) = nullptr;
+};
+const RcclApi& rccl()
+{
+    static RcclApi api;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* h = nullptr;
+        for (const char* n : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+            if ((h = dlopen(n, RTLD_NOW | RTLD_GLOBAL))) break;
+        if (!h) {
+            api.err = dlerror() ? dlerror() : "librccl not found";
+            return;
+        }
+        api.get_id = (decltype(api.get_id))dlsym(h, "ncclGetUniqueId");
+        api.init_rank = (decltype(api.init_rank))dlsym(h, "ncclCommInitRank");
+        api.all_reduce = (decltype(api.all_reduce))dlsym(h, "ncclAllReduce");
+        api.destroy = (decltype(api.destroy))dlsym(h, "ncclCommDestroy");
+        api.errstr = (decltype(api.errstr))dlsym(h, "ncclGetErrorString");
+        api.ok = api.get_id && api.init_rank && api.all_reduce && api.destroy && api.errstr;
+        if (!api.ok) api.err = "librccl lacks the nccl* entry points";
+    });
+    return api;
+}
+}  // namespace
+
+#define RCCLCHK(c, x)                                                                                        \
+    do {                                                                                                    \
+        const ncclResult_t r_ = (x);                                                                        \
+        if (r_ != ncclSuccess) return fail((c), HD_E_HIP, "%s failed: %s", #x, rccl().errstr(r_));          \
+    } while (0)
+
+extern "C" int hd_comm_unique_id(uint8_t* id)
+{
+    if (!id) return fail(nullptr, HD_E_INVAL, "hd_comm_unique_id: NULL id");
+    const RcclApi& r = rccl();
+    if (!r.ok) return fail(nullptr, HD_E_HIP, "hd_comm_unique_id: %s", r.err.c_str());
+    ncclUniqueId u;
+    RCCLCHK(nullptr, r.get_id(&u));
+    memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+    return HD_OK;
+}
+
+extern "C" int hd_comm_init(hd_ctx* c, const uint8_t* id, int32_t rank, int32_t world)
+{
+    if (!c || !id) return fail(c, HD_E_INVAL, "hd_comm_init: NULL argument");
+    if (world < 1 || rank < 0 || rank >= world) return fail(c, HD_E_INVAL, "hd_comm_init: rank %d of %d", rank, world);
+    if (c->comm) return fail(c, HD_E_STATE, "hd_comm_init: the context already has a communicator");
+    const RcclApi& r = rccl();
+    if (!r.ok) return fail(c, HD_E_HIP, "hd_comm_init: %s", r.err.c_str());
+    HIPCHK(c, hipSetDevice(c->device));
+    ncclUniqueId u;
+    memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+    ncclComm_t comm = nullptr;
+    RCCLCHK(c, r.init_rank(&comm, world, u, rank));       // collective: every rank of the id
+    c->comm = comm;
+    c->comm_rank = rank;
+    c->comm_world = world;
+    return HD_OK;
+}
+
+static int comm_scratch(hd_ctx* c, size_t bytes)
+{
+    if (c->comm_bytes >= bytes) return HD_OK;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    dfree(c->d_comm);
+    c->d_comm = nullptr;
+    c->comm_bytes = 0;
+    HIPCHK(c, hipMalloc(&c->d_comm, bytes));
+    c->comm_bytes = bytes;
+    return HD_OK;
+}
+
+extern "C" int hd_comm_allreduce_sum_f64(hd_ctx* c, double* buf, int64_t n)
+{
+    if (!c || (n > 0 && !buf) || n < 0) return fail(c, HD_E_INVAL, "hd_comm_allreduce_sum_f64: bad argument");
+    if (!c->comm) return fail(c, HD_E_STATE, "hd_comm_allreduce_sum_f64: no communicator (hd_comm_init)");
+    if (n == 0) return HD_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    hipPointerAttribute_t at{};
+    const bool dev = hipPointerGetAttributes(&at, buf) == hipSuccess && at.type == hipMemoryTypeDevice;
+    (void)hipGetLastError();
+    double* d = buf;
+    const size_t bytes = (size_t)n * sizeof(double);
+    if (!dev) {
+        int rc = comm_scratch(c, bytes);
+        if (rc) return rc;
+        d = c->d_comm;
+        HIPCHK(c, hipMemcpyAsync(d, buf, bytes, hipMemcpyHostToDevice, c->stream));
+    }
+    RCCLCHK(c, rccl().all_reduce(d, d, (size_t)n, ncclFloat64, ncclSum, (ncclComm_t)c->comm, c->stream));
+    if (!dev) HIPCHK(c, hipMemcpyAsync(buf, d, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return HD_OK;
+}
+
+extern "C" int hd_slice_exchange_clip(hd_ctx* c, int64_t nown, int64_t nblk_total)
+{
+    if (!c) return fail(nullptr, HD_E_INVAL, "hd_slice_exchange_clip: NULL context");
+    if (!c->comm) return fail(c, HD_E_STATE, "hd_slice_exchange_clip: no communicator (hd_comm_init)");
+    if (!(c->opts.clip_sigma > 0.0f)) return HD_OK;
+    if (nblk_total < 1 || nown < 0) return fail(c, HD_E_INVAL, "hd_slice_exchange_clip: bad block counts");
+    HIPCHK(c, hipSetDevice(c->device));
+    // the beam's [nblk_total][nchan + 3] statistics table on the device: this slice's own
+    // rows (hd_clip_stats), summed over the ranks, then clip_times finished (hd_clip_set_stats)
+    const size_t n = (size_t)nblk_total * ((size_t)c->obs.nchan + 3);
+    int rc = comm_scratch(c, n * sizeof(double));
+    if (rc) return rc;
+    HIPCHK(c, hipMemsetAsync(c->d_comm, 0, n * sizeof(double), c->stream));
+    rc = hd_clip_stats(c, nown, c->d_comm);
+    if (rc) return rc;
+    rc = hd_comm_allreduce_sum_f64(c, c->d_comm, (int64_t)n);
+    if (rc) return rc;
+    return hd_clip_set_stats(c, c->d_comm);
+}
+
+extern "C" int hd_comm_destroy(hd_ctx* c)
+{
+    if (!c) return HD_OK;
+    if (c->comm) {
+        (void)hipSetDevice(c->device);
+        (void)hipStreamSynchronize(c->stream);
+        (void)rccl().destroy((ncclComm_t)c->comm);
+        c->comm = nullptr;
+    }
+    dfree(c->d_comm);
+    c->d_comm = nullptr;
+    c->comm_bytes = 0;
+    c->comm_rank = c->comm_world = 0;
     return HD_OK;
 }

@@ -38,7 +38,8 @@ EXPORTED = [
     "hd_get_raw", "hd_plan_tables", "hd_run_subband_multi", "hd_push_raw_device", "hd_get_raw_device",
     "hd_push_raw_file", "hd_set_streams", "hd_touch_raw", "hd_stats_padvals", "hd_get_clean",
     "hd_get_subbands_window", "hd_get_series", "hd_write_series", "hd_wait_writes",
-    "hd_set_slice", "hd_clip_stats", "hd_clip_set_stats", "hd_series_sum", "hd_series_sum_multi", "hd_series_fill",
+    "hd_set_slice", "hd_clip_stats", "hd_clip_set_stats", "hd_series_sum", "hd_series_sum_multi", "hd_series_fill", "hd_comm_unique_id", "hd_comm_init",
+    "hd_comm_allreduce_sum_f64", "hd_slice_exchange_clip", "hd_comm_destroy",
     "hd_sp_widths", "hd_single_pulse", "hd_single_pulse_launch", "hd_single_pulse_collect", "hd_rfifind_stats",
     "hd_push_raw_file_band", "hd_fill_raw",
     "hd_realfft", "hd_fft_prepare", "hd_zap_ranges", "hd_zapbirds", "hd_rednoise_blocks", "hd_rednoise", "hd_get_fft",
@@ -164,6 +165,11 @@ def load():
         "hd_clip_set_stats": (ctypes.c_int, [vp, vp]),
         "hd_series_sum": (ctypes.c_int, [vp, i32, i64, i64, P(ctypes.c_double)]),
         "hd_series_sum_multi": (ctypes.c_int, [P(vp), i32, i32, P(i64), P(i64), P(ctypes.c_double)]),
+        "hd_comm_unique_id": (ctypes.c_int, [P(ctypes.c_uint8)]),
+        "hd_comm_init": (ctypes.c_int, [vp, P(ctypes.c_uint8), i32, i32]),
+        "hd_comm_allreduce_sum_f64": (ctypes.c_int, [vp, vp, i64]),
+        "hd_slice_exchange_clip": (ctypes.c_int, [vp, i64, i64]),
+        "hd_comm_destroy": (ctypes.c_int, [vp]),
         "hd_series_fill": (ctypes.c_int, [vp, i64, ctypes.c_float]),
         "hd_rfifind_stats": (ctypes.c_int, [vp, i32, f32p, f32p, f32p]),
         "hd_realfft": (ctypes.c_int, [vp]),

@@ -336,6 +336,37 @@ class Engine:
         ptr = stats if isinstance(stats, int) else stats.ctypes.data
         self._chk(self._L.hd_clip_set_stats(self._ctx, ctypes.c_void_p(ptr)), "hd_clip_set_stats")
 
+    # -- in-library collectives (hd_comm_*: RCCL, no torch.distributed) --
+    @staticmethod
+    def comm_unique_id():
+        """A new 128-byte communicator id (rank 0; hand it to every rank)."""
+        L = _lib.load()
+        buf = (ctypes.c_uint8 * 128)()
+        _check(L.hd_comm_unique_id(buf), "hd_comm_unique_id")
+        return bytes(buf)
+
+    def comm_init(self, uid, rank, world):
+        """Join the communicator `uid` as rank `rank` of `world` (collective)."""
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(bytes(uid))
+        self._chk(self._L.hd_comm_init(self._ctx, buf, int(rank), int(world)), "hd_comm_init")
+
+    def comm_allreduce(self, x):
+        """Sum a float64 numpy array (in place) or (address, n) of device doubles over the ranks."""
+        if isinstance(x, tuple):
+            ptr, n = x
+        else:
+            assert x.dtype == np.float64 and x.flags.c_contiguous
+            ptr, n = x.ctypes.data, x.size
+        self._chk(self._L.hd_comm_allreduce_sum_f64(self._ctx, ctypes.c_void_p(ptr), int(n)), "hd_comm_allreduce_sum_f64")
+        return x
+
+    def slice_exchange_clip(self, nown, nblk_total):
+        """hd_clip_stats -> all-reduce -> hd_clip_set_stats over the communicator."""
+        self._chk(self._L.hd_slice_exchange_clip(self._ctx, int(nown), int(nblk_total)), "hd_slice_exchange_clip")
+
+    def comm_destroy(self):
+        self._chk(self._L.hd_comm_destroy(self._ctx), "hd_comm_destroy")
+
     def synth_device(self, synth: hd_synth):
         self._chk(self._L.hd_synth_device(self._ctx, ctypes.byref(synth)), "hd_synth_device")
 

@@ -177,3 +177,39 @@ def test_clip_stats_device_pointer_path(engine):
         for e in engs:
             e.close()
         hip.hipFree(dtab)
+
+
+def test_in_library_comm_world1(engine):
+    """hd_comm_* (RCCL loaded by the library, no torch.distributed) at world size 1 -- the
+    collective path a C caller of a time-sliced beam takes: the all-reduce of host and device
+    doubles returns them unchanged, and hd_slice_exchange_clip on a one-slice context leaves
+    the same clip_times state as the whole-beam context; misuse is refused."""
+    import ctypes
+    from hipdedisp.engine import PrestoError
+    obs = palfa_obs(N=(1 << 17) + 777, nbits=8, nsblk=2048)
+    synth = spiky()
+    engine.set_obs(obs, Opts())
+    engine.synth_device(synth)
+    gpad, gclip, gzap, _ = engine.get_clean()
+    e = Engine(0)
+    try:
+        with pytest.raises(PrestoError, match="no communicator"):
+            e.comm_allreduce(np.zeros(3))
+        uid = Engine.comm_unique_id()
+        assert len(uid) == 128
+        e.comm_init(uid, 0, 1)
+        with pytest.raises(PrestoError, match="already has a communicator"):
+            e.comm_init(uid, 0, 1)
+        x = np.arange(1000, dtype=np.float64) * 0.5
+        assert np.array_equal(e.comm_allreduce(x.copy()), x)
+        e.set_obs(obs, Opts())
+        e.set_slice(0, obs.N)
+        e.synth_device(synth)
+        ts = S.TimeSlices(obs, small_plan(), 1)
+        e.slice_exchange_clip(ts.nown_blocks(0), ts.nblk_total)
+        lpad, lclip, lzap, _ = e.get_clean()
+        assert np.array_equal(lclip, gclip) and np.array_equal(lpad, gpad) and np.array_equal(lzap, gzap)
+        e.comm_destroy()
+        e.comm_destroy()                                 # idempotent
+    finally:
+        e.close()
