@@ -2414,7 +2414,11 @@ static int run_subband_chunk(hd_ctx* c, hd_plan** plans, int n)
     const bool tiled = !q8 && (v1 == 0 || v1 == 2) && stage1_tiling(c, p0->pass.nsub, p0->pass.ds, dmax, m, vw);
     int rc0 = ensure_blocks(c);
     if (rc0) return rc0;
-    for (int i = 0; i < n; i++) HIPCHK(c, hipMemsetAsync(plans[i]->d_maxabs, 0, sizeof(int32_t), c->stream));
+    {
+        hd::ZeroList z{};
+        for (int i = 0; i < n; i++) z.p[i] = plans[i]->d_maxabs;
+        HIPCHK(c, hd::launch_zero_list(z, n, c->stream));
+    }
     HIPCHK(c, hipEventRecord(p0->ev[0], c->stream));
     // the channel-major copy (once per raw block) on saux, beside clip_times' serial 30-block
     // recurrence (one workgroup): forked after clip_times' full-chip statistics kernels, or
@@ -2593,7 +2597,11 @@ static int run_subband_fused(hd_ctx* c, hd_plan** plans, int n)
     if (!alloc_rawT(c, dmax)) return 1;                          // (the fill reads the channel-major copy)
     int rc0 = ensure_blocks(c);
     if (rc0) return rc0;
-    for (int i = 0; i < n; i++) HIPCHK(c, hipMemsetAsync(plans[i]->d_maxabs, 0, sizeof(int32_t), c->stream));
+    {
+        hd::ZeroList z{};
+        for (int i = 0; i < n; i++) z.p[i] = plans[i]->d_maxabs;
+        HIPCHK(c, hd::launch_zero_list(z, n, c->stream));
+    }
     HIPCHK(c, hipEventRecord(p0->ev[0], c->stream));
     const bool clip_runs = c->opts.clip_sigma > 0.0f && !c->clip_valid;
     const bool fork_clip = clip_runs && !c->rawT_valid && alloc_rawT(c, dmax);

@@ -766,7 +766,8 @@ __device__ __forceinline__ float fix8_fold_pre(const Stage1Multi& a, const uint8
         pb[cc] = pad[G + lc0 + cc];
     }
     float acc = 0.0f;
-#pragma unroll 1
+    // (two steps in flight: their channel sums are independent, only acc is a chain)
+#pragma unroll 2
     for (int k = 0; k < ds; k++) {
         uint32_t fb[CPS], rb[CPS];
         float pv[CPS];

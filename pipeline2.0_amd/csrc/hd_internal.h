@@ -166,6 +166,12 @@ hipError_t launch_stage2_lds(const Stage2Args& a, int q, hipStream_t st);
 hipError_t launch_pad(float* out, int64_t out_stride, int numdms, int64_t nds, int64_t numout,
                       const double* partial, int ntiles, int pad_mode, hipStream_t st);
 hipError_t launch_series_sum(const float* x, int64_t n, double* part, int nparts, hipStream_t st);
+// zero the int32 at each of n (<= kMaxPass) addresses: one launch for a stage-1 call's
+// per-plan max|subband| words instead of n memsets
+struct ZeroList {
+    int32_t* p[kMaxPass];
+};
+hipError_t launch_zero_list(const ZeroList& z, int n, hipStream_t st);
 hipError_t launch_series_fill(float* out, int64_t out_stride, int numdms, int64_t t0, int64_t t1, float v,
                               hipStream_t st);
 

@@ -1419,6 +1419,19 @@ hipError_t launch_series_sum(const float* x, int64_t n, double* part, int nparts
     return hipGetLastError();
 }
 
+__global__ __launch_bounds__(64) void k_zero_list(ZeroList z, int n)
+{
+    if ((int)threadIdx.x < n) *z.p[threadIdx.x] = 0;
+}
+
+hipError_t launch_zero_list(const ZeroList& z, int n, hipStream_t st)
+{
+    if (n <= 0) return hipSuccess;
+    if (n > kMaxPass) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_zero_list, dim3(1), dim3(64), 0, st, z, n);
+    return hipGetLastError();
+}
+
 __global__ __launch_bounds__(256) void k_series_fill(float* out, int64_t out_stride, int64_t t0, int64_t t1, float v)
 {
     float* o = out + (int64_t)blockIdx.y * out_stride;
