@@ -2442,6 +2442,8 @@ static int run_subband_chunk(hd_ctx* c, hd_plan** plans, int n)
         // 5-7 also select the separate kernels)
         const bool env_qfix = getenv("HD_QFIX") && atoi(getenv("HD_QFIX")) != 0;
         m.qfix = clip && env_qfix && !(p0->probe & (32 | 64 | 128)) ? 1 : 0;
+        // HD_Q8_WPS2=1: 8-wave blocks at sg = 4, two waves per subband splitting the passes
+        m.wps2 = getenv("HD_Q8_WPS2") && atoi(getenv("HD_Q8_WPS2")) != 0 && !m.qfix ? 1 : 0;
         m.rd = raw_desc(c);
         m.rawT = rawT;
         if (!m.rawT && c->obs.nbits != 8) return fail(c, HD_E_HIP, "stage 1: 4-bit channel-major copy failed");

@@ -63,6 +63,7 @@ struct Stage1Multi {
                               // constant needs (float-fold error, plus the /ds rounding in mean mode)
     int32_t ntiles, ngroups;
     int32_t pass_ds;                // k_stage1_fix8: 1 = per-pass ds in pds[] (ds = their max)
+    int32_t wps2;                   // k_stage1_q8 with sg >= 4: 2 waves per subband (8-wave blocks)
     int32_t pds[kMaxPass];          // k_stage1_q8m / pass_ds: per-pass downsampling
     double ptie[kMaxPass];          // k_stage1_q8m: per-pass tie_eps (its ds)
     const int32_t* dly[kMaxPass];   // per-pass idispdt [nchan]

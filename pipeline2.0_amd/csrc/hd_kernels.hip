@@ -530,11 +530,11 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // hd_plan_set_variant's probe byte, value 16: one wave per subband, the spare waves idle).
 __host__ __device__ __forceinline__ int q8_waves_per_subband(const Stage1Multi& a)
 {
-    return (a.probe & 16) || a.sg >= 4 ? 1 : 4 / a.sg;
+    return (a.probe & 16) ? 1 : a.sg >= 4 ? (a.wps2 ? 2 : 1) : 4 / a.sg;
 }
 
 template <int CPS, int DS, int VB>
-__global__ __launch_bounds__(256) void k_stage1_q8(Stage1Multi a)
+__global__ __launch_bounds__(512) void k_stage1_q8(Stage1Multi a)
 {
     constexpr bool THREE = Q8Geom<DS>::THREE;
     using Gm = Q8Geom<DS>;
@@ -1137,7 +1137,8 @@ template <int CPS, int DS>
 static hipError_t launch_q8_ds(const Stage1Multi& a, int vb, size_t lds, hipStream_t st)
 {
     // at least 4 waves fill the tile (the fill is latency-bound); waves past sg then leave
-    const dim3 block((unsigned)(64 * (a.sg < 4 ? 4 : a.sg))), grid((unsigned)(a.ntiles * a.ngroups));
+    const dim3 block((unsigned)(64 * (a.sg < 4 ? 4 : a.sg) * (a.sg >= 4 && a.wps2 ? 2 : 1))),
+        grid((unsigned)(a.ntiles * a.ngroups));
     if (vb == 8) hipLaunchKernelGGL((k_stage1_q8<CPS, DS, 8>), grid, block, lds, st, a);
     else hipLaunchKernelGGL((k_stage1_q8<CPS, DS, 4>), grid, block, lds, st, a);
     return hipGetLastError();
