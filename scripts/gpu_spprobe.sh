@@ -5,7 +5,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 : > gpurun_out/spprobe.txt
-for pr in 0 1 8 16 4; do
+for pr in ${PROBES:-0 1 8 16 4}; do
   HD_SP_PROBE=$pr timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/spp_$pr -o run -- python3 bench.py \
       --steps 1 --warmup 0 --no-cpu --e2e-beams 0 --fft-beams 0 --rfi-beams 0 --stream-beams 0 --sp-beams 1 > gpurun_out/spp_$pr.log 2>&1 \
       || { echo "probe $pr failed"; tail -20 gpurun_out/spp_$pr.log; exit 1; }
