@@ -276,17 +276,36 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
     // bad blocks and past the searched length), staged as doubles in P[e + 1]; width 1 is
     // tested on the spot: every value above threshold outside the bad blocks is a hit (no
     // prune_related1), so the chunk's samples are not read and normalised a second time
-    for (int e = tid; e < kSpWin; e += NW * 64) {
+    // (the window's <= 10 blocks' coefficients staged in LDS and every sample load issued
+    // before the arithmetic: the loop no longer waits on two dependent global loads per step)
+    __shared__ double cfs[12][4];
+    const int64_t wlo = w0 > 0 ? w0 : 0, whi = w0 + kSpWin < a.ls ? w0 + kSpWin : a.ls;
+    const int64_t bl0 = wlo / kSpBlock;
+    const int nbk = whi > wlo ? (int)((whi - 1) / kSpBlock - bl0 + 1) : 0;
+    if (tid < nbk * 4) cfs[tid >> 2][tid & 3] = cf[(bl0 + (tid >> 2)) * 4 + (tid & 3)];
+    constexpr int NI = (kSpWin + NW * 64 - 1) / (NW * 64);
+    float xv[NI];
+#pragma unroll
+    for (int it = 0; it < NI; it++) {
+        const int e = tid + it * NW * 64;
+        const int64_t i = w0 + e;
+        xv[it] = e < kSpWin && i >= 0 && i < a.ls ? xs[i] : 0.0f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < NI; it++) {
+        const int e = tid + it * NW * 64;
+        if (e >= kSpWin) continue;
         const int64_t i = w0 + e;
         float v = 0.0f;
         bool isbad = false;
         if (i >= 0 && i < a.ls) {
             const int64_t b = i / kSpBlock;
-            const double* c = cf + b * 4;
+            const double* c = cfs[b - bl0];
             isbad = c[3] != 0.0;
             if (!isbad && c[2] != 0.0) {
                 const double t = (double)(i - b * kSpBlock) - 499.5;
-                const float d = (float)((double)xs[i] - (c[0] + c[1] * t));
+                const float d = (float)((double)xv[it] - (c[0] + c[1] * t));
                 v = (float)((double)d / c[2]);
             }
         }
