@@ -221,7 +221,13 @@ struct SpArgs {
     int64_t cap;
     int32_t probe;                               // profiling (HD_SP_PROBE): 1 no walk, 2 no width-1, 4 no bitmask,
                                                  // 8 no true chain, 16 no emission of the walk's survivors
+    uint32_t* stats;                             // profiling (HD_SP_STATS): kSpStats words per workgroup, or null
 };
+// HD_SP_STATS words: 0-6 wall clock (100 MHz) at the phase ends (normalise, prefix, bitmask,
+// spec walk, true chain, emission; round 1 for the last four); 7 sum over widths of the
+// busiest lane's walk steps, 8 of its batch loads; 9 true-chain pivots, 10 true-chain ballot
+// steps, 11 hits, 12 merges, 13 width of the slowest spec wave, 14 its ticks
+constexpr int kSpStats = 16;
 
 // The width-1 hits of the active lanes: one counter atomic per wave (a bright pulse gives
 // thousands of hits per chunk; one global atomic each serialised the whole grid on one address)
@@ -247,7 +253,7 @@ __device__ __forceinline__ void sp_emit_wave(const SpArgs& a, int dm, int64_t bi
     }
 }
 
-template <int NW>
+template <int NW, bool STATS>
 __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
 {
     constexpr int kSpRound = NW;
@@ -272,6 +278,11 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
     const int64_t c0 = (int64_t)ch * kSpChunk;               // first bin of the chunk
     const int tid = threadIdx.x;
     const int wv = tid >> 6, ln = tid & 63;
+    uint32_t* const sst = STATS ? a.stats + (int64_t)blockIdx.x * kSpStats : nullptr;
+    const uint64_t t_start = STATS ? wall_clock64() : 0;
+    auto stamp = [&](int k) {
+        if (sst && tid == 0) sst[k] = (uint32_t)(wall_clock64() - t_start);
+    };
     // the normalised samples of the window (detrended by the block's line, over its std; 0 in
     // bad blocks and past the searched length), staged as doubles in P[e + 1]; width 1 is
     // tested on the spot: every value above threshold outside the bad blocks is a hit (no
@@ -345,6 +356,7 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
         }
         P[0] = 0.0;
     }
+    stamp(0);
     __syncthreads();
     if (tid < 256) {
         const double base = tot[tid];
@@ -352,6 +364,7 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
         for (int j = 0; j < kSpSeg; j++) P[tid * kSpSeg + j + 1] = base + P[tid * kSpSeg + j + 1];
     }
     __syncthreads();
+    stamp(1);
     // boxcar value (width index wi > 0) at chunk bin o
     auto boxcar = [&](int wi, int o) -> double {
         const int w = a.widths[wi];
@@ -373,9 +386,11 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
             if (ln == 0) {
                 bits[j][2 * q] = (uint32_t)m;
                 bits[j][2 * q + 1] = (uint32_t)(m >> 32);
+                if (sst) atomicAdd(sst + 11, (uint32_t)__popcll(m));
             }
         }
         __syncthreads();
+        if (r0 == 1) stamp(2);
         // prune_related1 of width r0 + wv, by wave wv.  The script's walk is a chain through a
         // function of the pivot alone: next(p) = the first hit q > p with q - p > h or
         // x_q >= x_p (hits between are dropped), and p is kept when that step is a gap (or p is
@@ -412,51 +427,61 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
             for (int ww = kSpSegW * (sg + 1 + __builtin_ctzll(rest));; ww++)
                 if (bm[ww]) return ww;
         };
-        // next(p) and its value: the hits after p in batches of 8 from the word masks (their
-        // boxcar reads issue together; a dense run is thousands of hits).  The batch is kept:
-        // when the chain asks again from the pivot just returned, the batch's later hits are
-        // tested first, so a dense rising run steps through all 8 per LDS round trip instead
-        // of one (cache: hits cq/cx with bits cm, after pivot clastp; loading resumes at word
-        // cw with bits cmk)
-        int cq[8];
-        double cx[8];
-        uint32_t cm = 0, cmk = 0;
-        int cw = 0, clastp = -2;
-        auto nextpivot = [&](int p, double px, double& qx) -> int {
-            int w;
-            uint32_t m;
-            if (p == clastp) {
+        // The lane streams through the hits after its segment's first hit in bin order, eight
+        // per iteration (their boxcars read together), each tested against the current pivot,
+        // which moves to the first one that qualifies; the remaining hits of the batch are then
+        // tested against the new pivot.  One flat loop: the wave's trip count is the longest
+        // lane's batch count (a next-pivot search nested in a loop over pivots made it the sum
+        // over steps of the slowest lane's search).  Pivot / kept bits: bin - 128 * lane.
+        int n_step = 0, n_batch = 0;                          // (HD_SP_STATS)
+        const int sw0 = ln * kSpSegW;                             // this lane's words
+        const uint64_t t_spec = STATS ? wall_clock64() : 0;
+        if (walk) {
+            uint64_t sp_lo = 0, sp_hi = 0, em_lo = 0, em_hi = 0;
+            const int segbeg = 32 * sw0, segend = 32 * (sw0 + kSpSegW);
+            auto setbit = [&](uint64_t& lo, uint64_t& hi, int b) {
+                const int r = b - segbeg;
+                if (r < 64) lo |= 1ull << r;
+                else hi |= 1ull << (r - 64);
+            };
+            int ex = -1, nh = 0;
+            int p = -1;
 #pragma unroll
-                for (int k = 0; k < 8; k++)
-                    if ((cm >> k) & 1u) {
-                        cm &= ~(1u << k);
-                        if (cq[k] - p > h || cx[k] >= px) {
-                            qx = cx[k];
-                            clastp = cq[k];
-                            return cq[k];
-                        }
-                    }
-                w = cw;
-                m = cmk;
-            } else {
-                cm = 0;
-                w = (p + 1) >> 5;
-                if (w >= kSpWords) {
-                    clastp = -2;
-                    return -1;
-                }
-                m = bm[w] & (~0u << ((p + 1) & 31));
+            for (int k = 0; k < kSpSegW; k++) {
+                const uint32_t m = sw0 + k < kSpWords ? bm[sw0 + k] : 0u;
+                nh += __builtin_popcount(m);
+                if (p < 0 && m) p = 32 * (sw0 + k) + __builtin_ctz(m);
             }
-            while (true) {
+            segmask = __ballot(nh > 0);
+            bool act = p >= 0;
+            double px = 0.0;
+            int w = 0;
+            uint32_t m = 0;
+            if (act) {
+                px = boxcar(wi, p);
+                setbit(sp_lo, sp_hi, p);
+                w = (p + 1) >> 5;
+                if (w < kSpWords) {
+                    m = bm[w] & (~0u << ((p + 1) & 31));
+                } else {
+                    setbit(em_lo, em_hi, p);                  // the last bin: no next pivot
+                    act = false;
+                }
+            }
+            while (act) {
                 if (!m) {
                     w = nextword(w);
-                    if (w < 0) {
-                        clastp = -2;
-                        return -1;
+                    if (w < 0) {                              // no hit after p: p is kept
+                        setbit(em_lo, em_hi, p);
+                        act = false;
+                        break;
                     }
                     m = bm[w];
                 }
+                int cq[8];
+                double cx[8];
                 int n = 0;
+                n_batch++;
 #pragma unroll
                 for (int k = 0; k < 8; k++)
                     if (m) {
@@ -467,51 +492,28 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
 #pragma unroll
                 for (int k = 0; k < 8; k++)
                     if (k < n) cx[k] = boxcar(wi, cq[k]);
-                cm = (1u << n) - 1u;
 #pragma unroll
                 for (int k = 0; k < 8; k++)
-                    if (k < n) {
-                        cm &= ~(1u << k);
-                        if (cq[k] - p > h || cx[k] >= px) {
-                            qx = cx[k];
-                            clastp = cq[k];
-                            cw = w;
-                            cmk = m;
-                            return cq[k];
+                    if (act && k < n) {
+                        const int q = cq[k];
+                        if (q - p > h || cx[k] >= px) {
+                            n_step++;
+                            if (q - p > h) setbit(em_lo, em_hi, p);
+                            p = q;
+                            px = cx[k];
+                            if (p >= segend) {
+                                ex = p;
+                                act = false;
+                            } else {
+                                setbit(sp_lo, sp_hi, p);
+                            }
                         }
                     }
             }
-        };
-        const int sw0 = ln * kSpSegW;                             // this lane's words
-        if (walk) {
-            uint32_t sp[kSpSegW] = {0, 0, 0, 0}, em[kSpSegW] = {0, 0, 0, 0};
-            int ex = -1, nh = 0;
-            int p = -1;
-#pragma unroll
-            for (int k = 0; k < kSpSegW; k++) {
-                const uint32_t m = sw0 + k < kSpWords ? bm[sw0 + k] : 0u;
-                nh += __builtin_popcount(m);
-                if (p < 0 && m) p = 32 * (sw0 + k) + __builtin_ctz(m);
-            }
-            const int segend = 32 * (sw0 + kSpSegW);
-            segmask = __ballot(nh > 0);
-            if (p >= 0) {
-                double px = boxcar(wi, p);
-                while (true) {
-                    const int k = (p >> 5) - sw0;
-                    sp[k] |= 1u << (p & 31);
-                    double qx = 0.0;
-                    const int q = nextpivot(p, px, qx);
-                    if (q < 0 || q - p > h) em[k] |= 1u << (p & 31);
-                    if (q < 0) break;
-                    p = q;
-                    px = qx;
-                    if (p >= segend) {
-                        ex = p;
-                        break;
-                    }
-                }
-            }
+            const uint32_t sp[kSpSegW] = {(uint32_t)sp_lo, (uint32_t)(sp_lo >> 32), (uint32_t)sp_hi,
+                                          (uint32_t)(sp_hi >> 32)};
+            const uint32_t em[kSpSegW] = {(uint32_t)em_lo, (uint32_t)(em_lo >> 32), (uint32_t)em_hi,
+                                          (uint32_t)(em_hi >> 32)};
 #pragma unroll
             for (int k = 0; k < kSpSegW; k++)
                 if (sw0 + k < kSpWords) {
@@ -529,8 +531,24 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
             }
             W.hpre[jw][ln + 1] = (int16_t)inc;
             if (ln == 0) W.hpre[jw][0] = 0;
+            if (sst) {
+                int ms = n_step, mb = n_batch;
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) {
+                    ms = max(ms, __shfl_xor(ms, o, 64));
+                    mb = max(mb, __shfl_xor(mb, o, 64));
+                }
+                const uint32_t dt = (uint32_t)(wall_clock64() - t_spec);
+                if (ln == 0) {
+                    atomicAdd(sst + 7, (uint32_t)ms);
+                    atomicAdd(sst + 8, (uint32_t)mb);
+                    const uint32_t old = atomicMax(sst + 14, dt);
+                    if (dt > old) sst[13] = (uint32_t)a.widths[wi];
+                }
+            }
         }
         __syncthreads();
+        if (r0 == 1) stamp(3);
         // the true chain from the chunk's first hit, walked by the whole wave: each step tests
         // the 64 bins from the first hit after the pivot at once (lane l: bin start + l; the
         // first qualifying hit by ballot), so a step that skips a dense stretch of h bins costs
@@ -541,7 +559,9 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
             double px = p >= 0 ? boxcar(wi, p) : 0.0;
             while (p >= 0) {
                 const int sg = p >> 7;
+                if (sst && ln == 0) atomicAdd(sst + 9, 1u);
                 if ((W.spec[jw][p >> 5] >> (p & 31)) & 1u) {      // on the segment's chain from here
+                    if (sst && ln == 0) atomicAdd(sst + 12, 1u);
                     if (ln == 0) W.merge[jw][sg] = (int16_t)p;
                     p = W.exitb[jw][sg];
                     if (p >= 0) px = boxcar(wi, p);
@@ -559,6 +579,7 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
                         qual = b - p > h || xb >= px;
                     }
                     const uint64_t qm = __ballot(qual);
+                    if (sst && ln == 0) atomicAdd(sst + 10, 1u);
                     if (qm) {
                         const int fl = __ffsll((unsigned long long)qm) - 1;
                         q = start + fl;
@@ -573,6 +594,7 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
             }
         }
         __syncthreads();
+        if (r0 == 1) stamp(4);
         // emit the kept pivots of this lane's segment in bin order, with their ordinals
         if (walk && !(a.probe & 16)) {                           // (probe 16: profiling only)
             const int mg = W.merge[jw][ln];
@@ -667,7 +689,9 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
                 }
         }
         __syncthreads();
+        if (r0 == 1) stamp(5);
     }
+    stamp(6);
 }
 
 // The bad-block flags as bytes (the host needs ndm * nblocks bytes, not the 32-byte records).
@@ -723,12 +747,62 @@ hipError_t launch_sp_hits(const float* x, int64_t stride, int ndm, int nblocks, 
     a.cap = cap;
     a.probe = getenv("HD_SP_PROBE") ? atoi(getenv("HD_SP_PROBE")) : 0;
     if (a.nchunks <= 0 || ndm <= 0) return hipSuccess;
+    // HD_SP_STATS=1 (profiling): per-workgroup phase clocks and walk counters, summarised
+    // on stderr after each launch (synchronises the stream)
+    static uint32_t* d_stats = nullptr;
+    static int64_t stats_n = 0;
+    const int64_t nwg = (int64_t)ndm * a.nchunks;
+    const bool want_stats = getenv("HD_SP_STATS") && atoi(getenv("HD_SP_STATS"));
+    if (want_stats) {
+        if (stats_n < nwg) {
+            if (d_stats) (void)hipFree(d_stats);
+            if (hipMalloc(&d_stats, nwg * kSpStats * 4) != hipSuccess) return hipErrorOutOfMemory;
+            stats_n = nwg;
+        }
+        (void)hipMemsetAsync(d_stats, 0, nwg * kSpStats * 4, st);
+        a.stats = d_stats;
+    }
     // HD_SP_NW=4 (profiling): the 4-wave workgroup, four rounds of widths
     if (getenv("HD_SP_NW") && atoi(getenv("HD_SP_NW")) == 4)
-        hipLaunchKernelGGL(k_sp_hits<4>, dim3((unsigned)(ndm * a.nchunks)), dim3(256), 0, st, a);
+        hipLaunchKernelGGL((k_sp_hits<4, false>), dim3((unsigned)(ndm * a.nchunks)), dim3(256), 0, st, a);
+    else if (want_stats)
+        hipLaunchKernelGGL((k_sp_hits<16, true>), dim3((unsigned)(ndm * a.nchunks)), dim3(1024), 0, st, a);
     else
-        hipLaunchKernelGGL(k_sp_hits<16>, dim3((unsigned)(ndm * a.nchunks)), dim3(1024), 0, st, a);
-    return hipGetLastError();
+        hipLaunchKernelGGL((k_sp_hits<16, false>), dim3((unsigned)(ndm * a.nchunks)), dim3(1024), 0, st, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !want_stats) return e;
+    static int call = 0;
+    uint32_t* h = (uint32_t*)malloc(nwg * kSpStats * 4);
+    if (!h) return hipErrorOutOfMemory;
+    (void)hipStreamSynchronize(st);
+    (void)hipMemcpy(h, d_stats, nwg * kSpStats * 4, hipMemcpyDeviceToHost);
+    // phase sums over workgroups and the 6 slowest workgroups
+    double ph[7] = {0, 0, 0, 0, 0, 0, 0};
+    int64_t top[6] = {-1, -1, -1, -1, -1, -1};
+    for (int64_t g = 0; g < nwg; g++) {
+        const uint32_t* r = h + g * kSpStats;
+        for (int k = 0; k < 7; k++) ph[k] += (double)(r[k] - (k ? r[k - 1] : 0)) * 1e-5;  // ms
+        int64_t cur = g;
+        for (int k = 0; k < 6 && cur >= 0; k++)
+            if (top[k] < 0 || h[top[k] * kSpStats + 6] < h[cur * kSpStats + 6]) {
+                const int64_t t = top[k];
+                top[k] = cur;
+                cur = t;
+            }
+    }
+    fprintf(stderr, "sp_stats call %d ndm %d nchunks %d: workgroup-ms normalise %.1f prefix %.1f bitmask %.1f "
+            "spec %.1f true %.1f emit %.1f rest %.1f\n", call, ndm, a.nchunks, ph[0], ph[1], ph[2], ph[3], ph[4], ph[5], ph[6]);
+    for (int k = 0; k < 6 && top[k] >= 0; k++) {
+        const uint32_t* r = h + top[k] * kSpStats;
+        fprintf(stderr, "  wg dm %lld ch %lld: %.3f ms (phases %.3f %.3f %.3f %.3f %.3f %.3f) hits %u steps %u batches %u "
+                "true %u ballots %u merges %u slowest spec w %u %.3f ms\n", (long long)(top[k] / a.nchunks),
+                (long long)(top[k] % a.nchunks), r[6] * 1e-5, r[0] * 1e-5, (r[1] - r[0]) * 1e-5, (r[2] - r[1]) * 1e-5,
+                (r[3] - r[2]) * 1e-5, (r[4] - r[3]) * 1e-5, (r[5] - r[4]) * 1e-5, r[11], r[7], r[8], r[9], r[10], r[12],
+                r[13], r[14] * 1e-5);
+    }
+    call++;
+    free(h);
+    return hipSuccess;
 }
 
 }  // namespace hd
