@@ -89,30 +89,73 @@ __global__ __launch_bounds__(256) void k_sp_blocks(const float* __restrict__ x, 
         const int i = 16 * lane + r;
         v[r] = i < kSpBlock ? (float)((double)v[r] - (mean + slope * ((double)i - 499.5))) : __builtin_inff();
     }
-    // bitonic sort of the 1024 slots (element 16l + r in lane l, register r)
-    for (int k = 2; k <= 1024; k <<= 1) {
-        for (int j = k >> 1; j >= 16; j >>= 1) {              // partner in lane l ^ (j / 16)
-            const int lm = j >> 4;
-            const bool asc = ((16 * lane) & k) == 0, lower = (lane & lm) == 0;
+    // bitonic sort of the 1024 slots (element 16l + r in lane l, register r), fully unrolled,
+    // on order-preserving int keys (integer min / max / med3: no NaN canonicalisation).
+    // Merges of size k < 16 lie inside a lane, their directions fixed per register.  From
+    // k = 16 on, a lane's direction is one bit of its index: a descending lane holds its keys
+    // complemented, so every in-lane compare-exchange is ascending (min to the lower slot);
+    // across lanes the lower lane takes med3(v, o, INT_MIN) = min, the upper med3(v, o,
+    // INT_MAX) = max.  The sorted values are those of any sort (-0 before +0 here; equal
+    // squares either way), so the sum below is unchanged.
+    int32_t key[16];
 #pragma unroll
-            for (int r = 0; r < 16; r++) {
-                const float o = __shfl_xor(v[r], lm, 64);
-                v[r] = (asc == lower) ? fminf(v[r], o) : fmaxf(v[r], o);
-            }
-        }
-        for (int j = (k >> 1) < 8 ? (k >> 1) : 8; j >= 1; j >>= 1) {   // partner in this lane
+    for (int r = 0; r < 16; r++) {
+        const int32_t bb = __float_as_int(v[r]);
+        key[r] = bb ^ ((bb >> 31) & 0x7FFFFFFF);
+    }
+#pragma unroll
+    for (int lk = 1; lk <= 3; lk++) {
+        const int k = 1 << lk;
+#pragma unroll
+        for (int lj = lk - 1; lj >= 0; lj--) {
+            const int j = 1 << lj;
 #pragma unroll
             for (int r = 0; r < 16; r++) {
                 if (r & j) continue;
                 const int p = r | j;
-                const bool asc = ((16 * lane + r) & k) == 0;
-                const float a = v[r], c = v[p];
-                const float lo = fminf(a, c), hi = fmaxf(a, c);
-                v[r] = asc ? lo : hi;
-                v[p] = asc ? hi : lo;
+                const int32_t lo = min(key[r], key[p]), hi = max(key[r], key[p]);
+                const bool asc = (r & k) == 0;
+                key[r] = asc ? lo : hi;
+                key[p] = asc ? hi : lo;
             }
         }
     }
+    int32_t cpl = 0;                                           // current complement mask
+#pragma unroll
+    for (int lk = 4; lk <= 10; lk++) {
+        const int k = 1 << lk;
+        const int32_t want = ((16 * lane) & k) ? -1 : 0;
+        const int32_t flip = want ^ cpl;
+        cpl = want;
+#pragma unroll
+        for (int r = 0; r < 16; r++) key[r] ^= flip;
+#pragma unroll
+        for (int lj = lk - 1; lj >= 4; lj--) {                // partner in lane l ^ (j / 16)
+            const int lm = 1 << (lj - 4);
+            const int32_t bound = (lane & lm) ? 0x7FFFFFFF : (int32_t)0x80000000;
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int32_t o = __shfl_xor(key[r], lm, 64);
+                int32_t m3;
+                asm("v_med3_i32 %0, %1, %2, %3" : "=v"(m3) : "v"(key[r]), "v"(o), "v"(bound));
+                key[r] = m3;
+            }
+        }
+#pragma unroll
+        for (int lj = 3; lj >= 0; lj--) {                     // partner in this lane
+            const int j = 1 << lj;
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                if (r & j) continue;
+                const int p = r | j;
+                const int32_t lo = min(key[r], key[p]), hi = max(key[r], key[p]);
+                key[r] = lo;
+                key[p] = hi;
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; r++) v[r] = __int_as_float(key[r] ^ ((key[r] >> 31) & 0x7FFFFFFF));
     double q = 0.0;
 #pragma unroll
     for (int r = 0; r < 16; r++) {
@@ -379,6 +422,7 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
         // the above-threshold bins of widths r0 .. r0+nr-1 (bad blocks included: the script
         // prunes before it looks at blocks): lane = bin, one ballot per 64 bins (consecutive
         // lanes read consecutive P entries: no bank conflicts)
+        uint32_t nhit_wv = 0;                                 // (HD_SP_STATS)
         for (int t = wv; t < nr * (kSpChunk / 64); t += NW) {
             const int j = t / (kSpChunk / 64), q = t - j * (kSpChunk / 64);
             const bool hit = !(a.probe & 4) && boxcar(r0 + j, 64 * q + ln) > a.threshold;
@@ -386,9 +430,10 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
             if (ln == 0) {
                 bits[j][2 * q] = (uint32_t)m;
                 bits[j][2 * q + 1] = (uint32_t)(m >> 32);
-                if (sst) atomicAdd(sst + 11, (uint32_t)__popcll(m));
             }
+            nhit_wv += (uint32_t)__popcll(m);
         }
+        if (sst && ln == 0 && nhit_wv) atomicAdd(sst + 11, nhit_wv);
         __syncthreads();
         if (r0 == 1) stamp(2);
         // prune_related1 of width r0 + wv, by wave wv.  The script's walk is a chain through a
@@ -555,13 +600,14 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
         // h / 64 LDS round trips instead of h / 8 (one lane's batches) -- in a dense falling
         // run the chain hops by h + 1 and never meets the lanes' speculative chains
         if (walk && !(a.probe & 8)) {                             // (probe 8: profiling only)
+            uint32_t n_true = 0, n_merge = 0, n_ballot = 0;       // (HD_SP_STATS)
             int p = nexthit(-1);
             double px = p >= 0 ? boxcar(wi, p) : 0.0;
             while (p >= 0) {
                 const int sg = p >> 7;
-                if (sst && ln == 0) atomicAdd(sst + 9, 1u);
+                n_true++;
                 if ((W.spec[jw][p >> 5] >> (p & 31)) & 1u) {      // on the segment's chain from here
-                    if (sst && ln == 0) atomicAdd(sst + 12, 1u);
+                    n_merge++;
                     if (ln == 0) W.merge[jw][sg] = (int16_t)p;
                     p = W.exitb[jw][sg];
                     if (p >= 0) px = boxcar(wi, p);
@@ -579,7 +625,7 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
                         qual = b - p > h || xb >= px;
                     }
                     const uint64_t qm = __ballot(qual);
-                    if (sst && ln == 0) atomicAdd(sst + 10, 1u);
+                    n_ballot++;
                     if (qm) {
                         const int fl = __ffsll((unsigned long long)qm) - 1;
                         q = start + fl;
@@ -591,6 +637,11 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
                 if (ln == 0 && (q < 0 || q - p > h)) W.emt[jw][p >> 5] |= 1u << (p & 31);   // not in spec: kept pivot
                 p = q;
                 px = qx;
+            }
+            if (sst && ln == 0) {
+                atomicAdd(sst + 9, n_true);
+                atomicAdd(sst + 10, n_ballot);
+                atomicAdd(sst + 12, n_merge);
             }
         }
         __syncthreads();
