@@ -473,18 +473,27 @@ hipError_t launch_stage1_tiled(const Stage1Multi& a, int vw, const int* special,
 // straddling a mask interval boundary, and the last tile, are left to the float kernel
 // above (its SPECIAL launch over the same tiles).
 
-template <int DS>
+template <int DS, int MO = 0>
 struct Q8Geom {
-    static constexpr int M = DS == 1 ? 4 : DS == 2 ? 2 : 1;   // outputs per lane per quarter
+    static constexpr int M = MO ? MO : DS == 1 ? 4 : DS == 2 ? 2 : 1;   // outputs per lane per quarter
     static constexpr int JQ = 64 * M;                          // outputs per quarter
     static constexpr int S = JQ * DS;                          // dwords (raw rows) per quarter
     static constexpr bool THREE = DS >= 10;                    // 4S + dmax may exceed a 2048-row block
 };
 
+// HD_Q8_M1 (profiling): outputs per lane per quarter at ds 1 (4, or 2: half the tile, about
+// 5 instead of 3 workgroups per CU)
+int q8_m1()
+{
+    static int m = -1;
+    if (m < 0) m = getenv("HD_Q8_M1") && atoi(getenv("HD_Q8_M1")) == 2 ? 2 : 4;
+    return m;
+}
+
 int stage1_q8_quarter_rows(int ds)
 {
     switch (ds) {
-    case 1: return Q8Geom<1>::S;
+    case 1: return q8_m1() == 2 ? Q8Geom<1, 2>::S : Q8Geom<1>::S;
     case 2: return Q8Geom<2>::S;
     case 3: return Q8Geom<3>::S;
     case 5: return Q8Geom<5>::S;
@@ -496,11 +505,11 @@ int stage1_q8_quarter_rows(int ds)
 
 // Store the 4 quarter outputs of quarter-position j: integral -> the exact packed sums qv
 // (each already holding its pad constant, see k_stage1_q8), else the float folds qf.
-template <int DS>
+template <int DS, int MO>
 __device__ __forceinline__ void q8_store(const Stage1Multi& a, int p, int s, int64_t tO0, int j,
                                          const uint32_t* qv, const float* qf, bool integral, int& amax)
 {
-    constexpr int JQ = Q8Geom<DS>::JQ;
+    constexpr int JQ = Q8Geom<DS, MO>::JQ;
     if (a.sub_dtype == 0) {
         int16_t* o = (int16_t*)a.out[p] + (int64_t)s * a.ostride[p] + tO0 + j;
 #pragma unroll
@@ -533,11 +542,11 @@ __host__ __device__ __forceinline__ int q8_waves_per_subband(const Stage1Multi& 
     return (a.probe & 16) ? 1 : a.sg >= 4 ? (a.wps2 ? 2 : 1) : 4 / a.sg;
 }
 
-template <int CPS, int DS, int VB>
+template <int CPS, int DS, int VB, int MO = 0>
 __global__ __launch_bounds__(512) void k_stage1_q8(Stage1Multi a)
 {
-    constexpr bool THREE = Q8Geom<DS>::THREE;
-    using Gm = Q8Geom<DS>;
+    constexpr bool THREE = Q8Geom<DS, MO>::THREE;
+    using Gm = Q8Geom<DS, MO>;
     constexpr int M = Gm::M, JQ = Gm::JQ, S = Gm::S;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     uint32_t* lds = (uint32_t*)smem;
@@ -934,7 +943,7 @@ __global__ __launch_bounds__(512) void k_stage1_q8(Stage1Multi a)
 #pragma unroll
                 for (int m = 0; m < M; m++) {
                     const uint32_t qv[4] = {ae[m] & 0xFFFFu, ao[m] & 0xFFFFu, ae[m] >> 16, ao[m] >> 16};
-                    q8_store<DS>(a, p, s, tO0, lane + 64 * m, qv, nullptr, true, amax);
+                    q8_store<DS, MO>(a, p, s, tO0, lane + 64 * m, qv, nullptr, true, amax);
                 }
             }
         } else {
@@ -990,7 +999,7 @@ __global__ __launch_bounds__(512) void k_stage1_q8(Stage1Multi a)
                 if (mean)
 #pragma unroll
                     for (int q = 0; q < 4; q++) acc[q] = acc[q] / (float)DS;
-                q8_store<DS>(a, p, s, tO0, lane + 64 * m, nullptr, acc, false, amax);
+                q8_store<DS, MO>(a, p, s, tO0, lane + 64 * m, nullptr, acc, false, amax);
             }
         }
         if (a.sub_dtype == 0) {
@@ -1139,7 +1148,10 @@ static hipError_t launch_q8_ds(const Stage1Multi& a, int vb, size_t lds, hipStre
     // at least 4 waves fill the tile (the fill is latency-bound); waves past sg then leave
     const dim3 block((unsigned)(64 * (a.sg < 4 ? 4 : a.sg) * (a.sg >= 4 && a.wps2 ? 2 : 1))),
         grid((unsigned)(a.ntiles * a.ngroups));
-    if (vb == 8) hipLaunchKernelGGL((k_stage1_q8<CPS, DS, 8>), grid, block, lds, st, a);
+    if (DS == 1 && q8_m1() == 2) {
+        if (vb == 8) hipLaunchKernelGGL((k_stage1_q8<CPS, DS, 8, 2>), grid, block, lds, st, a);
+        else hipLaunchKernelGGL((k_stage1_q8<CPS, DS, 4, 2>), grid, block, lds, st, a);
+    } else if (vb == 8) hipLaunchKernelGGL((k_stage1_q8<CPS, DS, 8>), grid, block, lds, st, a);
     else hipLaunchKernelGGL((k_stage1_q8<CPS, DS, 4>), grid, block, lds, st, a);
     return hipGetLastError();
 }
@@ -1149,6 +1161,8 @@ static hipError_t set_lds_q8_ds(int bytes)
 {
     hipError_t e = set_max_lds((const void*)k_stage1_q8<CPS, DS, 8>, bytes);
     if (e == hipSuccess) e = set_max_lds((const void*)k_stage1_q8<CPS, DS, 4>, bytes);
+    if (DS == 1 && e == hipSuccess) e = set_max_lds((const void*)k_stage1_q8<CPS, DS, 8, 2>, bytes);
+    if (DS == 1 && e == hipSuccess) e = set_max_lds((const void*)k_stage1_q8<CPS, DS, 4, 2>, bytes);
     return e;
 }
 
