@@ -73,7 +73,8 @@ def parse():
     ap.add_argument("--comm", choices=["torch", "hd"], default="torch",
                     help="--mode slices: the two exchanges over torch.distributed (default) or over the library's own "
                          "RCCL communicator (hd_comm_*: hd_slice_exchange_clip, hd_comm_allreduce_sum_f64), the path a "
-                         "C caller takes")
+                         "C caller takes; inside this torch process it measured far slower (a second RCCL "
+                         "instance beside torch's, INTEGRATION.md), so it checks the path, not its speed")
     ap.add_argument("--sim-slice", default=None, metavar="R/G",
                     help="--mode slices on ONE process: run only rank R's slice of a G-way cut (no collectives; the "
                          "other ranks' clip statistics are absent, so only the timing is meaningful) -- the per-rank "
@@ -172,17 +173,30 @@ def single_pulse_leg(eng, stages, beams):
     hd_single_pulse on each pass's device-resident series (as left by the timed steps),
     candidates back on the host; wall seconds per beam and the candidate count."""
     from hipdedisp import single_pulse as SP
+    plans = [p for st in stages for p in st]
+
+    def beam():
+        n = 0
+        for _, hits, _ in SP.device_candidates_many(plans, 0.1, 5.0):
+            n += len(hits)
+        return n
+
     eng.sync()
+    t = time.perf_counter()
+    ncand0 = beam()                               # the first beam also sizes the context's search pool
+    first = time.perf_counter() - t
     t = time.perf_counter()
     ncand = 0
     for _ in range(beams):
-        for _, hits, _ in SP.device_candidates_many([p for plans in stages for p in plans], 0.1, 5.0):
-            ncand += len(hits)
+        ncand += beam()
     s = (time.perf_counter() - t) / beams
-    return {"s_per_beam": s, "candidates_per_beam": ncand // beams,
+    assert ncand == ncand0 * beams, "single-pulse candidates differ between beams"
+    return {"s_per_beam": s, "first_beam_s": first, "candidates_per_beam": ncand // beams,
             "note": "hd_single_pulse over the 57 passes' series in HBM (-m 0.1 -t 5.0): detrend, block stds, "
                     "boxcars, prune_related1 on the GPU; prune_related2 + border cases on the host, the device "
-                    "searches of the next 4 passes queued meanwhile (hd_single_pulse_launch/_collect); wall time"}
+                    "searches of the next 4 passes queued meanwhile (hd_single_pulse_launch/_collect); wall time "
+                    "per beam after one untimed beam (first_beam_s: that beam, which also allocates the "
+                    "context's pooled search buffers)"}
 
 
 def fft_leg(eng, stages, beams):
