@@ -122,6 +122,31 @@ def test_single_pulse_many_hits_and_short_series(engine, beam, tmp_path):
         p.destroy()
 
 
+def test_single_pulse_ties_constant_blocks_and_negatives(engine, beam, tmp_path):
+    """Crafted subbands (hd_set_subbands) instead of the synthetic beam: small-integer noise
+    (1000-sample blocks full of equal detrended values: the block-std sort's ties), a
+    constant stretch (zero-std blocks), a stretch of negative values and a bright pulse --
+    device bad blocks, hits and candidate lists equal to the oracle's, sigma bit-equal."""
+    obs, s = beam
+    pp = PassParams(subdm=4.0, lodm=0.2, dmstep=0.1, numdms=76, nsub=96, ds=1, numout=0)
+    p = engine.plan(pp)
+    try:
+        rng = np.random.default_rng(11)
+        nds = p.nds
+        sub = rng.integers(0, 4, size=(96, nds)).astype(np.int16)
+        sub[:, 20000:26000] = 3                                  # constant: zero-std blocks
+        sub[:, 40000:48000] = rng.integers(-3, 1, size=(96, 8000)).astype(np.int16)
+        sub[:, 100000:100040] += 6                               # a pulse at DM ~0
+        sub[:, 150000:150600] += rng.integers(0, 3, size=(96, 600)).astype(np.int16)   # a wide hump
+        p.set_subbands(sub)
+        series = p.run_dedisp()
+        dm_strs = ["%.2f" % (0.2 + 0.1 * k) for k in range(76)]
+        lists = check_pass(p, series, dm_strs, tmp_path)
+        assert sum(len(c) for c in lists) > 0
+    finally:
+        p.destroy()
+
+
 def test_candidate_lists_end_to_end_clip_vs_noclip(engine):
     """North-star 'identical candidate lists' on two independent paths, end to end: the
     product (stage 1 + stage 2 on the GPU, then hd_single_pulse on the series still in HBM)
