@@ -2505,6 +2505,10 @@ static int run_subband_chunk(hd_ctx* c, hd_plan** plans, int n)
         m.sub_round = c->opts.sub_round;
         m.nds = p0->nds;
         m.out_stride = p0->sub_stride;
+        // tiles over two read blocks stay in the main launch (per-row pads and zap bits of
+        // the two blocks, kModeTwo); only tiles over three or more take the special launch
+        // (HD_S1_TWO=0: every block-straddling tile special, as before)
+        m.two_ok = getenv("HD_S1_TWO") && atoi(getenv("HD_S1_TWO")) == 0 ? 0 : 1;
         m.ntiles = (int)((p0->nds + m.to - 1) / m.to);
         for (int i = 0; i < n; i++) {
             m.dly[i] = plans[i]->d_idispdt;

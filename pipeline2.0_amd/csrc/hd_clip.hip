@@ -73,6 +73,52 @@ __global__ __launch_bounds__(256) void k_clip_zdm_u4(RawDesc rd, float* __restri
     if (lane == 0) zdm[t] = (float)acc;
 }
 
+// The two int16 samples of a raw dword (low half first), either byte order.
+__device__ __forceinline__ void s16_pair(uint32_t w, bool be16, int& lo, int& hi)
+{
+    if (be16) w = __builtin_amdgcn_perm(0u, w, 0x02030001u);   // swap the bytes of each half
+    lo = (int)(int16_t)(w & 0xFFFFu);
+    hi = (int)(int16_t)(w >> 16);
+}
+
+// 16-bit data without calibration: a wave sums a spectrum's int16 samples as integers (8
+// per lane per 16-byte load) together with their magnitudes; when the magnitudes stay under
+// 2^24 no partial sum of the channel-order float fold can round, so the integer is that fold
+// exactly -- otherwise lane 0 folds the spectrum in channel order as the general kernel does.
+__global__ __launch_bounds__(256) void k_clip_zdm_u16(RawDesc rd, float* __restrict__ zdm)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (t >= rd.N) return;
+    const uint8_t* row = rd.raw + t * rd.rowbytes;
+    int acc = 0, mag = 0;
+    for (int o = lane * 16; o < rd.rowbytes; o += 1024) {
+        const uint4 v = *(const uint4*)(row + o);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            int lo, hi;
+            s16_pair(w[i], rd.be16, lo, hi);
+            acc += lo + hi;
+            mag += abs(lo) + abs(hi);
+        }
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        acc += __shfl_xor(acc, m, 64);
+        mag += __shfl_xor(mag, m, 64);
+    }
+    if (lane == 0) {
+        if (mag < (1 << 24)) {
+            zdm[t] = (float)acc;
+        } else {
+            float z = 0.0f;
+            for (int c = 0; c < rd.nchan; c++) z += raw_value(rd, t, c);
+            zdm[t] = z;
+        }
+    }
+}
+
 // General data: one thread per spectrum folds its channels in ascending-frequency order.
 __global__ __launch_bounds__(256) void k_clip_zdm(RawDesc rd, float* __restrict__ zdm)
 {
@@ -265,6 +311,52 @@ __global__ __launch_bounds__(256) void k_clip_chan_u4(ClipArgs a)
                 const bool hi = a.rd.nibble_hi_first ? j == 0 : j == 1;
                 a.chansum[(int64_t)b * nch + c] = (double)(hi ? sh[i] : sl[i]);
             }
+    }
+}
+
+// 16-bit data without calibration: a lane keeps the two int16 channels of one raw dword
+// over the block's good spectra (|sum| <= 8192 * 32768 < 2^31), exact like the double fold.
+__global__ __launch_bounds__(256) void k_clip_chan_u16(ClipArgs a)
+{
+    __shared__ uint8_t g[kClipMaxBlock];
+    const int nch = a.rd.nchan;
+    const int b = blockIdx.x;
+    const int64_t t0 = (int64_t)b * a.rd.blk;
+    const int nb = (int)min((int64_t)a.rd.blk, a.rd.N - t0);
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) g[i] = a.good[t0 + i];
+    __syncthreads();
+    const int nq = a.rd.rowbytes >> 2;                  // channel pairs per spectrum
+    const bool be = a.rd.be16;
+    for (int q = threadIdx.x; q < nq; q += blockDim.x) {
+        int s0 = 0, s1 = 0;
+        const uint8_t* base = a.rd.raw + t0 * a.rd.rowbytes + 4 * q;
+        int k = 0;
+        for (; k + 8 <= nb; k += 8) {
+            uint32_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) v[u] = g[k + u] ? *(const uint32_t*)(base + (int64_t)(k + u) * a.rd.rowbytes) : 0u;
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                int lo, hi;
+                s16_pair(v[u], be, lo, hi);
+                s0 += lo;
+                s1 += hi;
+            }
+        }
+        for (; k < nb; k++) {
+            const uint32_t v = g[k] ? *(const uint32_t*)(base + (int64_t)k * a.rd.rowbytes) : 0u;
+            int lo, hi;
+            s16_pair(v, be, lo, hi);
+            s0 += lo;
+            s1 += hi;
+        }
+        const int sv[2] = {s0, s1};
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            const int rc = 2 * q + i;                   // raw channel -> ascending channel
+            const int c = a.rd.flip ? nch - 1 - rc : rc;
+            a.chansum[(int64_t)b * nch + c] = (double)sv[i];
+        }
     }
 }
 
@@ -463,6 +555,8 @@ hipError_t launch_clip_stats(const ClipArgs& a, hipStream_t st, hipEvent_t after
         hipLaunchKernelGGL(k_clip_zdm_u8, dim3((unsigned)((rd.N + 3) / 4)), dim3(256), 0, st, rd, a.zdm);
     else if (rd.nbits == 4 && !calib && rd.rowbytes % 16 == 0)
         hipLaunchKernelGGL(k_clip_zdm_u4, dim3((unsigned)((rd.N + 3) / 4)), dim3(256), 0, st, rd, a.zdm);
+    else if (rd.nbits == 16 && !calib && rd.rowbytes % 16 == 0 && rd.blk <= kClipMaxBlock)
+        hipLaunchKernelGGL(k_clip_zdm_u16, dim3((unsigned)((rd.N + 3) / 4)), dim3(256), 0, st, rd, a.zdm);
     else
         hipLaunchKernelGGL(k_clip_zdm, dim3((unsigned)((rd.N + 255) / 256)), dim3(256), 0, st, rd, a.zdm);
     // the channel-major copy forks after the channel sums (beside the recurrence); forking it
@@ -479,6 +573,8 @@ hipError_t launch_clip_stats(const ClipArgs& a, hipStream_t st, hipEvent_t after
         hipLaunchKernelGGL(k_clip_chan_u8, dim3((unsigned)rd.nblk), dim3(256), 0, st, a);
     else if (rd.nbits == 4 && !calib && rd.rowbytes % 4 == 0)
         hipLaunchKernelGGL(k_clip_chan_u4, dim3((unsigned)rd.nblk), dim3(256), 0, st, a);
+    else if (rd.nbits == 16 && !calib && rd.rowbytes % 4 == 0)
+        hipLaunchKernelGGL(k_clip_chan_u16, dim3((unsigned)rd.nblk), dim3(256), 0, st, a);
     else
         hipLaunchKernelGGL(k_clip_chan, dim3((unsigned)(rd.nblk * ((rd.nchan + 255) / 256))), dim3(256), 0, st, a);
     if (after_stats && late) {  // the full-chip raw scans are done; the serial recurrence follows

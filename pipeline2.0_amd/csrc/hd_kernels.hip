@@ -328,8 +328,11 @@ void k_stage1_tiled(Stage1Multi a, const int* __restrict__ special_tiles)
         }
         int amax = 0;
         if (!SPECIAL) {
+            // (a tile over two read blocks stays here when the launch allows it, a.two_ok)
             if (!any_zap)
                 form_outputs<NBITS, CPS, CALIB, kModeClean, false>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax);
+            else if (mode == kModeTwo)
+                form_outputs<NBITS, CPS, CALIB, kModeTwo, false>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax);
             else
                 form_outputs<NBITS, CPS, CALIB, kModeFast, false>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax);
         } else if (!tail) {

@@ -34,6 +34,7 @@ def spiky_synth(nbits=8, frac=0.002):
 
 @pytest.mark.parametrize("nbits,calib,masked,nsblk", [(8, False, False, 2048), (8, False, True, 512),
                                                       (4, False, True, 1024), (16, False, False, 4096),
+                                                      (16, False, True, 1024),
                                                       (8, True, True, 2048)])
 def test_clean_state_matches_oracle(engine, nbits, calib, masked, nsblk):
     """Pad rows (running channel levels), clip flags and per-block zap rows of the device

@@ -248,6 +248,33 @@ def test_stage1_multipass_bitexact(engine, mask_pts, s1):
     engine.set_mask()
 
 
+@pytest.mark.parametrize("mask_pts", [2048, 32768])
+def test_stage1_16bit_masked_two_block_tiles(engine, mask_pts):
+    """16-bit data (the float stage-1 kernel) under a mask, clipping on: tiles over one interval
+    boundary run in the main launch (two blocks' pads and zap bits per row), only tiles over
+    three or more take the special launch; the clip state (16-bit zero-DM and channel-sum
+    kernels, big-endian samples) and every pass's subbands equal the oracle's."""
+    obs = palfa_obs(N=40000, nbits=16)
+    s = palfa_synth(nbits=16)
+    raw = load_beam(engine, obs, synth=s)
+    mask, pad = synth_mask(obs, s, mask_pts, frac=0.05)
+    engine.set_mask(mask, mask_pts, pad)
+    try:
+        gpad, gclip, gzap, ncl = engine.get_clean()
+        want = OR.prepare(obs, Opts(), raw, (None, None, None), mask, mask_pts, pad)
+        assert np.array_equal(gclip, want.clipped) and ncl == want.nclipped
+        assert np.array_equal(gzap, want.zap)
+        for ds, subdm in ((1, 30.0), (5, 612.0)):
+            pp = PassParams(subdm=subdm, lodm=subdm - 10.0, dmstep=0.5, numdms=8, nsub=96, ds=ds)
+            p = engine.plan(pp)
+            p.run_subband()
+            want = OR.stage1(obs, Opts(), raw, 96, ds, subdm, mask=mask, ptsperint=mask_pts, padvals=pad)
+            assert np.array_equal(p.get_subbands(), want), ds
+            p.destroy()
+    finally:
+        engine.set_mask()
+
+
 @pytest.mark.parametrize("ds", [1, 2, 3, 5, 6, 10])
 @pytest.mark.parametrize("flip,sub_dtype,ds_mode,masked", [(True, 0, 0, True), (False, 0, 1, False),
                                                           (False, 1, 0, True), (True, 1, 1, True)])
