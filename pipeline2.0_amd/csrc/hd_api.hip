@@ -2249,8 +2249,12 @@ static bool stage1_tiling(const hd_ctx* c, int nsub, int ds, int dmax, hd::Stage
     const int nbits = c->obs.nbits, nchan = c->obs.nchan, cps = nchan / nsub;
     if (c->rowbytes % 4 || !hd::stage1_tiled_supports_cps(cps)) return false;
     int sg = 0;
+    // HD_S1T_SG / HD_S1T_KB (profiling): at most this many subbands per workgroup / the first
+    // LDS budget (KiB) tried
+    const int sgcap = getenv("HD_S1T_SG") ? atoi(getenv("HD_S1T_SG")) : 8;
+    const size_t kb0 = getenv("HD_S1T_KB") ? (size_t)atoi(getenv("HD_S1T_KB")) : 64;
     for (int cand : {8, 4, 2, 1})
-        if (nsub % cand == 0 && ((int64_t)cand * cps * nbits) % 32 == 0) { sg = cand; break; }
+        if (cand <= sgcap && nsub % cand == 0 && ((int64_t)cand * cps * nbits) % 32 == 0) { sg = cand; break; }
     if (!sg) return false;
     const int G = sg * cps;
     const int gbytes = G * nbits / 8;
@@ -2262,7 +2266,8 @@ static bool stage1_tiling(const hd_ctx* c, int nsub, int ds, int dmax, hd::Stage
     int rs = (gbytes + 3) & ~3;
     if (((rs / 4) & 1) == 0) rs += 4;
     int to = 0;
-    for (size_t budget : {(size_t)64 * 1024, (size_t)96 * 1024, (size_t)156 * 1024}) {
+    for (size_t budget : {kb0 * 1024, (size_t)96 * 1024, (size_t)156 * 1024}) {
+        if (budget < kb0 * 1024) continue;
         const int64_t rows_max = (int64_t)((budget - 64) / (size_t)(rs + 4));
         to = (int)std::min<int64_t>(2048, (rows_max - dmax) / ds);
         if (to >= 256) break;
