@@ -203,29 +203,52 @@ __global__ __launch_bounds__(1024) void k_sp_robust(double* __restrict__ coef, i
             }
             __syncthreads();
         }
+    // (the scans and sums below stay sequential in index order, as the oracle's; their LDS
+    // reads go 16 at a time so the chains wait on their double ops, not on a round trip each)
     if (threadIdx.x == 0) {
         const int nb = nblocks, h = nb / 2;
         int locut = 1, hicut = 0;
         double best = -__builtin_inf();
-        for (int i = 0; i < h; i++) {
-            const double d = srt[i + 1] - srt[i];
-            if (d > best) { best = d; locut = i + 1; }
-        }
+        auto scan16 = [&](int i0, int i1, int base, int& arg) {   // first max of srt[i+1]-srt[i]
+            for (int i = i0; i < i1; i += 16) {
+                double v[17];
+#pragma unroll
+                for (int k = 0; k < 17; k++) v[k] = i + k < nb ? srt[i + k] : 0.0;
+#pragma unroll
+                for (int k = 0; k < 16; k++)
+                    if (i + k < i1) {
+                        const double d = v[k + 1] - v[k];
+                        if (d > best) { best = d; arg = i + k - base; }
+                    }
+            }
+        };
+        scan16(0, h, -1, locut);                              // locut = i + 1
         best = -__builtin_inf();
         int am = 0;
-        for (int i = h; i + 1 < nb; i++) {
-            const double d = srt[i + 1] - srt[i];
-            if (d > best) { best = d; am = i - h; }
-        }
+        scan16(h, nb - 1, h, am);                             // am = i - h
         hicut = am + h - 2;
         const int lo = locut, hi = hicut;
         double lo_std = __builtin_nan(""), hi_std = __builtin_nan(""), med = 0.0;
         if (nb >= 2 && hi > lo) {
             double m = 0.0;
-            for (int i = lo; i < hi; i++) m += srt[i];
+            for (int i = lo; i < hi; i += 16) {
+                double v[16];
+#pragma unroll
+                for (int k = 0; k < 16; k++) v[k] = i + k < hi ? srt[i + k] : 0.0;
+#pragma unroll
+                for (int k = 0; k < 16; k++)
+                    if (i + k < hi) m += v[k];
+            }
             m /= (double)(hi - lo);
             double var = 0.0;
-            for (int i = lo; i < hi; i++) var += (srt[i] - m) * (srt[i] - m);
+            for (int i = lo; i < hi; i += 16) {
+                double v[16];
+#pragma unroll
+                for (int k = 0; k < 16; k++) v[k] = i + k < hi ? srt[i + k] : 0.0;
+#pragma unroll
+                for (int k = 0; k < 16; k++)
+                    if (i + k < hi) var += (v[k] - m) * (v[k] - m);
+            }
             const double sd = sqrt(var / (double)(hi - lo));
             med = srt[(lo + hi) / 2];
             lo_std = med - 4.0 * sd;
