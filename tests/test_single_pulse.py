@@ -308,3 +308,24 @@ def test_host_prune_matches_script(padded):
         assert rc == 0
         got = [(int(r["dm"]), int(r["bin"]), widths[r["widx"]], float(r["sigma"])) for r in a[:nk.value]]
         assert got == want, trial
+
+
+def test_block_sort_int_keys_preserve_float_order():
+    """csrc/hd_sp.hip k_sp_blocks sorts the detrended f32 values as int32 keys
+    b ^ ((b >> 31) & 0x7FFFFFFF) (complemented keys for descending lanes): the key order is
+    the float order (-0 just below +0, infinities at the ends), the map is its own inverse
+    and complementing a key reverses the order -- so the sorted values, and the trimmed sum
+    of squares taken over them, equal a float sort's."""
+    rng = np.random.default_rng(5)
+    v = np.concatenate([rng.normal(0, 3, 5000), rng.normal(0, 1e-30, 50), [0.0, -0.0, np.inf, -np.inf, 7.0, 7.0]])
+    v = v.astype(np.float32)
+    b = v.view(np.int32)
+    key = b ^ ((b >> 31) & np.int32(0x7FFFFFFF))
+    assert np.array_equal((key ^ ((key >> 31) & np.int32(0x7FFFFFFF))).view(np.float32).view(np.int32), b)
+    by_key = v[np.argsort(key, kind="stable")]
+    assert np.array_equal(by_key, np.sort(v))                 # same values in the same order
+    assert np.all(np.diff(by_key.astype(np.float64)) >= 0)
+    assert np.all(np.diff(np.sort(~key)) >= 0) and np.array_equal(np.sort(v)[::-1], v[np.argsort(~key, kind="stable")])
+    i = np.flatnonzero(v == 0.0)
+    neg0, pos0 = i[np.signbit(v[i])], i[~np.signbit(v[i])]
+    assert key[neg0][0] < key[pos0][0]
