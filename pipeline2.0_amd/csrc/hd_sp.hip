@@ -184,25 +184,67 @@ __global__ __launch_bounds__(1024) void k_sp_robust(double* __restrict__ coef, i
     __shared__ double srt[kSpMaxBlocks];
     __shared__ double lim[3];                                  // lo, hi, median
     double* cf = coef + (int64_t)blockIdx.x * nblocks * 4;
-    int n2 = 1;
-    while (n2 < nblocks) n2 <<= 1;
-    for (int i = threadIdx.x; i < n2; i += blockDim.x) srt[i] = i < nblocks ? cf[(int64_t)i * 4 + 2] : __builtin_inf();
-    __syncthreads();
-    for (int k = 2; k <= n2; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < n2; i += blockDim.x) {
-                const int l = i ^ j;
-                if (l > i) {
-                    const double a = srt[i], c = srt[l];
-                    const bool up = (i & k) == 0;
-                    if (up ? a > c : a < c) {
-                        srt[i] = c;
-                        srt[l] = a;
-                    }
+    // bitonic sort of kSpMaxBlocks slots (+inf past nblocks) on order-preserving int64 keys,
+    // thread t owning slots 8t .. 8t+7 in registers: merges of j < 8 inside a thread, j < 512
+    // across the lanes of a wave (shuffles), only j >= 512 through LDS (10 barrier pairs instead
+    // of a barrier per stage); the sorted values equal any sort's
+    static_assert(kSpMaxBlocks == 8192, "k_sp_robust sorts 8192 slots with 1024 threads");
+    const int tid = threadIdx.x, lane = tid & 63;
+    int64_t* skey = (int64_t*)srt;
+    int64_t x[8];
+    auto dkey = [](double d) {
+        const int64_t bb = __double_as_longlong(d);
+        return bb ^ ((bb >> 63) & 0x7FFFFFFFFFFFFFFFll);
+    };
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+        const int i = 8 * tid + r;
+        x[r] = dkey(i < nblocks ? cf[(int64_t)i * 4 + 2] : __builtin_inf());
+    }
+#pragma unroll
+    for (int lk = 1; lk <= 13; lk++) {
+        const int k = 1 << lk;
+#pragma unroll
+        for (int lj = lk - 1; lj >= 0; lj--) {
+            const int j = 1 << lj;
+            if (j >= 512) {                                  // partner in another wave: via LDS
+#pragma unroll
+                for (int r = 0; r < 8; r++) skey[8 * tid + r] = x[r];
+                __syncthreads();
+#pragma unroll
+                for (int r = 0; r < 8; r++) {
+                    const int i = 8 * tid + r;
+                    const int64_t o = skey[i ^ j];
+                    const bool asc = (i & k) == 0, lower = (i & j) == 0;
+                    x[r] = asc == lower ? min(x[r], o) : max(x[r], o);
+                }
+                __syncthreads();
+            } else if (j >= 8) {                             // partner in lane ^ (j / 8)
+                const int lm = j >> 3;
+                const bool lower = (lane & lm) == 0;
+#pragma unroll
+                for (int r = 0; r < 8; r++) {
+                    const int64_t o = __shfl_xor(x[r], lm, 64);
+                    const bool asc = ((8 * tid + r) & k) == 0;
+                    x[r] = asc == lower ? min(x[r], o) : max(x[r], o);
+                }
+            } else {                                         // partner in this thread
+#pragma unroll
+                for (int r = 0; r < 8; r++) {
+                    if (r & j) continue;
+                    const int q = r | j;
+                    const int64_t lo = min(x[r], x[q]), hi = max(x[r], x[q]);
+                    const bool asc = ((8 * tid + r) & k) == 0;
+                    x[r] = asc ? lo : hi;
+                    x[q] = asc ? hi : lo;
                 }
             }
-            __syncthreads();
         }
+    }
+#pragma unroll
+    for (int r = 0; r < 8; r++)
+        srt[8 * tid + r] = __longlong_as_double(x[r] ^ ((x[r] >> 63) & 0x7FFFFFFFFFFFFFFFll));
+    __syncthreads();
     // (the scans and sums below stay sequential in index order, as the oracle's; their LDS
     // reads go 16 at a time so the chains wait on their double ops, not on a round trip each)
     if (threadIdx.x == 0) {
