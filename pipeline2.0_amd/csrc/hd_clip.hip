@@ -919,7 +919,7 @@ template <int CPS, int DS>
 __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm, const int32_t* __restrict__ events,
                                                     const int32_t* __restrict__ nevents, int boundaries)
 {
-    // dynamic LDS: raw [G][Wp] | flags [Wp] | zap [2][G] | pad [2][G] f32 | dly [npass][G] i16
+    // dynamic LDS: raw [G][Wp] | flags [Wp] | zap [2][G] | pad [2][G] f32 | dly [npass][SG][DST] i16
     //              | lo, cnt [npass][SG] (boundary items)
     extern __shared__ __attribute__((aligned(16))) char fsm[];
     const int G = gm.G, Wp = gm.Wp, SG = gm.SG, npass = a.npass;
@@ -928,8 +928,14 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
     uint8_t* flg = lraw + G * Wp;
     float* pad = (float*)(flg + Wp);                      // Wp is a multiple of 16
     uint8_t* zap = (uint8_t*)(pad + 2 * G);
+    // a subband's delays start on a 32-byte boundary (DST = 16 slots for the templated cps):
+    // packed 20-byte groups made the compiler's merged ds_read_b128 of a task's 10 delays
+    // misaligned (SQ_LDS_UNALIGNED_STALL); the runtime-cps kernel keeps the dense layout
+    constexpr int DSTC = CPS > 0 ? 16 : 0;
+    const int DST = CPS > 0 ? DSTC : cps;
     int16_t* dly = (int16_t*)(zap + ((2 * G + 15) & ~15));
-    int* lo_s = (int*)(dly + ((npass * G + 7) & ~7));
+    auto dix = [&](int p, int lc) { return (p * SG + lc / cps) * DST + lc % cps; };
+    int* lo_s = (int*)(dly + ((npass * SG * DST + 7) & ~7));
     int* cnt_s = lo_s + npass * SG;
     int* pre_s = cnt_s + npass * SG;                       // [npass * SG + 1] exclusive prefix of cnt_s
     uint16_t* tlist = (uint16_t*)(pre_s + npass * SG + 1);   // [npass * G] clipped-spectrum tasks to fold
@@ -961,7 +967,7 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
     const int c0 = chunk * G;
     for (int i = threadIdx.x; i < npass * G; i += blockDim.x) {
         const int p = i / G;
-        dly[i] = (int16_t)a.dly[p][c0 + i - p * G];
+        dly[dix(p, i - p * G)] = (int16_t)a.dly[p][c0 + i - p * G];
     }
     for (int e = blockIdx.x / gm.nchunk; e < nitems; e += gridDim.x / gm.nchunk) {
         const bool clip_ev = e < nev;
@@ -993,7 +999,7 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
                 bool need = false;
                 for (int cc = 0; cc < cps; cc++) {
                     const int lc = sl * cps + cc;
-                    const int d = dly[p * G + lc];
+                    const int d = dly[dix(p, lc)];
                     mind = min(mind, d);
                     maxd = max(maxd, d);
                     need |= zap[lc] && zap[G + lc] && pad[lc] != pad[G + lc];
@@ -1044,8 +1050,8 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
             // atomic per wave), so the folds run on dense lanes (~1 task in 6 folds)
             auto task = [&](int i, int& j) -> bool {             // (p, lc) = task i; j: its output
                 const int p = i / G, lc = i - p * G;
-                const int16_t* dl = dly + p * G;
                 const int lc0 = lc - lc % cps;
+                const int16_t* dl = dly + dix(p, lc0) - lc0;          // dl[lc0 .. lc0 + cps)
                 const int dsp = pds(p), ndsp = DS < 0 ? N / dsp : nds;
                 const int jn = r - dl[lc];
                 if (jn < 0) return false;
@@ -1080,8 +1086,8 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
                 int j = 0;
                 (void)task(i, j);
                 const int p = i / G, lc = i - p * G;
-                const int16_t* dl = dly + p * G;
                 const int lc0 = lc - lc % cps;
+                const int16_t* dl = dly + dix(p, lc0) - lc0;
                 const int dsp = pds(p);
                 float acc;
                 if constexpr (CPS > 0) {
@@ -1148,7 +1154,7 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
                 const int ps = lo, jj = t - pre_s[ps];
                 const int p = ps / SG, sl = ps - p * SG;
                 const int j = lo_s[ps] + jj;
-                const int16_t* dl = dly + p * G;
+                const int16_t* dl = dly + dix(p, sl * cps) - sl * cps;
                 const int dsp = pds(p);
                 float acc;
                 if constexpr (CPS > 0) {
@@ -1181,8 +1187,9 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
 
 static size_t fix8_lds_bytes(const Stage1Multi& a, const Fix8Geom& g)
 {
+    const int dst = (a.cps == 8 || a.cps == 10 || a.cps == 16) ? 16 : a.cps;   // k_stage1_fix8's DST
     return (size_t)g.G * g.Wp + g.Wp + (size_t)2 * g.G * 4 + (size_t)((2 * g.G + 15) & ~15) +
-           (size_t)2 * ((a.npass * g.G + 7) & ~7) + (size_t)(3 * a.npass * g.SG + 1) * 4 + (size_t)2 * a.npass * g.G;
+           (size_t)2 * ((a.npass * g.SG * dst + 7) & ~7) + (size_t)(3 * a.npass * g.SG + 1) * 4 + (size_t)2 * a.npass * g.G;
 }
 
 // LDS budget of one k_stage1_fix8 workgroup: smaller windows per workgroup mean more of
