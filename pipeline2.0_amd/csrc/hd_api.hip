@@ -2605,6 +2605,17 @@ static int run_subband_fused(hd_ctx* c, hd_plan** plans, int n)
     m.W = S + ((dmax + 15) & ~15);
     m.cps = cps;
     if (hd::stage1_q8m_lds_bytes(m) > 160 * 1024) return 1;     // 1: does not apply (per-stage launches)
+    // every DDplan stage's special tiles need a float tiling; check them all before anything
+    // is launched, so a miss falls back to the per-stage launches with nothing half-formed
+    for (int i0 = 0; i0 < n;) {
+        int i1 = i0;
+        while (i1 < n && plans[i1]->pass.ds == plans[i0]->pass.ds) i1++;
+        const int ds = plans[i0]->pass.ds;
+        hd::Stage1Multi t{};
+        int tvw = 4;
+        if (!stage1_tiling_fixed(c, nsub, ds, dmax, 4 * S / ds, t, tvw)) return 1;
+        i0 = i1;
+    }
     if (!alloc_rawT(c, dmax)) return 1;                          // (the fill reads the channel-major copy)
     int rc0 = ensure_blocks(c);
     if (rc0) return rc0;
@@ -2678,7 +2689,7 @@ static int run_subband_fused(hd_ctx* c, hd_plan** plans, int n)
             int fvw = 4;
             f.dmax = dmax;                            // the fused tiles' rows: 4 S + dmax
             f.to = 4 * S / ds;                        // (tile t: outputs from t * to, raw rows from t * 4 S)
-            if (!stage1_tiling_fixed(c, nsub, ds, dmax, 4 * S / ds, f, fvw))
+            if (!stage1_tiling_fixed(c, nsub, ds, dmax, 4 * S / ds, f, fvw))   // checked above, before any launch
                 return fail(c, HD_E_INVAL, "stage 1: no float tiling for the fused launch's special tiles (ds %d)", ds);
             f.ntiles = m.ntiles;
             const size_t flds = hd::stage1_tiled_lds_bytes(f);
@@ -3459,7 +3470,8 @@ extern "C" int hd_plan_set_bary(hd_plan* p, const int32_t* diffbins, int32_t ndi
 {
     if (!p) return fail(nullptr, HD_E_INVAL, "hd_plan_set_bary: NULL plan");
     hd_ctx* c = p->ctx;
-    if (ndiff < 0 || (ndiff > 0 && !diffbins)) return fail(c, HD_E_INVAL, "hd_plan_set_bary: bad diffbins");
+    if (ndiff < 0) return fail(c, HD_E_INVAL, "hd_plan_set_bary: bad diffbins");
+    if (!diffbins) ndiff = 0;              // header contract: ndiff = 0 or diffbins NULL turns it off
     // unchanged settings (the same list, or topocentric again): nothing to do, and no wait
     // on the plan's queued work (run_pass sets the table on every pass)
     if (ndiff == (int32_t)p->bary_diff.size() && (ndiff == 0 ? p->nbseg == 0 : p->nbseg > 0) &&
@@ -4089,10 +4101,14 @@ const RcclApi& rccl()
     static std::once_flag once;
     std::call_once(once, [] {
         void* h = nullptr;
-        for (const char* n : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
-            if ((h = dlopen(n, RTLD_NOW | RTLD_GLOBAL))) break;
+        // HD_TEST_NO_RCCL=1 (CPU tests) takes the not-found path without touching the loader
+        if (!getenv("HD_TEST_NO_RCCL"))
+            for (const char* n : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+                if ((h = dlopen(n, RTLD_NOW | RTLD_GLOBAL))) break;
         if (!h) {
-            api.err = dlerror() ? dlerror() : "librccl not found";
+            // dlerror() clears the message it returns: read it once
+            const char* de = getenv("HD_TEST_NO_RCCL") ? nullptr : dlerror();
+            api.err = de ? de : "librccl not found";
             return;
         }
         api.get_id = (decltype(api.get_id))dlsym(h, "ncclGetUniqueId");
@@ -4183,6 +4199,11 @@ extern "C" int hd_slice_exchange_clip(hd_ctx* c, int64_t nown, int64_t nblk_tota
     if (!c->comm) return fail(c, HD_E_STATE, "hd_slice_exchange_clip: no communicator (hd_comm_init)");
     if (!(c->opts.clip_sigma > 0.0f)) return HD_OK;
     if (nblk_total < 1 || nown < 0) return fail(c, HD_E_INVAL, "hd_slice_exchange_clip: bad block counts");
+    // hd_clip_stats writes rows up to slice_t0/blk + nown and hd_clip_set_stats reads rows up
+    // to slice_t0/blk + nblk of the [nblk_total] table
+    if (nown > c->nblk || nblk_total < c->slice_t0 / c->blk + c->nblk)
+        return fail(c, HD_E_INVAL, "hd_slice_exchange_clip: nown %lld > %d blocks, or nblk_total %lld < %lld",
+                    (long long)nown, c->nblk, (long long)nblk_total, (long long)(c->slice_t0 / c->blk + c->nblk));
     HIPCHK(c, hipSetDevice(c->device));
     // the beam's [nblk_total][nchan + 3] statistics table on the device: this slice's own
     // rows (hd_clip_stats), summed over the ranks, then clip_times finished (hd_clip_set_stats)

@@ -119,3 +119,25 @@ def test_host_synth_statistics():
     assert lvl[quiet][-1] > lvl[quiet][0]                    # positive bandpass slope
     assert (lvl[rfi] > lvl[quiet].mean() + 0.5 * s.rfi_amp).all()
     assert 0.8 * s.noise_sigma < a[:, quiet].std(axis=0).mean() < 1.3 * s.noise_sigma
+
+
+def test_comm_without_rccl_is_an_error_code():
+    """hd_comm_unique_id on a host without RCCL: HD_E_HIP and a message, not an abort
+    (the loader's dlerror() is read once).  HD_TEST_NO_RCCL makes the library skip dlopen;
+    a child process, since the loader runs once per process."""
+    import subprocess
+    import sys
+    code = (
+        "import ctypes, sys\n"
+        "sys.path[:0] = %r\n"
+        "from hipdedisp import _lib\n"
+        "L = _lib.load()\n"
+        "buf = (ctypes.c_uint8 * 128)()\n"
+        "rc = L.hd_comm_unique_id(buf)\n"
+        "print(rc, _lib.last_error())\n" % ([os.path.join(os.path.dirname(HEADER), "..", "pipeline2.0_amd")],))
+    env = dict(os.environ, HD_TEST_NO_RCCL="1")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=120)
+    assert out.returncode == 0, out.stderr
+    rc, msg = out.stdout.strip().split(" ", 1)
+    assert int(rc) == _lib.HD_E_HIP
+    assert "librccl not found" in msg
