@@ -231,10 +231,11 @@ struct hd_plan {
         int32_t umax = 0;               // [3] only: largest pattern count of a subband pair
         int32_t* d_omin = nullptr;      // [3]: the pair table (kPairTab ints per y-block and pair)
         int32_t* d_boff = nullptr;
-    } wide[6];                      // [2]: k_stage2_ring (16 waves, LDS-DMA staging ring);
+    } wide[7];                      // [2]: k_stage2_ring (16 waves, LDS-DMA staging ring);
                                     // [3]: k_stage2_pair (the ring over subband-pair partials),
                                     // [4]: the same with two pairs per chunk (half the chunks),
-                                    // [5]: k_stage2_rw (register windows, one copy, 2 WGs per CU)
+                                    // [5]: k_stage2_rw (register windows, one copy, 2 WGs per CU),
+                                    // [6]: k_stage2_qp (quarter-layout pair partials; sc = pairs per chunk)
     bool sub_nonneg = false;        // every subband value >= 0 (known on the host with sub_bound)
     int32_t sub_bound = -1;         // bound on |subband| known on the host (-1: none), set when
                                     // the subbands are formed or uploaded (pair variant gate)
@@ -1642,6 +1643,99 @@ static void pair_tables(hd_plan* p, bool i16, int ppc, hd_plan::Wide& w, std::ve
     w.umax = umax;
 }
 
+// The quarter-layout pair kernel as the auto stage-2 choice (HD_S2_QP=0/1 overrides for A/B).
+static bool qp_auto()
+{
+    static const int v = [] {
+        const char* e = getenv("HD_S2_QP");
+        return e ? atoi(e) : 0;
+    }();
+    return v != 0;
+}
+
+// Tables of the quarter-layout pair kernel (k_stage2_qp): y-blocks of 16 waves x Q DMs (Q 4
+// or 5), tiles of T = 4 S = 768 samples, ppc pairs per chunk.  Per (y-block, pair) the pair
+// kernel's {base0, b1, U, k1[U]} and [9] E_k = the pair's entries per pattern (S + its own
+// DM sweep, a multiple of 4).  boff[yb][c][k] = LDS byte offset (from the expanded area) of
+// DM k's entry 0: buffer ((c / ppc) & 1) * ppc + c % ppc, pattern u(k), entry o2 = o0 - base0.
+static void qp_tables(hd_plan* p, bool i16, int ppc, hd_plan::Wide& w, std::vector<int32_t>& ptab,
+                      std::vector<int32_t>& boff)
+{
+    w = hd_plan::Wide{};
+    constexpr int NW = 16, RQ = 3, S = 64 * RQ, T = 4 * S;
+    const int nsub = p->pass.nsub, numdms = p->pass.numdms;
+    // an even chunk count per tile keeps a pair's expanded-buffer parity fixed in every tile
+    if (!i16 || nsub % (4 * ppc) || numdms < 1) return;
+    int nyb = (numdms + 5 * NW - 1) / (5 * NW);
+    const int per = (numdms + nyb - 1) / nyb;
+    const int Q = (per + NW - 1) / NW > 4 ? 5 : 4;
+    const int dpb = NW * Q;
+    nyb = (numdms + dpb - 1) / dpb;
+    const int npair = nsub / 2;
+    ptab.assign((size_t)nyb * npair * hd::kPairTab, 0);
+    std::vector<std::vector<int32_t>> rs((size_t)nyb * npair);
+    int32_t Emax = 0, k1max = 0;
+    int umax = 0;
+    auto dmof = [&](int yb, int k) { return std::min(yb * dpb + k, numdms - 1); };
+    for (int yb = 0; yb < nyb; yb++)
+        for (int c = 0; c < npair; c++) {
+            int32_t lo = INT32_MAX, hi = INT32_MIN;
+            std::vector<int32_t>& r = rs[(size_t)yb * npair + c];
+            for (int k = 0; k < dpb; k++) {
+                const int dm = dmof(yb, k);
+                const int32_t o0 = p->off[(size_t)dm * nsub + 2 * c], o1 = p->off[(size_t)dm * nsub + 2 * c + 1];
+                lo = std::min(lo, o0);
+                hi = std::max(hi, o0);
+                r.push_back(o1 - o0);
+            }
+            std::sort(r.begin(), r.end());
+            r.erase(std::unique(r.begin(), r.end()), r.end());
+            if ((int)r.size() > hd::kPairUMax) return;
+            const int32_t b1 = lo + r[0];
+            int32_t* t = &ptab[((size_t)yb * npair + c) * hd::kPairTab];
+            t[0] = lo;
+            t[1] = b1;
+            t[2] = (int32_t)r.size();
+            for (size_t u = 0; u < r.size(); u++) {
+                t[3 + u] = r[u] - r[0] + (b1 & 1);
+                k1max = std::max(k1max, t[3 + u]);
+            }
+            t[9] = (int32_t)round_up((size_t)(S + hi - lo), 4);
+            Emax = std::max(Emax, t[9]);
+            umax = std::max(umax, (int)r.size());
+        }
+    // the expand reads staging elements up to 4 g + 3 S + k + 7 < E + 3 S + k1max + 8
+    const int npw = (int)((((size_t)Emax + 3 * S + k1max + 8) * 2 + 1023) / 1024);
+    const int nbp = (int)(((size_t)ppc * dpb * 4 + 1023) / 1024);
+    if (2 * ppc * npw + nbp > 32 || hd::stage2_qp_lds_bytes(Emax, npw, nbp, nsub, umax, ppc) > 160 * 1024 ||
+        !hd::stage2_qp_supports(Q, RQ) || (size_t)npw * 512 > 4096)
+        return;
+    boff.assign((size_t)nyb * npair * dpb + 256, 0);   // the last DMA piece may over-read
+    for (int yb = 0; yb < nyb; yb++)
+        for (int c = 0; c < npair; c++) {
+            const std::vector<int32_t>& r = rs[(size_t)yb * npair + c];
+            const int32_t base0 = ptab[((size_t)yb * npair + c) * hd::kPairTab];
+            for (int k = 0; k < dpb; k++) {
+                const int dm = dmof(yb, k);
+                const int32_t o0 = p->off[(size_t)dm * nsub + 2 * c], o1 = p->off[(size_t)dm * nsub + 2 * c + 1];
+                const int u = (int)(std::lower_bound(r.begin(), r.end(), o1 - o0) - r.begin());
+                const int buf = ((c / ppc) & 1) * ppc + c % ppc;
+                boff[((size_t)yb * npair + c) * dpb + k] = (int32_t)((((int64_t)buf * umax + u) * Emax + (o0 - base0)) * 8);
+            }
+        }
+    (void)T;
+    w.ok = true;
+    w.q = Q;
+    w.r = RQ;                      // 256 * r = the tile (ntiles, partial sums)
+    w.nw = NW;
+    w.dpb = dpb;
+    w.ws = Emax;
+    w.sc = ppc;
+    w.npw = npw;
+    w.nbp = nbp;
+    w.umax = umax;
+}
+
 // Tables of the register-window pair kernel (k_stage2_rw): y-blocks of 8 waves x Q DMs, two
 // pairs per chunk, 768-sample tiles (lane l: samples 12l .. 12l+11).  Per (y-block, pair) the
 // pair kernel's {base0, b1, U, k1[U]} over the block's DMs.  Per (y-block, chunk) one block of
@@ -1829,16 +1923,20 @@ extern "C" int hd_plan_create(hd_ctx* c, const hd_pass* ps, hd_plan** out)
                 boff[((size_t)yb * nsub + s) * p->dpb + k] = ((sl * 4 + (o2 & 3)) * p->wstride + (o2 & ~3)) * 2;
             }
 
-    std::vector<int32_t> womin[6], wboff[6];
+    std::vector<int32_t> womin[7], wboff[7];
     for (int k = 0; k < 3; k++)
         wide_tables(p, k == 1 ? 8 : 16, k != 1, c->opts.sub_dtype == HD_SUB_I16, p->wide[k], womin[k], wboff[k], k == 2);
     pair_tables(p, c->opts.sub_dtype == HD_SUB_I16, 1, p->wide[3], womin[3], wboff[3]);
     pair_tables(p, c->opts.sub_dtype == HD_SUB_I16, 2, p->wide[4], womin[4], wboff[4]);
     rw_tables(p, c->opts.sub_dtype == HD_SUB_I16, p->wide[5], womin[5], wboff[5]);
+    for (int ppc : {4, 3, 2}) {        // the most pairs per chunk whose LDS fits
+        qp_tables(p, c->opts.sub_dtype == HD_SUB_I16, ppc, p->wide[6], womin[6], wboff[6]);
+        if (p->wide[6].ok) break;
+    }
 
     int rc = HD_OK;
     hipError_t e = hipSetDevice(c->device);
-    for (int k = 0; k < 6 && e == hipSuccess; k++) {
+    for (int k = 0; k < 7 && e == hipSuccess; k++) {
         hd_plan::Wide& w = p->wide[k];
         if (!w.ok) continue;
         e = hipMalloc(&w.d_omin, sizeof(int32_t) * womin[k].size());
@@ -1906,11 +2004,12 @@ extern "C" int hd_plan_set_variant(hd_plan* p, int32_t v)
     p->probe = (v >> 16) & 0xFF;     // profiling only (results invalid): see hipdedisp.h
     p->pair_persist = (v >> 24) & 0x3;   // pair kernel: 0/1 persistent workgroups (default), 2 one per tile
     v &= 0xFF;
-    if (v < 0 || v > 8 || v1 > 3) return fail(p->ctx, HD_E_INVAL, "variant must be (s1<<8)|s2 with s1 in 0..3, s2 in 0..8");
+    if (v < 0 || v > 9 || v1 > 3) return fail(p->ctx, HD_E_INVAL, "variant must be (s1<<8)|s2 with s1 in 0..3, s2 in 0..9");
     p->s1_variant = v1;
     if (v == 2 && !p->lds_ok) return fail(p->ctx, HD_E_INVAL, "LDS variant unavailable for this plan (needs int16 subbands and a window that fits 64 KiB)");
     if ((v == 3 && !p->wide[0].ok) || (v == 4 && !p->wide[1].ok) || (v == 5 && !p->wide[2].ok) ||
-        (v == 6 && !p->wide[3].ok) || (v == 7 && !p->wide[4].ok) || (v == 8 && !p->wide[5].ok))
+        (v == 6 && !p->wide[3].ok) || (v == 7 && !p->wide[4].ok) || (v == 8 && !p->wide[5].ok) ||
+        (v == 9 && !p->wide[6].ok))
         return fail(p->ctx, HD_E_INVAL, "wide-tile variant unavailable for this plan (needs int16 subbands and a window that fits LDS)");
     p->variant = v;
     return HD_OK;
@@ -3560,7 +3659,7 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
     const bool pair_bound = p->sub_bound >= 0 && 2 * p->sub_bound <= 32767;
     const bool pair_ok = p->wide[3].ok && pair_bound;
     if ((p->variant == 6 && !pair_ok) || (p->variant == 7 && !(p->wide[4].ok && pair_bound)) ||
-        (p->variant == 8 && !(p->wide[5].ok && pair_bound)))
+        (p->variant == 8 && !(p->wide[5].ok && pair_bound)) || (p->variant == 9 && !(p->wide[6].ok && pair_bound)))
         return fail(c, HD_E_INVAL, "hd_run_dedisp: pair variant needs 2 * max|subband| <= 32767 known on the host "
                     "(bound %d)", (int)p->sub_bound);
     int wk = -1;                       // wide variant in use (index into p->wide), or -1
@@ -3576,7 +3675,8 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         const bool pair2_auto = p->wide[4].ok && pair_bound;
         // (the register-window kernel, variant 8, measured slower at every DDplan stage: 1.63 vs
         // 1.07 ms per stage-0 pass, profiles/r04_stage2_rw_probe.txt -- not an auto choice)
-        wk = pair2_auto ? 4 : pair_auto ? 3 : p->wide[2].ok ? 2 : p->wide[0].ok ? 0 : (p->wide[1].ok ? 1 : -1);
+        const bool qp = p->wide[6].ok && pair_bound && qp_auto();
+        wk = qp ? 6 : pair2_auto ? 4 : pair_auto ? 3 : p->wide[2].ok ? 2 : p->wide[0].ok ? 0 : (p->wide[1].ok ? 1 : -1);
     }
     const bool use_wide = wk >= 0;
     const bool use_lds = !use_wide && (p->variant == 2 || (p->variant == 0 && p->lds_ok));
@@ -3632,17 +3732,20 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         if (wk == 0) HIPCHK(c, hd::launch_stage2_wide(a, w.q, w.r, w.nw, st));
         else if (wk == 1) HIPCHK(c, hd::launch_stage2_wide2(a, w.q, w.r, w.nw, st));
         else if (wk == 2) HIPCHK(c, hd::launch_stage2_ring(a, w.q, w.r, st));
-        else if (wk == 5) {
+        else if (wk == 5 || wk == 6) {
             hd::S2Multi m{};
             m.npass = 1;
             m.p[0] = hd::stage2_pass_of(a);
-            HIPCHK(c, hd::launch_stage2_rw_multi(a, m, w.q, st));
+            if (wk == 5) HIPCHK(c, hd::launch_stage2_rw_multi(a, m, w.q, st));
+            else HIPCHK(c, hd::launch_stage2_qp_multi(a, m, w.q, w.r, w.sc, st));
         } else HIPCHK(c, hd::launch_stage2_pair(a, w.q, w.r, wk == 4 ? 2 : 1, st));
         // the names rocprofv3 prints (template arguments as the compiler spells them)
         if (wk == 0) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_wide<%d, %d, %d>", w.q, w.r, w.sc);
         else if (wk == 1) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_wide2<%d, %d, %d>", w.q, w.r, w.sc);
         else if (wk == 2) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_ring<%d, %d>", w.q, w.r);
         else if (wk == 5) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_rw<%d>", w.q);
+        else if (wk == 6) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_qp<%d, %d, %d, %s>", w.q, w.r, w.sc,
+                                   a.nonneg && !(p->probe & 64) ? "true" : "false");
         else snprintf(p->s2name, sizeof(p->s2name), "k_stage2_pair<%d, %d, %d, %s>", w.q, w.r, wk == 4 ? 2 : 1,
                       a.nonneg && !(p->probe & 64) ? "true" : "false");
     } else if (use_lds) {
@@ -3686,6 +3789,7 @@ static int dedisp_multi_kernel(const hd_plan* p)
     const bool pair_bound = p->sub_bound >= 0 && 2 * p->sub_bound <= 32767;
     if (!p->sub_valid || !pair_bound || p->nbseg != 0 || p->pair_persist == 2) return -1;
     if (p->variant == 8 && p->wide[5].ok) return 5;
+    if ((p->variant == 9 || (p->variant == 0 && qp_auto())) && p->wide[6].ok) return 6;
     if ((p->variant == 0 || p->variant == 7) && p->wide[4].ok) return 4;
     return -1;
 }
@@ -3697,7 +3801,7 @@ static bool dedisp_same_group(const hd_plan* a, const hd_plan* b)
     const int ka = dedisp_multi_kernel(a);
     if (ka != dedisp_multi_kernel(b)) return false;
     const hd_plan::Wide &x = a->wide[ka], &y = b->wide[ka];
-    return a->ctx == b->ctx && x.q == y.q && x.r == y.r && x.dpb == y.dpb && a->pass.numdms == b->pass.numdms &&
+    return a->ctx == b->ctx && x.q == y.q && x.r == y.r && x.dpb == y.dpb && x.sc == y.sc && a->pass.numdms == b->pass.numdms &&
            a->pass.nsub == b->pass.nsub && a->nds == b->nds && a->nvalid == b->nvalid && a->numout == b->numout &&
            a->out_stride == b->out_stride && a->sub_nonneg == b->sub_nonneg && a->probe == b->probe;
 }
@@ -3797,6 +3901,7 @@ static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
     }
     HIPCHK(c, hipEventRecord(p0->ev[2], st));
     if (wk == 5) HIPCHK(c, hd::launch_stage2_rw_multi(a, m, w0.q, st));
+    else if (wk == 6) HIPCHK(c, hd::launch_stage2_qp_multi(a, m, w0.q, w0.r, w0.sc, st));
     else HIPCHK(c, hd::launch_stage2_pair_multi(a, m, w0.q, w0.r, 2, st));
     if (pad)
         for (int i = 0; i < n; i++)
@@ -3810,6 +3915,8 @@ static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
         p->dd_stream = st;
         p->s2passes = i == 0 ? n : 0;
         if (wk == 5) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_rw<%d>", w0.q);
+        else if (wk == 6) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_qp<%d, %d, %d, %s>", w0.q, w0.r, w0.sc,
+                                   a.nonneg && !(a.probe & 64) ? "true" : "false");
         else snprintf(p->s2name, sizeof(p->s2name), "k_stage2_pair<%d, %d, 2, %s>", w0.q, w0.r,
                       a.nonneg && !(a.probe & 64) ? "true" : "false");
     }

@@ -1969,4 +1969,382 @@ hipError_t launch_stage2_wide(const Stage2Args& a, int q, int r, int nw, hipStre
     return hipErrorInvalidValue;
 }
 
+// ---------------------------------------------------------------------------------------
+// Quarter-layout pair kernel (k_stage2_qp, round 5).  The pair partials of k_stage2_pair,
+// P_u[x] = sub[s0][base0 + x] + sub[s1][base0 + r_u + x], stored ONCE per tile in a
+// quarter-interleaved layout instead of four shifted copies: entry e of pattern u holds the
+// four int16 P_u[e], P_u[e + S], P_u[e + 2S], P_u[e + 3S] (8 bytes; tile T = 4 S samples,
+// S = 64 RQ).  A DM whose pair offset is o then reads entries o + lane + 64 m (m < RQ) with one
+// aligned ds_read_b64 each for ANY o -- four output samples (one per quarter) per read, as
+// before -- but the expand writes 8 (S + span) bytes per pattern instead of 8 (T + span)
+// (2.5x fewer LDS write cycles, the cost that dominated it), and a pattern's buffer is 2.5x
+// smaller, so a chunk carries PPC = 3 or 4 pairs (fewer barriers) in the same 160 KiB.
+// Per pair the entries cover only that pair's own DM sweep (S + span_k, not the plan's
+// widest), which trims the expand of the high-frequency pairs.
+// The staging windows stay plain (LDS-DMA of the subband rows); the expand reads 4 elements
+// of each quarter (two aligned ds_read_b64 + a dword select + v_alignbit), adds the pair,
+// and transposes the four quarters into entries with v_perm (two ds_write_b128 per item).
+// Output lane l, read m, quarter j is sample t0 + j S + 64 m + l: dword stores, 256 bytes
+// contiguous per wave-instruction.
+// Table per (y-block, pair): [0] base0, [1] b1, [2] U, [3..3+U) k1[u], [9] E_k (entries,
+// multiple of 4).  Offsets block per chunk: int32 LDS byte offsets from the expanded area,
+// [pair k][DM slot] = ((buf * umax + u) * E + o2) * 8, buf = (chunk & 1) * PPC + k.
+
+// 4 int16 elements x .. x+3 of a staging window (any x) as 2 packed pairs: two aligned
+// ds_read_b64 cover dwords (x>>1 & ~1) .. +3, a select picks the 3 that hold them.
+__device__ __forceinline__ void qp_load4(const uint32_t* w32, int x, uint32_t& o0, uint32_t& o1)
+{
+    const int dw = x >> 1;
+    const uint2 a = *(const uint2*)(w32 + (dw & ~1));
+    const uint2 b = *(const uint2*)(w32 + (dw & ~1) + 2);
+    const bool odd = dw & 1;
+    const uint32_t w0 = odd ? a.y : a.x, w1 = odd ? b.x : a.y, w2 = odd ? b.y : b.x;
+    const uint32_t sh = (uint32_t)(x & 1) * 16u;
+    o0 = __builtin_amdgcn_alignbit(w1, w0, sh);
+    o1 = __builtin_amdgcn_alignbit(w2, w1, sh);
+}
+
+template <int PPC>
+constexpr int qp_ns() { return PPC >= 4 ? 3 : 4; }
+
+template <int Q, int RQ, int PPC, bool NN>
+__global__ __launch_bounds__(1024) void k_stage2_qp(Stage2Args a, S2Multi m)
+{
+    extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+    const int pi = (int)blockIdx.y / m.nyblk;
+    const S2Pass& P = m.p[pi];
+    constexpr int NS = qp_ns<PPC>(), S = 64 * RQ, T = 4 * S;
+    int tb, ntl;
+    if (a.nwg == 0) {
+        tb = xcd_remap(blockIdx.x, gridDim.x);
+        ntl = 1;
+    } else {
+        const int nt = (int)((a.nvalid + T - 1) / T);
+        tb = (int)((int64_t)blockIdx.x * nt / gridDim.x);
+        ntl = (int)((int64_t)(blockIdx.x + 1) * nt / gridDim.x) - tb;
+    }
+    const int yb = (int)blockIdx.y - pi * m.nyblk;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nthr = blockDim.x;
+    const int dpb = a.dms_per_blk;
+    const int dblk0 = yb * dpb;
+    const int E = P.ws;                          // entries per pattern buffer (max over pairs)
+    const int npw = P.npw;                       // 1 KiB DMA pieces per window
+    const int nbp = P.nbp;                       // pieces of a chunk's offset block
+    const int umax = P.umax;
+    const int npiece = 2 * PPC * npw + nbp;      // DMA pieces per chunk (<= 32: two per wave)
+    const int pw = (npiece - wave + 15) >> 4;    // this wave's pieces per chunk: 0, 1 or 2
+    const int slot_bytes = npiece * 1024;
+    const int npair = a.nsub >> 1;
+    const int tab_bytes = npair * kPairTab * 4;
+    int32_t* ltab = (int32_t*)lds_raw;
+    const uint32_t ring0 = (uint32_t)tab_bytes;
+    const uint32_t exp0 = ring0 + (uint32_t)(NS * slot_bytes);
+    const uint32_t lane_byte = exp0 + (uint32_t)lane * 8u;
+    const int16_t* sub = (const int16_t*)P.sub;
+    const int32_t* bo_g = P.off + (int64_t)yb * npair * dpb;
+    const int nchunk = npair / PPC;
+
+    for (int i = threadIdx.x; i < npair * kPairTab; i += nthr) ltab[i] = P.ptab[(int64_t)yb * npair * kPairTab + i];
+    __syncthreads();
+
+    int maxabs = *P.maxabs;
+    maxabs = maxabs < 1 ? 1 : maxabs;
+    int G = (NN ? 65535 : 32767) / (2 * maxabs);
+    G = G < 1 ? 1 : (G > 64 ? 64 : G);
+    G = __builtin_amdgcn_readfirstlane(G);
+
+    int acc32[Q][RQ][4];
+    short2v acc16[Q][RQ][2];
+#pragma unroll
+    for (int q = 0; q < Q; q++)
+#pragma unroll
+        for (int r = 0; r < RQ; r++) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) acc32[q][r][j] = 0;
+            acc16[q][r][0] = short2v{0, 0};
+            acc16[q][r][1] = short2v{0, 0};
+        }
+    int gcount = 0;
+    auto widen = [&]() {
+#pragma unroll
+        for (int qq = 0; qq < Q; qq++)
+#pragma unroll
+            for (int r = 0; r < RQ; r++) {
+                if (NN) {
+                    const uint32_t lo = __builtin_bit_cast(uint32_t, acc16[qq][r][0]);
+                    const uint32_t hi = __builtin_bit_cast(uint32_t, acc16[qq][r][1]);
+                    acc32[qq][r][0] += (int)(lo & 0xFFFFu);
+                    acc32[qq][r][1] += (int)(lo >> 16);
+                    acc32[qq][r][2] += (int)(hi & 0xFFFFu);
+                    acc32[qq][r][3] += (int)(hi >> 16);
+                } else {
+                    acc32[qq][r][0] += acc16[qq][r][0].x;
+                    acc32[qq][r][1] += acc16[qq][r][0].y;
+                    acc32[qq][r][2] += acc16[qq][r][1].x;
+                    acc32[qq][r][3] += acc16[qq][r][1].y;
+                }
+                acc16[qq][r][0] = short2v{0, 0};
+                acc16[qq][r][1] = short2v{0, 0};
+            }
+    };
+
+    const int ntot = ntl * nchunk;
+    int dchunk = 0, dtile = 0, dcount = 0;
+    // the DMA of one chunk: piece pc of the chunk from wave pc % 16 (pc / 16: its second piece)
+    auto dma = [&](int cc) {
+        const int c2 = dchunk;
+        const int64_t t0 = (int64_t)(tb + dtile) * T;
+        if (dcount + 1 < ntot) {
+            dcount++;
+            if (++dchunk == nchunk) { dchunk = 0; dtile++; }
+        }
+        const uint32_t slot = ring0 + (uint32_t)((cc % NS) * slot_bytes);
+        for (int pc = wave; pc < npiece; pc += 16) {
+            if (pc < 2 * PPC * npw) {
+                const int win = pc / npw, pcs = pc - win * npw;      // window win: pair win / 2, side win % 2
+                const int pr = PPC * c2 + (win >> 1);
+                const int s = 2 * pr + (win & 1);
+                const int b = __builtin_amdgcn_readfirstlane(ltab[pr * kPairTab + (win & 1)]);
+                const int64_t e0 = t0 + b - (b & 1);
+                const char* src = (const char*)(sub + (int64_t)s * P.sub_stride + e0) + pcs * 1024;
+                dma16s(src, (uint32_t)lane * 16u, slot + (uint32_t)(pc * 1024));
+            } else {
+                const int bp = pc - 2 * PPC * npw;
+                const char* src = (const char*)(bo_g + (int64_t)PPC * c2 * dpb) + bp * 1024;
+                dma16s(src, (uint32_t)lane * 16u, slot + (uint32_t)(pc * 1024));
+            }
+        }
+    };
+    // wait until this chunk's DMA is in LDS: at most (NS - 3) chunks of this wave's pieces
+    // (and nothing older: series stores included) outstanding
+    auto wait_ring = [&]() {
+        if constexpr (NS - 3 == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+            if (pw >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * (NS - 3)) : "memory");
+            else if (pw == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NS - 3) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    };
+    // staging slot of chunk cc -> quarter entries of every pattern of its PPC pairs.
+    // Item (pair k, entry group g): entries 4g .. 4g+3 of each of the pair's U patterns.
+    auto expand = [&](int cc, int chk) {
+        const char* slot = lds_raw + ring0 + (cc % NS) * slot_bytes;
+        int nk[PPC + 1];
+        nk[0] = 0;
+#pragma unroll
+        for (int k = 0; k < PPC; k++) {
+            const int32_t* pt = ltab + (PPC * chk + k) * kPairTab;
+            nk[k + 1] = nk[k] + pt[2] * (pt[9] >> 2);
+        }
+        // item (pair k, pattern u, entry group g): entries 4g .. 4g+3 of pattern u
+        for (int idx = threadIdx.x; idx < nk[PPC]; idx += nthr) {
+            int k = 0;
+#pragma unroll
+            for (int kk = 1; kk < PPC; kk++)
+                if (idx >= nk[kk]) k = kk;
+            const int32_t* pt = ltab + (PPC * chk + k) * kPairTab;
+            const int ng = pt[9] >> 2;
+            int g = idx - nk[k], u = 0;
+#pragma unroll
+            for (int uu = 1; uu < kPairUMax; uu++)
+                if (g >= ng) { g -= ng; u++; }
+            const uint32_t* S0 = (const uint32_t*)(slot + (2 * k) * npw * 1024);
+            const uint32_t* S1 = (const uint32_t*)(slot + (2 * k + 1) * npw * 1024);
+            const int x0 = 4 * g + (pt[0] & 1), x1 = 4 * g + pt[3 + u];
+            uint32_t Pq[4][2];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                uint32_t a0, a1, b0, b1;
+                qp_load4(S0, x0 + j * S, a0, a1);
+                qp_load4(S1, x1 + j * S, b0, b1);
+                Pq[j][0] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(short2v, a0) + __builtin_bit_cast(short2v, b0));
+                Pq[j][1] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(short2v, a1) + __builtin_bit_cast(short2v, b1));
+            }
+            // entry i = (q0, q1 | q2, q3) of element i: the low halves of a pair-dword are element 2h
+            constexpr uint32_t LO = 0x05040100u, HI = 0x07060302u;
+            uint4* d = (uint4*)(lds_raw + exp0) + ((size_t)(((((cc & 1) * PPC + k) * umax) + u) * E + 4 * g) >> 1);
+            d[0] = make_uint4(__builtin_amdgcn_perm(Pq[1][0], Pq[0][0], LO), __builtin_amdgcn_perm(Pq[3][0], Pq[2][0], LO),
+                              __builtin_amdgcn_perm(Pq[1][0], Pq[0][0], HI), __builtin_amdgcn_perm(Pq[3][0], Pq[2][0], HI));
+            d[1] = make_uint4(__builtin_amdgcn_perm(Pq[1][1], Pq[0][1], LO), __builtin_amdgcn_perm(Pq[3][1], Pq[2][1], LO),
+                              __builtin_amdgcn_perm(Pq[1][1], Pq[0][1], HI), __builtin_amdgcn_perm(Pq[3][1], Pq[2][1], HI));
+        }
+    };
+
+    auto flush = [&](int tile) {
+        const int64_t t0 = (int64_t)tile * T;
+        widen();
+#pragma unroll
+        for (int q = 0; q < Q; q++) {
+            const int dl = wave * Q + q;
+            const int d = dblk0 + dl;
+            const bool dv = dl < dpb && d < a.numdms;
+            int64_t part = 0;
+            if (dv && !(a.probe & 4)) {
+                float* o = P.out + (int64_t)d * a.out_stride + t0 + lane;
+                if (t0 + T <= a.nvalid) {
+#pragma unroll
+                    for (int r = 0; r < RQ; r++)
+#pragma unroll
+                        for (int j = 0; j < 4; j++) {
+                            o[j * S + 64 * r] = (float)acc32[q][r][j];
+                            part += acc32[q][r][j];
+                        }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < RQ; r++)
+#pragma unroll
+                        for (int j = 0; j < 4; j++)
+                            if (t0 + j * S + 64 * r + lane < a.nvalid) {
+                                o[j * S + 64 * r] = (float)acc32[q][r][j];
+                                part += acc32[q][r][j];
+                            }
+                }
+            }
+            if (dv && P.partial) {
+#pragma unroll
+                for (int mm = 32; mm >= 1; mm >>= 1) part += __shfl_xor(part, mm, 64);
+                if (lane == 0) P.partial[(int64_t)d * a.ntiles + tile] = (double)part;
+            }
+        }
+        gcount = 0;
+#pragma unroll
+        for (int q = 0; q < Q; q++)
+#pragma unroll
+            for (int r = 0; r < RQ; r++) {
+#pragma unroll
+                for (int j = 0; j < 4; j++) acc32[q][r][j] = 0;
+                acc16[q][r][0] = short2v{0, 0};
+                acc16[q][r][1] = short2v{0, 0};
+            }
+    };
+
+#pragma unroll
+    for (int cc = 0; cc < NS - 1; cc++) dma(cc);
+    if constexpr (NS - 3 == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+        if (pw >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * (NS - 3)) : "memory");
+        else if (pw == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NS - 3) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    ring_barrier();
+    expand(0, 0);
+    ring_barrier();
+
+    int chk = 0, ktile = 0;
+    for (int c = 0; c < ntot; c++) {
+        if (!(a.probe & 2)) dma(c + NS - 1);
+        const int chn = chk + 1 == nchunk ? 0 : chk + 1;
+        if (c + 1 < ntot && !(a.probe & 8)) expand(c + 1, chn);
+        const int32_t* sboff = (const int32_t*)(lds_raw + ring0 + (c % NS) * slot_bytes + 2 * PPC * npw * 1024);
+        // this chunk's (pair, DM) byte offsets in ONE register: lane k * Q + q holds pair k, DM q
+        const int voff = lane < PPC * Q ? sboff[(lane / Q) * dpb + wave * Q + lane % Q] : 0;
+        if (!(a.probe & 1)) {
+            constexpr int nsteps = PPC * Q, LA0 = ring_la<Q, RQ>() < Q - 1 ? ring_la<Q, RQ>() : Q - 1, LA = LA0;
+            uint64_t bb[LA + 1][RQ];
+#pragma unroll
+            for (int e = 0; e < LA; e++)
+                lds_read_r<RQ>(bb[e], (uint32_t)__builtin_amdgcn_readlane(voff, e) + lane_byte);
+#pragma unroll
+            for (int e = 0; e < nsteps; e++) {
+                uint64_t (&cur)[RQ] = bb[e % (LA + 1)];
+                if (e + LA < nsteps) {
+                    lds_read_r<RQ>(bb[(e + LA) % (LA + 1)],
+                                   (uint32_t)__builtin_amdgcn_readlane(voff, e + LA) + lane_byte);
+                    lds_wait_n<LA * RQ>(cur);
+                } else if (e + 3 == nsteps && LA >= 2) {
+                    lds_wait_n<2 * RQ>(cur);
+                } else if (e + 2 == nsteps && LA >= 1) {
+                    lds_wait_n<RQ>(cur);
+                } else {
+                    lds_wait_n<0>(cur);
+                }
+                const int q = e % Q;
+#pragma unroll
+                for (int r = 0; r < RQ; r++) {
+                    acc16[q][r][0] += __builtin_bit_cast(short2v, (uint32_t)cur[r]);
+                    acc16[q][r][1] += __builtin_bit_cast(short2v, (uint32_t)(cur[r] >> 32));
+                }
+                if (q == Q - 1 && ++gcount == G) {
+                    gcount = 0;
+                    widen();
+                }
+            }
+        }
+        wait_ring();
+        ring_barrier();
+        if (chk == nchunk - 1) flush(tb + ktile++);
+        chk = chn;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may land after the workgroup ends
+}
+
+size_t stage2_qp_lds_bytes(int E, int npw, int nbp, int nsub, int umax, int ppc)
+{
+    const int ns = ppc >= 4 ? 3 : 4;
+    return (size_t)(nsub / 2) * kPairTab * 4 + (size_t)ns * (2 * ppc * npw + nbp) * 1024 +
+           (size_t)2 * ppc * umax * E * 8;
+}
+
+template <int Q, int RQ, int PPC, bool NN>
+static hipError_t launch_qp_n(const Stage2Args& a, const S2Multi& m, int nyblk, hipStream_t st)
+{
+    {
+        const hipError_t e = set_max_lds((const void*)k_stage2_qp<Q, RQ, PPC, NN>, 160 * 1024);
+        if (e != hipSuccess) return e;
+    }
+    const unsigned ntiles = (unsigned)((a.nvalid + 256 * RQ - 1) / (256 * RQ));
+    const unsigned nx = a.nwg > 0 && (unsigned)a.nwg < ntiles ? (unsigned)a.nwg : ntiles;
+    Stage2Args b = a;
+    if (nx == ntiles) b.nwg = 0;
+    size_t lds = 0;
+    for (int i = 0; i < m.npass; i++) {
+        if (2 * PPC * m.p[i].npw + m.p[i].nbp > 32) return hipErrorInvalidValue;
+        lds = std::max(lds, stage2_qp_lds_bytes(m.p[i].ws, m.p[i].npw, m.p[i].nbp, a.nsub, m.p[i].umax, PPC));
+    }
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    S2Multi mm = m;
+    mm.nyblk = nyblk;
+    hipLaunchKernelGGL((k_stage2_qp<Q, RQ, PPC, NN>), dim3(nx, (unsigned)(nyblk * m.npass)), dim3(1024), lds, st, b, mm);
+    return hipGetLastError();
+}
+
+template <int Q, int RQ, int PPC>
+static hipError_t launch_qp_p(const Stage2Args& a, const S2Multi& m, int nyblk, hipStream_t st)
+{
+    if (a.nonneg && !(a.probe & 64)) return launch_qp_n<Q, RQ, PPC, true>(a, m, nyblk, st);
+    return launch_qp_n<Q, RQ, PPC, false>(a, m, nyblk, st);
+}
+
+#define HD_QP_QR(X) X(5, 3) X(4, 3)
+
+bool stage2_qp_supports(int q, int r)
+{
+#define HD_QS(QQ, RR) if (q == QQ && r == RR) return true;
+    HD_QP_QR(HD_QS)
+#undef HD_QS
+    return false;
+}
+
+hipError_t launch_stage2_qp_multi(const Stage2Args& a, const S2Multi& m, int q, int r, int ppc, hipStream_t st)
+{
+    if (a.nvalid <= 0 || m.npass <= 0) return hipSuccess;
+    if (m.npass > kS2MaxPass) return hipErrorInvalidValue;
+    const int nyblk = (a.numdms + a.dms_per_blk - 1) / a.dms_per_blk;
+#define HD_QL(QQ, RR)                                                                         \
+    if (q == QQ && r == RR) {                                                                 \
+        if (ppc == 4) return launch_qp_p<QQ, RR, 4>(a, m, nyblk, st);                         \
+        if (ppc == 3) return launch_qp_p<QQ, RR, 3>(a, m, nyblk, st);                         \
+        if (ppc == 2) return launch_qp_p<QQ, RR, 2>(a, m, nyblk, st);                         \
+        return hipErrorInvalidValue;                                                          \
+    }
+    HD_QP_QR(HD_QL)
+#undef HD_QL
+    return hipErrorInvalidValue;
+}
+#undef HD_QP_QR
+
 }  // namespace hd

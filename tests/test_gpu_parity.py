@@ -87,7 +87,7 @@ def test_stage1_calib_mask_bitexact(engine, sub_dtype, ds_mode):
 
 @pytest.mark.parametrize("numdms,ds,numout_mode", [(76, 1, "none"), (64, 2, "none"), (76, 3, "pad"),
                                                    (5, 1, "trunc"), (100, 5, "pad"), (76, 10, "pad")])
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9])
 def test_stage2_bitexact(engine, numdms, ds, numout_mode, variant):
     obs = palfa_obs(N=3 * 8192, nbits=8)
     raw = load_beam(engine, obs)
@@ -100,14 +100,14 @@ def test_stage2_bitexact(engine, numdms, ds, numout_mode, variant):
     try:
         p.set_variant(variant)
     except PrestoError:
-        if variant in (6, 7, 8):   # wide DM steps: > kPairUMax patterns per pair or LDS (the DDplan passes apply, below)
+        if variant in (6, 7, 8, 9):   # wide DM steps: > kPairUMax patterns per pair or LDS (the DDplan passes apply, below)
             pytest.skip("pair variant not applicable to this plan")
         raise
     p.run_subband()
     try:
         got = p.run_dedisp()
     except PrestoError:
-        if variant in (6, 7, 8) and ds == 10:
+        if variant in (6, 7, 8, 9) and ds == 10:
             pytest.skip("pair variant not applicable (subband bound)")
         raise
     sub, want = OR.run_pass(obs, Opts(), raw, pp)
@@ -131,16 +131,18 @@ def test_stage2_pair_ddplan_passes(engine, stage, passnum):
     p = engine.plan(pp)
     p.run_subband()
     outs = []
-    vs = [6, 0, 5, 7, 8]
+    vs = [6, 0, 5, 7, 8, 9]
     for v in list(vs):
         try:
             p.set_variant(v)
-        except PrestoError:                                    # variants 7, 8: when their tables fit
-            assert v in (7, 8)
+        except PrestoError:                                    # variants 7, 8, 9: when their tables fit
+            assert v in (7, 8, 9)
             vs.remove(v)
             continue
         outs.append(p.run_dedisp())
-    assert 8 in vs                                             # the register-window kernel takes every Mock pass
+        if v == 9:
+            assert p.kernel().startswith("k_stage2_qp<")
+    assert 8 in vs and 9 in vs                                 # the rw and quarter kernels take every Mock pass
     _, want = OR.run_pass(obs, Opts(), raw, pp, mask=mask, ptsperint=pts, padvals=pad)
     for v, got in zip(vs, outs):
         assert_series(got, want, obs.N // pp.ds)
@@ -166,11 +168,12 @@ def test_stage2_pair_persistent_bitexact(engine, stage):
     p = engine.plan(pp)
     p.run_subband()
     outs = []
-    for v in (6 | (1 << 24), 6 | (2 << 24), 7 | (1 << 24), 7 | (2 << 24), 8 | (1 << 24), 8 | (2 << 24)):
+    for v in (6 | (1 << 24), 6 | (2 << 24), 7 | (1 << 24), 7 | (2 << 24), 8 | (1 << 24), 8 | (2 << 24),
+              9 | (1 << 24), 9 | (2 << 24)):
         try:
             p.set_variant(v)
-        except PrestoError:                                    # variants 7, 8: when their tables fit
-            assert v & 0xFF in (7, 8)
+        except PrestoError:                                    # variants 7, 8, 9: when their tables fit
+            assert v & 0xFF in (7, 8, 9)
             continue
         outs.append(p.run_dedisp())
     p.destroy()
@@ -181,12 +184,14 @@ def test_stage2_pair_persistent_bitexact(engine, stage):
         assert np.array_equal(o, outs[0])
 
 
+@pytest.mark.parametrize("variant", [8, 9])
 @pytest.mark.parametrize("numdms,lodm,dmstep", [(76, 30.0, 0.1), (64, 240.0, 0.3), (17, 500.0, 0.5), (1, 12.0, 0.1)])
-def test_stage2_rw_signed_uploaded_subbands(engine, numdms, lodm, dmstep):
-    """The register-window kernel (variant 8) on uploaded int16 subbands of both signs
-    (hd_set_subbands; |sub| <= 8000, so pairs stay within int16): its one-copy partials are
-    read as sign-extended words -- bit-exact against the oracle's stage 2, for y-blocks of
-    Q = 5, 4, 3 and 1 DMs per wave, with a ragged last tile."""
+def test_stage2_rw_signed_uploaded_subbands(engine, numdms, lodm, dmstep, variant):
+    """The register-window kernel (variant 8) and the quarter-layout pair kernel (variant 9)
+    on uploaded int16 subbands of both signs (hd_set_subbands; |sub| <= 8000, so pairs stay
+    within int16): their one-copy partials are read as sign-extended words -- bit-exact
+    against the oracle's stage 2, for y-blocks of Q = 5, 4, 3 and 1 DMs per wave (the
+    quarter kernel: 5 or 4), with a ragged last tile."""
     obs = palfa_obs(N=3 * 8192 + 555, nbits=8)
     engine.set_obs(obs, Opts())
     pp = PassParams(subdm=lodm + 3.0, lodm=lodm, dmstep=dmstep, numdms=numdms, nsub=96, ds=1, numout=0)
@@ -195,12 +200,12 @@ def test_stage2_rw_signed_uploaded_subbands(engine, numdms, lodm, dmstep):
         rng = np.random.default_rng(numdms)
         sub = rng.integers(-8000, 8001, size=(96, p.nds), dtype=np.int16)
         p.set_subbands(sub)
-        p.set_variant(8)
+        p.set_variant(variant)
         got = p.run_dedisp()
         _, off = p.delays()
         want = OR.stage2(sub, off, 0, p.nds, omp=True)
         assert np.array_equal(got, want)
-        assert p.kernel().startswith("k_stage2_rw<")
+        assert p.kernel().startswith("k_stage2_rw<" if variant == 8 else "k_stage2_qp<")
     finally:
         p.destroy()
 

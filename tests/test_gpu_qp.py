@@ -1,0 +1,67 @@
+"""The quarter-layout pair kernel (k_stage2_qp, hd_plan_set_variant s2 = 9) through the bench's
+multi-pass launch (hd_run_dedisp_multi): for every Mock DDplan stage (PALFA2_presto_search.py:
+319-326), three passes of a ragged masked beam with more tiles than CUs share one launch; each
+series equals the two-pairs-per-chunk pair kernel's (variant 7) one-pass result bit for bit,
+and one pass per stage equals the oracle.  Stage 2 reference: PALFA2_presto_search.py:514-520.
+"""
+import numpy as np
+import pytest
+
+import oracle as OR
+from hipdedisp import Opts, PassParams, plan
+from hipdedisp.synth import palfa_obs, palfa_synth, synth_mask
+from test_gpu_parity import assert_series, load_beam
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("stage", range(6))
+def test_qp_multipass_stage_matches_pair_and_oracle(engine, stage):
+    obs = palfa_obs(N=(1 << 19) + 777, nbits=8)
+    synth = palfa_synth()
+    raw = load_beam(engine, obs, synth=synth)
+    pts = 2048
+    mask, pad = synth_mask(obs, synth, pts)
+    engine.set_mask(mask, pts, pad)
+    d = plan.ddplans_for("pdev")[stage]
+    idx = sorted({0, d.numpasses // 2, d.numpasses - 1})
+    pps = [PassParams(subdm=float(d.subdmlist[i]), lodm=float(d.lodm_arg(i)), dmstep=float(d.dmstep_arg()),
+                      numdms=d.dmsperpass, nsub=d.numsub, ds=d.sub_downsamp, numout=plan.choose_N(obs.N / d.downsamp))
+           for i in idx]
+    plans = [engine.plan(pp) for pp in pps]
+    try:
+        engine.run_subband_multi(plans)
+        ref = []
+        for p in plans:
+            p.set_variant(7)
+            ref.append(p.run_dedisp())
+        for p in plans:
+            p.set_variant(9)
+        engine.run_dedisp_multi(plans)
+        assert [p.launch_passes() for p in plans] == [len(plans)] + [0] * (len(plans) - 1)
+        for p, r in zip(plans, ref):
+            assert p.kernel().startswith("k_stage2_qp<"), p.kernel()
+            assert np.array_equal(p.get_series(0, None, 0, p.numout), r)
+        _, want = OR.run_pass(obs, Opts(), raw, pps[-1], mask=mask, ptsperint=pts, padvals=pad, omp=True)
+        assert_series(ref[-1], want, obs.N // pps[-1].ds)
+    finally:
+        for p in plans:
+            p.destroy()
+        engine.set_mask()
+
+
+@pytest.mark.parametrize("N", [700, 767, 768, 769, 5000])
+def test_qp_short_beams(engine, N):
+    """Beams of less than one to a few 768-sample tiles (every quarter's ragged tail)."""
+    obs = palfa_obs(N=N, nbits=8)
+    raw = load_beam(engine, obs)
+    pp = PassParams(subdm=3.8, lodm=0.0, dmstep=0.1, numdms=76, nsub=96, ds=1, numout=0)
+    p = engine.plan(pp)
+    try:
+        p.run_subband()
+        p.set_variant(9)
+        got = p.run_dedisp()
+        _, want = OR.run_pass(obs, Opts(), raw, pp)
+        assert_series(got, want, obs.N)
+    finally:
+        p.destroy()
