@@ -18,6 +18,8 @@
 namespace hd {
 
 constexpr int kQ8mS = 960;                    // raw rows per quarter of the tile
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) u32x2 lds_u32x2;     // (volatile LDS loads keep their address space)
 #ifndef Q8M_UNROLL
 #define Q8M_UNROLL 4
 #endif
@@ -71,7 +73,9 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
         const int br1 = brow, br2 = brow2;
         auto kof = [=](int row) { return k0c + (row >= br1 ? k1c - k0c : 0u) + (row >= br2 ? k2c - k1c : 0u); };
         int mx = 0;
-#pragma unroll Q8M_UNROLL
+        // (even DS: its two read paths per channel need the registers of a wider unroll)
+        constexpr int UNR = DS % 2 == 0 ? 1 : Q8M_UNROLL;
+#pragma unroll UNR
         for (int m = 0; m < M; m++) {
             const bool act = (m + 1) * 64 <= JQ || lane + 64 * m < JQ;
             uint32_t ae, ao;
@@ -88,11 +92,38 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
             for (int cc = 0; cc < CPS; cc++) {
                 const uint32_t keep = ((zall >> cc) & 1u) ? 0u : 0xFFFFFFFFu;
                 const uint32_t* b = lbase + lrb[cc] + dl[cc] + mo;
-#pragma unroll
-                for (int k = 0; k < DS; k++) {
-                    const uint32_t x = b[k] & keep;
+                auto add1 = [&](uint32_t x) {
+                    x &= keep;
                     ae += x & 0x00FF00FFu;
                     ao += __builtin_amdgcn_perm(0u, x, 0x0c030c01u);
+                };
+                if constexpr (DS % 2 == 0) {
+                    // even DS: lanes DS dwords apart, so ds_read2_b32 runs 2-way bank-conflicted;
+                    // the rows' dword parity is the channel delay's (lbase, lrb, mo are even),
+                    // uniform per wave: aligned ds_read_b64 (conflict-free at any even stride;
+                    // volatile so they are not merged into ds_read2_b64, half the rate on gfx950)
+                    if (((lrb[cc] + dl[cc]) & 1) == 0) {
+                        const volatile lds_u32x2* b2 = (const volatile lds_u32x2*)__builtin_assume_aligned(b, 8);
+#pragma unroll
+                        for (int j = 0; j < DS / 2; j++) {
+                            const u32x2 v = b2[j];
+                            add1(v.x);
+                            add1(v.y);
+                        }
+                    } else {
+                        add1(b[0]);
+                        const volatile lds_u32x2* b2 = (const volatile lds_u32x2*)__builtin_assume_aligned(b + 1, 8);
+#pragma unroll
+                        for (int j = 0; j < DS / 2 - 1; j++) {
+                            const u32x2 v = b2[j];
+                            add1(v.x);
+                            add1(v.y);
+                        }
+                        add1(b[DS - 1]);
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < DS; k++) add1(b[k]);
                 }
             }
             if (!act) continue;
