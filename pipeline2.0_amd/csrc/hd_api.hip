@@ -4208,14 +4208,41 @@ const RcclApi& rccl()
     static std::once_flag once;
     std::call_once(once, [] {
         void* h = nullptr;
+        // The RCCL must run on the HIP runtime this library runs on.  A process can hold two:
+        // torch's wheel ships its own libamdhip64/librccl, and when this library is loaded
+        // before torch, torch maps a second HIP runtime and its librccl.so.1 -- which a plain
+        // dlopen("librccl.so.1") then returns (soname match), an RCCL whose runtime knows
+        // neither our device buffers nor our streams (bench --comm hd measured 3.9 s per beam
+        // that way).  So load librccl from OUR runtime's directory, by path, and check it.
+        hipError_t (*const ours)(int*) = hipGetDeviceCount;    // a runtime entry point, as bound for us
+        Dl_info di{};
+        std::string rtdir;
+        if (dladdr((void*)ours, &di) && di.dli_fname) {
+            rtdir = di.dli_fname;
+            rtdir = rtdir.substr(0, rtdir.find_last_of('/') + 1);
+        }
         // HD_TEST_NO_RCCL=1 (CPU tests) takes the not-found path without touching the loader
-        if (!getenv("HD_TEST_NO_RCCL"))
-            for (const char* n : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
-                if ((h = dlopen(n, RTLD_NOW | RTLD_GLOBAL))) break;
+        if (!getenv("HD_TEST_NO_RCCL")) {
+            for (const char* n : {"librccl.so.1", "librccl.so"})
+                if (!rtdir.empty() && (h = dlopen((rtdir + n).c_str(), RTLD_NOW | RTLD_LOCAL))) break;
+            if (!h)
+                for (const char* n : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+                    if ((h = dlopen(n, RTLD_NOW | RTLD_LOCAL))) break;
+        }
         if (!h) {
             // dlerror() clears the message it returns: read it once
             const char* de = getenv("HD_TEST_NO_RCCL") ? nullptr : dlerror();
             api.err = de ? de : "librccl not found";
+            return;
+        }
+        // the HIP runtime the loaded RCCL resolves against must be ours
+        void* their = dlsym(h, "hipGetDeviceCount");
+        Dl_info dr{};
+        if (their && their != (void*)ours) {
+            std::string rp = dladdr(their, &dr) && dr.dli_fname ? dr.dli_fname : "?";
+            api.err = "librccl in this process runs on another HIP runtime (" + rp + ", this library: " +
+                      (di.dli_fname ? std::string(di.dli_fname) : std::string("?")) +
+                      "); load libhipdedisp after torch, or use torch.distributed for the exchanges";
             return;
         }
         api.get_id = (decltype(api.get_id))dlsym(h, "ncclGetUniqueId");
