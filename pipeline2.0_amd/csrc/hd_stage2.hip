@@ -908,7 +908,9 @@ __device__ __forceinline__ void load12_shift(const uint32_t* w32, int x, uint32_
     for (int m = 0; m < 6; m++) o[m] = __builtin_amdgcn_alignbit(w[m + 1], w[m], sh);
 }
 
-template <int Q, int R, int PPC, bool NN>
+// PRB: profiling build of the kernel (a.probe bits switch phases off); the production
+// instantiation (PRB = false) carries no probe tests
+template <int Q, int R, int PPC, bool NN, bool PRB>
 __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, S2Multi m)
 {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
@@ -1081,7 +1083,7 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, S2Multi m)
     #pragma unroll
             for (int r = 0; r < R; r++) {
                 const int64_t tl = t0 + 256 * r + 4 * lane;
-                if (dv && !(a.probe & 4)) {
+                if (dv && !(PRB && (a.probe & 4))) {
                     float* o = P.out + (int64_t)d * a.out_stride + tl;
                     if (tl + 3 < a.nvalid) {
                         *(float4*)o = make_float4((float)acc32[q][r][0], (float)acc32[q][r][1], (float)acc32[q][r][2],
@@ -1124,15 +1126,15 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, S2Multi m)
 
     int chk = 0, ktile = 0;                            // chunk (within the tile) and tile of chunk c
     for (int c = 0; c < ntot; c++) {
-        if (!(a.probe & 2)) dma(c + NS - 1);   // probe 2: no window DMA after the prologue
+        if (!(PRB && (a.probe & 2))) dma(c + NS - 1);   // probe 2: no window DMA after the prologue
         const int chn = chk + 1 == nchunk ? 0 : chk + 1;
-        if (c + 1 < ntot && !(a.probe & 8)) expand(c + 1, chn);
+        if (c + 1 < ntot && !(PRB && (a.probe & 8))) expand(c + 1, chn);
         // this chunk's per-DM byte offsets: pair k, DM entry q in lane q of voff[k]
         const int32_t* sboff = (const int32_t*)(lds_raw + ring0 + (c % NS) * slot_bytes + 2 * PPC * npw * 1024);
         int voff[PPC];
 #pragma unroll
         for (int k = 0; k < PPC; k++) voff[k] = lane < Q ? sboff[k * dpb + wave * Q + lane] : 0;
-        if (!(a.probe & 1)) {
+        if (!(PRB && (a.probe & 1))) {
             constexpr int nsteps = PPC * Q, LA0 = ring_la<Q, R>() < Q - 1 ? ring_la<Q, R>() : Q - 1, LA = LA0;
             uint64_t bb[LA + 1][R];
 #pragma unroll
@@ -1616,11 +1618,11 @@ size_t stage2_pair_lds_bytes(int wstride, int npw, int nbp, int nsub, int umax, 
            (size_t)2 * ppc * umax * 4 * wstride * 2;
 }
 
-template <int Q, int R, int PPC, bool NN>
+template <int Q, int R, int PPC, bool NN, bool PRB>
 static hipError_t launch_pair_qrpn(const Stage2Args& a, const S2Multi& m, int nyblk, hipStream_t st)
 {
     {
-        const hipError_t e = set_max_lds((const void*)k_stage2_pair<Q, R, PPC, NN>, 160 * 1024);
+        const hipError_t e = set_max_lds((const void*)k_stage2_pair<Q, R, PPC, NN, PRB>, 160 * 1024);
         if (e != hipSuccess) return e;
     }
     const unsigned ntiles = (unsigned)((a.nvalid + 256 * R - 1) / (256 * R));
@@ -1632,7 +1634,7 @@ static hipError_t launch_pair_qrpn(const Stage2Args& a, const S2Multi& m, int ny
         lds = std::max(lds, stage2_pair_lds_bytes(m.p[i].ws, m.p[i].npw, m.p[i].nbp, a.nsub, m.p[i].umax, PPC));
     S2Multi mm = m;
     mm.nyblk = nyblk;
-    hipLaunchKernelGGL((k_stage2_pair<Q, R, PPC, NN>), dim3(nx, (unsigned)(nyblk * m.npass)), dim3(1024), lds, st, b,
+    hipLaunchKernelGGL((k_stage2_pair<Q, R, PPC, NN, PRB>), dim3(nx, (unsigned)(nyblk * m.npass)), dim3(1024), lds, st, b,
                        mm);
     return hipGetLastError();
 }
@@ -1642,8 +1644,12 @@ static hipError_t launch_pair_qrpn(const Stage2Args& a, const S2Multi& m, int ny
 template <int Q, int R, int PPC>
 static hipError_t launch_pair_qrp(const Stage2Args& a, const S2Multi& m, int nyblk, hipStream_t st)
 {
-    if (a.nonneg && !(a.probe & 64)) return launch_pair_qrpn<Q, R, PPC, true>(a, m, nyblk, st);
-    return launch_pair_qrpn<Q, R, PPC, false>(a, m, nyblk, st);
+    const bool prb = (a.probe & 15) != 0;
+    if (a.nonneg && !(a.probe & 64))
+        return prb ? launch_pair_qrpn<Q, R, PPC, true, true>(a, m, nyblk, st)
+                   : launch_pair_qrpn<Q, R, PPC, true, false>(a, m, nyblk, st);
+    return prb ? launch_pair_qrpn<Q, R, PPC, false, true>(a, m, nyblk, st)
+               : launch_pair_qrpn<Q, R, PPC, false, false>(a, m, nyblk, st);
 }
 
 // Two workgroups per CU: 8 waves x Q DMs (<= 40) per workgroup, one LDS window buffer, no
@@ -2007,7 +2013,7 @@ __device__ __forceinline__ void qp_load4(const uint32_t* w32, int x, uint32_t& o
 template <int PPC>
 constexpr int qp_ns() { return PPC >= 4 ? 3 : 4; }
 
-template <int Q, int RQ, int PPC, bool NN>
+template <int Q, int RQ, int PPC, bool NN, bool PRB>
 __global__ __launch_bounds__(1024) void k_stage2_qp(Stage2Args a, S2Multi m)
 {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
@@ -2182,7 +2188,7 @@ __global__ __launch_bounds__(1024) void k_stage2_qp(Stage2Args a, S2Multi m)
             const int d = dblk0 + dl;
             const bool dv = dl < dpb && d < a.numdms;
             int64_t part = 0;
-            if (dv && !(a.probe & 4)) {
+            if (dv && !(PRB && (a.probe & 4))) {
                 float* o = P.out + (int64_t)d * a.out_stride + t0 + lane;
                 if (t0 + T <= a.nvalid) {
 #pragma unroll
@@ -2236,13 +2242,13 @@ __global__ __launch_bounds__(1024) void k_stage2_qp(Stage2Args a, S2Multi m)
 
     int chk = 0, ktile = 0;
     for (int c = 0; c < ntot; c++) {
-        if (!(a.probe & 2)) dma(c + NS - 1);
+        if (!(PRB && (a.probe & 2))) dma(c + NS - 1);
         const int chn = chk + 1 == nchunk ? 0 : chk + 1;
-        if (c + 1 < ntot && !(a.probe & 8)) expand(c + 1, chn);
+        if (c + 1 < ntot && !(PRB && (a.probe & 8))) expand(c + 1, chn);
         const int32_t* sboff = (const int32_t*)(lds_raw + ring0 + (c % NS) * slot_bytes + 2 * PPC * npw * 1024);
         // this chunk's (pair, DM) byte offsets in ONE register: lane k * Q + q holds pair k, DM q
         const int voff = lane < PPC * Q ? sboff[(lane / Q) * dpb + wave * Q + lane % Q] : 0;
-        if (!(a.probe & 1)) {
+        if (!(PRB && (a.probe & 1))) {
             constexpr int nsteps = PPC * Q, LA0 = ring_la<Q, RQ>() < Q - 1 ? ring_la<Q, RQ>() : Q - 1, LA = LA0;
             uint64_t bb[LA + 1][RQ];
 #pragma unroll
@@ -2289,11 +2295,11 @@ size_t stage2_qp_lds_bytes(int E, int npw, int nbp, int nsub, int umax, int ppc)
            (size_t)2 * ppc * umax * E * 8;
 }
 
-template <int Q, int RQ, int PPC, bool NN>
+template <int Q, int RQ, int PPC, bool NN, bool PRB>
 static hipError_t launch_qp_n(const Stage2Args& a, const S2Multi& m, int nyblk, hipStream_t st)
 {
     {
-        const hipError_t e = set_max_lds((const void*)k_stage2_qp<Q, RQ, PPC, NN>, 160 * 1024);
+        const hipError_t e = set_max_lds((const void*)k_stage2_qp<Q, RQ, PPC, NN, PRB>, 160 * 1024);
         if (e != hipSuccess) return e;
     }
     const unsigned ntiles = (unsigned)((a.nvalid + 256 * RQ - 1) / (256 * RQ));
@@ -2308,15 +2314,17 @@ static hipError_t launch_qp_n(const Stage2Args& a, const S2Multi& m, int nyblk, 
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     S2Multi mm = m;
     mm.nyblk = nyblk;
-    hipLaunchKernelGGL((k_stage2_qp<Q, RQ, PPC, NN>), dim3(nx, (unsigned)(nyblk * m.npass)), dim3(1024), lds, st, b, mm);
+    hipLaunchKernelGGL((k_stage2_qp<Q, RQ, PPC, NN, PRB>), dim3(nx, (unsigned)(nyblk * m.npass)), dim3(1024), lds, st, b, mm);
     return hipGetLastError();
 }
 
 template <int Q, int RQ, int PPC>
 static hipError_t launch_qp_p(const Stage2Args& a, const S2Multi& m, int nyblk, hipStream_t st)
 {
-    if (a.nonneg && !(a.probe & 64)) return launch_qp_n<Q, RQ, PPC, true>(a, m, nyblk, st);
-    return launch_qp_n<Q, RQ, PPC, false>(a, m, nyblk, st);
+    const bool prb = (a.probe & 15) != 0;
+    if (a.nonneg && !(a.probe & 64))
+        return prb ? launch_qp_n<Q, RQ, PPC, true, true>(a, m, nyblk, st) : launch_qp_n<Q, RQ, PPC, true, false>(a, m, nyblk, st);
+    return prb ? launch_qp_n<Q, RQ, PPC, false, true>(a, m, nyblk, st) : launch_qp_n<Q, RQ, PPC, false, false>(a, m, nyblk, st);
 }
 
 #define HD_QP_QR(X) X(5, 3) X(4, 3)

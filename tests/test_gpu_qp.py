@@ -51,7 +51,7 @@ def test_qp_multipass_stage_matches_pair_and_oracle(engine, stage):
 
 
 @pytest.mark.parametrize("N", [700, 767, 768, 769, 5000])
-def test_qp_short_beams(engine, N):
+def test_qp_stage2_short_beams(engine, N):
     """Beams of less than one to a few 768-sample tiles (every quarter's ragged tail)."""
     obs = palfa_obs(N=N, nbits=8)
     raw = load_beam(engine, obs)

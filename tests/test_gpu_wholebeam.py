@@ -99,7 +99,7 @@ def test_c2_bench_path_kernels(c2_beam):
     """The beam ran through the kernels the bench reports (not a fallback variant)."""
     obs, raw, cl, stages, plans = c2_beam
     kern = {p.kernel() for st in plans for p in st}
-    assert any("k_stage2_pair" in k for k in kern), kern
+    assert any(k.startswith(("k_stage2_pair<", "k_stage2_qp<")) and k.endswith(", false>") for k in kern), kern
 
 
 @pytest.mark.parametrize("stage,i0", c2_cases())
