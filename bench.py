@@ -61,11 +61,18 @@ def parse():
     ap.add_argument("--stream-beams", type=int, default=-1,
                     help="beams of the overlapped PSRFITS-streaming leg (configs[4]; prefetch thread; 3 at world "
                          "size 1), run last; 0 = skip")
-    ap.add_argument("--mode", choices=["beam", "slices", "shard"], default="beam",
+    ap.add_argument("--beams", type=int, default=7,
+                    help="--mode pointing: beams of the ALFA pointing (configs[4]: 7)")
+    ap.add_argument("--helper-frac", type=float, default=None,
+                    help="--mode pointing: each home rank's share of its beam (default: balanced by the slice "
+                         "cost model, sharding.helper_fraction)")
+    ap.add_argument("--mode", choices=["beam", "slices", "shard", "pointing"], default="beam",
                     help="beam: one beam per rank (weak scaling, configs[4]); slices: ONE beam cut into per-rank "
                          "time slices, every rank runs all 57 passes on its slice (strong, configs[2]; RCCL carries "
                          "only the clip statistics and padding sums); shard: ONE beam's passes LPT-sharded after "
-                         "an RCCL broadcast of the raw block (strong, the round-1 design, kept for comparison)")
+                         "an RCCL broadcast of the raw block (strong, the round-1 design, kept for comparison); "
+                         "pointing: --beams beams on the node's ranks (configs[4]): ranks 0..beams-1 take the head of "
+                         "their beam, the remaining ranks the tails of every beam (time slices, one-way exchanges)")
     ap.add_argument("--check-union", action="store_true",
                     help="--mode slices: after the timed steps, gather every rank's exact per-DM sums of its owned "
                          "series (and the last rank's padding values) and check, on rank 0, that their union equals a "
@@ -537,8 +544,105 @@ def cpu_baseline(obs, synth, ddplans, target_s, mask, pts, pad, omp):
             "est_full_beam_s": est_full}
 
 
+def pointing_main(args, world, rank, local, dist, torch):
+    """configs[4]: the beams of one ALFA pointing over the node's ranks (sharding.Pointing):
+    each rank runs its (beam, time slice) units -- one context each -- through all 57 passes;
+    the exchanges are one-way point-to-point messages.  value = output samples of every
+    beam / max-over-ranks wall time per pointing."""
+    import numpy as np
+    from hipdedisp import Engine, Opts, plan as P
+    from hipdedisp import sharding as S
+    from hipdedisp.synth import palfa_obs, palfa_synth, rfifind_ptsperint, synth_mask
+    obs = palfa_obs(N=args.nspec, nbits=args.nbits)
+    ddplans = P.ddplans_for("pdev")
+    pt = S.Pointing(obs, ddplans, args.beams, world, frac=args.helper_frac)
+    ts = pt.ts
+    pts = rfifind_ptsperint(obs.dt)
+    work, out_per_step = [], 0
+    for b, sl in pt.units(rank):
+        synth = palfa_synth(beam=b, nbits=args.nbits)
+        eng = Engine(local)
+        eng.set_obs(ts.local_obs(sl), Opts())
+        eng.set_slice(ts.slice(sl)[0], obs.N)
+        eng.set_streams(args.streams)
+        eng.synth_device(synth)
+        mask, pad = synth_mask(obs, synth, pts)
+        eng.set_mask(mask, pts, pad)
+        plans = [p for st in slice_stages(eng, ts, sl, args.variant) for p in st]
+        out_per_step += sum(p.pp.numdms * ts.out_range(sl, p.pp.ds)[1] for p in plans)
+        work.append((b, sl, eng, plans))
+    on_gpu = dist is not None and dist.get_backend() == "nccl"
+    for _ in range(args.warmup):
+        S.pointing_step(pt, rank, work, dist, torch, on_gpu)
+    barrier(dist, torch)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        S.pointing_step(pt, rank, work, dist, torch, on_gpu)
+    barrier(dist, torch)
+    dt = time.perf_counter() - t0
+    dt_max = max_over_ranks(dt, dist, torch)
+    total_out = out_per_step
+    if dist is not None:
+        tt = torch.tensor([float(out_per_step)], dtype=torch.float64, device="cuda" if on_gpu else "cpu")
+        dist.all_reduce(tt)
+        total_out = tt.item()
+    ms1 = sum(p.last_ms()[0] for _, _, _, pl in work for p in pl)
+    ms2 = sum(p.last_ms()[1] for _, _, _, pl in work for p in pl)
+    line = {
+        "metric": METRIC, "value": total_out * args.steps / dt_max, "unit": "samples/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt_max / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+        "dtype": "u8->f32 subbanding, i16 subbands, i16x2/i32 exact sums, f32 out", "data": "synthetic",
+        "config": {"workload": "C5: an ALFA pointing of %d PALFA Mock beams (960 ch x 2^%d x %d-bit), 57-pass "
+                               "DDplan each, rfifind-style masks" % (args.beams, int(np.log2(obs.N)), args.nbits),
+                   "parallelism": "beam x time: %d home ranks take the first %.4f of their beam, %d helper rank(s) "
+                                  "the tails of every beam; one-way clip-row and first-DM-sum messages"
+                                  % (min(args.beams, world), pt.frac, pt.nhelpers),
+                   "cuts": ts.cuts, "halo": ts.halo},
+        "this_rank": {"rank": rank, "units": pt.units(rank), "kernel_ms_per_step": {"stage1": ms1, "stage2": ms2}},
+        "predicted_ms_per_pointing": pt.predicted_ms(),
+        "prediction_note": "sharding.Pointing.predicted_ms: slice cost t(x) = 6.0 + 61.9 x ms from the round-4 "
+                           "one-rank slice timings (a prediction, not a measurement)",
+    }
+    if args.check_union:
+        mine_ck = {(b, sl): slice_checksums(ts, sl, [pl]) for b, sl, _, pl in work}
+        gathered = [None] * world
+        if dist is not None:
+            dist.all_gather_object(gathered, mine_ck)
+        else:
+            gathered = [mine_ck]
+        if rank == 0:
+            allck = {}
+            for g in gathered:
+                allck.update(g)
+            res = []
+            for b in range(args.beams):
+                synth = palfa_synth(beam=b, nbits=args.nbits)
+                mask, pad = synth_mask(obs, synth, pts)
+                per_slice = [allck[(b, k)] for k in range(pt.nslices())]
+                res.append(union_check(lambda: Engine(local), obs, synth, ddplans, mask, pts, pad, per_slice))
+            line["union_check"] = {"beams": len(res), "equal": all(r["equal"] for r in res),
+                                   "dm_trials": sum(r["dm_trials"] for r in res),
+                                   "mismatches": [m for r in res for m in r["mismatches"]][:8],
+                                   "note": res[0]["note"] if res else ""}
+        barrier(dist, torch)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    for _, _, eng, pl in work:
+        for p in pl:
+            p.destroy()
+        eng.close()
+    if "union_check" in line and not line["union_check"]["equal"]:
+        sys.exit("union check failed: %s" % line["union_check"]["mismatches"])
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.mode == "pointing":
+        world, rank, local, dist, torch = dist_setup(args)
+        return pointing_main(args, world, rank, local, dist, torch)
     global DD_MULTI, S1_FUSE
     DD_MULTI = not args.dd_single
     S1_FUSE = not args.s1_per_stage

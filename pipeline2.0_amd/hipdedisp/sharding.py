@@ -187,10 +187,13 @@ class TimeSlices:
         j0, nj = ts.out_range(rank, ds)        # output samples [j0, j0 + nj) this rank owns
     """
 
-    def __init__(self, obs, ddplans, world, opts=None):
+    def __init__(self, obs, ddplans, world, opts=None, fractions=None):
+        """fractions: optional relative slice lengths (one per rank; default equal slices)."""
         from .engine import Opts, PassParams, plan_tables
         if world < 1:
             raise ValueError("world must be >= 1")
+        if fractions is not None and (len(fractions) != world or min(fractions) < 0 or sum(fractions) <= 0):
+            raise ValueError("fractions: one non-negative length per slice")
         self.obs, self.ddplans, self.world = obs, list(ddplans), world
         self.opts = opts or Opts()
         if world > 1 and self.opts.pad_mode == 0:        # HD_PAD_MEAN: one value per DM
@@ -210,7 +213,11 @@ class TimeSlices:
         self.blk, self.unit = blk, unit
         self.halo = -(-reach // blk) * blk
         N = obs.N
-        cuts = [0] + [min(N, round(k * N / world / unit) * unit) for k in range(1, world)] + [N]
+        if fractions is None:
+            cuts = [0] + [min(N, round(k * N / world / unit) * unit) for k in range(1, world)] + [N]
+        else:
+            cum = np.cumsum(np.asarray(fractions, np.float64)) / float(np.sum(fractions))
+            cuts = [0] + [min(N, int(round(c * N / unit)) * unit) for c in cum[:-1]] + [N]
         for k in range(1, len(cuts)):
             cuts[k] = max(cuts[k], cuts[k - 1])
         self.cuts = cuts
@@ -276,3 +283,184 @@ class TimeSlices:
                 nds = self.obs.N // p.pp.ds
                 v = np.float32(s / nds) if self.opts.pad_mode == 2 and nds > 0 else np.float32(0.0)
                 p.series_fill(nj, float(v))
+
+
+# ---------------------------------------------------------------------------------------
+# configs[4]: the 7 beams of an ALFA pointing on one node (beam x time partitioning)
+# ---------------------------------------------------------------------------------------
+
+def helper_fraction(nbeams, nhelpers, fixed_ms, beam_ms):
+    """Home share f of each beam that balances a home rank (one slice of f N spectra) against
+    a helper (its share of every beam's tail), for a slice cost t(x) = a + b x (a = fixed_ms,
+    b = beam_ms): a + b f = k (a + b (1 - f) / 1) with k = nbeams / nhelpers tails per helper,
+    solved for f and clamped to [0.5, 1].  With no helpers every rank keeps whole beams."""
+    if nhelpers <= 0:
+        return 1.0
+    k = nbeams / float(nhelpers)                 # beam tails per helper
+    a, b = float(fixed_ms), float(beam_ms)
+    # home: a + b f ;  helper: k (a + b (1 - f))
+    f = (k * a + k * b - a) / (b * (1.0 + k))
+    return min(1.0, max(0.5, f))
+
+
+class Pointing:
+    """configs[4] (BASELINE.json): the `nbeams` beams of an ALFA pointing on a node of `world`
+    ranks.  The reference runs one beam per batch job (queue_managers/pbs.py:67), which on 8
+    GPUs leaves one idle for a 7-beam pointing.  Here ranks 0 .. nbeams-1 are HOME ranks:
+    rank b dedisperses the first `f` of beam b's spectra through all passes (a time slice,
+    TimeSlices semantics: its own rows plus the halo); the H = world - nbeams HELPER ranks
+    split the tail of EVERY beam between them (slice 1 + h of beam b is helper h's).  The
+    exchanges are one-way, so no home rank ever waits for a helper mid-beam:
+
+    * clip_times (its running statistics carry across read blocks, forwards only): the home
+      rank computes the statistics rows of every block it holds (own + halo) itself, so it
+      needs nothing; each slice owner sends its OWN blocks' rows to the later slice owners of
+      the beam, which sum them into their table before finishing clip_times;
+    * padding (the observation's first-DM mean): every slice owner but the last sends its
+      first-DM sums per pass to the last owner, which pads -- after all its beams.
+
+    With world <= nbeams there are no helpers: rank r keeps beams r, r + world, ... whole.
+    `units(rank)` lists (beam, slice) pairs in processing order; `slices(beam)` the beam's
+    TimeSlices; `owner(beam, slice)` the rank."""
+
+    def __init__(self, obs, ddplans, nbeams, world, frac=None, opts=None, fixed_ms=6.0, beam_ms=61.9):
+        if nbeams < 1 or world < 1:
+            raise ValueError("need nbeams >= 1 and world >= 1")
+        self.obs, self.ddplans, self.nbeams, self.world = obs, list(ddplans), nbeams, world
+        self.nhelpers = max(0, world - nbeams)
+        self.frac = float(frac) if frac is not None else helper_fraction(nbeams, self.nhelpers, fixed_ms, beam_ms)
+        if self.nhelpers:
+            tail = (1.0 - self.frac) / self.nhelpers
+            fr = [self.frac] + [tail] * self.nhelpers
+            self.ts = TimeSlices(obs, ddplans, 1 + self.nhelpers, opts=opts, fractions=fr)
+        else:
+            self.ts = TimeSlices(obs, ddplans, 1, opts=opts)
+
+    def nslices(self):
+        return self.ts.world
+
+    def owner(self, beam, sl):
+        if self.nhelpers == 0:
+            return beam % self.world
+        return beam if sl == 0 else self.nbeams + sl - 1
+
+    def units(self, rank):
+        if self.nhelpers == 0:
+            return [(b, 0) for b in range(rank, self.nbeams, self.world)]
+        if rank < self.nbeams:
+            return [(rank, 0)]
+        return [(b, rank - self.nbeams + 1) for b in range(self.nbeams)]
+
+    def slices(self, beam):
+        return self.ts                           # every beam is cut the same way
+
+    def clip_sources(self, beam, sl):
+        """Ranks whose own-block clip rows slice `sl` of `beam` must receive (earlier slices)."""
+        return [self.owner(beam, k) for k in range(sl)]
+
+    def clip_targets(self, beam, sl):
+        return [self.owner(beam, k) for k in range(sl + 1, self.nslices())]
+
+    def pad_owner(self, beam):
+        return self.owner(beam, self.nslices() - 1)
+
+    def clip_rows(self, sl):
+        """(first block, blocks) of slice sl's own read blocks in the beam's stats table."""
+        t0 = self.ts.slice(sl)[0]
+        return t0 // self.ts.blk, self.ts.nown_blocks(sl)
+
+    def predicted_ms(self, fixed_ms=6.0, beam_ms=61.9):
+        """Predicted node time per pointing from the slice cost model (a prediction, not a
+        measurement): the slowest rank's units."""
+        fr = [(self.ts.slice(k)[1]) / float(self.obs.N) for k in range(self.nslices())]
+        best = 0.0
+        for r in range(self.world):
+            t = sum(fixed_ms + beam_ms * fr[sl] for _, sl in self.units(r))
+            best = max(best, t)
+        return best
+
+
+def pointing_step(pt, rank, work, dist, torch, on_gpu):
+    """One pointing on this rank: `work` = [(beam, slice, engine, plans)] in pt.units(rank)
+    order.  Per unit: clip statistics (earlier slices' own-block rows received, every held
+    block's rows computed here), clip_times finished, every pass, first-DM sums kept.  Sends
+    are non-blocking and ordered so each (source, destination) pair sees clip rows of every
+    beam first, then the sums (NCCL matches point-to-point messages in order); the last slice
+    of a beam pads after this rank's beams are done.  Returns the per-unit first-DM sums."""
+    import numpy as np
+    ts = pt.ts
+    width = ts.obs.nchan + 3
+    reqs, keep, sums_of = [], [], []
+
+    def tensor(a):
+        t = torch.from_numpy(np.ascontiguousarray(a))
+        return t.cuda() if on_gpu else t
+
+    for b, sl, eng, plans in work:
+        eng.touch_raw()
+        if eng.opts.clip_sigma > 0:
+            if on_gpu:
+                table = torch.zeros((ts.nblk_total, width), dtype=torch.float64, device="cuda")
+                tp = table.data_ptr()
+            else:
+                table = torch.zeros((ts.nblk_total, width), dtype=torch.float64)
+                tp = table.numpy()
+            for k in range(sl):                               # earlier slices' own rows
+                r0, n = pt.clip_rows(k)
+                if n:
+                    v = table[r0:r0 + n]
+                    dist.recv(v, src=pt.owner(b, k))
+            if on_gpu:
+                torch.cuda.current_stream().synchronize()
+            # every block this unit holds (own + halo): the recurrence is causal, so rows of the
+            # halo blocks computed here equal the next slice's own
+            t0, own, nloc = ts.slice(sl)
+            nheld = -(-nloc // ts.blk)
+            eng.clip_stats(nheld, tp)
+            r0, n = pt.clip_rows(sl)
+            for dst in pt.clip_targets(b, sl):
+                if n:
+                    v = table[r0:r0 + n].clone()
+                    keep.append(v)
+                    reqs.append(dist.isend(v, dst=dst))
+            eng.clip_set_stats(tp)
+        # bench.run_step's launches: the ds = 1 stage alone, the ds >= 2 stages' stage 1 in one
+        # call, stage 2 per DDplan stage
+        grp = {}
+        for p in plans:
+            grp.setdefault(p.pp.ds, []).append(p)
+        lone = [g for d, g in grp.items() if d < 2]
+        multi = [p for d, g in sorted(grp.items()) if d >= 2 for p in g]
+        for g in lone:
+            eng.run_subband_multi(g)
+            eng.run_dedisp_multi(g)
+        if multi:
+            eng.run_subband_multi(multi)
+            for d, g in sorted(grp.items()):
+                if d >= 2:
+                    eng.run_dedisp_multi(g)
+        sums_of.append(ts.pass_sums(sl, plans))
+    # the sums, after every beam's clip rows (message order per pair)
+    for (b, sl, eng, plans), sums in zip(work, sums_of):
+        dst = pt.pad_owner(b)
+        if dst != rank:
+            v = tensor(sums)
+            keep.append(v)
+            reqs.append(dist.isend(v, dst=dst))
+    for (b, sl, eng, plans), sums in zip(work, sums_of):
+        if sl != pt.nslices() - 1:
+            continue
+        total = np.array(sums, np.float64)
+        for k in range(sl):
+            src = pt.owner(b, k)
+            if src == rank:
+                continue
+            v = tensor(np.zeros(len(sums), np.float64))
+            dist.recv(v, src=src)
+            total = total + v.cpu().numpy()
+        ts.pad_passes(sl, plans, total)
+    for r in reqs:
+        r.wait()
+    for _, _, eng, _ in work:
+        eng.sync()
+    return sums_of

@@ -275,3 +275,162 @@ def test_time_slice_exchanges_gloo_world2():
         total += k
         assert sums == [3.0, 6.0]
     assert total == whole.nclipped
+
+
+# ---- configs[4]: the pointing schedule (beam x time partitioning) ---------------------------
+
+def test_pointing_schedule_shapes():
+    """7 beams on 8 ranks: 7 home ranks with the first f of their beam, one helper with every
+    tail; the cut balances the slice cost model; every (beam, slice) has exactly one owner;
+    on 7 or fewer ranks the ranks keep whole beams."""
+    obs = palfa_obs(N=1 << 22)
+    pt = S.Pointing(obs, P.ddplans_for("pdev"), 7, 8)
+    assert 0.5 < pt.frac < 1.0 and pt.nslices() == 2
+    owned = {}
+    for r in range(8):
+        for u in pt.units(r):
+            assert u not in owned
+            owned[u] = r
+    assert set(owned) == {(b, s) for b in range(7) for s in range(2)}
+    assert [pt.owner(b, 0) for b in range(7)] == list(range(7)) and {pt.pad_owner(b) for b in range(7)} == {7}
+    t0, own, nloc = pt.ts.slice(1)
+    assert t0 % pt.ts.unit == 0 and t0 + own == obs.N
+    assert pt.predicted_ms() < 67.9                           # below one beam per GPU with an idle GPU
+    pt7 = S.Pointing(obs, P.ddplans_for("pdev"), 7, 4)
+    assert [pt7.units(r) for r in range(4)] == [[(0, 0), (4, 0)], [(1, 0), (5, 0)], [(2, 0), (6, 0)], [(3, 0)]]
+    assert S.helper_fraction(7, 0, 6.0, 62.0) == 1.0
+
+
+class _FakePlan:
+    def __init__(self, eng, idx, ds, numout):
+        from hipdedisp import PassParams
+        self.eng, self.idx = eng, idx
+        self.pp = PassParams(subdm=1.0, lodm=0.0, dmstep=0.1, numdms=2, nsub=96, ds=ds)
+        self.numout = numout
+        self.filled = None
+
+    def series_fill(self, t0, v):
+        self.filled = (t0, v)
+
+
+class _FakeEngine:
+    """The pieces of Engine that sharding.pointing_step drives, with the oracle's clip_times
+    rows standing in for hd_clip_stats / hd_clip_set_stats (same table layout)."""
+
+    def __init__(self, obs, synth, beam, sl, ts, mask, pts, pad):
+        from hipdedisp import Opts
+        from hipdedisp.synth import host_spectra
+        self.obs, self.beam, self.sl, self.ts = obs, beam, sl, ts
+        self.opts = Opts()
+        self.t0, self.own, self.nloc = ts.slice(sl)
+        self.raw = host_spectra(obs, synth, self.t0, self.nloc)
+        self.mask, self.pts, self.pad = mask, pts, pad
+        self.result = None
+
+    def touch_raw(self):
+        pass
+
+    def clip_stats(self, n, table):
+        import oracle as OR
+        b0 = self.t0 // self.ts.blk
+        table[b0:b0 + n] = OR.clip_rows(self.obs, self.opts, self.raw, b0, n, mask=self.mask, ptsperint=self.pts)
+
+    def clip_set_stats(self, table):
+        import oracle as OR
+        self.result = OR.clip_finish(self.obs, self.opts, self.raw[:self.own], np.array(table), self.t0, self.own,
+                                     mask=self.mask, ptsperint=self.pts, padvals=self.pad)
+
+    def run_subband_multi(self, plans):
+        pass
+
+    def run_dedisp_multi(self, plans):
+        pass
+
+    def sync(self):
+        pass
+
+    def series_sums(self, plans, dm, t0s, counts):
+        # a stand-in per (beam, slice, pass) that the pad owner's sum must reassemble
+        return np.array([1000.0 * self.beam + 10.0 * self.sl + p.idx for p in plans], np.float64)
+
+
+def _pointing_worker(rank, world, nbeams, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        obs, _, pts, _, _ = _slice_beam()
+        pt = S.Pointing(obs, P.ddplans_for("pdev"), nbeams, world, frac=0.7)
+        work = []
+        for b, sl in pt.units(rank):
+            synth, mask, pad = _pointing_beam(obs, b, pts)
+            eng = _FakeEngine(obs, synth, b, sl, pt.ts, mask, pts, pad)
+            plans = [_FakePlan(eng, i, ds, obs.N // ds + 100) for i, ds in enumerate((1, 2, 2, 3))]
+            work.append((b, sl, eng, plans))
+        S.pointing_step(pt, rank, work, dist, torch, on_gpu=False)
+        out = []
+        for b, sl, eng, plans in work:
+            lpad, lclip, k = eng.result
+            nhb = -(-(eng.t0 + eng.nloc) // pt.ts.blk)           # blocks up to the held end
+            out.append((b, sl, eng.t0, eng.own, lpad[:nhb], lclip, k, [p.filled for p in plans]))
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def _pointing_beam(obs, beam, pts):
+    from hipdedisp.synth import palfa_synth, synth_mask
+    s = palfa_synth(beam=beam)
+    s.spike_frac, s.spike_amp = 0.003, 40.0
+    mask, pad = synth_mask(obs, s, pts, frac=0.03)
+    return s, mask, pad
+
+
+def test_pointing_exchanges_gloo_world3():
+    """Two beams on three gloo ranks (two home ranks, one helper taking both tails), with real
+    clip_times statistics: the one-way exchanges (own-block rows to later slices, first-DM
+    sums to the last slice) give every slice the pad values of every block it holds and the
+    clip flags of its own spectra exactly as clip_times over its whole beam, and the helper
+    pads each pass with the sum over the beam's slices."""
+    import torch.multiprocessing as mp
+    import oracle as OR
+    from hipdedisp import Opts
+    from hipdedisp.synth import host_spectra
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world, nbeams = 3, 2
+    procs = [ctx.Process(target=_pointing_worker, args=(r, world, nbeams, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    obs, _, pts, _, _ = _slice_beam()
+    units = {}
+    for rank, out in res:
+        for b, sl, t0, own, lpad, lclip, k, filled in out:
+            units[(b, sl)] = (rank, t0, own, lpad, lclip, k, filled)
+    assert set(units) == {(0, 0), (0, 1), (1, 0), (1, 1)}
+    assert units[(0, 1)][0] == units[(1, 1)][0] == 2
+    for b in range(nbeams):
+        synth, mask, pad = _pointing_beam(obs, b, pts)
+        whole = OR.prepare(obs, Opts(), host_spectra(obs, synth), mask=mask, ptsperint=pts, padvals=pad)
+        assert whole.nclipped > 100
+        total = 0
+        for sl in range(2):
+            rank, t0, own, lpad, lclip, k, filled = units[(b, sl)]
+            # the pads of every block the slice holds (the home slice never sees the tail's rows)
+            assert np.array_equal(lpad, whole.pad[:len(lpad)]), (b, sl)
+            assert np.array_equal(lclip, whole.clipped[t0:t0 + own]), (b, sl)
+            total += k
+        assert total == whole.nclipped
+        filled = units[(b, 1)][6]
+        for i, ds in enumerate((1, 2, 2, 3)):
+            want = (1000.0 * b + i) + (1000.0 * b + 10.0 + i)     # slice 0 + slice 1 sums
+            assert filled[i] is not None
+            assert filled[i][1] == float(np.float32(want / (obs.N // ds))), (b, i)
+        assert all(f is None for f in units[(b, 0)][6])           # only the last slice pads
