@@ -77,6 +77,9 @@ struct hd_ctx {
     // per read block (obs.nsblk spectra): check_mask rows, deduplicated (zidx -> zrows)
     int32_t blk = 1, nblk = 1;
     bool blocks_valid = false;
+    std::vector<int32_t> h_zidx;       // host copies of zidx / zrows (the fixup's boundary lists)
+    std::vector<uint8_t> h_zrows;
+    std::map<int, std::pair<int32_t*, int32_t*>> fixb;   // per fixup chunk width G: device {list, offsets}
     int32_t* d_zidx = nullptr;
     uint8_t* d_zrows = nullptr;
     uint8_t* d_allzap = nullptr;
@@ -412,6 +415,13 @@ extern "C" int hd_open(int device, hd_ctx** out)
 
 static void free_blocks(hd_ctx* c)
 {
+    for (auto& kv : c->fixb) {
+        dfree(kv.second.first);
+        dfree(kv.second.second);
+    }
+    c->fixb.clear();
+    c->h_zidx.clear();
+    c->h_zrows.clear();
     dfree(c->d_zidx); c->d_zidx = nullptr;
     dfree(c->d_zrows); c->d_zrows = nullptr;
     dfree(c->d_allzap); c->d_allzap = nullptr;
@@ -2063,6 +2073,53 @@ static hd::RawDesc raw_desc(const hd_ctx* c)
     return rd;
 }
 
+// k_stage1_fix8's boundary items, per chunk of G channels: the boundaries bb (read blocks bb-1
+// and bb) where some channel of the chunk is zapped in both blocks -- the only ones whose
+// outputs the fixup may change (it still checks that the two pads differ).  Built once per G
+// from the host copy of the block masks; with a mask the bench beam's ~2,047 boundaries x 96
+// chunks shrink to the chunks of its persistently masked channels.
+static void fix8_bounds(hd_ctx* c, hd::Stage1Multi& m)
+{
+    m.fix_blist = m.fix_bofs = nullptr;
+    m.fix_G = 0;
+    if (!m.rd.zidx || c->h_zidx.empty() || getenv("HD_FIX8_ALLB")) return;
+    const int G = hd::fix8_chunk_channels(m);
+    const int nchan = c->obs.nchan, nblk = (int)c->h_zidx.size();
+    if (G <= 0 || nchan % G) return;
+    auto it = c->fixb.find(G);
+    if (it == c->fixb.end()) {
+        const int nchunk = nchan / G;
+        std::vector<int32_t> ofs((size_t)nchunk + 1, 0), list;
+        for (int k = 0; k < nchunk; k++) {
+            ofs[k] = (int32_t)list.size();
+            for (int bb = 1; bb < nblk; bb++) {
+                const uint8_t* za = &c->h_zrows[(size_t)c->h_zidx[bb - 1] * nchan + (size_t)k * G];
+                const uint8_t* zb = &c->h_zrows[(size_t)c->h_zidx[bb] * nchan + (size_t)k * G];
+                for (int i = 0; i < G; i++)
+                    if (za[i] && zb[i]) {
+                        list.push_back(bb);
+                        break;
+                    }
+            }
+        }
+        ofs[nchunk] = (int32_t)list.size();
+        int32_t *dl = nullptr, *dofs = nullptr;
+        if (hipMalloc(&dl, sizeof(int32_t) * std::max<size_t>(list.size(), 1)) != hipSuccess ||
+            hipMalloc(&dofs, sizeof(int32_t) * ofs.size()) != hipSuccess ||
+            (list.size() && hipMemcpy(dl, list.data(), sizeof(int32_t) * list.size(), hipMemcpyHostToDevice) != hipSuccess) ||
+            hipMemcpy(dofs, ofs.data(), sizeof(int32_t) * ofs.size(), hipMemcpyHostToDevice) != hipSuccess) {
+            dfree(dl);
+            dfree(dofs);
+            (void)hipGetLastError();
+            return;                      // (every boundary is tried: correct, slower)
+        }
+        it = c->fixb.emplace(G, std::make_pair(dl, dofs)).first;
+    }
+    m.fix_blist = it->second.first;
+    m.fix_bofs = it->second.second;
+    m.fix_G = G;
+}
+
 // check_mask per read block [PRESTO-ext, mask.c]: block b spans [b*blk*dt, b*blk*dt +
 // blk*dt); its zapped channels are the union of the lists of the intervals holding its
 // start and end time (clamped to the last interval), or all channels when either is a
@@ -2114,6 +2171,8 @@ static int ensure_blocks(hd_ctx* c)
             for (int ch = 0; ch < nchan; ch++)
                 dst[ch] = all || c->h_mask[(size_t)lo * nchan + ch] || c->h_mask[(size_t)hi * nchan + ch];
         }
+        c->h_zidx = zidx;
+        c->h_zrows = rows;
         HIPCHK(c, hipMalloc(&c->d_zidx, sizeof(int32_t) * zidx.size()));
         HIPCHK(c, hipMemcpy(c->d_zidx, zidx.data(), sizeof(int32_t) * zidx.size(), hipMemcpyHostToDevice));
         HIPCHK(c, hipMalloc(&c->d_zrows, rows.size()));
@@ -2593,11 +2652,14 @@ static int run_subband_chunk(hd_ctx* c, hd_plan** plans, int n)
         // k_stage1_q8 did not redo them itself (probe bits 5/6 skip the boundary /
         // clipped-spectrum items: profiling only)
         if (m.qfix) {
-        } else if (clip && !(p0->probe & 64))
+        } else if (clip && !(p0->probe & 64)) {
+            fix8_bounds(c, m);
             HIPCHK(c, hd::launch_stage1_fixup(m, c->clip.events, c->clip.nevents,
                                               m.rd.zidx != nullptr && !(p0->probe & 32), c->stream));
-        else if (clip && !(p0->probe & 32) && m.rd.zidx)
+        } else if (clip && !(p0->probe & 32) && m.rd.zidx) {
+            fix8_bounds(c, m);
             HIPCHK(c, hd::launch_stage1_fixup(m, c->clip.events, c->clip.nzero, 1, c->stream));
+        }
     } else if (tiled) {
         m.rd = raw_desc(c);
         m.npass = n;
@@ -2810,12 +2872,15 @@ static int run_subband_fused(hd_ctx* c, hd_plan** plans, int n)
         fx.pass_ds = 1;
         fx.nds = c->obs.N / fx.ds;
         const bool env_off = getenv("HD_FIX8M") && atoi(getenv("HD_FIX8M")) == 0;
+        fix8_bounds(c, fx);
         const hipError_t e = env_off ? hipErrorNotSupported
                                      : hd::launch_stage1_fixup(fx, c->clip.events, c->clip.nevents, fx.rd.zidx != nullptr,
                                                                c->stream);
         if (e == hipErrorNotSupported) {
-            for (const auto& g : groups)
+            for (auto g : groups) {
+                fix8_bounds(c, g);
                 HIPCHK(c, hd::launch_stage1_fixup(g, c->clip.events, c->clip.nevents, g.rd.zidx != nullptr, c->stream));
+            }
         } else {
             HIPCHK(c, e);
         }

@@ -958,12 +958,16 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
     const int fprobe = boundaries >> 8;                   // HD_FIX8_PROBE (profiling): 1 no folds, 2 no window
     boundaries &= 1;
     const int nev = *nevents;
-    const int nbound = boundaries ? a.rd.nblk - 1 : 0;
-    const int nitems = nev + nbound;
-    const int N = (int)a.rd.N, nds = (int)a.nds, nchan = a.rd.nchan;
     // the grid is a multiple of nchunk: a workgroup keeps one chunk, so its delays of every
     // pass are staged once for all its items
     const int chunk = blockIdx.x % gm.nchunk;
+    // boundary items: the host's list of this chunk's boundaries with a channel zapped on both
+    // sides (the only ones whose outputs can change), else every boundary
+    const bool blist = boundaries && a.fix_blist && a.fix_G == G;
+    const int bofs0 = blist ? a.fix_bofs[chunk] : 0;
+    const int nbound = !boundaries ? 0 : blist ? a.fix_bofs[chunk + 1] - bofs0 : a.rd.nblk - 1;
+    const int nitems = nev + nbound;
+    const int N = (int)a.rd.N, nds = (int)a.nds, nchan = a.rd.nchan;
     const int c0 = chunk * G;
     for (int i = threadIdx.x; i < npass * G; i += blockDim.x) {
         const int p = i / G;
@@ -971,7 +975,7 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
     }
     for (int e = blockIdx.x / gm.nchunk; e < nitems; e += gridDim.x / gm.nchunk) {
         const bool clip_ev = e < nev;
-        const int r = clip_ev ? events[e] : (e - nev + 1) * a.rd.blk;
+        const int r = clip_ev ? events[e] : (blist ? a.fix_blist[bofs0 + e - nev] : e - nev + 1) * a.rd.blk;
         const int wlo = max(r - a.dmax - ds + 1, 0) & ~15;
         const int b0 = (int)blk_of(a.rd, wlo);
         const int b1 = min(b0 + 1, a.rd.nblk - 1);
@@ -1234,6 +1238,12 @@ static bool fix8_geom(const Stage1Multi& a, Fix8Geom& g)
         for (int p = 0; p < a.npass; p++) dsmin = std::min(dsmin, (int)a.pds[p]);
     g.jmax = (a.dmax + dsmin - 1) / dsmin + 1;
     return true;
+}
+
+int fix8_chunk_channels(const Stage1Multi& a)
+{
+    Fix8Geom g;
+    return !(a.probe & 128) && fix8_geom(a, g) ? g.G : 0;
 }
 
 hipError_t launch_stage1_fixup(const Stage1Multi& a, const int32_t* events, const int32_t* nevents, int boundaries,

@@ -74,7 +74,15 @@ struct Stage1Multi {
     // channel order, zero tail) or nullptr (row-major fill from rd.raw)
     const uint8_t* rawT;
     int64_t tstride;
+    // k_stage1_fix8 boundary items (host list): per chunk of fix_G channels, the read-block
+    // boundaries bb (blocks bb-1, bb) where a channel of the chunk is zapped in both blocks --
+    // fix_blist[fix_bofs[k] .. fix_bofs[k+1]); nullptr: every boundary is tried
+    const int32_t* fix_blist;
+    const int32_t* fix_bofs;
+    int32_t fix_G;
 };
+// channels per k_stage1_fix8 chunk for these arguments (0: that kernel does not apply)
+int fix8_chunk_channels(const Stage1Multi& a);
 
 struct Stage2Args {
     const void* sub;          // [nsub][sub_stride]
