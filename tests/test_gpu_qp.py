@@ -1,8 +1,8 @@
 """The quarter-layout pair kernel (k_stage2_qp, hd_plan_set_variant s2 = 9) through the bench's
 multi-pass launch (hd_run_dedisp_multi): for every Mock DDplan stage (PALFA2_presto_search.py:
 319-326), three passes of a ragged masked beam with more tiles than CUs share one launch; each
-series equals the two-pairs-per-chunk pair kernel's (variant 7) one-pass result bit for bit,
-and one pass per stage equals the oracle.  Stage 2 reference: PALFA2_presto_search.py:514-520.
+series equals the auto kernel's one-pass result (the pair kernel, or the ring where the pair
+kernel's LDS does not fit) bit for bit, and one pass per stage equals the oracle.  Stage 2 reference: PALFA2_presto_search.py:514-520.
 """
 import numpy as np
 import pytest
@@ -33,7 +33,7 @@ def test_qp_multipass_stage_matches_pair_and_oracle(engine, stage):
         engine.run_subband_multi(plans)
         ref = []
         for p in plans:
-            p.set_variant(7)
+            p.set_variant(0)                 # the auto one-pass kernel (pair, or the ring where its LDS does not fit)
             ref.append(p.run_dedisp())
         for p in plans:
             p.set_variant(9)
