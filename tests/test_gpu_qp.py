@@ -38,7 +38,8 @@ def test_qp_multipass_stage_matches_pair_and_oracle(engine, stage):
         for p in plans:
             p.set_variant(9)
         engine.run_dedisp_multi(plans)
-        assert [p.launch_passes() for p in plans] == [len(plans)] + [0] * (len(plans) - 1)
+        n = [p.launch_passes() for p in plans]      # shared launches (passes of unequal pairs-per-chunk split)
+        assert sum(n) == len(plans) and n[0] >= 1, n
         for p, r in zip(plans, ref):
             assert p.kernel().startswith("k_stage2_qp<"), p.kernel()
             assert np.array_equal(p.get_series(0, None, 0, p.numout), r)
