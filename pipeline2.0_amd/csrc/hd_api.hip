@@ -1668,14 +1668,12 @@ static bool qp_auto()
 // kernel's {base0, b1, U, k1[U]} and [9] E_k = the pair's entries per pattern (S + its own
 // DM sweep, a multiple of 4).  boff[yb][c][k] = LDS byte offset (from the expanded area) of
 // DM k's entry 0: buffer ((c / ppc) & 1) * ppc + c % ppc, pattern u(k), entry o2 = o0 - base0.
-static void qp_tables(hd_plan* p, bool i16, int ppc, hd_plan::Wide& w, std::vector<int32_t>& ptab,
-                      std::vector<int32_t>& boff)
+static void qp_tables(hd_plan* p, bool i16, hd_plan::Wide& w, std::vector<int32_t>& ptab, std::vector<int32_t>& boff)
 {
     w = hd_plan::Wide{};
     constexpr int NW = 16, RQ = 3, S = 64 * RQ, T = 4 * S;
     const int nsub = p->pass.nsub, numdms = p->pass.numdms;
-    // an even chunk count per tile keeps a pair's expanded-buffer parity fixed in every tile
-    if (!i16 || nsub % (4 * ppc) || numdms < 1) return;
+    if (!i16 || nsub % 2 || numdms < 1) return;
     int nyb = (numdms + 5 * NW - 1) / (5 * NW);
     const int per = (numdms + nyb - 1) / nyb;
     const int Q = (per + NW - 1) / NW > 4 ? 5 : 4;
@@ -1715,11 +1713,18 @@ static void qp_tables(hd_plan* p, bool i16, int ppc, hd_plan::Wide& w, std::vect
             umax = std::max(umax, (int)r.size());
         }
     // the expand reads staging elements up to 4 g + 3 S + k + 7 < E + 3 S + k1max + 8
+    // the most pairs per chunk (4, 3, 2 dividing the pair count) whose LDS fits; a shared launch
+    // takes the smallest of its passes' (the offset block per chunk is sized for 4 pairs)
     const int npw = (int)((((size_t)Emax + 3 * S + k1max + 8) * 2 + 1023) / 1024);
-    const int nbp = (int)(((size_t)ppc * dpb * 4 + 1023) / 1024);
-    if (2 * ppc * npw + nbp > 32 || hd::stage2_qp_lds_bytes(Emax, npw, nbp, nsub, umax, ppc) > 160 * 1024 ||
-        !hd::stage2_qp_supports(Q, RQ) || (size_t)npw * 512 > 4096)
-        return;
+    const int nbp = (int)(((size_t)4 * dpb * 4 + 1023) / 1024);
+    int ppc = 0;
+    for (int cand : {4, 3, 2})
+        if ((nsub / 2) % cand == 0 && 2 * cand * npw + nbp <= 32 &&
+            hd::stage2_qp_lds_bytes(Emax, npw, nbp, nsub, umax, cand) <= 160 * 1024) {
+            ppc = cand;
+            break;
+        }
+    if (!ppc || !hd::stage2_qp_supports(Q, RQ) || (size_t)npw * 512 > 4096) return;
     boff.assign((size_t)nyb * npair * dpb + 256, 0);   // the last DMA piece may over-read
     for (int yb = 0; yb < nyb; yb++)
         for (int c = 0; c < npair; c++) {
@@ -1729,8 +1734,7 @@ static void qp_tables(hd_plan* p, bool i16, int ppc, hd_plan::Wide& w, std::vect
                 const int dm = dmof(yb, k);
                 const int32_t o0 = p->off[(size_t)dm * nsub + 2 * c], o1 = p->off[(size_t)dm * nsub + 2 * c + 1];
                 const int u = (int)(std::lower_bound(r.begin(), r.end(), o1 - o0) - r.begin());
-                const int buf = ((c / ppc) & 1) * ppc + c % ppc;
-                boff[((size_t)yb * npair + c) * dpb + k] = (int32_t)((((int64_t)buf * umax + u) * Emax + (o0 - base0)) * 8);
+                boff[((size_t)yb * npair + c) * dpb + k] = (int32_t)(((int64_t)u * Emax + (o0 - base0)) * 8);
             }
         }
     (void)T;
@@ -1939,10 +1943,7 @@ extern "C" int hd_plan_create(hd_ctx* c, const hd_pass* ps, hd_plan** out)
     pair_tables(p, c->opts.sub_dtype == HD_SUB_I16, 1, p->wide[3], womin[3], wboff[3]);
     pair_tables(p, c->opts.sub_dtype == HD_SUB_I16, 2, p->wide[4], womin[4], wboff[4]);
     rw_tables(p, c->opts.sub_dtype == HD_SUB_I16, p->wide[5], womin[5], wboff[5]);
-    for (int ppc : {4, 3, 2}) {        // the most pairs per chunk whose LDS fits
-        qp_tables(p, c->opts.sub_dtype == HD_SUB_I16, ppc, p->wide[6], womin[6], wboff[6]);
-        if (p->wide[6].ok) break;
-    }
+    qp_tables(p, c->opts.sub_dtype == HD_SUB_I16, p->wide[6], womin[6], wboff[6]);
 
     int rc = HD_OK;
     hipError_t e = hipSetDevice(c->device);
@@ -3866,7 +3867,8 @@ static bool dedisp_same_group(const hd_plan* a, const hd_plan* b)
     const int ka = dedisp_multi_kernel(a);
     if (ka != dedisp_multi_kernel(b)) return false;
     const hd_plan::Wide &x = a->wide[ka], &y = b->wide[ka];
-    return a->ctx == b->ctx && x.q == y.q && x.r == y.r && x.dpb == y.dpb && x.sc == y.sc && a->pass.numdms == b->pass.numdms &&
+    return a->ctx == b->ctx && x.q == y.q && x.r == y.r && x.dpb == y.dpb && (ka == 6 || x.sc == y.sc) &&
+           a->pass.numdms == b->pass.numdms &&
            a->pass.nsub == b->pass.nsub && a->nds == b->nds && a->nvalid == b->nvalid && a->numout == b->numout &&
            a->out_stride == b->out_stride && a->sub_nonneg == b->sub_nonneg && a->probe == b->probe;
 }
@@ -3948,6 +3950,8 @@ static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
     a.nwg = c->ncu;
     hd::S2Multi m{};
     m.npass = n;
+    int ppc6 = 4;                       // k_stage2_qp: the smallest pairs-per-chunk of the passes
+    for (int i = 0; i < n; i++) ppc6 = std::min(ppc6, (int)g[i]->wide[wk].sc);
     for (int i = 0; i < n; i++) {
         const hd_plan* p = g[i];
         const hd_plan::Wide& w = p->wide[wk];
@@ -3966,7 +3970,7 @@ static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
     }
     HIPCHK(c, hipEventRecord(p0->ev[2], st));
     if (wk == 5) HIPCHK(c, hd::launch_stage2_rw_multi(a, m, w0.q, st));
-    else if (wk == 6) HIPCHK(c, hd::launch_stage2_qp_multi(a, m, w0.q, w0.r, w0.sc, st));
+    else if (wk == 6) HIPCHK(c, hd::launch_stage2_qp_multi(a, m, w0.q, w0.r, ppc6, st));
     else HIPCHK(c, hd::launch_stage2_pair_multi(a, m, w0.q, w0.r, 2, st));
     if (pad)
         for (int i = 0; i < n; i++)
@@ -3980,7 +3984,7 @@ static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
         p->dd_stream = st;
         p->s2passes = i == 0 ? n : 0;
         if (wk == 5) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_rw<%d>", w0.q);
-        else if (wk == 6) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_qp<%d, %d, %d, %s, %s>", w0.q, w0.r, w0.sc,
+        else if (wk == 6) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_qp<%d, %d, %d, %s, %s>", w0.q, w0.r, ppc6,
                                    a.nonneg && !(a.probe & 64) ? "true" : "false", (a.probe & 15) ? "true" : "false");
         else snprintf(p->s2name, sizeof(p->s2name), "k_stage2_pair<%d, %d, 2, %s, %s>", w0.q, w0.r,
                       a.nonneg && !(a.probe & 64) ? "true" : "false", (a.probe & 15) ? "true" : "false");
