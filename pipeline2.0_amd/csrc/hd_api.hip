@@ -1653,12 +1653,15 @@ static void pair_tables(hd_plan* p, bool i16, int ppc, hd_plan::Wide& w, std::ve
     w.umax = umax;
 }
 
-// The quarter-layout pair kernel as the auto stage-2 choice (HD_S2_QP=0/1 overrides for A/B).
+// The quarter-layout pair kernel as the auto stage-2 choice (HD_S2_QP=0 keeps the four-copy
+// pair kernel, for A/B): measured in the bench context 62.4 vs 67.1 ms per C2 beam, stage 2
+// 32.9 vs 37.5 ms (k_stage2_qp<5,3,4> 5.55 vs k_stage2_pair<5,3,2> 6.35 ms per stage-0 launch;
+// scripts/r5_ab.sh, profiles/r05_ab_qp.txt).
 static bool qp_auto()
 {
     static const int v = [] {
         const char* e = getenv("HD_S2_QP");
-        return e ? atoi(e) : 0;
+        return e ? atoi(e) : 1;
     }();
     return v != 0;
 }

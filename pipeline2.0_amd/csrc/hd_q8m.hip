@@ -19,7 +19,17 @@ namespace hd {
 
 constexpr int kQ8mS = 960;                    // raw rows per quarter of the tile
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(3))) u32x2 lds_u32x2;     // (volatile LDS loads keep their address space)
+typedef __attribute__((address_space(3))) u32x2 lds_u32x2;
+
+// an aligned ds_read_b64 of the 8 bytes at p (an LDS address, 8-byte aligned): the address
+// passes through an empty asm, so two such loads never share a base register and the
+// compiler cannot merge them into one ds_read2_b64 (8 cycles for what two ds_read_b64 do in 4)
+__device__ __forceinline__ u32x2 lds_b64(const uint32_t* p)
+{
+    const lds_u32x2* q = (const lds_u32x2*)__builtin_assume_aligned(p, 8);
+    asm volatile("" : "+v"(q));
+    return *q;
+}
 #ifndef Q8M_UNROLL
 #define Q8M_UNROLL 4
 #endif
@@ -73,9 +83,7 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
         const int br1 = brow, br2 = brow2;
         auto kof = [=](int row) { return k0c + (row >= br1 ? k1c - k0c : 0u) + (row >= br2 ? k2c - k1c : 0u); };
         int mx = 0;
-        // (even DS: its two read paths per channel need the registers of a wider unroll)
-        constexpr int UNR = DS % 2 == 0 ? 1 : Q8M_UNROLL;
-#pragma unroll UNR
+#pragma unroll Q8M_UNROLL
         for (int m = 0; m < M; m++) {
             const bool act = (m + 1) * 64 <= JQ || lane + 64 * m < JQ;
             uint32_t ae, ao;
@@ -100,22 +108,21 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
                 if constexpr (DS % 2 == 0) {
                     // even DS: lanes DS dwords apart, so ds_read2_b32 runs 2-way bank-conflicted;
                     // the rows' dword parity is the channel delay's (lbase, lrb, mo are even),
-                    // uniform per wave: aligned ds_read_b64 (conflict-free at any even stride;
-                    // volatile so they are not merged into ds_read2_b64, half the rate on gfx950)
+                    // uniform per wave: aligned ds_read_b64 (conflict-free at any even stride; each
+                    // from its own base register so they are not merged into ds_read2_b64, half
+                    // the rate on gfx950)
                     if (((lrb[cc] + dl[cc]) & 1) == 0) {
-                        const volatile lds_u32x2* b2 = (const volatile lds_u32x2*)__builtin_assume_aligned(b, 8);
 #pragma unroll
                         for (int j = 0; j < DS / 2; j++) {
-                            const u32x2 v = b2[j];
+                            const u32x2 v = lds_b64(b + 2 * j);
                             add1(v.x);
                             add1(v.y);
                         }
                     } else {
                         add1(b[0]);
-                        const volatile lds_u32x2* b2 = (const volatile lds_u32x2*)__builtin_assume_aligned(b + 1, 8);
 #pragma unroll
                         for (int j = 0; j < DS / 2 - 1; j++) {
-                            const u32x2 v = b2[j];
+                            const u32x2 v = lds_b64(b + 1 + 2 * j);
                             add1(v.x);
                             add1(v.y);
                         }
