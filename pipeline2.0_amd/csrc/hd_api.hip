@@ -234,6 +234,7 @@ struct hd_plan {
         int32_t umax = 0;               // [3] only: largest pattern count of a subband pair
         int32_t* d_omin = nullptr;      // [3]: the pair table (kPairTab ints per y-block and pair)
         int32_t* d_boff = nullptr;
+        int32_t* d_boffp[3] = {nullptr, nullptr, nullptr};   // [6]: the offsets for 4, 3, 2 pairs per chunk
     } wide[7];                      // [2]: k_stage2_ring (16 waves, LDS-DMA staging ring);
                                     // [3]: k_stage2_pair (the ring over subband-pair partials),
                                     // [4]: the same with two pairs per chunk (half the chunks),
@@ -1391,6 +1392,7 @@ static void plan_free(hd_plan* p)
     for (auto& w : p->wide) {
         dfree(w.d_omin);
         dfree(w.d_boff);
+        for (auto& q : w.d_boffp) dfree(q);
     }
     dfree(p->d_out);
     dfree(p->d_sub);
@@ -1671,7 +1673,8 @@ static bool qp_auto()
 // kernel's {base0, b1, U, k1[U]} and [9] E_k = the pair's entries per pattern (S + its own
 // DM sweep, a multiple of 4).  boff[yb][c][k] = LDS byte offset (from the expanded area) of
 // DM k's entry 0: buffer ((c / ppc) & 1) * ppc + c % ppc, pattern u(k), entry o2 = o0 - base0.
-static void qp_tables(hd_plan* p, bool i16, hd_plan::Wide& w, std::vector<int32_t>& ptab, std::vector<int32_t>& boff)
+static void qp_tables(hd_plan* p, bool i16, hd_plan::Wide& w, std::vector<int32_t>& ptab, std::vector<int32_t>& boff,
+                      std::vector<int32_t> (&boffp)[3])
 {
     w = hd_plan::Wide{};
     constexpr int NW = 16, RQ = 3, S = 64 * RQ, T = 4 * S;
@@ -1728,18 +1731,28 @@ static void qp_tables(hd_plan* p, bool i16, hd_plan::Wide& w, std::vector<int32_
             break;
         }
     if (!ppc || !hd::stage2_qp_supports(Q, RQ) || (size_t)npw * 512 > 4096) return;
-    boff.assign((size_t)nyb * npair * dpb + 256, 0);   // the last DMA piece may over-read
-    for (int yb = 0; yb < nyb; yb++)
-        for (int c = 0; c < npair; c++) {
-            const std::vector<int32_t>& r = rs[(size_t)yb * npair + c];
-            const int32_t base0 = ptab[((size_t)yb * npair + c) * hd::kPairTab];
-            for (int k = 0; k < dpb; k++) {
-                const int dm = dmof(yb, k);
-                const int32_t o0 = p->off[(size_t)dm * nsub + 2 * c], o1 = p->off[(size_t)dm * nsub + 2 * c + 1];
-                const int u = (int)(std::lower_bound(r.begin(), r.end(), o1 - o0) - r.begin());
-                boff[((size_t)yb * npair + c) * dpb + k] = (int32_t)(((int64_t)u * Emax + (o0 - base0)) * 8);
+    // one offsets table per pairs-per-chunk a shared launch may take (ppc and every smaller
+    // candidate dividing the pair count): buffer ((c / q) & 1) * q + c % q of pair c
+    for (int qi = 0; qi < 3; qi++) {
+        const int q = 4 - qi;
+        std::vector<int32_t>& bo = boffp[qi];
+        bo.clear();
+        if (q > ppc || (nsub / 2) % q) continue;
+        bo.assign((size_t)nyb * npair * dpb + 256, 0);   // the last DMA piece may over-read
+        for (int yb = 0; yb < nyb; yb++)
+            for (int c = 0; c < npair; c++) {
+                const std::vector<int32_t>& r = rs[(size_t)yb * npair + c];
+                const int32_t base0 = ptab[((size_t)yb * npair + c) * hd::kPairTab];
+                const int buf = ((c / q) & 1) * q + c % q;
+                for (int k = 0; k < dpb; k++) {
+                    const int dm = dmof(yb, k);
+                    const int32_t o0 = p->off[(size_t)dm * nsub + 2 * c], o1 = p->off[(size_t)dm * nsub + 2 * c + 1];
+                    const int u = (int)(std::lower_bound(r.begin(), r.end(), o1 - o0) - r.begin());
+                    bo[((size_t)yb * npair + c) * dpb + k] = (int32_t)((((int64_t)buf * umax + u) * Emax + (o0 - base0)) * 8);
+                }
             }
-        }
+    }
+    boff = boffp[4 - ppc];
     (void)T;
     w.ok = true;
     w.q = Q;
@@ -1946,7 +1959,8 @@ extern "C" int hd_plan_create(hd_ctx* c, const hd_pass* ps, hd_plan** out)
     pair_tables(p, c->opts.sub_dtype == HD_SUB_I16, 1, p->wide[3], womin[3], wboff[3]);
     pair_tables(p, c->opts.sub_dtype == HD_SUB_I16, 2, p->wide[4], womin[4], wboff[4]);
     rw_tables(p, c->opts.sub_dtype == HD_SUB_I16, p->wide[5], womin[5], wboff[5]);
-    qp_tables(p, c->opts.sub_dtype == HD_SUB_I16, p->wide[6], womin[6], wboff[6]);
+    std::vector<int32_t> qpb[3];
+    qp_tables(p, c->opts.sub_dtype == HD_SUB_I16, p->wide[6], womin[6], wboff[6], qpb);
 
     int rc = HD_OK;
     hipError_t e = hipSetDevice(c->device);
@@ -1957,6 +1971,12 @@ extern "C" int hd_plan_create(hd_ctx* c, const hd_pass* ps, hd_plan** out)
         if (e == hipSuccess) e = hipMemcpy(w.d_omin, womin[k].data(), sizeof(int32_t) * womin[k].size(), hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMalloc(&w.d_boff, sizeof(int32_t) * wboff[k].size());
         if (e == hipSuccess) e = hipMemcpy(w.d_boff, wboff[k].data(), sizeof(int32_t) * wboff[k].size(), hipMemcpyHostToDevice);
+    }
+    for (int qi = 0; qi < 3 && e == hipSuccess && p->wide[6].ok; qi++) {
+        if (qpb[qi].empty()) continue;
+        e = hipMalloc(&p->wide[6].d_boffp[qi], sizeof(int32_t) * qpb[qi].size());
+        if (e == hipSuccess)
+            e = hipMemcpy(p->wide[6].d_boffp[qi], qpb[qi].data(), sizeof(int32_t) * qpb[qi].size(), hipMemcpyHostToDevice);
     }
     if (e == hipSuccess) e = hipMalloc(&p->d_idispdt, sizeof(int32_t) * nchan);
     if (e == hipSuccess) e = hipMemcpy(p->d_idispdt, p->idispdt.data(), sizeof(int32_t) * nchan, hipMemcpyHostToDevice);
@@ -2308,9 +2328,13 @@ extern "C" int hd_clip_stats(hd_ctx* c, int64_t nown, double* stats)
     }
     const size_t w = (size_t)c->obs.nchan + 3;
     HIPCHK(c, hd::launch_clip_pack(a, c->clip.xbuf, (int)nown, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));     // then a blocking copy (stats may be pageable host memory)
-    HIPCHK(c, hipMemcpy(stats + (size_t)(c->slice_t0 / c->blk) * w, c->clip.xbuf, (size_t)nown * w * 8,
-                        hipMemcpyDefault));
+    // on the context stream, then a wait: a device-to-device hipMemcpy on the null stream may
+    // return before it lands and is not ordered with this non-blocking stream -- with a device
+    // table (hd_slice_exchange_clip) the all-reduce and hd_clip_set_stats's copy then raced it
+    // and read partly unwritten rows (bench --comm hd: mass clipping, 4 s per beam)
+    HIPCHK(c, hipMemcpyAsync(stats + (size_t)(c->slice_t0 / c->blk) * w, c->clip.xbuf, (size_t)nown * w * 8,
+                             hipMemcpyDefault, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     return HD_OK;
 }
 
@@ -3961,7 +3985,7 @@ static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
         hd::S2Pass& q = m.p[i];
         q.sub = p->d_sub;
         q.ptab = w.d_omin;
-        q.off = w.d_boff;
+        q.off = wk == 6 ? w.d_boffp[4 - ppc6] : w.d_boff;
         q.maxabs = p->d_maxabs;
         q.out = p->d_out;
         q.partial = partial ? partial + per * i : nullptr;

@@ -18,18 +18,6 @@
 namespace hd {
 
 constexpr int kQ8mS = 960;                    // raw rows per quarter of the tile
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(3))) u32x2 lds_u32x2;
-
-// an aligned ds_read_b64 of the 8 bytes at p (an LDS address, 8-byte aligned): the address
-// passes through an empty asm, so two such loads never share a base register and the
-// compiler cannot merge them into one ds_read2_b64 (8 cycles for what two ds_read_b64 do in 4)
-__device__ __forceinline__ u32x2 lds_b64(const uint32_t* p)
-{
-    const lds_u32x2* q = (const lds_u32x2*)__builtin_assume_aligned(p, 8);
-    asm volatile("" : "+v"(q));
-    return *q;
-}
 #ifndef Q8M_UNROLL
 #define Q8M_UNROLL 4
 #endif
@@ -100,37 +88,11 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
             for (int cc = 0; cc < CPS; cc++) {
                 const uint32_t keep = ((zall >> cc) & 1u) ? 0u : 0xFFFFFFFFu;
                 const uint32_t* b = lbase + lrb[cc] + dl[cc] + mo;
-                auto add1 = [&](uint32_t x) {
-                    x &= keep;
+#pragma unroll
+                for (int k = 0; k < DS; k++) {
+                    const uint32_t x = b[k] & keep;
                     ae += x & 0x00FF00FFu;
                     ao += __builtin_amdgcn_perm(0u, x, 0x0c030c01u);
-                };
-                if constexpr (DS % 2 == 0) {
-                    // even DS: lanes DS dwords apart, so ds_read2_b32 runs 2-way bank-conflicted;
-                    // the rows' dword parity is the channel delay's (lbase, lrb, mo are even),
-                    // uniform per wave: aligned ds_read_b64 (conflict-free at any even stride; each
-                    // from its own base register so they are not merged into ds_read2_b64, half
-                    // the rate on gfx950)
-                    if (((lrb[cc] + dl[cc]) & 1) == 0) {
-#pragma unroll
-                        for (int j = 0; j < DS / 2; j++) {
-                            const u32x2 v = lds_b64(b + 2 * j);
-                            add1(v.x);
-                            add1(v.y);
-                        }
-                    } else {
-                        add1(b[0]);
-#pragma unroll
-                        for (int j = 0; j < DS / 2 - 1; j++) {
-                            const u32x2 v = lds_b64(b + 1 + 2 * j);
-                            add1(v.x);
-                            add1(v.y);
-                        }
-                        add1(b[DS - 1]);
-                    }
-                } else {
-#pragma unroll
-                    for (int k = 0; k < DS; k++) add1(b[k]);
                 }
             }
             if (!act) continue;

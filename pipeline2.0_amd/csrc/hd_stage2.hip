@@ -1993,8 +1993,9 @@ hipError_t launch_stage2_wide(const Stage2Args& a, int q, int r, int nw, hipStre
 // Output lane l, read m, quarter j is sample t0 + j S + 64 m + l: dword stores, 256 bytes
 // contiguous per wave-instruction.
 // Table per (y-block, pair): [0] base0, [1] b1, [2] U, [3..3+U) k1[u], [9] E_k (entries,
-// multiple of 4).  Offsets block per chunk: int32 LDS byte offsets within the pair's buffer,
-// [pair k][DM slot] = (u * E + o2) * 8; the kernel adds the buffer ((chunk & 1) * PPC + k).
+// multiple of 4).  Offsets block per chunk: int32 LDS byte offsets from the expanded area,
+// [pair k][DM slot] = ((buf * umax + u) * E + o2) * 8, buf = (chunk & 1) * PPC + k (the host
+// keeps one such table per pairs-per-chunk a launch may take).
 
 // 4 int16 elements x .. x+3 of a staging window (any x) as 2 packed pairs: two aligned
 // ds_read_b64 cover dwords (x>>1 & ~1) .. +3, a select picks the 3 that hold them.
@@ -2247,11 +2248,7 @@ __global__ __launch_bounds__(1024) void k_stage2_qp(Stage2Args a, S2Multi m)
         if (c + 1 < ntot && !(PRB && (a.probe & 8))) expand(c + 1, chn);
         const int32_t* sboff = (const int32_t*)(lds_raw + ring0 + (c % NS) * slot_bytes + 2 * PPC * npw * 1024);
         // this chunk's (pair, DM) byte offsets in ONE register: lane k * Q + q holds pair k, DM q
-        // (the table holds the offset within the pair's buffer; its buffer base is added here, so
-        // the tables do not depend on the pairs per chunk)
-        const int voff = lane < PPC * Q ? sboff[(lane / Q) * dpb + wave * Q + lane % Q] +
-                                              (((c & 1) * PPC + lane / Q) * umax * E) * 8
-                                        : 0;
+        const int voff = lane < PPC * Q ? sboff[(lane / Q) * dpb + wave * Q + lane % Q] : 0;
         if (!(PRB && (a.probe & 1))) {
             constexpr int nsteps = PPC * Q, LA0 = ring_la<Q, RQ>() < Q - 1 ? ring_la<Q, RQ>() : Q - 1, LA = LA0;
             uint64_t bb[LA + 1][RQ];

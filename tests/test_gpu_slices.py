@@ -179,14 +179,16 @@ def test_clip_stats_device_pointer_path(engine):
         hip.hipFree(dtab)
 
 
-def test_in_library_comm_world1(engine):
+@pytest.mark.parametrize("N", [(1 << 17) + 777, 1 << 22])
+def test_in_library_comm_world1(engine, N):
     """hd_comm_* (RCCL loaded by the library, no torch.distributed) at world size 1 -- the
     collective path a C caller of a time-sliced beam takes: the all-reduce of host and device
     doubles returns them unchanged, and hd_slice_exchange_clip on a one-slice context leaves
-    the same clip_times state as the whole-beam context; misuse is refused."""
-    import ctypes
+    the same clip_times state as the whole-beam context; misuse is refused.  At the full C2
+    size the device table's copies are large enough that an unordered copy (round 4: a
+    null-stream device-to-device hipMemcpy) shows as wrong clip state."""
     from hipdedisp.engine import PrestoError
-    obs = palfa_obs(N=(1 << 17) + 777, nbits=8, nsblk=2048)
+    obs = palfa_obs(N=N, nbits=8, nsblk=2048)
     synth = spiky()
     engine.set_obs(obs, Opts())
     engine.synth_device(synth)
