@@ -915,6 +915,52 @@ __device__ __forceinline__ float fix8_fold(const Stage1Multi& a, const uint8_t* 
 
 // DS > 0: compile-time ds; 0: a.ds; -1: per pass (a.pds[p], the fused k_stage1_q8m launch's
 // passes of several DDplan stages: one window per item, of the widest stage)
+// k_stage1_fix8's window of an item: the chunk's channels' raw bytes (16-byte runs of the
+// channel-major copy) and the rows' replaced flags (clipped, or past N)
+__device__ __forceinline__ void fix8_window(const Stage1Multi& a, uint8_t* lraw, uint8_t* flg, int G, int Wp, int c0,
+                                            int wlo, int N, int nchan, int fprobe, int& anyflag)
+{
+    if (fprobe & 2) return;
+    const int nq = Wp >> 4;
+    for (int i = threadIdx.x; i < G * nq; i += blockDim.x) {
+        const int lc = i / nq, q = i - lc * nq;
+        const int c = c0 + lc;
+        const int rc = a.rd.flip ? nchan - 1 - c : c;
+        const uint4 v = *(const uint4*)(a.rawT + (int64_t)rc * a.tstride + wlo + 16 * q);
+        *(uint4*)(lraw + lc * Wp + 16 * q) = v;
+    }
+    int fl = 0;
+    for (int i = threadIdx.x; i < Wp; i += blockDim.x) {
+        const int t = wlo + i;
+        flg[i] = t >= N ? 1 : (a.rd.clipped ? a.rd.clipped[t] : 0);
+        fl |= flg[i];
+    }
+    if (__ballot(fl != 0) && (threadIdx.x & 63) == 0) anyflag = 1;
+}
+
+// Task i = (pass p, chunk channel lc) of a clipped spectrum r: its output j, unless an earlier
+// channel of the subband maps r to the same output.  Delays fall with frequency within a
+// subband, so the outputs its channels map r to rise with the channel and equal ones are
+// adjacent: only channel lc - 1 can name j first.
+__device__ __forceinline__ bool fix8_task(const int16_t* dly, int i, int G, int cps, int DST, int SG, int r, int N,
+                                          int nds, int DSt, const int* pds_s, int ds, int& j)
+{
+    const int p = i / G, lc = i - p * G;
+    const int lc0 = lc - lc % cps;
+    const int16_t* dl = dly + (p * SG + lc0 / cps) * DST - lc0;          // dl[lc0 .. lc0 + cps)
+    const int dsp = DSt > 0 ? DSt : DSt == 0 ? ds : pds_s[p];
+    const int ndsp = DSt < 0 ? N / dsp : nds;
+    const int jn = r - dl[lc];
+    if (jn < 0) return false;
+    j = jn / dsp;
+    if (j >= ndsp) return false;
+    if (lc > lc0) {
+        const int jn2 = r - dl[lc - 1];
+        if (jn2 >= 0 && jn2 / dsp == j) return false;
+    }
+    return true;
+}
+
 template <int CPS, int DS>
 __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm, const int32_t* __restrict__ events,
                                                     const int32_t* __restrict__ nevents, int boundaries)
@@ -940,7 +986,8 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
     int* pre_s = cnt_s + npass * SG;                       // [npass * SG + 1] exclusive prefix of cnt_s
     uint16_t* tlist = (uint16_t*)(pre_s + npass * SG + 1);   // [npass * G] clipped-spectrum tasks to fold
     __shared__ int amax_s[kMaxPass];
-    __shared__ int needany, anyflag, ntask_s;
+    __shared__ int needany, anyflag;
+    __shared__ int ntask2[2];                             // clipped-spectrum task counts, by item parity
     __shared__ int wsum_s[8];
     __shared__ uint32_t zbm_s[CPS > 0 ? 1024 / (CPS > 0 ? CPS : 1) : 1];   // per subband: zap bits of both blocks
     // per-pass output rows staged once: indexing the kernel argument arrays with a per-lane
@@ -973,25 +1020,62 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
         const int p = i / G;
         dly[dix(p, i - p * G)] = (int16_t)a.dly[p][c0 + i - p * G];
     }
-    for (int e = blockIdx.x / gm.nchunk; e < nitems; e += gridDim.x / gm.nchunk) {
+    // the largest |subband| of every pass over all this workgroup's items, published once
+    if (threadIdx.x < kMaxPass) amax_s[threadIdx.x] = 0;
+    if (threadIdx.x < 2) ntask2[threadIdx.x] = 0;
+    int it = 0;
+    for (int e = blockIdx.x / gm.nchunk; e < nitems; e += gridDim.x / gm.nchunk, it++) {
         const bool clip_ev = e < nev;
+        const int par = it & 1;
         const int r = clip_ev ? events[e] : (blist ? a.fix_blist[bofs0 + e - nev] : e - nev + 1) * a.rd.blk;
         const int wlo = max(r - a.dmax - ds + 1, 0) & ~15;
         const int b0 = (int)blk_of(a.rd, wlo);
         const int b1 = min(b0 + 1, a.rd.nblk - 1);
         const int bndrel = (b0 + 1) * a.rd.blk - wlo;
         __syncthreads();                                  // the previous item is done with LDS
-        if (threadIdx.x < kMaxPass) amax_s[threadIdx.x] = 0;
         if (threadIdx.x == 0) {
             needany = clip_ev;
             anyflag = 0;
-            ntask_s = 0;
+            ntask2[par ^ 1] = 0;                          // the next item's count (this one's was cleared before)
         }
         for (int i = threadIdx.x; i < G; i += blockDim.x) {
             zap[i] = zap_at(a.rd, b0, c0 + i);
             zap[G + i] = zap_at(a.rd, b1, c0 + i);
             pad[i] = pad_at(a.rd, b0, c0 + i);
             pad[G + i] = pad_at(a.rd, b1, c0 + i);
+        }
+        // a clipped spectrum needs every phase: its window, flags, zap bits and task list are all
+        // issued in this one phase (no barrier or global round trip between them)
+        if (clip_ev) {
+            fix8_window(a, lraw, flg, G, Wp, c0, wlo, N, nchan, fprobe, anyflag);
+            if constexpr (CPS > 0) {
+                for (int i = threadIdx.x; i < SG; i += blockDim.x) {
+                    uint32_t zb = 0;                      // bit cc: zapped in block slot 0; 16 + cc: slot 1
+#pragma unroll
+                    for (int cc = 0; cc < CPS; cc++)
+                        zb |= ((uint32_t)zap_at(a.rd, b0, c0 + i * CPS + cc) << cc) |
+                              ((uint32_t)zap_at(a.rd, b1, c0 + i * CPS + cc) << (16 + cc));
+                    zbm_s[i] = zb;
+                }
+            }
+            if (!(fprobe & 1)) {
+                // task (p, lc): the output channel lc maps r to, unless an earlier channel of its
+                // subband maps r to the same output.  The tasks that fold are listed first (one
+                // LDS atomic per wave), so the folds run on dense lanes (~1 task in 6 folds)
+                for (int i0 = 0; i0 < npass * G; i0 += blockDim.x) {
+                    const int i = i0 + threadIdx.x;
+                    int j = 0;
+                    const bool keep = i < npass * G && fix8_task(dly, i, G, cps, DST, SG, r, N, nds, DS, pds_s, ds, j);
+                    const uint64_t m = __ballot(keep);
+                    if (m) {
+                        const int ln = threadIdx.x & 63;
+                        int base = 0;
+                        if (ln == 0) base = atomicAdd(&ntask2[par], __popcll(m));
+                        base = __shfl(base, 0, 64);
+                        if (keep) tlist[base + __popcll(m & ((1ull << ln) - 1ull))] = (uint16_t)i;
+                    }
+                }
+            }
         }
         __syncthreads();
         if (!clip_ev) {
@@ -1019,76 +1103,27 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
             __syncthreads();
             if (!needany) continue;                       // uniform
         }
-        // the window: raw bytes of the chunk's channels (16-byte runs), replaced-row flags
-        if (!(fprobe & 2)) {
-            const int nq = Wp >> 4;
-            for (int i = threadIdx.x; i < G * nq; i += blockDim.x) {
-                const int lc = i / nq, q = i - lc * nq;
-                const int c = c0 + lc;
-                const int rc = a.rd.flip ? nchan - 1 - c : c;
-                const uint4 v = *(const uint4*)(a.rawT + (int64_t)rc * a.tstride + wlo + 16 * q);
-                *(uint4*)(lraw + lc * Wp + 16 * q) = v;
-            }
-            int fl = 0;
-            for (int i = threadIdx.x; i < Wp; i += blockDim.x) {
-                const int t = wlo + i;
-                flg[i] = t >= N ? 1 : (a.rd.clipped ? a.rd.clipped[t] : 0);
-                fl |= flg[i];
-            }
-            if (__ballot(fl != 0) && (threadIdx.x & 63) == 0) anyflag = 1;
-        }
-        if constexpr (CPS > 0) {
-            for (int i = threadIdx.x; i < SG; i += blockDim.x) {
-                uint32_t zb = 0;                          // bit cc: zapped in block slot 0; 16 + cc: slot 1
+        if (!clip_ev) {
+            // a boundary that needs outputs redone: the window, flags and zap bits now
+            fix8_window(a, lraw, flg, G, Wp, c0, wlo, N, nchan, fprobe, anyflag);
+            if constexpr (CPS > 0) {
+                for (int i = threadIdx.x; i < SG; i += blockDim.x) {
+                    uint32_t zb = 0;                      // bit cc: zapped in block slot 0; 16 + cc: slot 1
 #pragma unroll
-                for (int cc = 0; cc < CPS; cc++)
-                    zb |= ((uint32_t)zap[i * CPS + cc] << cc) | ((uint32_t)zap[G + i * CPS + cc] << (16 + cc));
-                zbm_s[i] = zb;
-            }
-        }
-        __syncthreads();
-        if (fprobe & 1) {
-        } else if (clip_ev) {
-            // task (p, lc): the output channel lc maps r to, unless an earlier channel of its
-            // subband maps r to the same output.  The tasks that fold are listed first (one LDS
-            // atomic per wave), so the folds run on dense lanes (~1 task in 6 folds)
-            auto task = [&](int i, int& j) -> bool {             // (p, lc) = task i; j: its output
-                const int p = i / G, lc = i - p * G;
-                const int lc0 = lc - lc % cps;
-                const int16_t* dl = dly + dix(p, lc0) - lc0;          // dl[lc0 .. lc0 + cps)
-                const int dsp = pds(p), ndsp = DS < 0 ? N / dsp : nds;
-                const int jn = r - dl[lc];
-                if (jn < 0) return false;
-                j = jn / dsp;
-                if (j >= ndsp) return false;
-                // delays fall with frequency within a subband, so the outputs its channels map r
-                // to rise with the channel and equal ones are adjacent: only channel lc - 1 can
-                // name j first
-                if (lc > lc0) {
-                    const int jn2 = r - dl[lc - 1];
-                    if (jn2 >= 0 && jn2 / dsp == j) return false;
-                }
-                return true;
-            };
-            for (int i0 = 0; i0 < npass * G; i0 += blockDim.x) {
-                const int i = i0 + threadIdx.x;
-                int j = 0;
-                const bool keep = i < npass * G && task(i, j);
-                const uint64_t m = __ballot(keep);
-                if (m) {
-                    const int ln = threadIdx.x & 63;
-                    int base = 0;
-                    if (ln == 0) base = atomicAdd(&ntask_s, __popcll(m));
-                    base = __shfl(base, 0, 64);
-                    if (keep) tlist[base + __popcll(m & ((1ull << ln) - 1ull))] = (uint16_t)i;
+                    for (int cc = 0; cc < CPS; cc++)
+                        zb |= ((uint32_t)zap[i * CPS + cc] << cc) | ((uint32_t)zap[G + i * CPS + cc] << (16 + cc));
+                    zbm_s[i] = zb;
                 }
             }
             __syncthreads();
-            const int ntask = ntask_s;
+        }
+        if (fprobe & 1) {
+        } else if (clip_ev) {
+            const int ntask = ntask2[par];
             for (int t = threadIdx.x; t < ntask; t += blockDim.x) {
                 const int i = tlist[t];
                 int j = 0;
-                (void)task(i, j);
+                (void)fix8_task(dly, i, G, cps, DST, SG, r, N, nds, DS, pds_s, ds, j);
                 const int p = i / G, lc = i - p * G;
                 const int lc0 = lc - lc % cps;
                 const int16_t* dl = dly + dix(p, lc0) - lc0;
@@ -1184,9 +1219,9 @@ __global__ __launch_bounds__(256) void k_stage1_fix8(Stage1Multi a, Fix8Geom gm,
                 }
             }
         }
-        __syncthreads();
-        if (a.sub_dtype == 0 && threadIdx.x < npass) publish_max(a.maxabs[threadIdx.x], amax_s[threadIdx.x]);
     }
+    __syncthreads();
+    if (a.sub_dtype == 0 && threadIdx.x < npass) publish_max(a.maxabs[threadIdx.x], amax_s[threadIdx.x]);
 }
 
 static size_t fix8_lds_bytes(const Stage1Multi& a, const Fix8Geom& g)
