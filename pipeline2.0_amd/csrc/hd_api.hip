@@ -1677,12 +1677,15 @@ static void qp_tables(hd_plan* p, bool i16, hd_plan::Wide& w, std::vector<int32_
                       std::vector<int32_t> (&boffp)[3])
 {
     w = hd_plan::Wide{};
-    constexpr int NW = 16, RQ = 3, S = 64 * RQ, T = 4 * S;
+    constexpr int RQ = 3, S = 64 * RQ, T = 4 * S;
+    // 16 waves x Q = 4..5 DMs, or (HD_QP_NW=8) 8 waves x Q = 8..10 DMs with twice the registers
+    static const int NW = getenv("HD_QP_NW") && atoi(getenv("HD_QP_NW")) == 8 ? 8 : 16;
+    const int qlo = NW == 16 ? 4 : 8, qhi = NW == 16 ? 5 : 10;
     const int nsub = p->pass.nsub, numdms = p->pass.numdms;
     if (!i16 || nsub % 2 || numdms < 1) return;
-    int nyb = (numdms + 5 * NW - 1) / (5 * NW);
+    int nyb = (numdms + qhi * NW - 1) / (qhi * NW);
     const int per = (numdms + nyb - 1) / nyb;
-    const int Q = (per + NW - 1) / NW > 4 ? 5 : 4;
+    const int Q = (per + NW - 1) / NW > qlo ? qhi : qlo;
     const int dpb = NW * Q;
     nyb = (numdms + dpb - 1) / dpb;
     const int npair = nsub / 2;

@@ -2014,13 +2014,32 @@ __device__ __forceinline__ void qp_load4(const uint32_t* w32, int x, uint32_t& o
 template <int PPC>
 constexpr int qp_ns() { return PPC >= 4 ? 3 : 4; }
 
+// waves per workgroup: 16 x Q <= 5 DMs (4 waves per SIMD, 128 VGPRs), or 8 x Q = 8..10 DMs
+// (2 waves per SIMD, 256 VGPRs: the same accumulators per CU, fewer waves and a deeper LDS
+// read lookahead in the sums)
+template <int Q>
+constexpr int qp_nw() { return Q > 5 ? 8 : 16; }
+
+// LDS read lookahead of the sums (steps of RQ reads) in the VGPRs left beside the accumulators
+template <int Q, int RQ>
+constexpr int qp_la()
+{
+    // (16 waves: 1 step fits beside the 90 accumulator registers.  8 waves x 10 DMs: the
+    // compiler spills at 2-4 steps although ~50 registers are free -- 63-223 VGPRs of scratch
+    // measured in the resource usage -- so 1 step there too)
+    const int budget = qp_nw<Q>() == 16 ? 128 : 256;
+    const int spare = budget - 26 - Q * RQ * 6;
+    const int la = spare / (2 * RQ) - 1;
+    return la < 1 ? 1 : (la > 1 ? 1 : la);
+}
+
 template <int Q, int RQ, int PPC, bool NN, bool PRB>
-__global__ __launch_bounds__(1024) void k_stage2_qp(Stage2Args a, S2Multi m)
+__global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2Multi m)
 {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
     const int pi = (int)blockIdx.y / m.nyblk;
     const S2Pass& P = m.p[pi];
-    constexpr int NS = qp_ns<PPC>(), S = 64 * RQ, T = 4 * S;
+    constexpr int NS = qp_ns<PPC>(), S = 64 * RQ, T = 4 * S, NW = qp_nw<Q>();
     int tb, ntl;
     if (a.nwg == 0) {
         tb = xcd_remap(blockIdx.x, gridDim.x);
@@ -2041,7 +2060,7 @@ __global__ __launch_bounds__(1024) void k_stage2_qp(Stage2Args a, S2Multi m)
     const int nbp = P.nbp;                       // pieces of a chunk's offset block
     const int umax = P.umax;
     const int npiece = 2 * PPC * npw + nbp;      // DMA pieces per chunk (<= 32: two per wave)
-    const int pw = (npiece - wave + 15) >> 4;    // this wave's pieces per chunk: 0, 1 or 2
+    const int pw = (npiece - wave + NW - 1) / NW;  // this wave's pieces per chunk: 0 .. 3
     const int slot_bytes = npiece * 1024;
     const int npair = a.nsub >> 1;
     const int tab_bytes = npair * kPairTab * 4;
@@ -2108,7 +2127,7 @@ __global__ __launch_bounds__(1024) void k_stage2_qp(Stage2Args a, S2Multi m)
             if (++dchunk == nchunk) { dchunk = 0; dtile++; }
         }
         const uint32_t slot = ring0 + (uint32_t)((cc % NS) * slot_bytes);
-        for (int pc = wave; pc < npiece; pc += 16) {
+        for (int pc = wave; pc < npiece; pc += NW) {
             if (pc < 2 * PPC * npw) {
                 const int win = pc / npw, pcs = pc - win * npw;      // window win: pair win / 2, side win % 2
                 const int pr = PPC * c2 + (win >> 1);
@@ -2130,7 +2149,8 @@ __global__ __launch_bounds__(1024) void k_stage2_qp(Stage2Args a, S2Multi m)
         if constexpr (NS - 3 == 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else {
-            if (pw >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * (NS - 3)) : "memory");
+            if (pw >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * (NS - 3)) : "memory");
+            else if (pw == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * (NS - 3)) : "memory");
             else if (pw == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NS - 3) : "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
@@ -2233,7 +2253,8 @@ __global__ __launch_bounds__(1024) void k_stage2_qp(Stage2Args a, S2Multi m)
     if constexpr (NS - 3 == 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
-        if (pw >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * (NS - 3)) : "memory");
+        if (pw >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * (NS - 3)) : "memory");
+        else if (pw == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * (NS - 3)) : "memory");
         else if (pw == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NS - 3) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -2250,7 +2271,7 @@ __global__ __launch_bounds__(1024) void k_stage2_qp(Stage2Args a, S2Multi m)
         // this chunk's (pair, DM) byte offsets in ONE register: lane k * Q + q holds pair k, DM q
         const int voff = lane < PPC * Q ? sboff[(lane / Q) * dpb + wave * Q + lane % Q] : 0;
         if (!(PRB && (a.probe & 1))) {
-            constexpr int nsteps = PPC * Q, LA0 = ring_la<Q, RQ>() < Q - 1 ? ring_la<Q, RQ>() : Q - 1, LA = LA0;
+            constexpr int nsteps = PPC * Q, LA = qp_la<Q, RQ>() < nsteps - 1 ? qp_la<Q, RQ>() : nsteps - 1;
             uint64_t bb[LA + 1][RQ];
 #pragma unroll
             for (int e = 0; e < LA; e++)
@@ -2262,6 +2283,8 @@ __global__ __launch_bounds__(1024) void k_stage2_qp(Stage2Args a, S2Multi m)
                     lds_read_r<RQ>(bb[(e + LA) % (LA + 1)],
                                    (uint32_t)__builtin_amdgcn_readlane(voff, e + LA) + lane_byte);
                     lds_wait_n<LA * RQ>(cur);
+                } else if (e + 4 == nsteps && LA >= 3) {
+                    lds_wait_n<3 * RQ>(cur);
                 } else if (e + 3 == nsteps && LA >= 2) {
                     lds_wait_n<2 * RQ>(cur);
                 } else if (e + 2 == nsteps && LA >= 1) {
@@ -2315,7 +2338,8 @@ static hipError_t launch_qp_n(const Stage2Args& a, const S2Multi& m, int nyblk, 
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     S2Multi mm = m;
     mm.nyblk = nyblk;
-    hipLaunchKernelGGL((k_stage2_qp<Q, RQ, PPC, NN, PRB>), dim3(nx, (unsigned)(nyblk * m.npass)), dim3(1024), lds, st, b, mm);
+    hipLaunchKernelGGL((k_stage2_qp<Q, RQ, PPC, NN, PRB>), dim3(nx, (unsigned)(nyblk * m.npass)), dim3(qp_nw<Q>() * 64),
+                       lds, st, b, mm);
     return hipGetLastError();
 }
 
@@ -2328,7 +2352,7 @@ static hipError_t launch_qp_p(const Stage2Args& a, const S2Multi& m, int nyblk, 
     return prb ? launch_qp_n<Q, RQ, PPC, false, true>(a, m, nyblk, st) : launch_qp_n<Q, RQ, PPC, false, false>(a, m, nyblk, st);
 }
 
-#define HD_QP_QR(X) X(5, 3) X(4, 3)
+#define HD_QP_QR(X) X(5, 3) X(4, 3) X(10, 3) X(8, 3)
 
 bool stage2_qp_supports(int q, int r)
 {
