@@ -2033,7 +2033,30 @@ constexpr int qp_la()
     return la < 1 ? 1 : (la > 1 ? 1 : la);
 }
 
-template <int Q, int RQ, int PPC, bool NN, bool PRB>
+// 4 x 4 transpose inside each quad of lanes (DPP quad_perm): lane 4a + b ends with quarter b
+// of lanes 4a .. 4a+3, i.e. 4 consecutive samples of one quarter, so a tile's series go out as
+// float4 stores instead of four dword stores
+__device__ __forceinline__ void quad_transpose4(int (&v)[4])
+{
+    const int lane = __lane_id();
+    const bool b0 = lane & 1, b1 = lane & 2;
+#pragma unroll
+    for (int j = 0; j < 4; j += 2) {                       // exchange across lane bit 0
+        const int send = b0 ? v[j] : v[j + 1];
+        const int recv = __builtin_amdgcn_mov_dpp(send, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+        if (b0) v[j] = recv;
+        else v[j + 1] = recv;
+    }
+#pragma unroll
+    for (int j = 0; j < 2; j++) {                          // exchange across lane bit 1
+        const int send = b1 ? v[j] : v[j + 2];
+        const int recv = __builtin_amdgcn_mov_dpp(send, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+        if (b1) v[j] = recv;
+        else v[j + 2] = recv;
+    }
+}
+
+template <int Q, int RQ, int PPC, bool NN, bool PRB, bool FQ = false>
 __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2Multi m)
 {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
@@ -2211,7 +2234,18 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
             int64_t part = 0;
             if (dv && !(PRB && (a.probe & 4))) {
                 float* o = P.out + (int64_t)d * a.out_stride + t0 + lane;
-                if (t0 + T <= a.nvalid) {
+                if (FQ && t0 + T <= a.nvalid) {
+                    // lane 4a + b: samples 4a .. 4a+3 of quarter b (out_stride and S are
+                    // multiples of 4, so the float4 is aligned)
+                    float* o4 = P.out + (int64_t)d * a.out_stride + t0 + (lane & 3) * S + (lane & ~3);
+#pragma unroll
+                    for (int r = 0; r < RQ; r++) {
+                        int v[4] = {acc32[q][r][0], acc32[q][r][1], acc32[q][r][2], acc32[q][r][3]};
+                        part += (int64_t)v[0] + v[1] + v[2] + v[3];
+                        quad_transpose4(v);
+                        *(float4*)(o4 + 64 * r) = make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
+                    }
+                } else if (t0 + T <= a.nvalid) {
 #pragma unroll
                     for (int r = 0; r < RQ; r++)
 #pragma unroll
@@ -2319,11 +2353,11 @@ size_t stage2_qp_lds_bytes(int E, int npw, int nbp, int nsub, int umax, int ppc)
            (size_t)2 * ppc * umax * E * 8;
 }
 
-template <int Q, int RQ, int PPC, bool NN, bool PRB>
+template <int Q, int RQ, int PPC, bool NN, bool PRB, bool FQ = false>
 static hipError_t launch_qp_n(const Stage2Args& a, const S2Multi& m, int nyblk, hipStream_t st)
 {
     {
-        const hipError_t e = set_max_lds((const void*)k_stage2_qp<Q, RQ, PPC, NN, PRB>, 160 * 1024);
+        const hipError_t e = set_max_lds((const void*)k_stage2_qp<Q, RQ, PPC, NN, PRB, FQ>, 160 * 1024);
         if (e != hipSuccess) return e;
     }
     const unsigned ntiles = (unsigned)((a.nvalid + 256 * RQ - 1) / (256 * RQ));
@@ -2338,7 +2372,7 @@ static hipError_t launch_qp_n(const Stage2Args& a, const S2Multi& m, int nyblk, 
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     S2Multi mm = m;
     mm.nyblk = nyblk;
-    hipLaunchKernelGGL((k_stage2_qp<Q, RQ, PPC, NN, PRB>), dim3(nx, (unsigned)(nyblk * m.npass)), dim3(qp_nw<Q>() * 64),
+    hipLaunchKernelGGL((k_stage2_qp<Q, RQ, PPC, NN, PRB, FQ>), dim3(nx, (unsigned)(nyblk * m.npass)), dim3(qp_nw<Q>() * 64),
                        lds, st, b, mm);
     return hipGetLastError();
 }
@@ -2347,9 +2381,14 @@ template <int Q, int RQ, int PPC>
 static hipError_t launch_qp_p(const Stage2Args& a, const S2Multi& m, int nyblk, hipStream_t st)
 {
     const bool prb = (a.probe & 15) != 0;
+    static const bool fq = getenv("HD_QP_FQ") && atoi(getenv("HD_QP_FQ")) != 0;   // A/B: float4 series stores
     if (a.nonneg && !(a.probe & 64))
-        return prb ? launch_qp_n<Q, RQ, PPC, true, true>(a, m, nyblk, st) : launch_qp_n<Q, RQ, PPC, true, false>(a, m, nyblk, st);
-    return prb ? launch_qp_n<Q, RQ, PPC, false, true>(a, m, nyblk, st) : launch_qp_n<Q, RQ, PPC, false, false>(a, m, nyblk, st);
+        return prb ? launch_qp_n<Q, RQ, PPC, true, true>(a, m, nyblk, st)
+               : fq ? launch_qp_n<Q, RQ, PPC, true, false, true>(a, m, nyblk, st)
+                    : launch_qp_n<Q, RQ, PPC, true, false>(a, m, nyblk, st);
+    return prb ? launch_qp_n<Q, RQ, PPC, false, true>(a, m, nyblk, st)
+           : fq ? launch_qp_n<Q, RQ, PPC, false, false, true>(a, m, nyblk, st)
+                : launch_qp_n<Q, RQ, PPC, false, false>(a, m, nyblk, st);
 }
 
 #define HD_QP_QR(X) X(5, 3) X(4, 3) X(10, 3) X(8, 3)

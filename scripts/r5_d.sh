@@ -4,7 +4,7 @@
 # 8-wave qp (HD_QP_NW=8) and the restructured k_stage1_fix8.
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-bash scripts/ab_env.sh HD_S2_QP=0 HD_QP_NW=8 || exit 1
+bash scripts/ab_env.sh HD_S2_QP=0 HD_QP_NW=8 HD_QP_FQ=1 || exit 1
 WORDS="stage2 q8m fix8 q8<" bash scripts/ab_envk.sh "" || exit 1
 timeout -k 10 300 python3 bench.py --mode slices --comm hd --steps 3 --warmup 1 --no-cpu --e2e-beams 0 --sp-beams 0 \
     --fft-beams 0 --rfi-beams 0 --stream-beams 0 > gpurun_out/r5d_commhd.log 2>&1 || { echo "comm hd failed"; tail -5 gpurun_out/r5d_commhd.log; exit 1; }
