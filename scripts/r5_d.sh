@@ -4,6 +4,12 @@
 # 8-wave qp (HD_QP_NW=8) and the restructured k_stage1_fix8.
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
+# the two qp variants must be bit-exact before they are timed
+for e in HD_QP_NW=8 HD_QP_FQ=1; do
+  env $e timeout -k 10 400 python -u -m pytest tests/test_gpu_qp.py -m gpu -x -q --timeout 300 --timeout-method thread \
+      > gpurun_out/r5d_qpvar.log 2>&1 || { echo "qp variant $e failed"; tail -20 gpurun_out/r5d_qpvar.log; exit 1; }
+  echo "$e: $(tail -1 gpurun_out/r5d_qpvar.log)"
+done
 bash scripts/ab_env.sh HD_S2_QP=0 HD_QP_NW=8 HD_QP_FQ=1 || exit 1
 WORDS="stage2 q8m fix8 q8<" bash scripts/ab_envk.sh "" || exit 1
 timeout -k 10 300 python3 bench.py --mode slices --comm hd --steps 3 --warmup 1 --no-cpu --e2e-beams 0 --sp-beams 0 \
