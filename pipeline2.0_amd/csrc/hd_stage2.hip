@@ -2381,7 +2381,7 @@ template <int Q, int RQ, int PPC>
 static hipError_t launch_qp_p(const Stage2Args& a, const S2Multi& m, int nyblk, hipStream_t st)
 {
     const bool prb = (a.probe & 15) != 0;
-    static const bool fq = getenv("HD_QP_FQ") && atoi(getenv("HD_QP_FQ")) != 0;   // A/B: float4 series stores
+    const bool fq = stage2_qp_fq();
     if (a.nonneg && !(a.probe & 64))
         return prb ? launch_qp_n<Q, RQ, PPC, true, true>(a, m, nyblk, st)
                : fq ? launch_qp_n<Q, RQ, PPC, true, false, true>(a, m, nyblk, st)
@@ -2392,6 +2392,12 @@ static hipError_t launch_qp_p(const Stage2Args& a, const S2Multi& m, int nyblk, 
 }
 
 #define HD_QP_QR(X) X(5, 3) X(4, 3) X(10, 3) X(8, 3)
+
+bool stage2_qp_fq()
+{
+    static const bool fq = getenv("HD_QP_FQ") && atoi(getenv("HD_QP_FQ")) != 0;   // A/B: float4 series stores
+    return fq;
+}
 
 bool stage2_qp_supports(int q, int r)
 {
