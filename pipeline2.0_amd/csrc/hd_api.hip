@@ -1678,9 +1678,7 @@ static void qp_tables(hd_plan* p, bool i16, hd_plan::Wide& w, std::vector<int32_
 {
     w = hd_plan::Wide{};
     constexpr int RQ = 3, S = 64 * RQ, T = 4 * S;
-    // 16 waves x Q = 4..5 DMs, or (HD_QP_NW=8) 8 waves x Q = 8..10 DMs with twice the registers
-    static const int NW = getenv("HD_QP_NW") && atoi(getenv("HD_QP_NW")) == 8 ? 8 : 16;
-    const int qlo = NW == 16 ? 4 : 8, qhi = NW == 16 ? 5 : 10;
+    constexpr int NW = 16, qlo = 4, qhi = 5;            // 16 waves x Q = 4..5 DMs
     const int nsub = p->pass.nsub, numdms = p->pass.numdms;
     if (!i16 || nsub % 2 || numdms < 1) return;
     int nyb = (numdms + qhi * NW - 1) / (qhi * NW);

@@ -2014,24 +2014,16 @@ __device__ __forceinline__ void qp_load4(const uint32_t* w32, int x, uint32_t& o
 template <int PPC>
 constexpr int qp_ns() { return PPC >= 4 ? 3 : 4; }
 
-// waves per workgroup: 16 x Q <= 5 DMs (4 waves per SIMD, 128 VGPRs), or 8 x Q = 8..10 DMs
-// (2 waves per SIMD, 256 VGPRs: the same accumulators per CU, fewer waves and a deeper LDS
-// read lookahead in the sums)
+// 16 waves per workgroup x Q = 4..5 DMs (4 waves per SIMD, 128 VGPRs).  (An 8-wave x 8..10 DM
+// variant with 256 VGPRs was tried in round 5: the compiler spills its accumulators beyond one
+// step of LDS read lookahead, which removed its point, and it was dropped.)
 template <int Q>
-constexpr int qp_nw() { return Q > 5 ? 8 : 16; }
+constexpr int qp_nw() { return 16; }
 
-// LDS read lookahead of the sums (steps of RQ reads) in the VGPRs left beside the accumulators
+// LDS read lookahead of the sums (steps of RQ reads) in the VGPRs left beside the accumulators:
+// one step fits beside the 90 accumulator registers
 template <int Q, int RQ>
-constexpr int qp_la()
-{
-    // (16 waves: 1 step fits beside the 90 accumulator registers.  8 waves x 10 DMs: the
-    // compiler spills at 2-4 steps although ~50 registers are free -- 63-223 VGPRs of scratch
-    // measured in the resource usage -- so 1 step there too)
-    const int budget = qp_nw<Q>() == 16 ? 128 : 256;
-    const int spare = budget - 26 - Q * RQ * 6;
-    const int la = spare / (2 * RQ) - 1;
-    return la < 1 ? 1 : (la > 1 ? 1 : la);
-}
+constexpr int qp_la() { return 1; }
 
 // 4 x 4 transpose inside each quad of lanes (DPP quad_perm): lane 4a + b ends with quarter b
 // of lanes 4a .. 4a+3, i.e. 4 consecutive samples of one quarter, so a tile's series go out as
@@ -2391,7 +2383,7 @@ static hipError_t launch_qp_p(const Stage2Args& a, const S2Multi& m, int nyblk, 
                 : launch_qp_n<Q, RQ, PPC, false, false>(a, m, nyblk, st);
 }
 
-#define HD_QP_QR(X) X(5, 3) X(4, 3) X(10, 3) X(8, 3)
+#define HD_QP_QR(X) X(5, 3) X(4, 3)
 
 bool stage2_qp_fq()
 {
