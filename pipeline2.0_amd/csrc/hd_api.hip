@@ -2773,7 +2773,8 @@ static bool q8m_ok(const hd_ctx* c, hd_plan* const* plans, int n)
     int nds = 0, ds0 = plans[0]->pass.ds;
     for (int i = 0; i < n; i++) {
         const hd_plan* p = plans[i];
-        if (p->pass.nsub != nsub || (p->s1_variant != 0 && p->s1_variant != 3) || p->probe) return false;
+        if (p->pass.nsub != nsub || (p->s1_variant != 0 && p->s1_variant != 3)) return false;
+        if (p->probe && (i > 0 || (p->probe & ~(1 | 2 | 8 | 32 | 64)))) return false;   // q8m's probe bits, on plans[0]
         if (!hd::stage1_q8m_supports_ds(p->pass.ds) || !hd::stage1_q8_supports(cps, p->pass.ds)) return false;
         if (p->pass.ds != ds0) nds = 1;
     }
@@ -2853,7 +2854,11 @@ static int run_subband_fused(hd_ctx* c, hd_plan** plans, int n)
     int nsp = 0, *d_sp = nullptr;
     int rc = special_tiles(c, m, &d_sp, &nsp);
     if (rc) return rc;
-    HIPCHK(c, hd::launch_stage1_q8m(m, c->stream));
+    {
+        hd::Stage1Multi mp = m;
+        mp.probe = p0->probe & (1 | 2 | 8);        // profiling (results invalid): skip sums / fill / stores
+        HIPCHK(c, hd::launch_stage1_q8m(mp, c->stream));
+    }
     // per DDplan stage (ds): the special tiles on the float kernel
     std::vector<hd::Stage1Multi> groups;
     for (int i0 = 0; i0 < n;) {
@@ -2894,7 +2899,7 @@ static int run_subband_fused(hd_ctx* c, hd_plan** plans, int n)
     }
     // the clipped-spectrum and block-boundary outputs of every pass in one k_stage1_fix8 launch
     // (per-pass ds: one raw window per item for all the stages), else per DDplan stage
-    if (clip) {
+    if (clip && !(p0->probe & (32 | 64))) {       // (probe bits 5-6: fixups skipped, profiling)
         hd::Stage1Multi fx = m;
         fx.ds = 0;
         for (int i = 0; i < n; i++) fx.ds = std::max(fx.ds, (int)m.pds[i]);
@@ -3840,7 +3845,7 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         else if (wk == 5) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_rw<%d>", w.q);
         else if (wk == 6) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_qp<%d, %d, %d, %s, %s, %s>", w.q, w.r, w.sc,
                                    a.nonneg && !(p->probe & 64) ? "true" : "false", (p->probe & 15) ? "true" : "false",
-                                   !(p->probe & 15) && hd::stage2_qp_fq() ? "true" : "false");
+                                   (p->probe & 15) || hd::stage2_qp_deep() ? "true" : "false");
         else snprintf(p->s2name, sizeof(p->s2name), "k_stage2_pair<%d, %d, %d, %s, %s>", w.q, w.r, wk == 4 ? 2 : 1,
                       a.nonneg && !(p->probe & 64) ? "true" : "false", (p->probe & 15) ? "true" : "false");
     } else if (use_lds) {
@@ -4015,7 +4020,7 @@ static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
         if (wk == 5) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_rw<%d>", w0.q);
         else if (wk == 6) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_qp<%d, %d, %d, %s, %s, %s>", w0.q, w0.r, ppc6,
                                    a.nonneg && !(a.probe & 64) ? "true" : "false", (a.probe & 15) ? "true" : "false",
-                                   !(a.probe & 15) && hd::stage2_qp_fq() ? "true" : "false");
+                                   (a.probe & 15) || hd::stage2_qp_deep() ? "true" : "false");
         else snprintf(p->s2name, sizeof(p->s2name), "k_stage2_pair<%d, %d, 2, %s, %s>", w0.q, w0.r,
                       a.nonneg && !(a.probe & 64) ? "true" : "false", (a.probe & 15) ? "true" : "false");
     }

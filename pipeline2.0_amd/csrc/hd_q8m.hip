@@ -96,6 +96,10 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
                 }
             }
             if (!act) continue;
+            if (a.probe & 8) {                            // (profiling: sums without the stores)
+                mx = max(mx, (int)((ae ^ ao) & 0x7FFFu));
+                continue;
+            }
             if (a.sub_dtype == 0) {
                 if (mean && DS > 1) {
                     const float inv = 1.0f / (float)DS, half = 0.5f / (float)DS;

@@ -2025,30 +2025,7 @@ constexpr int qp_nw() { return 16; }
 template <int Q, int RQ>
 constexpr int qp_la() { return 1; }
 
-// 4 x 4 transpose inside each quad of lanes (DPP quad_perm): lane 4a + b ends with quarter b
-// of lanes 4a .. 4a+3, i.e. 4 consecutive samples of one quarter, so a tile's series go out as
-// float4 stores instead of four dword stores
-__device__ __forceinline__ void quad_transpose4(int (&v)[4])
-{
-    const int lane = __lane_id();
-    const bool b0 = lane & 1, b1 = lane & 2;
-#pragma unroll
-    for (int j = 0; j < 4; j += 2) {                       // exchange across lane bit 0
-        const int send = b0 ? v[j] : v[j + 1];
-        const int recv = __builtin_amdgcn_mov_dpp(send, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
-        if (b0) v[j] = recv;
-        else v[j + 1] = recv;
-    }
-#pragma unroll
-    for (int j = 0; j < 2; j++) {                          // exchange across lane bit 1
-        const int send = b1 ? v[j] : v[j + 2];
-        const int recv = __builtin_amdgcn_mov_dpp(send, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
-        if (b1) v[j] = recv;
-        else v[j + 2] = recv;
-    }
-}
-
-template <int Q, int RQ, int PPC, bool NN, bool PRB, bool FQ = false>
+template <int Q, int RQ, int PPC, bool NN, bool PRB, bool DEEP = true>
 __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2Multi m)
 {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
@@ -2158,15 +2135,19 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
             }
         }
     };
-    // wait until this chunk's DMA is in LDS: at most (NS - 3) chunks of this wave's pieces
-    // (and nothing older: series stores included) outstanding
+    // wait until the next chunk's DMA is in LDS: at most DL chunks of this wave's pieces newer
+    // than it (and nothing older: series stores included) outstanding.  DEEP: a chunk's DMA
+    // is issued two iterations before its expand (the ring slot it overwrites was expanded in
+    // the previous iteration, and that chunk's DM offsets were read into a register before
+    // that iteration's barrier), else one.
+    constexpr int DL = DEEP ? NS - 2 : NS - 3;
     auto wait_ring = [&]() {
-        if constexpr (NS - 3 == 0) {
+        if constexpr (DL == 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else {
-            if (pw >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * (NS - 3)) : "memory");
-            else if (pw == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * (NS - 3)) : "memory");
-            else if (pw == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NS - 3) : "memory");
+            if (pw >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * DL) : "memory");
+            else if (pw == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * DL) : "memory");
+            else if (pw == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(DL) : "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
     };
@@ -2226,18 +2207,7 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
             int64_t part = 0;
             if (dv && !(PRB && (a.probe & 4))) {
                 float* o = P.out + (int64_t)d * a.out_stride + t0 + lane;
-                if (FQ && t0 + T <= a.nvalid) {
-                    // lane 4a + b: samples 4a .. 4a+3 of quarter b (out_stride and S are
-                    // multiples of 4, so the float4 is aligned)
-                    float* o4 = P.out + (int64_t)d * a.out_stride + t0 + (lane & 3) * S + (lane & ~3);
-#pragma unroll
-                    for (int r = 0; r < RQ; r++) {
-                        int v[4] = {acc32[q][r][0], acc32[q][r][1], acc32[q][r][2], acc32[q][r][3]};
-                        part += (int64_t)v[0] + v[1] + v[2] + v[3];
-                        quad_transpose4(v);
-                        *(float4*)(o4 + 64 * r) = make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
-                    }
-                } else if (t0 + T <= a.nvalid) {
+                if (t0 + T <= a.nvalid) {
 #pragma unroll
                     for (int r = 0; r < RQ; r++)
 #pragma unroll
@@ -2274,28 +2244,27 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
             }
     };
 
+    // this chunk's (pair, DM) byte offsets in ONE register: lane k * Q + q holds pair k, DM q
+    auto read_voff = [&](int cc) {
+        const int32_t* sboff = (const int32_t*)(lds_raw + ring0 + (cc % NS) * slot_bytes + 2 * PPC * npw * 1024);
+        return lane < PPC * Q ? sboff[(lane / Q) * dpb + wave * Q + lane % Q] : 0;
+    };
+    // prologue: chunks 0 and 1 in LDS (chunk 1 is expanded in iteration 0); DEEP issues every
+    // slot's DMA, else NS - 1
 #pragma unroll
-    for (int cc = 0; cc < NS - 1; cc++) dma(cc);
-    if constexpr (NS - 3 == 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-        if (pw >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * (NS - 3)) : "memory");
-        else if (pw == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * (NS - 3)) : "memory");
-        else if (pw == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NS - 3) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    for (int cc = 0; cc < (DEEP ? NS : NS - 1); cc++) dma(cc);
+    wait_ring();
     ring_barrier();
     expand(0, 0);
+    int voff = DEEP ? read_voff(0) : 0;
     ring_barrier();
 
     int chk = 0, ktile = 0;
     for (int c = 0; c < ntot; c++) {
-        if (!(PRB && (a.probe & 2))) dma(c + NS - 1);
+        if (!(PRB && (a.probe & 2))) dma(c + (DEEP ? NS : NS - 1));
         const int chn = chk + 1 == nchunk ? 0 : chk + 1;
         if (c + 1 < ntot && !(PRB && (a.probe & 8))) expand(c + 1, chn);
-        const int32_t* sboff = (const int32_t*)(lds_raw + ring0 + (c % NS) * slot_bytes + 2 * PPC * npw * 1024);
-        // this chunk's (pair, DM) byte offsets in ONE register: lane k * Q + q holds pair k, DM q
-        const int voff = lane < PPC * Q ? sboff[(lane / Q) * dpb + wave * Q + lane % Q] : 0;
+        if (!DEEP) voff = read_voff(c);
         if (!(PRB && (a.probe & 1))) {
             constexpr int nsteps = PPC * Q, LA = qp_la<Q, RQ>() < nsteps - 1 ? qp_la<Q, RQ>() : nsteps - 1;
             uint64_t bb[LA + 1][RQ];
@@ -2330,6 +2299,7 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
                 }
             }
         }
+        if (DEEP && c + 1 < ntot) voff = read_voff(c + 1);    // (before the barrier: its slot is reused next)
         wait_ring();
         ring_barrier();
         if (chk == nchunk - 1) flush(tb + ktile++);
@@ -2345,11 +2315,11 @@ size_t stage2_qp_lds_bytes(int E, int npw, int nbp, int nsub, int umax, int ppc)
            (size_t)2 * ppc * umax * E * 8;
 }
 
-template <int Q, int RQ, int PPC, bool NN, bool PRB, bool FQ = false>
+template <int Q, int RQ, int PPC, bool NN, bool PRB, bool DEEP = true>
 static hipError_t launch_qp_n(const Stage2Args& a, const S2Multi& m, int nyblk, hipStream_t st)
 {
     {
-        const hipError_t e = set_max_lds((const void*)k_stage2_qp<Q, RQ, PPC, NN, PRB, FQ>, 160 * 1024);
+        const hipError_t e = set_max_lds((const void*)k_stage2_qp<Q, RQ, PPC, NN, PRB, DEEP>, 160 * 1024);
         if (e != hipSuccess) return e;
     }
     const unsigned ntiles = (unsigned)((a.nvalid + 256 * RQ - 1) / (256 * RQ));
@@ -2364,7 +2334,7 @@ static hipError_t launch_qp_n(const Stage2Args& a, const S2Multi& m, int nyblk, 
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     S2Multi mm = m;
     mm.nyblk = nyblk;
-    hipLaunchKernelGGL((k_stage2_qp<Q, RQ, PPC, NN, PRB, FQ>), dim3(nx, (unsigned)(nyblk * m.npass)), dim3(qp_nw<Q>() * 64),
+    hipLaunchKernelGGL((k_stage2_qp<Q, RQ, PPC, NN, PRB, DEEP>), dim3(nx, (unsigned)(nyblk * m.npass)), dim3(qp_nw<Q>() * 64),
                        lds, st, b, mm);
     return hipGetLastError();
 }
@@ -2373,22 +2343,23 @@ template <int Q, int RQ, int PPC>
 static hipError_t launch_qp_p(const Stage2Args& a, const S2Multi& m, int nyblk, hipStream_t st)
 {
     const bool prb = (a.probe & 15) != 0;
-    const bool fq = stage2_qp_fq();
+    const bool deep = stage2_qp_deep();
     if (a.nonneg && !(a.probe & 64))
         return prb ? launch_qp_n<Q, RQ, PPC, true, true>(a, m, nyblk, st)
-               : fq ? launch_qp_n<Q, RQ, PPC, true, false, true>(a, m, nyblk, st)
-                    : launch_qp_n<Q, RQ, PPC, true, false>(a, m, nyblk, st);
+               : deep ? launch_qp_n<Q, RQ, PPC, true, false, true>(a, m, nyblk, st)
+                      : launch_qp_n<Q, RQ, PPC, true, false, false>(a, m, nyblk, st);
     return prb ? launch_qp_n<Q, RQ, PPC, false, true>(a, m, nyblk, st)
-           : fq ? launch_qp_n<Q, RQ, PPC, false, false, true>(a, m, nyblk, st)
-                : launch_qp_n<Q, RQ, PPC, false, false>(a, m, nyblk, st);
+           : deep ? launch_qp_n<Q, RQ, PPC, false, false, true>(a, m, nyblk, st)
+                  : launch_qp_n<Q, RQ, PPC, false, false, false>(a, m, nyblk, st);
 }
 
 #define HD_QP_QR(X) X(5, 3) X(4, 3)
 
-bool stage2_qp_fq()
+bool stage2_qp_deep()
 {
-    static const bool fq = getenv("HD_QP_FQ") && atoi(getenv("HD_QP_FQ")) != 0;   // A/B: float4 series stores
-    return fq;
+    // HD_QP_DEEP=0 (A/B): each chunk's DMA issued one iteration ahead instead of two
+    static const bool d = !(getenv("HD_QP_DEEP") && atoi(getenv("HD_QP_DEEP")) == 0);
+    return d;
 }
 
 bool stage2_qp_supports(int q, int r)
