@@ -99,7 +99,13 @@ def test_c2_bench_path_kernels(c2_beam):
     """The beam ran through the kernels the bench reports (not a fallback variant)."""
     obs, raw, cl, stages, plans = c2_beam
     kern = {p.kernel() for st in plans for p in st}
-    assert any(k.startswith(("k_stage2_pair<", "k_stage2_qp<")) and k.endswith(", false>") for k in kern), kern
+
+    def unprobed_pair_kernel(k):      # k_stage2_pair / k_stage2_qp with the probe flag (5th argument) off
+        if not k.startswith(("k_stage2_pair<", "k_stage2_qp<")):
+            return False
+        args = [x.strip() for x in k[k.index("<") + 1:-1].split(",")]
+        return len(args) >= 5 and args[4] == "false"
+    assert any(unprobed_pair_kernel(k) for k in kern), kern
 
 
 @pytest.mark.parametrize("stage,i0", c2_cases())
