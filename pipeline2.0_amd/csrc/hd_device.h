@@ -120,4 +120,16 @@ __device__ __forceinline__ void publish_max(int32_t* addr, int v)
     if (v > cur) atomicMax(addr, v);
 }
 
+// N consecutive ints of a wave-uniform, read-only table (a pass's channel delays) through the
+// scalar cache: s_load is counted by lgkmcnt, so waiting for it never waits for the wave's
+// outstanding global stores (a vector load of the same words is counted by vmcnt with them).
+template <int N>
+__device__ __forceinline__ void sload_i32(const int32_t* p, int (&v)[N])
+{
+    typedef const int32_t __attribute__((address_space(4))) cint32;
+    const cint32* q = (const cint32*)p;
+#pragma unroll
+    for (int i = 0; i < N; i++) v[i] = q[i];
+}
+
 }  // namespace hd

@@ -824,20 +824,17 @@ __global__ __launch_bounds__(512) void k_stage1_q8(Stage1Multi a)
     // channel delays of pass p live in lanes 0..CPS-1 of vd; pass p+1's are loaded while
     // pass p is formed, so no global-load latency sits at the head of a pass
     // (unconditional, clamped loads: a branch around them would cost a vmcnt(0) drain)
-    const int dlane = c0 + cl0 + min(lane, CPS - 1);
-    int vd = a.dly[min(pw, a.npass - 1)][dlane];
     int pmax = 0;                                         // lane p: max |subband| of pass p
 
     const int npass = (a.probe & 1) ? 0 : a.npass;
     for (int p = pw; p < npass; p += wps) {
-        const int vd_next = a.dly[min(p + wps, a.npass - 1)][dlane];
+        // the pass's channel delays through the scalar cache (a vector load here would make
+        // the loop head wait for the previous pass's output stores as well)
         int dl[CPS];
+        sload_i32<CPS>(a.dly[p] + c0 + cl0, dl);
         int dmx = 0;
 #pragma unroll
-        for (int cc = 0; cc < CPS; cc++) {
-            dl[cc] = __builtin_amdgcn_readlane(vd, cc);
-            dmx = max(dmx, dl[cc]);
-        }
+        for (int cc = 0; cc < CPS; cc++) dmx = max(dmx, dl[cc]);
         int amax = 0;
         if (intpath) {
             uint32_t ae[M], ao[M];
@@ -1009,7 +1006,6 @@ __global__ __launch_bounds__(512) void k_stage1_q8(Stage1Multi a)
             amax = wave_max_i32(amax);
             pmax = lane == p ? amax : pmax;
         }
-        vd = vd_next;
     }
     if (a.sub_dtype == 0 && lane < a.npass) publish_max(a.maxabs[lane], pmax);
     }                                                     // per-wave section

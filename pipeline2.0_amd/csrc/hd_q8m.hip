@@ -315,19 +315,14 @@ __global__ __launch_bounds__(256, 3) void k_stage1_q8m(Stage1Multi a)
             intpad &= pad0[cc] == floorf(pad0[cc]) && pad1[cc] == floorf(pad1[cc]) && pad2[cc] == floorf(pad2[cc]);
         }
     const bool splitfree = zsplit == 0;
-    const int dlane = c0 + cl0 + min(lane, CPS - 1);
-    int vd = a.dly[min(pw, a.npass - 1)][dlane];
     int pmax = 0;
     const int npass = (a.probe & 1) ? 0 : a.npass;
     for (int p = pw; p < npass; p += wps) {
-        const int vd_next = a.dly[min(p + wps, a.npass - 1)][dlane];
         int dl[CPS];
+        sload_i32<CPS>(a.dly[p] + c0 + cl0, dl);          // (scalar loads: see k_stage1_q8)
         int dmx = 0;
 #pragma unroll
-        for (int cc = 0; cc < CPS; cc++) {
-            dl[cc] = __builtin_amdgcn_readlane(vd, cc);
-            dmx = max(dmx, dl[cc]);
-        }
+        for (int cc = 0; cc < CPS; cc++) dmx = max(dmx, dl[cc]);
         int amax = 0;
         const int ds = a.pds[p];
 #define HD_Q8M_CASE(D)                                                                                        \
@@ -348,7 +343,6 @@ __global__ __launch_bounds__(256, 3) void k_stage1_q8m(Stage1Multi a)
             amax = wave_max_i32(amax);
             pmax = lane == p ? amax : pmax;
         }
-        vd = vd_next;
     }
     if (a.sub_dtype == 0 && lane < a.npass) publish_max(a.maxabs[lane], pmax);
 }
