@@ -373,11 +373,10 @@ HD_API int hd_wait_writes(hd_ctx* ctx, double* write_seconds, int64_t* bytes);
 /* Device-time of the last hd_run_subband / hd_run_dedisp of this plan, ms.           */
 HD_API int hd_plan_last_ms(const hd_plan* plan, float* ms_subband, float* ms_dedisp);
 /* Name of the stage-2 kernel the last hd_run_dedisp of this plan launched, as rocprofv3
- * prints it without namespace and arguments (e.g. "k_stage2_qp<5, 3, 4, true, false, true>":
- * every template argument: for the pair kernels the non-negative-subband flag, then the
- * profiling build flag, false unless probe bits are set; k_stage2_qp adds its DMA-lookahead
- * flag): lets a benchmark key its roofline and PMC counters by kernel.  NUL-terminated in
- * name[cap].   */
+ * prints it without namespace and arguments (e.g. "k_stage2_qp<5, 3, 4, true, false>": every
+ * template argument: for the pair kernels the non-negative-subband flag, then the profiling
+ * build flag, false unless probe bits are set): lets a benchmark key its roofline and PMC
+ * counters by kernel.  NUL-terminated in name[cap].   */
 HD_API int hd_plan_kernel(const hd_plan* plan, char* name, int32_t cap);
 /* Kernel variants: (s1 << 8) | s2.  s2: 0 auto, 1 direct, 2 LDS-tiled (4 waves x 256 samples),
  * 3 wide LDS tiles (up to 16 waves share one window), 4 two workgroups per CU, 5 LDS-DMA

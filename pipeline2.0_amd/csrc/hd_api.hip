@@ -3843,9 +3843,8 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         else if (wk == 1) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_wide2<%d, %d, %d>", w.q, w.r, w.sc);
         else if (wk == 2) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_ring<%d, %d>", w.q, w.r);
         else if (wk == 5) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_rw<%d>", w.q);
-        else if (wk == 6) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_qp<%d, %d, %d, %s, %s, %s>", w.q, w.r, w.sc,
-                                   a.nonneg && !(p->probe & 64) ? "true" : "false", (p->probe & 15) ? "true" : "false",
-                                   (p->probe & 15) || hd::stage2_qp_deep() ? "true" : "false");
+        else if (wk == 6) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_qp<%d, %d, %d, %s, %s>", w.q, w.r, w.sc,
+                                   a.nonneg && !(p->probe & 64) ? "true" : "false", (p->probe & 15) ? "true" : "false");
         else snprintf(p->s2name, sizeof(p->s2name), "k_stage2_pair<%d, %d, %d, %s, %s>", w.q, w.r, wk == 4 ? 2 : 1,
                       a.nonneg && !(p->probe & 64) ? "true" : "false", (p->probe & 15) ? "true" : "false");
     } else if (use_lds) {
@@ -4018,9 +4017,8 @@ static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
         p->dd_stream = st;
         p->s2passes = i == 0 ? n : 0;
         if (wk == 5) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_rw<%d>", w0.q);
-        else if (wk == 6) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_qp<%d, %d, %d, %s, %s, %s>", w0.q, w0.r, ppc6,
-                                   a.nonneg && !(a.probe & 64) ? "true" : "false", (a.probe & 15) ? "true" : "false",
-                                   (a.probe & 15) || hd::stage2_qp_deep() ? "true" : "false");
+        else if (wk == 6) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_qp<%d, %d, %d, %s, %s>", w0.q, w0.r, ppc6,
+                                   a.nonneg && !(a.probe & 64) ? "true" : "false", (a.probe & 15) ? "true" : "false");
         else snprintf(p->s2name, sizeof(p->s2name), "k_stage2_pair<%d, %d, 2, %s, %s>", w0.q, w0.r,
                       a.nonneg && !(a.probe & 64) ? "true" : "false", (a.probe & 15) ? "true" : "false");
     }

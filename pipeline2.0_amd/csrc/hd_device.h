@@ -110,6 +110,20 @@ __device__ __forceinline__ int wave_max_i32(int v)
     return v;
 }
 
+// The same maximum, wave-uniform, by DPP steps inside the VALU (quad permutes, row mirrors,
+// row broadcasts 15 / 31) instead of six dependent ds_bpermute round trips.  Every lane of the
+// wave must be active (EXEC all ones): the stage-1 pass loops, once per pass.
+__device__ __forceinline__ int wave_max_full(int v)
+{
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false));    // quad_perm [1,0,3,2]
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false));    // quad_perm [2,3,0,1]
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false));   // row_half_mirror
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x140, 0xF, 0xF, false));   // row_mirror
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x142, 0xA, 0xF, false));   // row_bcast:15 -> rows 1, 3
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x143, 0xC, 0xF, false));   // row_bcast:31 -> rows 2, 3
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
 // Raise *addr to v.  Every wave of a pass targets the same word, and same-address atomics
 // serialise at the memory side, so read first (a stale value only costs an extra atomic;
 // atomicMax is monotone, so the result is exact) and publish only a new maximum.
@@ -118,6 +132,32 @@ __device__ __forceinline__ void publish_max(int32_t* addr, int v)
     if (v <= 0) return;
     const int cur = __hip_atomic_load(addr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (v > cur) atomicMax(addr, v);
+}
+
+// Stage-1 tiles (k_stage1_q8 / k_stage1_q8m): the LDS rows of channels masked in every read
+// block the tile touches (b0 .. b0 + nb - 1) are zeroed after the fill, so the integer sums
+// add every channel without a per-channel mask (those channels' pads are in the per-block
+// constants; the float folds replace their values by the pads).  LDS row r holds channel
+// c0 + r (c0 + G - 1 - r on a flipped band), W dwords (a multiple of 4).  Every thread of the
+// block calls it; the first barrier is the fill's.
+__device__ __forceinline__ void s1_zero_masked_rows(uint32_t* lds, int G, int W, const RawDesc& rd, int64_t b0, int nb,
+                                                    int c0, uint8_t* zrow)
+{
+    bool zf = false;
+    if ((int)threadIdx.x < G) {
+        const int r = threadIdx.x;
+        const int c = c0 + (rd.flip ? G - 1 - r : r);
+        zf = rd.zidx != nullptr;
+        for (int i = 0; i < nb && zf; i++) zf = zap_at(rd, b0 + i, c);
+        zrow[r] = zf;
+    }
+    if (!__syncthreads_or(zf)) return;
+    const int w4 = W >> 2;
+    for (int i = threadIdx.x; i < G * w4; i += blockDim.x) {
+        const int r = i / w4;
+        if (zrow[r]) ((uint4*)(lds + (size_t)r * W))[i - r * w4] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    __syncthreads();
 }
 
 // N consecutive ints of a wave-uniform, read-only table (a pass's channel delays) through the

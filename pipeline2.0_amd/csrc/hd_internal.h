@@ -172,7 +172,6 @@ hipError_t launch_stage2_pair_multi(const Stage2Args& a, const S2Multi& m, int q
 // quarter-layout pair kernel (k_stage2_qp): ws = entries per pattern buffer, ppc 2..4 pairs per chunk
 size_t stage2_qp_lds_bytes(int E, int npw, int nbp, int nsub, int umax, int ppc);
 bool stage2_qp_supports(int q, int r);
-bool stage2_qp_deep();             // HD_QP_DEEP=0: the one-iteration DMA lookahead (A/B)
 hipError_t launch_stage2_qp_multi(const Stage2Args& a, const S2Multi& m, int q, int r, int ppc, hipStream_t st);
 hipError_t launch_stage2_wide2(const Stage2Args& a, int q, int r, int nw, hipStream_t st);
 hipError_t launch_stage2_direct(const Stage2Args& a, hipStream_t st);

@@ -698,6 +698,11 @@ __global__ __launch_bounds__(512) void k_stage1_q8(Stage1Multi a)
         if (threadIdx.x < 8) fneed[threadIdx.x] = 0;
     }
     anyclip = __syncthreads_or(anyclip);
+    __shared__ uint8_t zrow[256];
+    if (a.rd.zidx) {                                      // (uniform) channels masked in every block: rows zeroed
+        const int64_t bz = tR0 / a.rd.blk;
+        s1_zero_masked_rows(lds, G, W, a.rd, bz, (int)((tR0 + 4 * S + a.dmax - 1) / a.rd.blk - bz) + 1, c0, zrow);
+    }
 
     // ---- per-wave subband state: wave w serves subband w / wps and passes p = w % wps (mod
     //      wps), so every wave of the block (at least 4) sums: sg = 2 gives 2 waves per
@@ -860,11 +865,11 @@ __global__ __launch_bounds__(512) void k_stage1_q8(Stage1Multi a)
                 }
             }
             // the channel sums, branch-free so every LDS read of the pass can be in flight
-            // before the first add; channels masked in every block of the tile (their pads are
-            // in the constants) are ANDed away by a uniform mask
-            if (zall == 0) {
-                // all reads of a group of channels first (a scheduling barrier keeps the
-                // compiler from interleaving a wait after every read pair), then the adds
+            // before the first add; channels masked in every block of the tile add zeros (their
+            // rows were zeroed after the fill, their pads are in the constants).  All reads of
+            // a group of channels first (a scheduling barrier keeps the compiler from
+            // interleaving a wait after every read pair), then the adds.
+            {
                 constexpr int PER = M * DS, CG = PER * CPS <= 40 ? CPS : (40 / PER < 1 ? 1 : 40 / PER);
 #pragma unroll
                 for (int c0g = 0; c0g < CPS; c0g += CG) {
@@ -890,20 +895,6 @@ __global__ __launch_bounds__(512) void k_stage1_q8(Stage1Multi a)
                                 ao[m] += __builtin_amdgcn_perm(0u, x, 0x0c030c01u);    // quarters 1, 3
                             }
                     }
-                }
-            } else {
-#pragma unroll
-                for (int cc = 0; cc < CPS; cc++) {
-                    const uint32_t keep = ((zall >> cc) & 1u) ? 0u : 0xFFFFFFFFu;
-                    const uint32_t* b = lbase + lrb[cc] + dl[cc];
-#pragma unroll
-                    for (int m = 0; m < M; m++)
-#pragma unroll
-                        for (int k = 0; k < DS; k++) {
-                            const uint32_t x = b[m * 64 * DS + k] & keep;
-                            ae[m] += x & 0x00FF00FFu;
-                            ao[m] += __builtin_amdgcn_perm(0u, x, 0x0c030c01u);
-                        }
                 }
             }
             if (a.sub_dtype == 0) {
@@ -1003,7 +994,7 @@ __global__ __launch_bounds__(512) void k_stage1_q8(Stage1Multi a)
             }
         }
         if (a.sub_dtype == 0) {
-            amax = wave_max_i32(amax);
+            amax = wave_max_full(amax);
             pmax = lane == p ? amax : pmax;
         }
     }

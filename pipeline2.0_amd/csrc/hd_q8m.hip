@@ -82,15 +82,15 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
                 ae = kof(lastrow) | (kof(lastrow + 2 * S) << 16);
                 ao = kof(lastrow + S) | (kof(lastrow + 3 * S) << 16);
             }
-            // lanes past JQ outputs per quarter read a clamped (in-tile) dword, discarded
+            // lanes past JQ outputs per quarter read a clamped (in-tile) dword, discarded.
+            // Channels masked in every block of the tile add zeros (rows zeroed after the fill).
             const int mo = act ? m * 64 * DS : -lane * DS;
 #pragma unroll
             for (int cc = 0; cc < CPS; cc++) {
-                const uint32_t keep = ((zall >> cc) & 1u) ? 0u : 0xFFFFFFFFu;
                 const uint32_t* b = lbase + lrb[cc] + dl[cc] + mo;
 #pragma unroll
                 for (int k = 0; k < DS; k++) {
-                    const uint32_t x = b[k] & keep;
+                    const uint32_t x = b[k];
                     ae += x & 0x00FF00FFu;
                     ao += __builtin_amdgcn_perm(0u, x, 0x0c030c01u);
                 }
@@ -262,7 +262,13 @@ __global__ __launch_bounds__(256, 3) void k_stage1_q8m(Stage1Multi a)
             }
         }
     }
-    __syncthreads();
+    __shared__ uint8_t zrow[256];
+    if (a.rd.zidx) {            // (uniform) channels masked in every block of the tile: rows zeroed
+        const int64_t bz = tR0 / a.rd.blk;
+        s1_zero_masked_rows(lds, G, W, a.rd, bz, (int)((tR0 + 4 * S + a.dmax - 1) / a.rd.blk - bz) + 1, c0, zrow);
+    } else {
+        __syncthreads();
+    }
 
     // ---- per-wave subband state (k_stage1_q8): wave w serves subband w / wps and the passes
     //      p = w % wps (mod wps); the tile may straddle two read-block boundaries
@@ -340,7 +346,7 @@ __global__ __launch_bounds__(256, 3) void k_stage1_q8m(Stage1Multi a)
         }
 #undef HD_Q8M_CASE
         if (a.sub_dtype == 0) {
-            amax = wave_max_i32(amax);
+            amax = wave_max_full(amax);
             pmax = lane == p ? amax : pmax;
         }
     }

@@ -2025,7 +2025,7 @@ constexpr int qp_nw() { return 16; }
 template <int Q, int RQ>
 constexpr int qp_la() { return 1; }
 
-template <int Q, int RQ, int PPC, bool NN, bool PRB, bool DEEP = true>
+template <int Q, int RQ, int PPC, bool NN, bool PRB>
 __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2Multi m)
 {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
@@ -2136,11 +2136,10 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
         }
     };
     // wait until the next chunk's DMA is in LDS: at most DL chunks of this wave's pieces newer
-    // than it (and nothing older: series stores included) outstanding.  DEEP: a chunk's DMA
-    // is issued two iterations before its expand (the ring slot it overwrites was expanded in
-    // the previous iteration, and that chunk's DM offsets were read into a register before
-    // that iteration's barrier), else one.
-    constexpr int DL = DEEP ? NS - 2 : NS - 3;
+    // than it (and nothing older: series stores included) outstanding.  (Issuing each chunk's
+    // DMA one iteration earlier, with the offsets read into a register before the slot is
+    // reused, measured slower: 34.3 vs 33.3 ms of stage 2 per beam.)
+    constexpr int DL = NS - 3;
     auto wait_ring = [&]() {
         if constexpr (DL == 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2249,22 +2248,20 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
         const int32_t* sboff = (const int32_t*)(lds_raw + ring0 + (cc % NS) * slot_bytes + 2 * PPC * npw * 1024);
         return lane < PPC * Q ? sboff[(lane / Q) * dpb + wave * Q + lane % Q] : 0;
     };
-    // prologue: chunks 0 and 1 in LDS (chunk 1 is expanded in iteration 0); DEEP issues every
-    // slot's DMA, else NS - 1
+    // prologue: chunks 0 and 1 in LDS (chunk 1 is expanded in iteration 0)
 #pragma unroll
-    for (int cc = 0; cc < (DEEP ? NS : NS - 1); cc++) dma(cc);
+    for (int cc = 0; cc < NS - 1; cc++) dma(cc);
     wait_ring();
     ring_barrier();
     expand(0, 0);
-    int voff = DEEP ? read_voff(0) : 0;
     ring_barrier();
 
     int chk = 0, ktile = 0;
     for (int c = 0; c < ntot; c++) {
-        if (!(PRB && (a.probe & 2))) dma(c + (DEEP ? NS : NS - 1));
+        if (!(PRB && (a.probe & 2))) dma(c + NS - 1);
         const int chn = chk + 1 == nchunk ? 0 : chk + 1;
         if (c + 1 < ntot && !(PRB && (a.probe & 8))) expand(c + 1, chn);
-        if (!DEEP) voff = read_voff(c);
+        const int voff = read_voff(c);
         if (!(PRB && (a.probe & 1))) {
             constexpr int nsteps = PPC * Q, LA = qp_la<Q, RQ>() < nsteps - 1 ? qp_la<Q, RQ>() : nsteps - 1;
             uint64_t bb[LA + 1][RQ];
@@ -2299,7 +2296,6 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
                 }
             }
         }
-        if (DEEP && c + 1 < ntot) voff = read_voff(c + 1);    // (before the barrier: its slot is reused next)
         wait_ring();
         ring_barrier();
         if (chk == nchunk - 1) flush(tb + ktile++);
@@ -2315,11 +2311,11 @@ size_t stage2_qp_lds_bytes(int E, int npw, int nbp, int nsub, int umax, int ppc)
            (size_t)2 * ppc * umax * E * 8;
 }
 
-template <int Q, int RQ, int PPC, bool NN, bool PRB, bool DEEP = true>
+template <int Q, int RQ, int PPC, bool NN, bool PRB>
 static hipError_t launch_qp_n(const Stage2Args& a, const S2Multi& m, int nyblk, hipStream_t st)
 {
     {
-        const hipError_t e = set_max_lds((const void*)k_stage2_qp<Q, RQ, PPC, NN, PRB, DEEP>, 160 * 1024);
+        const hipError_t e = set_max_lds((const void*)k_stage2_qp<Q, RQ, PPC, NN, PRB>, 160 * 1024);
         if (e != hipSuccess) return e;
     }
     const unsigned ntiles = (unsigned)((a.nvalid + 256 * RQ - 1) / (256 * RQ));
@@ -2334,7 +2330,7 @@ static hipError_t launch_qp_n(const Stage2Args& a, const S2Multi& m, int nyblk, 
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     S2Multi mm = m;
     mm.nyblk = nyblk;
-    hipLaunchKernelGGL((k_stage2_qp<Q, RQ, PPC, NN, PRB, DEEP>), dim3(nx, (unsigned)(nyblk * m.npass)), dim3(qp_nw<Q>() * 64),
+    hipLaunchKernelGGL((k_stage2_qp<Q, RQ, PPC, NN, PRB>), dim3(nx, (unsigned)(nyblk * m.npass)), dim3(qp_nw<Q>() * 64),
                        lds, st, b, mm);
     return hipGetLastError();
 }
@@ -2343,24 +2339,12 @@ template <int Q, int RQ, int PPC>
 static hipError_t launch_qp_p(const Stage2Args& a, const S2Multi& m, int nyblk, hipStream_t st)
 {
     const bool prb = (a.probe & 15) != 0;
-    const bool deep = stage2_qp_deep();
     if (a.nonneg && !(a.probe & 64))
-        return prb ? launch_qp_n<Q, RQ, PPC, true, true>(a, m, nyblk, st)
-               : deep ? launch_qp_n<Q, RQ, PPC, true, false, true>(a, m, nyblk, st)
-                      : launch_qp_n<Q, RQ, PPC, true, false, false>(a, m, nyblk, st);
-    return prb ? launch_qp_n<Q, RQ, PPC, false, true>(a, m, nyblk, st)
-           : deep ? launch_qp_n<Q, RQ, PPC, false, false, true>(a, m, nyblk, st)
-                  : launch_qp_n<Q, RQ, PPC, false, false, false>(a, m, nyblk, st);
+        return prb ? launch_qp_n<Q, RQ, PPC, true, true>(a, m, nyblk, st) : launch_qp_n<Q, RQ, PPC, true, false>(a, m, nyblk, st);
+    return prb ? launch_qp_n<Q, RQ, PPC, false, true>(a, m, nyblk, st) : launch_qp_n<Q, RQ, PPC, false, false>(a, m, nyblk, st);
 }
 
 #define HD_QP_QR(X) X(5, 3) X(4, 3)
-
-bool stage2_qp_deep()
-{
-    // HD_QP_DEEP=0 (A/B): each chunk's DMA issued one iteration ahead instead of two
-    static const bool d = !(getenv("HD_QP_DEEP") && atoi(getenv("HD_QP_DEEP")) == 0);
-    return d;
-}
 
 bool stage2_qp_supports(int q, int r)
 {
