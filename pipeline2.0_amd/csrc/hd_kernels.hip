@@ -843,7 +843,9 @@ __global__ __launch_bounds__(512) void k_stage1_q8(Stage1Multi a)
         int amax = 0;
         if (intpath) {
             uint32_t ae[M], ao[M];
-            if (brow >= (1 << 30)) {                   // uniform: the tile lies in one read block
+            // uniform: the tile lies in one read block, or every block's constant is the same
+            // (no channel of the subband masked in every block: the constant is D/2)
+            if (brow >= (1 << 30) || (cadd0 == cadd1 && cadd1 == cadd2)) {
                 const uint32_t kk = (uint32_t)cadd0 | ((uint32_t)cadd0 << 16);
 #pragma unroll
                 for (int m = 0; m < M; m++) ae[m] = ao[m] = kk;

@@ -75,7 +75,7 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
         for (int m = 0; m < M; m++) {
             const bool act = (m + 1) * 64 <= JQ || lane + 64 * m < JQ;
             uint32_t ae, ao;
-            if (brow >= (1 << 30)) {
+            if (brow >= (1 << 30) || (cadd0 == cadd1 && cadd1 == cadd2)) {   // (uniform: one constant)
                 ae = ao = (uint32_t)cadd0 | ((uint32_t)cadd0 << 16);
             } else {
                 const int lastrow = (lane + 64 * m) * DS + DS - 1 + dmx;
