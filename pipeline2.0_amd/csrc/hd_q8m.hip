@@ -24,6 +24,32 @@ constexpr int kQ8mS = 960;                    // raw rows per quarter of the til
 
 bool stage1_q8m_supports_ds(int ds) { return ds == 2 || ds == 3 || ds == 5 || ds == 6 || ds == 10; }
 
+// The DS consecutive dwords of one channel row at LDS byte address addr, as NR = ceil(DS / 2)
+// ds_read2_b32 (for odd DS the last read's second dword is past the row's needed range: the
+// LDS allocation has 16 bytes of slack).  Inline asm, so the compiler cannot put a wait after
+// each read; q8m_wait<N> below waits until at most N LDS operations are outstanding and ties b,
+// so no use of b moves above it.
+template <int NR>
+__device__ __forceinline__ void q8m_rd(uint64_t (&b)[NR], uint32_t addr)
+{
+#pragma unroll
+    for (int r = 0; r < NR; r++)
+        asm volatile("ds_read2_b32 %0, %1 offset0:%2 offset1:%3" : "=v"(b[r]) : "v"(addr), "i"(2 * r), "i"(2 * r + 1));
+}
+
+template <int N, int NR>
+__device__ __forceinline__ void q8m_wait(uint64_t (&b)[NR])
+{
+    if constexpr (NR == 1) asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(b[0]) : "i"(N));
+    else if constexpr (NR == 2) asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(b[0]), "+v"(b[1]) : "i"(N));
+    else if constexpr (NR == 3) asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]) : "i"(N));
+    else if constexpr (NR == 4)
+        asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]) : "i"(N));
+    else if constexpr (NR == 5)
+        asm volatile("s_waitcnt lgkmcnt(%5)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]), "+v"(b[4]) : "i"(N));
+    else static_assert(NR >= 1 && NR <= 5, "NR");
+}
+
 // One pass at compile-time DS over the tile (the body of k_stage1_q8's pass loop, with the
 // quarter length S = 960 and ceil(960 / DS / 64) output positions per lane and quarter).
 template <int CPS, int DS>
@@ -41,6 +67,8 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
     int ln = lane;
     asm volatile("" : "+v"(ln));
     const uint32_t* lbase = lds + ln * DS;
+    // this lane's LDS byte address of the tile (the reads below are inline asm)
+    const uint32_t lb = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) uint32_t*)lds) + 4u * (uint32_t)(ln * DS);
     // the per-block pad constants of the channels masked in every block of the tile (see
     // k_stage1_q8): C = DS * P + D/2, integer path while frac(C) keeps clear of 0 and 1
     const int Dh = mean ? DS / 2 : 0;
@@ -84,16 +112,29 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
             }
             // lanes past JQ outputs per quarter read a clamped (in-tile) dword, discarded.
             // Channels masked in every block of the tile add zeros (rows zeroed after the fill).
+            // Software pipeline over the channels: channel cc + 1's reads are in flight while
+            // channel cc is added.
             const int mo = act ? m * 64 * DS : -lane * DS;
+            constexpr int NR = (DS + 1) / 2;
+            uint64_t ba[NR], bb[NR];
+            q8m_rd<NR>(ba, lb + 4u * (uint32_t)(lrb[0] + dl[0] + mo));
 #pragma unroll
             for (int cc = 0; cc < CPS; cc++) {
-                const uint32_t* b = lbase + lrb[cc] + dl[cc] + mo;
+                uint64_t (&cur)[NR] = (cc & 1) ? bb : ba;
+                uint64_t (&nxt)[NR] = (cc & 1) ? ba : bb;
+                if (cc + 1 < CPS) {
+                    q8m_rd<NR>(nxt, lb + 4u * (uint32_t)(lrb[cc + 1] + dl[cc + 1] + mo));
+                    q8m_wait<NR, NR>(cur);
+                } else {
+                    q8m_wait<0, NR>(cur);
+                }
 #pragma unroll
                 for (int k = 0; k < DS; k++) {
-                    const uint32_t x = b[k];
+                    const uint32_t x = (k & 1) ? (uint32_t)(cur[k >> 1] >> 32) : (uint32_t)cur[k >> 1];
                     ae += x & 0x00FF00FFu;
                     ao += __builtin_amdgcn_perm(0u, x, 0x0c030c01u);
                 }
+                asm volatile("" : "+v"(ae), "+v"(ao));   // (channel by channel: no add tree over the pass)
             }
             if (!act) continue;
             if (a.probe & 8) {                            // (profiling: sums without the stores)
@@ -353,7 +394,7 @@ __global__ __launch_bounds__(256, 3) void k_stage1_q8m(Stage1Multi a)
     if (a.sub_dtype == 0 && lane < a.npass) publish_max(a.maxabs[lane], pmax);
 }
 
-size_t stage1_q8m_lds_bytes(const Stage1Multi& a) { return (size_t)a.sg * a.cps * a.W * 4; }
+size_t stage1_q8m_lds_bytes(const Stage1Multi& a) { return (size_t)a.sg * a.cps * a.W * 4 + 16; }   // (+ read slack)
 
 hipError_t launch_stage1_q8m(const Stage1Multi& a, hipStream_t st)
 {
