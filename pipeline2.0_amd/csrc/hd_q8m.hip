@@ -37,6 +37,16 @@ __device__ __forceinline__ void q8m_rd(uint64_t (&b)[NR], uint32_t addr)
         asm volatile("ds_read2_b32 %0, %1 offset0:%2 offset1:%3" : "=v"(b[r]) : "v"(addr), "i"(2 * r), "i"(2 * r + 1));
 }
 
+// The same dwords by ds_read_b64 when the row address is 8-byte aligned (even DS and an even
+// channel delay: lanes DS dwords apart then hit all 64 banks once, where the dword pairs of
+// ds_read2_b32 are 2-way bank-conflicted)
+template <int NR>
+__device__ __forceinline__ void q8m_rd64(uint64_t (&b)[NR], uint32_t addr)
+{
+#pragma unroll
+    for (int r = 0; r < NR; r++) asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(b[r]) : "v"(addr), "i"(8 * r));
+}
+
 template <int N, int NR>
 __device__ __forceinline__ void q8m_wait(uint64_t (&b)[NR])
 {
@@ -117,13 +127,19 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
             const int mo = act ? m * 64 * DS : -lane * DS;
             constexpr int NR = (DS + 1) / 2;
             uint64_t ba[NR], bb[NR];
-            q8m_rd<NR>(ba, lb + 4u * (uint32_t)(lrb[0] + dl[0] + mo));
+            // (even DS: the address parity is the delay's, uniform per channel)
+            auto rd = [&](uint64_t (&b)[NR], int cc) {
+                const uint32_t ad = lb + 4u * (uint32_t)(lrb[cc] + dl[cc] + mo);
+                if (DS % 2 == 0 && !(dl[cc] & 1)) q8m_rd64<NR>(b, ad);
+                else q8m_rd<NR>(b, ad);
+            };
+            rd(ba, 0);
 #pragma unroll
             for (int cc = 0; cc < CPS; cc++) {
                 uint64_t (&cur)[NR] = (cc & 1) ? bb : ba;
                 uint64_t (&nxt)[NR] = (cc & 1) ? ba : bb;
                 if (cc + 1 < CPS) {
-                    q8m_rd<NR>(nxt, lb + 4u * (uint32_t)(lrb[cc + 1] + dl[cc + 1] + mo));
+                    rd(nxt, cc + 1);
                     q8m_wait<NR, NR>(cur);
                 } else {
                     q8m_wait<0, NR>(cur);
