@@ -2774,7 +2774,7 @@ static bool q8m_ok(const hd_ctx* c, hd_plan* const* plans, int n)
     for (int i = 0; i < n; i++) {
         const hd_plan* p = plans[i];
         if (p->pass.nsub != nsub || (p->s1_variant != 0 && p->s1_variant != 3)) return false;
-        if (p->probe && (i > 0 || (p->probe & ~(1 | 2 | 8 | 32 | 64)))) return false;   // q8m's probe bits, on plans[0]
+        if (p->probe && (i > 0 || (p->probe & ~(1 | 2 | 4 | 8 | 32 | 64)))) return false;   // q8m's probe bits, on plans[0]
         if (!hd::stage1_q8m_supports_ds(p->pass.ds) || !hd::stage1_q8_supports(cps, p->pass.ds)) return false;
         if (p->pass.ds != ds0) nds = 1;
     }
@@ -2856,7 +2856,7 @@ static int run_subband_fused(hd_ctx* c, hd_plan** plans, int n)
     if (rc) return rc;
     {
         hd::Stage1Multi mp = m;
-        mp.probe = p0->probe & (1 | 2 | 8);        // profiling (results invalid): skip sums / fill / stores
+        mp.probe = p0->probe & (1 | 2 | 4 | 8);    // profiling (results invalid): skip sums / fill / float folds / stores
         HIPCHK(c, hd::launch_stage1_q8m(mp, c->stream));
     }
     // per DDplan stage (ds): the special tiles on the float kernel

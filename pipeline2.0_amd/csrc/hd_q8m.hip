@@ -100,6 +100,7 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
         }
     }
     intpath = __builtin_amdgcn_readfirstlane((int)intpath) != 0;
+    if (a.probe & 4) intpath = true;                      // (profiling: the float fold never taken)
     cadd0 = __builtin_amdgcn_readfirstlane(cadd0);
     cadd1 = __builtin_amdgcn_readfirstlane(cadd1);
     cadd2 = __builtin_amdgcn_readfirstlane(cadd2);
