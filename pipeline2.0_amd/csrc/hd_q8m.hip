@@ -40,11 +40,11 @@ __device__ __forceinline__ void q8m_rd(uint64_t (&b)[NR], uint32_t addr)
 // The same dwords by ds_read_b64 when the row address is 8-byte aligned (even DS and an even
 // channel delay: lanes DS dwords apart then hit all 64 banks once, where the dword pairs of
 // ds_read2_b32 are 2-way bank-conflicted)
-template <int NR>
-__device__ __forceinline__ void q8m_rd64(uint64_t (&b)[NR], uint32_t addr)
+template <int N, int NB>
+__device__ __forceinline__ void q8m_rd64(uint64_t (&b)[NB], uint32_t addr)
 {
 #pragma unroll
-    for (int r = 0; r < NR; r++) asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(b[r]) : "v"(addr), "i"(8 * r));
+    for (int r = 0; r < N; r++) asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(b[r]) : "v"(addr), "i"(8 * r));
 }
 
 template <int N, int NR>
@@ -57,7 +57,10 @@ __device__ __forceinline__ void q8m_wait(uint64_t (&b)[NR])
         asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]) : "i"(N));
     else if constexpr (NR == 5)
         asm volatile("s_waitcnt lgkmcnt(%5)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]), "+v"(b[4]) : "i"(N));
-    else static_assert(NR >= 1 && NR <= 5, "NR");
+    else if constexpr (NR == 6)
+        asm volatile("s_waitcnt lgkmcnt(%6)"
+                     : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]), "+v"(b[4]), "+v"(b[5]) : "i"(N));
+    else static_assert(NR >= 1 && NR <= 6, "NR");
 }
 
 // One pass at compile-time DS over the tile (the body of k_stage1_q8's pass loop, with the
@@ -126,31 +129,47 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
             // Software pipeline over the channels: channel cc + 1's reads are in flight while
             // channel cc is added.
             const int mo = act ? m * 64 * DS : -lane * DS;
+            // Even DS: every read is an aligned ds_read_b64 (lanes DS dwords apart hit all 64
+            // banks once) -- DS / 2 of them at an even channel delay, DS / 2 + 1 from one dword
+            // earlier at an odd one (the adds then start at the second dword); the delay's
+            // parity is uniform per channel.  Odd DS: ds_read2_b32 pairs (lanes an odd number of
+            // dwords apart: conflict-free).
             constexpr int NR = (DS + 1) / 2;
-            uint64_t ba[NR], bb[NR];
-            // (even DS: the address parity is the delay's, uniform per channel)
-            auto rd = [&](uint64_t (&b)[NR], int cc) {
+            constexpr bool EV = DS % 2 == 0;
+            constexpr int NB = EV ? NR + 1 : NR;
+            uint64_t ba[NB], bb[NB];
+            auto rd = [&](uint64_t (&b)[NB], int cc) {
                 const uint32_t ad = lb + 4u * (uint32_t)(lrb[cc] + dl[cc] + mo);
-                if (DS % 2 == 0 && !(dl[cc] & 1)) q8m_rd64<NR>(b, ad);
-                else q8m_rd<NR>(b, ad);
+                if constexpr (EV) {
+                    if (dl[cc] & 1) q8m_rd64<NR + 1, NB>(b, ad - 4u);
+                    else q8m_rd64<NR, NB>(b, ad);
+                } else {
+                    q8m_rd<NR>(b, ad);
+                }
+            };
+            auto adds = [&](const uint64_t (&b)[NB], int off) {
+#pragma unroll
+                for (int k = 0; k < DS; k++) {
+                    const int kk = k + off;
+                    const uint32_t x = (kk & 1) ? (uint32_t)(b[kk >> 1] >> 32) : (uint32_t)b[kk >> 1];
+                    ae += x & 0x00FF00FFu;
+                    ao += __builtin_amdgcn_perm(0u, x, 0x0c030c01u);
+                }
             };
             rd(ba, 0);
 #pragma unroll
             for (int cc = 0; cc < CPS; cc++) {
-                uint64_t (&cur)[NR] = (cc & 1) ? bb : ba;
-                uint64_t (&nxt)[NR] = (cc & 1) ? ba : bb;
+                uint64_t (&cur)[NB] = (cc & 1) ? bb : ba;
+                uint64_t (&nxt)[NB] = (cc & 1) ? ba : bb;
                 if (cc + 1 < CPS) {
                     rd(nxt, cc + 1);
-                    q8m_wait<NR, NR>(cur);
+                    if (EV && (dl[cc + 1] & 1)) q8m_wait<EV ? NR + 1 : NR, NB>(cur);
+                    else q8m_wait<NR, NB>(cur);
                 } else {
-                    q8m_wait<0, NR>(cur);
+                    q8m_wait<0, NB>(cur);
                 }
-#pragma unroll
-                for (int k = 0; k < DS; k++) {
-                    const uint32_t x = (k & 1) ? (uint32_t)(cur[k >> 1] >> 32) : (uint32_t)cur[k >> 1];
-                    ae += x & 0x00FF00FFu;
-                    ao += __builtin_amdgcn_perm(0u, x, 0x0c030c01u);
-                }
+                if (EV && (dl[cc] & 1)) adds(cur, 1);
+                else adds(cur, 0);
                 asm volatile("" : "+v"(ae), "+v"(ao));   // (channel by channel: no add tree over the pass)
             }
             if (!act) continue;
