@@ -172,13 +172,4 @@ __device__ __forceinline__ void sload_i32(const int32_t* p, int (&v)[N])
     for (int i = 0; i < N; i++) v[i] = q[i];
 }
 
-template <int N>
-__device__ __forceinline__ void sload_f32(const float* p, float (&v)[N])
-{
-    typedef const float __attribute__((address_space(4))) cf32;
-    const cf32* q = (const cf32*)p;
-#pragma unroll
-    for (int i = 0; i < N; i++) v[i] = q[i];
-}
-
 }  // namespace hd

@@ -70,7 +70,7 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
                                          const int (&lrb)[CPS], const int (&dl)[CPS], int dmx, int brow, int brow2,
                                          uint32_t z0, uint32_t z1, uint32_t z2, uint32_t zany, uint32_t zall,
                                          int fz, bool splitfree, double P0, double P1, double P2, bool negpad,
-                                         bool intpad, const float* pb0, const float* pb1, const float* pb2, int& amax)
+                                         bool intpad, int64_t b0, int cbase, int& amax)
 {
     constexpr int S = kQ8mS, JQ = S / DS, M = (JQ + 63) / 64;
     const bool mean = a.ds_mode == 1;
@@ -207,20 +207,7 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
         }
         amax = mx;
     } else {
-        // the float fold (subbands with a channel masked in some but not all blocks of the tile,
-        // near-ties, f32 output): the oracle's order -- per ds step the channels from 0.0f, the
-        // integer prefix up to the first masked channel exact, then float adds -- with the
-        // delays, LDS rows, pads and zap bits of the channels in registers (the pads of the
-        // tile's read blocks by scalar loads here: kept live across the pass loop they pushed
-        // the integer path's delays and rows out of SGPRs)
-        float pad0[CPS], pad1[CPS], pad2[CPS];
-#pragma unroll
-        for (int cc = 0; cc < CPS; cc++) pad0[cc] = pad1[cc] = pad2[cc] = 0.0f;
-        if (pb0) {
-            sload_f32<CPS>(pb0, pad0);
-            sload_f32<CPS>(pb1, pad1);
-            sload_f32<CPS>(pb2, pad2);
-        }
+        // (the rare float fold: one output position at a time, kept out of the register budget)
 #pragma unroll 1
         for (int m = 0; m < M; m++) {
             if ((m + 1) * 64 > JQ && lane + 64 * m >= JQ) continue;
@@ -228,14 +215,15 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
 #pragma unroll 1
             for (int k = 0; k < DS; k++) {
                 const int t = (lane + 64 * m) * DS + k;    // quarter-relative raw row
-                uint32_t xs[CPS];
-#pragma unroll
-                for (int cc = 0; cc < CPS; cc++) xs[cc] = lbase[lrb[cc] + dl[cc] + m * 64 * DS + k];
                 uint32_t pe = 0, po = 0;
                 float sk[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
+                // (channel loop not unrolled: each channel's LDS row and delay re-derived)
+#pragma unroll 1
                 for (int cc = 0; cc < CPS; cc++) {
-                    const uint32_t x = xs[cc];
+                    const int lr = a.rd.flip ? a.sg * CPS - 1 - (cbase - (cbase / (a.sg * CPS)) * (a.sg * CPS) + cc)
+                                             : cbase - (cbase / (a.sg * CPS)) * (a.sg * CPS) + cc;
+                    const int dcc = a.dly[p][cbase + cc];
+                    const uint32_t x = lbase[lr * a.W + dcc + m * 64 * DS + k];
                     if (cc < fz) {
                         pe += x & 0x00FF00FFu;
                         po += __builtin_amdgcn_perm(0u, x, 0x0c030c01u);
@@ -249,13 +237,13 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
                         float v[4] = {(float)(x & 0xFFu), (float)((x >> 8) & 0xFFu), (float)((x >> 16) & 0xFFu),
                                       (float)(x >> 24)};
                         if (zany & (1u << cc)) {
-                            const int rr = t + dl[cc];
+                            const int rr = t + dcc;
+                            const bool za = (z0 >> cc) & 1, zb = (z1 >> cc) & 1, zc = (z2 >> cc) & 1;
 #pragma unroll
                             for (int q = 0; q < 4; q++) {
                                 const int row = rr + q * S;
-                                const bool h1 = row >= brow, h2 = row >= brow2;
-                                const uint32_t zb = h2 ? z2 : h1 ? z1 : z0;
-                                if ((zb >> cc) & 1u) v[q] = h2 ? pad2[cc] : h1 ? pad1[cc] : pad0[cc];
+                                const int bi = row < brow ? 0 : row < brow2 ? 1 : 2;
+                                if (bi == 0 ? za : bi == 1 ? zb : zc) v[q] = pad_at(a.rd, b0 + bi, cbase + cc);
                             }
                         }
 #pragma unroll
@@ -410,10 +398,6 @@ __global__ __launch_bounds__(256, 3) void k_stage1_q8m(Stage1Multi a)
             intpad &= pad0[cc] == floorf(pad0[cc]) && pad1[cc] == floorf(pad1[cc]) && pad2[cc] == floorf(pad2[cc]);
         }
     const bool splitfree = zsplit == 0;
-    // the float fold's pads: the channels' rows of the pad table for the tile's read blocks
-    const float* pb0 = a.rd.pad ? a.rd.pad + b0 * a.rd.pad_stride + c0 + cl0 : nullptr;
-    const float* pb1 = a.rd.pad ? a.rd.pad + b1 * a.rd.pad_stride + c0 + cl0 : nullptr;
-    const float* pb2 = a.rd.pad ? a.rd.pad + b2 * a.rd.pad_stride + c0 + cl0 : nullptr;
     int pmax = 0;
     const int npass = (a.probe & 1) ? 0 : a.npass;
     for (int p = pw; p < npass; p += wps) {
@@ -427,7 +411,7 @@ __global__ __launch_bounds__(256, 3) void k_stage1_q8m(Stage1Multi a)
 #define HD_Q8M_CASE(D)                                                                                        \
         case D:                                                                                               \
             q8m_pass<CPS, D>(a, p, s, tile, lane, lds, lrb, dl, dmx, brow, brow2, z0, z1, z2, zany, zall, fz, \
-                             splitfree, P0, P1, P2, negpad, intpad, pb0, pb1, pb2, amax);                  \
+                             splitfree, P0, P1, P2, negpad, intpad, b0, c0 + cl0, amax);                  \
             break;
         switch (ds) {
             HD_Q8M_CASE(2)
