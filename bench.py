@@ -382,6 +382,9 @@ def slice_stages(eng, ts, rank, variant):
 
 
 SLICE_COMM = ["torch"]
+# --sim-slice R/G with R > 0: the other slices' clip statistics rows (what the all-reduce would
+# bring), computed once from a whole-beam context before the timed steps
+SLICE_SIM_TABLE = [None]
 
 
 def run_slice_step(eng, ts, rank, stages, dist, torch):
@@ -401,7 +404,7 @@ def run_slice_step(eng, ts, rank, stages, dist, torch):
             torch.cuda.current_stream().synchronize()
             eng.clip_set_stats(table.data_ptr())
         else:
-            table = ts.stats_table()
+            table = ts.stats_table() if SLICE_SIM_TABLE[0] is None else SLICE_SIM_TABLE[0].copy()
             ts.contribute_clip_stats(eng, rank, table)
             if dist is not None:
                 t = torch.from_numpy(table)
@@ -671,6 +674,20 @@ def main():
                 sys.exit("--sim-slice runs one process")
             srank, sworld = (int(x) for x in args.sim_slice.split("/"))
         ts = TimeSlices(obs, ddplans, sworld)
+        if args.sim_slice and srank > 0 and Opts().clip_sigma > 0:
+            # the earlier slices' clip statistics, as the all-reduce would bring them (untimed):
+            # without them a later slice's clip_times runs from empty blocks
+            full = Engine(local)
+            full.set_obs(obs, Opts())
+            full.set_slice(0, obs.N)
+            full.synth_device(synth)
+            fm, fpad = synth_mask(obs, synth, rfifind_ptsperint(obs.dt))
+            full.set_mask(fm, rfifind_ptsperint(obs.dt), fpad)
+            t1 = TimeSlices(obs, ddplans, 1)
+            SLICE_SIM_TABLE[0] = t1.stats_table()
+            t1.contribute_clip_stats(full, 0, SLICE_SIM_TABLE[0])
+            full.close()
+            del full
         eng.set_obs(ts.local_obs(srank), Opts())
         eng.set_slice(ts.slice(srank)[0], obs.N)
     else:
