@@ -129,11 +129,13 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
             // Software pipeline over the channels: channel cc + 1's reads are in flight while
             // channel cc is added.
             const int mo = act ? m * 64 * DS : -lane * DS;
-            // Even DS: every read is an aligned ds_read_b64 (lanes DS dwords apart hit all 64
-            // banks once) -- DS / 2 of them at an even channel delay, DS / 2 + 1 from one dword
-            // earlier at an odd one (the adds then start at the second dword); the delay's
-            // parity is uniform per channel.  Odd DS: ds_read2_b32 pairs (lanes an odd number of
-            // dwords apart: conflict-free).
+            // Even DS: DS / 2 + 1 aligned ds_read_b64 from the channel's address rounded down to
+            // 8 bytes (lanes DS dwords apart hit all 64 banks once); the adds start at the
+            // second dword when the channel delay is odd (uniform per channel).  Odd DS:
+            // ds_read2_b32 pairs (lanes an odd number of dwords apart: conflict-free).  No
+            // branch may sit between a read and its wait: the compiler resolves the branch
+            // with register copies, which it places before the wait (the asm outputs look
+            // ready to it) and which would then copy registers the LDS has not yet written.
             constexpr int NR = (DS + 1) / 2;
             constexpr bool EV = DS % 2 == 0;
             constexpr int NB = EV ? NR + 1 : NR;
@@ -141,8 +143,7 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
             auto rd = [&](uint64_t (&b)[NB], int cc) {
                 const uint32_t ad = lb + 4u * (uint32_t)(lrb[cc] + dl[cc] + mo);
                 if constexpr (EV) {
-                    if (dl[cc] & 1) q8m_rd64<NR + 1, NB>(b, ad - 4u);
-                    else q8m_rd64<NR, NB>(b, ad);
+                    q8m_rd64<NB, NB>(b, ad & ~7u);
                 } else {
                     q8m_rd<NR>(b, ad);
                 }
@@ -163,8 +164,7 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
                 uint64_t (&nxt)[NB] = (cc & 1) ? ba : bb;
                 if (cc + 1 < CPS) {
                     rd(nxt, cc + 1);
-                    if (EV && (dl[cc + 1] & 1)) q8m_wait<EV ? NR + 1 : NR, NB>(cur);
-                    else q8m_wait<NR, NB>(cur);
+                    q8m_wait<NB, NB>(cur);
                 } else {
                     q8m_wait<0, NB>(cur);
                 }
