@@ -65,12 +65,12 @@ __device__ __forceinline__ void q8m_wait(uint64_t (&b)[NR])
 
 // One pass at compile-time DS over the tile (the body of k_stage1_q8's pass loop, with the
 // quarter length S = 960 and ceil(960 / DS / 64) output positions per lane and quarter).
-template <int CPS, int DS>
+template <int CPS, int DS, bool B64>
 __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int tile, int lane, const uint32_t* lds,
                                          const int (&lrb)[CPS], const int (&dl)[CPS], int dmx, int brow, int brow2,
                                          uint32_t z0, uint32_t z1, uint32_t z2, uint32_t zany, uint32_t zall,
                                          int fz, bool splitfree, double P0, double P1, double P2, bool negpad,
-                                         bool intpad, int64_t b0, int cbase, int& amax)
+                                         bool intpad, const float* padw, int& amax)
 {
     constexpr int S = kQ8mS, JQ = S / DS, M = (JQ + 63) / 64;
     const bool mean = a.ds_mode == 1;
@@ -129,24 +129,21 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
             // Software pipeline over the channels: channel cc + 1's reads are in flight while
             // channel cc is added.
             const int mo = act ? m * 64 * DS : -lane * DS;
-            // Even DS: DS / 2 + 1 aligned ds_read_b64 from the channel's address rounded down to
-            // 8 bytes (lanes DS dwords apart hit all 64 banks once); the adds start at the
-            // second dword when the channel delay is odd (uniform per channel).  Odd DS:
-            // ds_read2_b32 pairs (lanes an odd number of dwords apart: conflict-free).  No
-            // branch may sit between a read and its wait: the compiler resolves the branch
-            // with register copies, which it places before the wait (the asm outputs look
-            // ready to it) and which would then copy registers the LDS has not yet written.
+            // Odd DS, or B64 off: ds_read2_b32 pairs (at even DS lanes DS dwords apart then
+            // 2-way bank-conflict).  B64 (HD_Q8M_B64=1, even DS): DS / 2 + 1 aligned ds_read_b64
+            // from the channel's address rounded down to 8 bytes (all 64 banks once); the adds
+            // start at the second dword when the channel delay is odd (uniform per channel).
+            // No branch may sit between a read and its wait: the compiler resolves a branch with
+            // register copies placed before the wait (the asm outputs look ready to it), copies
+            // of registers the LDS has not yet written (tests/test_asm_lds.py checks).
             constexpr int NR = (DS + 1) / 2;
-            constexpr bool EV = DS % 2 == 0;
+            constexpr bool EV = B64 && DS % 2 == 0;
             constexpr int NB = EV ? NR + 1 : NR;
             uint64_t ba[NB], bb[NB];
             auto rd = [&](uint64_t (&b)[NB], int cc) {
                 const uint32_t ad = lb + 4u * (uint32_t)(lrb[cc] + dl[cc] + mo);
-                if constexpr (EV) {
-                    q8m_rd64<NB, NB>(b, ad & ~7u);
-                } else {
-                    q8m_rd<NR>(b, ad);
-                }
+                if constexpr (EV) q8m_rd64<NB, NB>(b, ad & ~7u);
+                else q8m_rd<NR>(b, ad);
             };
             auto adds = [&](const uint64_t (&b)[NB], int off) {
 #pragma unroll
@@ -207,7 +204,23 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
         }
         amax = mx;
     } else {
-        // (the rare float fold: one output position at a time, kept out of the register budget)
+        // the float fold (subbands with a channel masked in some but not all blocks of the tile,
+        // near-ties, f32 output): the oracle's order -- per ds step the channels from 0.0f, the
+        // integer prefix up to the first masked channel exact, then float adds.  The channels'
+        // rows and delays are the integer path's registers; their pads per read block come
+        // from the wave's LDS table (padw[bi * 16 + cc]), so nothing extra stays live across
+        // the pass loop (the fold had re-derived each channel's delay and pad by dependent
+        // global loads: 2.9 of the fused launch's 10.5 ms for 3.8 % of its subband tiles)
+        // the channels' LDS rows and delays go to the wave's table too (read back below, so
+        // the unrolled fold holds no scalar registers of its own)
+        int* chw = (int*)(padw + 48);
+        if (lane == 0) {
+#pragma unroll
+            for (int cc = 0; cc < CPS; cc++) {
+                chw[cc] = lrb[cc] + dl[cc];
+                chw[16 + cc] = dl[cc];
+            }
+        }
 #pragma unroll 1
         for (int m = 0; m < M; m++) {
             if ((m + 1) * 64 > JQ && lane + 64 * m >= JQ) continue;
@@ -215,15 +228,14 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
 #pragma unroll 1
             for (int k = 0; k < DS; k++) {
                 const int t = (lane + 64 * m) * DS + k;    // quarter-relative raw row
+                uint32_t xs[CPS];
+#pragma unroll
+                for (int cc = 0; cc < CPS; cc++) xs[cc] = lbase[chw[cc] + m * 64 * DS + k];
                 uint32_t pe = 0, po = 0;
                 float sk[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-                // (channel loop not unrolled: each channel's LDS row and delay re-derived)
-#pragma unroll 1
+#pragma unroll
                 for (int cc = 0; cc < CPS; cc++) {
-                    const int lr = a.rd.flip ? a.sg * CPS - 1 - (cbase - (cbase / (a.sg * CPS)) * (a.sg * CPS) + cc)
-                                             : cbase - (cbase / (a.sg * CPS)) * (a.sg * CPS) + cc;
-                    const int dcc = a.dly[p][cbase + cc];
-                    const uint32_t x = lbase[lr * a.W + dcc + m * 64 * DS + k];
+                    const uint32_t x = xs[cc];
                     if (cc < fz) {
                         pe += x & 0x00FF00FFu;
                         po += __builtin_amdgcn_perm(0u, x, 0x0c030c01u);
@@ -237,13 +249,13 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
                         float v[4] = {(float)(x & 0xFFu), (float)((x >> 8) & 0xFFu), (float)((x >> 16) & 0xFFu),
                                       (float)(x >> 24)};
                         if (zany & (1u << cc)) {
-                            const int rr = t + dcc;
-                            const bool za = (z0 >> cc) & 1, zb = (z1 >> cc) & 1, zc = (z2 >> cc) & 1;
+                            const int rr = t + chw[16 + cc];
 #pragma unroll
                             for (int q = 0; q < 4; q++) {
                                 const int row = rr + q * S;
-                                const int bi = row < brow ? 0 : row < brow2 ? 1 : 2;
-                                if (bi == 0 ? za : bi == 1 ? zb : zc) v[q] = pad_at(a.rd, b0 + bi, cbase + cc);
+                                const int bi = row >= brow2 ? 2 : row >= brow ? 1 : 0;
+                                const uint32_t zb = bi == 2 ? z2 : bi == 1 ? z1 : z0;
+                                if ((zb >> cc) & 1u) v[q] = padw[bi * 16 + cc];
                             }
                         }
 #pragma unroll
@@ -271,7 +283,7 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
     }
 }
 
-template <int CPS>
+template <int CPS, bool B64>
 __global__ __launch_bounds__(256, 3) void k_stage1_q8m(Stage1Multi a)
 {
     constexpr int S = kQ8mS;
@@ -398,6 +410,14 @@ __global__ __launch_bounds__(256, 3) void k_stage1_q8m(Stage1Multi a)
             intpad &= pad0[cc] == floorf(pad0[cc]) && pad1[cc] == floorf(pad1[cc]) && pad2[cc] == floorf(pad2[cc]);
         }
     const bool splitfree = zsplit == 0;
+    // the float fold's pads: this wave's table [read block slot 0..2][channel] (written and read
+    // by the wave itself, so no barrier)
+    __shared__ float padtab[4][3 * 16 + 32];              // (<= 4 waves per workgroup; + rows, delays)
+    float* padw = padtab[wv];
+    if (lane < 3 * CPS) {
+        const int bi = lane / CPS, cc = lane - bi * CPS;
+        padw[bi * 16 + cc] = pad_at(a.rd, bi == 0 ? b0 : bi == 1 ? b1 : b2, c0 + cl0 + cc);
+    }
     int pmax = 0;
     const int npass = (a.probe & 1) ? 0 : a.npass;
     for (int p = pw; p < npass; p += wps) {
@@ -410,8 +430,8 @@ __global__ __launch_bounds__(256, 3) void k_stage1_q8m(Stage1Multi a)
         const int ds = a.pds[p];
 #define HD_Q8M_CASE(D)                                                                                        \
         case D:                                                                                               \
-            q8m_pass<CPS, D>(a, p, s, tile, lane, lds, lrb, dl, dmx, brow, brow2, z0, z1, z2, zany, zall, fz, \
-                             splitfree, P0, P1, P2, negpad, intpad, b0, c0 + cl0, amax);                  \
+            q8m_pass<CPS, D, B64>(a, p, s, tile, lane, lds, lrb, dl, dmx, brow, brow2, z0, z1, z2, zany, zall, fz, \
+                                  splitfree, P0, P1, P2, negpad, intpad, padw, amax);                       \
             break;
         switch (ds) {
             HD_Q8M_CASE(2)
@@ -437,9 +457,12 @@ hipError_t launch_stage1_q8m(const Stage1Multi& a, hipStream_t st)
     if (a.npass <= 0 || a.ntiles <= 0) return hipSuccess;
     const size_t lds = stage1_q8m_lds_bytes(a);
     const void* fn = nullptr;
-    if (a.cps == 10) fn = (const void*)k_stage1_q8m<10>;
-    else if (a.cps == 8) fn = (const void*)k_stage1_q8m<8>;
-    else if (a.cps == 16) fn = (const void*)k_stage1_q8m<16>;
+    // HD_Q8M_B64=1 (A/B): the even-ds reads as aligned ds_read_b64 (bank-conflict free, one more
+    // read and a branch per channel)
+    static const bool b64 = getenv("HD_Q8M_B64") && atoi(getenv("HD_Q8M_B64")) != 0;
+    if (a.cps == 10) fn = b64 ? (const void*)k_stage1_q8m<10, true> : (const void*)k_stage1_q8m<10, false>;
+    else if (a.cps == 8) fn = b64 ? (const void*)k_stage1_q8m<8, true> : (const void*)k_stage1_q8m<8, false>;
+    else if (a.cps == 16) fn = b64 ? (const void*)k_stage1_q8m<16, true> : (const void*)k_stage1_q8m<16, false>;
     else return hipErrorInvalidValue;
     {
         const hipError_t e = set_max_lds(fn, (int)std::max<size_t>(lds, 64 * 1024));
