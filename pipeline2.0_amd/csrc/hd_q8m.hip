@@ -221,6 +221,8 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
                 chw[16 + cc] = dl[cc];
             }
         }
+        asm volatile("" ::: "memory");                    // (as for the pads above)
+        __builtin_amdgcn_wave_barrier();
 #pragma unroll 1
         for (int m = 0; m < M; m++) {
             if ((m + 1) * 64 > JQ && lane + 64 * m >= JQ) continue;
@@ -418,6 +420,10 @@ __global__ __launch_bounds__(256, 3) void k_stage1_q8m(Stage1Multi a)
         const int bi = lane / CPS, cc = lane - bi * CPS;
         padw[bi * 16 + cc] = pad_at(a.rd, bi == 0 ? b0 : bi == 1 ? b1 : b2, c0 + cl0 + cc);
     }
+    // (other lanes of the wave read these: keep every later LDS access after the writes -- the
+    // compiler, seeing no write in a reading lane's own program, could otherwise hoist its read)
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
     int pmax = 0;
     const int npass = (a.probe & 1) ? 0 : a.npass;
     for (int p = pw; p < npass; p += wps) {
