@@ -1757,10 +1757,17 @@ static void qp_tables(hd_plan* p, bool i16, hd_plan::Wide& w, std::vector<int32_
         }
         return nip;
     };
+    // pieces of a chunk's item list at q pairs per chunk, or 0 (items derived in the kernel)
+    // when the list does not fit beside the windows
+    auto nip_fit = [&](int q) {
+        const int nip = items_for(q, nullptr);
+        return 2 * q * npw + nbp + nip <= 32 && hd::stage2_qp_lds_bytes(Emax, npw, nbp + nip, nsub, umax, q) <= 160 * 1024
+                   ? nip : 0;
+    };
     int ppc = 0;
     for (int cand : {4, 3, 2}) {
         if ((nsub / 2) % cand) continue;
-        const int nip = items_for(cand, nullptr);
+        const int nip = nip_fit(cand);
         if (2 * cand * npw + nbp + nip <= 32 &&
             hd::stage2_qp_lds_bytes(Emax, npw, nbp + nip, nsub, umax, cand) <= 160 * 1024) {
             ppc = cand;
@@ -1776,7 +1783,8 @@ static void qp_tables(hd_plan* p, bool i16, hd_plan::Wide& w, std::vector<int32_
         std::vector<int32_t>& bo = boffp[qi];
         bo.clear();
         if (q > ppc || (nsub / 2) % q) continue;
-        w.nipp[qi] = items_for(q, &itemsp[qi]);
+        w.nipp[qi] = nip_fit(q);
+        if (w.nipp[qi]) items_for(q, &itemsp[qi]);
         bo.assign((size_t)nyb * npair * dpb + 256, 0);   // the last DMA piece may over-read
         for (int yb = 0; yb < nyb; yb++)
             for (int c = 0; c < npair; c++) {
@@ -2016,9 +2024,11 @@ extern "C" int hd_plan_create(hd_ctx* c, const hd_pass* ps, hd_plan** out)
         e = hipMalloc(&p->wide[6].d_boffp[qi], sizeof(int32_t) * qpb[qi].size());
         if (e == hipSuccess)
             e = hipMemcpy(p->wide[6].d_boffp[qi], qpb[qi].data(), sizeof(int32_t) * qpb[qi].size(), hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMalloc(&p->wide[6].d_itemsp[qi], sizeof(int32_t) * qpi[qi].size());
-        if (e == hipSuccess)
-            e = hipMemcpy(p->wide[6].d_itemsp[qi], qpi[qi].data(), sizeof(int32_t) * qpi[qi].size(), hipMemcpyHostToDevice);
+        if (e == hipSuccess && !qpi[qi].empty()) {
+            e = hipMalloc(&p->wide[6].d_itemsp[qi], sizeof(int32_t) * qpi[qi].size());
+            if (e == hipSuccess)
+                e = hipMemcpy(p->wide[6].d_itemsp[qi], qpi[qi].data(), sizeof(int32_t) * qpi[qi].size(), hipMemcpyHostToDevice);
+        }
     }
     if (e == hipSuccess) e = hipMalloc(&p->d_idispdt, sizeof(int32_t) * nchan);
     if (e == hipSuccess) e = hipMemcpy(p->d_idispdt, p->idispdt.data(), sizeof(int32_t) * nchan, hipMemcpyHostToDevice);

@@ -178,7 +178,7 @@ hipError_t launch_stage2_pair_multi(const Stage2Args& a, const S2Multi& m, int q
 size_t stage2_qp_lds_bytes(int E, int npw, int nbp, int nsub, int umax, int ppc);
 // one k_stage2_qp expand item: entries 4 g .. 4 g + 3 of pattern u of the chunk's pair k; the
 // pair's first-subband base parity and the pattern's second-subband offset k1
-inline int32_t stage2_qp_item(int g, int k, int u, int par, int k1)
+__host__ __device__ inline int32_t stage2_qp_item(int g, int k, int u, int par, int k1)
 {
     return (int32_t)((uint32_t)g | ((uint32_t)k << 10) | ((uint32_t)u << 12) | ((uint32_t)par << 15) |
                      ((uint32_t)k1 << 16));

@@ -2160,11 +2160,35 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
     // staging slot of chunk cc -> quarter entries of every pattern of its PPC pairs.  Items
     // (pair k, pattern u, entry group g: entries 4g .. 4g+3 of pattern u) come from the host's
     // per-chunk list in the slot (one word per thread: no table walk, no index arithmetic).
-    auto expand = [&](int cc) {
+    // (a plan whose item list does not fit the slot has nip = 0: the items are then derived
+    // from the pair table here, the walk the list replaces)
+    auto item_of = [&](int idx, int chk, const int (&nk)[PPC + 1]) {
+        int k = 0;
+#pragma unroll
+        for (int kk = 1; kk < PPC; kk++)
+            if (idx >= nk[kk]) k = kk;
+        const int32_t* pt = ltab + (PPC * chk + k) * kPairTab;
+        const int ng = pt[9] >> 2;
+        int g = idx - nk[k], u = 0;
+#pragma unroll
+        for (int uu = 1; uu < kPairUMax; uu++)
+            if (g >= ng) { g -= ng; u++; }
+        return stage2_qp_item(g, k, u, pt[0] & 1, pt[3 + u]);
+    };
+    auto expand = [&](int cc, int chk) {
         const char* slot = lds_raw + ring0 + (cc % NS) * slot_bytes;
         const int32_t* iw = (const int32_t*)(slot + (2 * PPC * npw + nbp) * 1024);
-        for (int idx = threadIdx.x; idx < nip * 256; idx += nthr) {
-            const int w = iw[idx];
+        int nk[PPC + 1];
+        nk[0] = 0;
+        if (nip == 0)
+#pragma unroll
+            for (int k = 0; k < PPC; k++) {
+                const int32_t* pt = ltab + (PPC * chk + k) * kPairTab;
+                nk[k + 1] = nk[k] + pt[2] * (pt[9] >> 2);
+            }
+        const int nit = nip > 0 ? nip * 256 : nk[PPC];
+        for (int idx = threadIdx.x; idx < nit; idx += nthr) {
+            const int w = nip > 0 ? iw[idx] : item_of(idx, chk, nk);
             if (w < 0) continue;
             const int g = w & 1023, k = (w >> 10) & 3, u = (w >> 12) & 7;
             const uint32_t* S0 = (const uint32_t*)(slot + (2 * k) * npw * 1024);
@@ -2247,14 +2271,14 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
     for (int cc = 0; cc < NS - 1; cc++) dma(cc);
     wait_ring();
     ring_barrier();
-    expand(0);
+    expand(0, 0);
     ring_barrier();
 
     int chk = 0, ktile = 0;
     for (int c = 0; c < ntot; c++) {
         if (!(PRB && (a.probe & 2))) dma(c + NS - 1);
         const int chn = chk + 1 == nchunk ? 0 : chk + 1;
-        if (c + 1 < ntot && !(PRB && (a.probe & 8))) expand(c + 1);
+        if (c + 1 < ntot && !(PRB && (a.probe & 8))) expand(c + 1, chn);
         const int voff = read_voff(c);
         if (!(PRB && (a.probe & 1))) {
             constexpr int nsteps = PPC * Q, LA = qp_la<Q, RQ>() < nsteps - 1 ? qp_la<Q, RQ>() : nsteps - 1;
@@ -2319,7 +2343,7 @@ static hipError_t launch_qp_n(const Stage2Args& a, const S2Multi& m, int nyblk, 
     size_t lds = 0;
     for (int i = 0; i < m.npass; i++) {
         // (the expand items are nip more pieces of the chunk, like the offset block's)
-        if (2 * PPC * m.p[i].npw + m.p[i].nbp + m.p[i].nip > 32 || m.p[i].nip < 1 || !m.p[i].items)
+        if (2 * PPC * m.p[i].npw + m.p[i].nbp + m.p[i].nip > 32 || m.p[i].nip < 0 || (m.p[i].nip > 0 && !m.p[i].items))
             return hipErrorInvalidValue;
         lds = std::max(lds, stage2_qp_lds_bytes(m.p[i].ws, m.p[i].npw, m.p[i].nbp + m.p[i].nip, a.nsub, m.p[i].umax, PPC));
     }
