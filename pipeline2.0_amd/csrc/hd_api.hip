@@ -235,8 +235,6 @@ struct hd_plan {
         int32_t* d_omin = nullptr;      // [3]: the pair table (kPairTab ints per y-block and pair)
         int32_t* d_boff = nullptr;
         int32_t* d_boffp[3] = {nullptr, nullptr, nullptr};   // [6]: the offsets for 4, 3, 2 pairs per chunk
-        int32_t* d_itemsp[3] = {nullptr, nullptr, nullptr};  // [6]: the expand items for 4, 3, 2 pairs per chunk
-        int32_t nipp[3] = {0, 0, 0};                          //      (their 1 KiB pieces per chunk)
     } wide[7];                      // [2]: k_stage2_ring (16 waves, LDS-DMA staging ring);
                                     // [3]: k_stage2_pair (the ring over subband-pair partials),
                                     // [4]: the same with two pairs per chunk (half the chunks),
@@ -1395,7 +1393,6 @@ static void plan_free(hd_plan* p)
         dfree(w.d_omin);
         dfree(w.d_boff);
         for (auto& q : w.d_boffp) dfree(q);
-        for (auto& q : w.d_itemsp) dfree(q);
     }
     dfree(p->d_out);
     dfree(p->d_sub);
@@ -1677,7 +1674,7 @@ static bool qp_auto()
 // DM sweep, a multiple of 4).  boff[yb][c][k] = LDS byte offset (from the expanded area) of
 // DM k's entry 0: buffer ((c / ppc) & 1) * ppc + c % ppc, pattern u(k), entry o2 = o0 - base0.
 static void qp_tables(hd_plan* p, bool i16, hd_plan::Wide& w, std::vector<int32_t>& ptab, std::vector<int32_t>& boff,
-                      std::vector<int32_t> (&boffp)[3], std::vector<int32_t> (&itemsp)[3])
+                      std::vector<int32_t> (&boffp)[3])
 {
     w = hd_plan::Wide{};
     constexpr int RQ = 3, S = 64 * RQ, T = 4 * S;
@@ -1727,55 +1724,14 @@ static void qp_tables(hd_plan* p, bool i16, hd_plan::Wide& w, std::vector<int32_
     // takes the smallest of its passes' (the offset block per chunk is sized for 4 pairs)
     const int npw = (int)((((size_t)Emax + 3 * S + k1max + 8) * 2 + 1023) / 1024);
     const int nbp = (int)(((size_t)4 * dpb * 4 + 1023) / 1024);
-    // the expand items per (y-block, chunk) for q pairs per chunk: entry group g of pattern u of
-    // the chunk's pair k (stage2_qp_item), padded with -1 to nip * 256 words
-    auto items_for = [&](int q, std::vector<int32_t>* out) {
-        int most = 0;
-        for (int yb = 0; yb < nyb; yb++)
-            for (int c0 = 0; c0 + q <= npair; c0 += q) {
-                int n = 0;
-                for (int k = 0; k < q; k++) {
-                    const int32_t* t = &ptab[((size_t)yb * npair + c0 + k) * hd::kPairTab];
-                    n += t[2] * (t[9] / 4);
-                }
-                most = std::max(most, n);
-            }
-        const int nip = (most + 255) / 256;
-        if (out) {
-            const int nchunk = npair / q;
-            out->assign((size_t)nyb * nchunk * nip * 256, -1);
-            for (int yb = 0; yb < nyb; yb++)
-                for (int ch = 0; ch < nchunk; ch++) {
-                    int32_t* o = &(*out)[((size_t)yb * nchunk + ch) * nip * 256];
-                    int n = 0;
-                    for (int k = 0; k < q; k++) {
-                        const int32_t* t = &ptab[((size_t)yb * npair + ch * q + k) * hd::kPairTab];
-                        for (int u = 0; u < t[2]; u++)
-                            for (int g = 0; g < t[9] / 4; g++) o[n++] = hd::stage2_qp_item(g, k, u, t[0] & 1, t[3 + u]);
-                    }
-                }
-        }
-        return nip;
-    };
-    // pieces of a chunk's item list at q pairs per chunk, or 0 (items derived in the kernel)
-    // when the list does not fit beside the windows
-    auto nip_fit = [&](int q) {
-        const int nip = items_for(q, nullptr);
-        return 2 * q * npw + nbp + nip <= 32 && hd::stage2_qp_lds_bytes(Emax, npw, nbp + nip, nsub, umax, q) <= 160 * 1024
-                   ? nip : 0;
-    };
     int ppc = 0;
-    for (int cand : {4, 3, 2}) {
-        if ((nsub / 2) % cand) continue;
-        const int nip = nip_fit(cand);
-        if (2 * cand * npw + nbp + nip <= 32 &&
-            hd::stage2_qp_lds_bytes(Emax, npw, nbp + nip, nsub, umax, cand) <= 160 * 1024) {
+    for (int cand : {4, 3, 2})
+        if ((nsub / 2) % cand == 0 && 2 * cand * npw + nbp <= 32 &&
+            hd::stage2_qp_lds_bytes(Emax, npw, nbp, nsub, umax, cand) <= 160 * 1024) {
             ppc = cand;
             break;
         }
-    }
-    // (item fields: g < 1024, k1 < 65536)
-    if (!ppc || !hd::stage2_qp_supports(Q, RQ) || (size_t)npw * 512 > 4096 || Emax / 4 > 1023 || k1max > 65535) return;
+    if (!ppc || !hd::stage2_qp_supports(Q, RQ) || (size_t)npw * 512 > 4096) return;
     // one offsets table per pairs-per-chunk a shared launch may take (ppc and every smaller
     // candidate dividing the pair count): buffer ((c / q) & 1) * q + c % q of pair c
     for (int qi = 0; qi < 3; qi++) {
@@ -1783,8 +1739,6 @@ static void qp_tables(hd_plan* p, bool i16, hd_plan::Wide& w, std::vector<int32_
         std::vector<int32_t>& bo = boffp[qi];
         bo.clear();
         if (q > ppc || (nsub / 2) % q) continue;
-        w.nipp[qi] = nip_fit(q);
-        if (w.nipp[qi]) items_for(q, &itemsp[qi]);
         bo.assign((size_t)nyb * npair * dpb + 256, 0);   // the last DMA piece may over-read
         for (int yb = 0; yb < nyb; yb++)
             for (int c = 0; c < npair; c++) {
@@ -2006,8 +1960,8 @@ extern "C" int hd_plan_create(hd_ctx* c, const hd_pass* ps, hd_plan** out)
     pair_tables(p, c->opts.sub_dtype == HD_SUB_I16, 1, p->wide[3], womin[3], wboff[3]);
     pair_tables(p, c->opts.sub_dtype == HD_SUB_I16, 2, p->wide[4], womin[4], wboff[4]);
     rw_tables(p, c->opts.sub_dtype == HD_SUB_I16, p->wide[5], womin[5], wboff[5]);
-    std::vector<int32_t> qpb[3], qpi[3];
-    qp_tables(p, c->opts.sub_dtype == HD_SUB_I16, p->wide[6], womin[6], wboff[6], qpb, qpi);
+    std::vector<int32_t> qpb[3];
+    qp_tables(p, c->opts.sub_dtype == HD_SUB_I16, p->wide[6], womin[6], wboff[6], qpb);
 
     int rc = HD_OK;
     hipError_t e = hipSetDevice(c->device);
@@ -2024,11 +1978,6 @@ extern "C" int hd_plan_create(hd_ctx* c, const hd_pass* ps, hd_plan** out)
         e = hipMalloc(&p->wide[6].d_boffp[qi], sizeof(int32_t) * qpb[qi].size());
         if (e == hipSuccess)
             e = hipMemcpy(p->wide[6].d_boffp[qi], qpb[qi].data(), sizeof(int32_t) * qpb[qi].size(), hipMemcpyHostToDevice);
-        if (e == hipSuccess && !qpi[qi].empty()) {
-            e = hipMalloc(&p->wide[6].d_itemsp[qi], sizeof(int32_t) * qpi[qi].size());
-            if (e == hipSuccess)
-                e = hipMemcpy(p->wide[6].d_itemsp[qi], qpi[qi].data(), sizeof(int32_t) * qpi[qi].size(), hipMemcpyHostToDevice);
-        }
     }
     if (e == hipSuccess) e = hipMalloc(&p->d_idispdt, sizeof(int32_t) * nchan);
     if (e == hipSuccess) e = hipMemcpy(p->d_idispdt, p->idispdt.data(), sizeof(int32_t) * nchan, hipMemcpyHostToDevice);
@@ -3879,8 +3828,6 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         a.umax = w.umax;
         a.nonneg = p->sub_nonneg ? 1 : 0;
         a.nwg = p->pair_persist != 2 ? c->ncu : 0;   // persistent by default (measured 1.29 vs 1.36 ms, stage-0 pass)
-        a.items = wk == 6 ? w.d_itemsp[4 - w.sc] : nullptr;
-        a.nip = wk == 6 ? w.nipp[4 - w.sc] : 0;
         if (wk == 0) HIPCHK(c, hd::launch_stage2_wide(a, w.q, w.r, w.nw, st));
         else if (wk == 1) HIPCHK(c, hd::launch_stage2_wide2(a, w.q, w.r, w.nw, st));
         else if (wk == 2) HIPCHK(c, hd::launch_stage2_ring(a, w.q, w.r, st));
@@ -4045,8 +3992,6 @@ static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
         q.sub = p->d_sub;
         q.ptab = w.d_omin;
         q.off = wk == 6 ? w.d_boffp[4 - ppc6] : w.d_boff;
-        q.items = wk == 6 ? w.d_itemsp[4 - ppc6] : nullptr;
-        q.nip = wk == 6 ? w.nipp[4 - ppc6] : 0;
         q.maxabs = p->d_maxabs;
         q.out = p->d_out;
         q.partial = partial ? partial + per * i : nullptr;

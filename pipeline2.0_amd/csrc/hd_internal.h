@@ -108,9 +108,6 @@ struct Stage2Args {
     const int32_t* ptab;
     int32_t umax;
     int32_t nonneg;           // pair variant: every subband value is >= 0 (unsigned packed halves)
-    // k_stage2_qp: per (y-block, chunk) nip * 256 expand items (stage2_qp_item), -1 padded
-    const int32_t* items;
-    int32_t nip;
 };
 
 hipError_t launch_stage1_direct(const Stage1Args& a, hipStream_t st);
@@ -158,8 +155,6 @@ struct S2Pass {
     double* partial;
     int64_t sub_stride;
     int32_t ws, npw, nbp, umax;
-    const int32_t* items;     // k_stage2_qp: the expand items (Stage2Args::items)
-    int32_t nip;
 };
 constexpr int kS2MaxPass = 28;
 struct S2Multi {
@@ -176,13 +171,6 @@ hipError_t launch_stage2_rw_multi(const Stage2Args& a, const S2Multi& m, int q, 
 hipError_t launch_stage2_pair_multi(const Stage2Args& a, const S2Multi& m, int q, int r, int ppc, hipStream_t st);
 // quarter-layout pair kernel (k_stage2_qp): ws = entries per pattern buffer, ppc 2..4 pairs per chunk
 size_t stage2_qp_lds_bytes(int E, int npw, int nbp, int nsub, int umax, int ppc);
-// one k_stage2_qp expand item: entries 4 g .. 4 g + 3 of pattern u of the chunk's pair k; the
-// pair's first-subband base parity and the pattern's second-subband offset k1
-__host__ __device__ inline int32_t stage2_qp_item(int g, int k, int u, int par, int k1)
-{
-    return (int32_t)((uint32_t)g | ((uint32_t)k << 10) | ((uint32_t)u << 12) | ((uint32_t)par << 15) |
-                     ((uint32_t)k1 << 16));
-}
 bool stage2_qp_supports(int q, int r);
 hipError_t launch_stage2_qp_multi(const Stage2Args& a, const S2Multi& m, int q, int r, int ppc, hipStream_t st);
 hipError_t launch_stage2_wide2(const Stage2Args& a, int q, int r, int nw, hipStream_t st);

@@ -1897,8 +1897,6 @@ S2Pass stage2_pass_of(const Stage2Args& a)
     p.npw = a.ring_npw;
     p.nbp = a.ring_nbp;
     p.umax = a.umax;
-    p.items = a.items;
-    p.nip = a.nip;
     return p;
 }
 
@@ -2052,9 +2050,8 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
     const int E = P.ws;                          // entries per pattern buffer (max over pairs)
     const int npw = P.npw;                       // 1 KiB DMA pieces per window
     const int nbp = P.nbp;                       // pieces of a chunk's offset block
-    const int nip = P.nip;                       // pieces of a chunk's expand items
     const int umax = P.umax;
-    const int npiece = 2 * PPC * npw + nbp + nip;   // DMA pieces per chunk (<= 32: two per wave)
+    const int npiece = 2 * PPC * npw + nbp;      // DMA pieces per chunk (<= 32: two per wave)
     const int pw = (npiece - wave + NW - 1) / NW;  // this wave's pieces per chunk: 0 .. 3
     const int slot_bytes = npiece * 1024;
     const int npair = a.nsub >> 1;
@@ -2131,13 +2128,9 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
                 const int64_t e0 = t0 + b - (b & 1);
                 const char* src = (const char*)(sub + (int64_t)s * P.sub_stride + e0) + pcs * 1024;
                 dma16s(src, (uint32_t)lane * 16u, slot + (uint32_t)(pc * 1024));
-            } else if (pc < 2 * PPC * npw + nbp) {
+            } else {
                 const int bp = pc - 2 * PPC * npw;
                 const char* src = (const char*)(bo_g + (int64_t)PPC * c2 * dpb) + bp * 1024;
-                dma16s(src, (uint32_t)lane * 16u, slot + (uint32_t)(pc * 1024));
-            } else {
-                const int ip = pc - 2 * PPC * npw - nbp;
-                const char* src = (const char*)(P.items + ((int64_t)yb * nchunk + c2) * (nip * 256)) + ip * 1024;
                 dma16s(src, (uint32_t)lane * 16u, slot + (uint32_t)(pc * 1024));
             }
         }
@@ -2157,43 +2150,32 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
     };
-    // staging slot of chunk cc -> quarter entries of every pattern of its PPC pairs.  Items
-    // (pair k, pattern u, entry group g: entries 4g .. 4g+3 of pattern u) come from the host's
-    // per-chunk list in the slot (one word per thread: no table walk, no index arithmetic).
-    // (a plan whose item list does not fit the slot has nip = 0: the items are then derived
-    // from the pair table here, the walk the list replaces)
-    auto item_of = [&](int idx, int chk, const int (&nk)[PPC + 1]) {
-        int k = 0;
-#pragma unroll
-        for (int kk = 1; kk < PPC; kk++)
-            if (idx >= nk[kk]) k = kk;
-        const int32_t* pt = ltab + (PPC * chk + k) * kPairTab;
-        const int ng = pt[9] >> 2;
-        int g = idx - nk[k], u = 0;
-#pragma unroll
-        for (int uu = 1; uu < kPairUMax; uu++)
-            if (g >= ng) { g -= ng; u++; }
-        return stage2_qp_item(g, k, u, pt[0] & 1, pt[3 + u]);
-    };
+    // staging slot of chunk cc -> quarter entries of every pattern of its PPC pairs.
+    // Item (pair k, entry group g): entries 4g .. 4g+3 of each of the pair's U patterns.
     auto expand = [&](int cc, int chk) {
         const char* slot = lds_raw + ring0 + (cc % NS) * slot_bytes;
-        const int32_t* iw = (const int32_t*)(slot + (2 * PPC * npw + nbp) * 1024);
         int nk[PPC + 1];
         nk[0] = 0;
-        if (nip == 0)
 #pragma unroll
-            for (int k = 0; k < PPC; k++) {
-                const int32_t* pt = ltab + (PPC * chk + k) * kPairTab;
-                nk[k + 1] = nk[k] + pt[2] * (pt[9] >> 2);
-            }
-        const int nit = nip > 0 ? nip * 256 : nk[PPC];
-        for (int idx = threadIdx.x; idx < nit; idx += nthr) {
-            const int w = nip > 0 ? iw[idx] : item_of(idx, chk, nk);
-            if (w < 0) continue;
-            const int g = w & 1023, k = (w >> 10) & 3, u = (w >> 12) & 7;
+        for (int k = 0; k < PPC; k++) {
+            const int32_t* pt = ltab + (PPC * chk + k) * kPairTab;
+            nk[k + 1] = nk[k] + pt[2] * (pt[9] >> 2);
+        }
+        // item (pair k, pattern u, entry group g): entries 4g .. 4g+3 of pattern u
+        for (int idx = threadIdx.x; idx < nk[PPC]; idx += nthr) {
+            int k = 0;
+#pragma unroll
+            for (int kk = 1; kk < PPC; kk++)
+                if (idx >= nk[kk]) k = kk;
+            const int32_t* pt = ltab + (PPC * chk + k) * kPairTab;
+            const int ng = pt[9] >> 2;
+            int g = idx - nk[k], u = 0;
+#pragma unroll
+            for (int uu = 1; uu < kPairUMax; uu++)
+                if (g >= ng) { g -= ng; u++; }
             const uint32_t* S0 = (const uint32_t*)(slot + (2 * k) * npw * 1024);
             const uint32_t* S1 = (const uint32_t*)(slot + (2 * k + 1) * npw * 1024);
-            const int x0 = 4 * g + ((w >> 15) & 1), x1 = 4 * g + (int)((uint32_t)w >> 16);
+            const int x0 = 4 * g + (pt[0] & 1), x1 = 4 * g + pt[3 + u];
             uint32_t Pq[4][2];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -2342,10 +2324,8 @@ static hipError_t launch_qp_n(const Stage2Args& a, const S2Multi& m, int nyblk, 
     if (nx == ntiles) b.nwg = 0;
     size_t lds = 0;
     for (int i = 0; i < m.npass; i++) {
-        // (the expand items are nip more pieces of the chunk, like the offset block's)
-        if (2 * PPC * m.p[i].npw + m.p[i].nbp + m.p[i].nip > 32 || m.p[i].nip < 0 || (m.p[i].nip > 0 && !m.p[i].items))
-            return hipErrorInvalidValue;
-        lds = std::max(lds, stage2_qp_lds_bytes(m.p[i].ws, m.p[i].npw, m.p[i].nbp + m.p[i].nip, a.nsub, m.p[i].umax, PPC));
+        if (2 * PPC * m.p[i].npw + m.p[i].nbp > 32) return hipErrorInvalidValue;
+        lds = std::max(lds, stage2_qp_lds_bytes(m.p[i].ws, m.p[i].npw, m.p[i].nbp, a.nsub, m.p[i].umax, PPC));
     }
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     S2Multi mm = m;
