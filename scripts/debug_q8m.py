@@ -7,7 +7,7 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [os.path.join(ROOT, "pipeline2.0_amd"), ROOT]
+sys.path[:0] = [os.path.join(ROOT, "oracle"), os.path.join(ROOT, "pipeline2.0_amd"), ROOT]
 import oracle as OR  # noqa: E402
 from hipdedisp import Engine, Opts, PassParams, plan as P  # noqa: E402
 from hipdedisp.synth import host_spectra, palfa_obs, palfa_synth, rfifind_ptsperint, synth_mask  # noqa: E402
