@@ -33,3 +33,11 @@ def engine():
     eng = Engine(0)
     yield eng
     eng.close()
+
+
+def pytest_runtest_logreport(report):
+    """A failing test's report printed at once: the session's engine closes at teardown, and a
+    process that aborts there would otherwise take the failure summary with it."""
+    if report.failed and report.when == "call":
+        sys.stderr.write("\n==== failure of %s ====\n%s\n" % (report.nodeid, str(report.longrepr)[-6000:]))
+        sys.stderr.flush()
