@@ -124,6 +124,20 @@ __device__ __forceinline__ int wave_max_full(int v)
     return __builtin_amdgcn_readlane(v, 63);
 }
 
+// The exact sum over the wave of int v, by DPP steps inside the VALU (quad permutes, row
+// mirrors, row broadcast 15) and two lane reads, instead of six dependent ds_bpermute round
+// trips of an int64.  The caller guarantees every partial fits int32: |v| * 32 < 2^31.  Every
+// lane of the wave must be active (EXEC all ones).
+__device__ __forceinline__ int64_t wave_sum_i32_small(int v)
+{
+    v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]: quad sums
+    v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false);  // row_half_mirror: 8-lane sums
+    v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false);  // row_mirror: row sums
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    return (int64_t)__builtin_amdgcn_readlane(v, 31) + (int64_t)__builtin_amdgcn_readlane(v, 63);
+}
+
 // Raise *addr to v.  Every wave of a pass targets the same word, and same-address atomics
 // serialise at the memory side, so read first (a stale value only costs an extra atomic;
 // atomicMax is monotone, so the result is exact) and publish only a new maximum.

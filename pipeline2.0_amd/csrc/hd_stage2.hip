@@ -2069,6 +2069,7 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
 
     int maxabs = *P.maxabs;
     maxabs = maxabs < 1 ? 1 : maxabs;
+    const bool small_part = (int64_t)a.nsub * maxabs * (RQ * 4) * 32 < ((int64_t)1 << 31);
     int G = (NN ? 65535 : 32767) / (2 * maxabs);
     G = G < 1 ? 1 : (G > 64 ? 64 : G);
     G = __builtin_amdgcn_readfirstlane(G);
@@ -2226,8 +2227,14 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
                 }
             }
             if (dv && P.partial) {
+                // (uniform) a lane's partial is at most RQ * 4 series values of |v| <= nsub *
+                // max|subband|: when 32 of them fit int32, the DPP sum; else the int64 butterfly
+                if (small_part) {
+                    part = wave_sum_i32_small((int)part);
+                } else {
 #pragma unroll
-                for (int mm = 32; mm >= 1; mm >>= 1) part += __shfl_xor(part, mm, 64);
+                    for (int mm = 32; mm >= 1; mm >>= 1) part += __shfl_xor(part, mm, 64);
+                }
                 if (lane == 0) P.partial[(int64_t)d * a.ntiles + tile] = (double)part;
             }
         }
