@@ -289,6 +289,13 @@ class TimeSlices:
 # configs[4]: the 7 beams of an ALFA pointing on one node (beam x time partitioning)
 # ---------------------------------------------------------------------------------------
 
+# slice cost model t(x) = a + b x (ms per slice of x of a beam), fitted to round 5's one-rank
+# measurements (profiles/r05_simslice.jsonl, profiles/r05_bench.jsonl): the whole beam 58.2 ms,
+# slice 0 of 8 12.7 ms, the last slice of 8 13.2 ms -> b = 52.0, a = 6.5 (between the first
+# and the last slice's fixed cost)
+POINTING_FIXED_MS, POINTING_BEAM_MS = 6.5, 52.0
+
+
 def helper_fraction(nbeams, nhelpers, fixed_ms, beam_ms):
     """Home share f of each beam that balances a home rank (one slice of f N spectra) against
     a helper (its share of every beam's tail), for a slice cost t(x) = a + b x (a = fixed_ms,
@@ -323,7 +330,8 @@ class Pointing:
     `units(rank)` lists (beam, slice) pairs in processing order; `slices(beam)` the beam's
     TimeSlices; `owner(beam, slice)` the rank."""
 
-    def __init__(self, obs, ddplans, nbeams, world, frac=None, opts=None, fixed_ms=6.0, beam_ms=61.9):
+    def __init__(self, obs, ddplans, nbeams, world, frac=None, opts=None, fixed_ms=POINTING_FIXED_MS,
+                 beam_ms=POINTING_BEAM_MS):
         if nbeams < 1 or world < 1:
             raise ValueError("need nbeams >= 1 and world >= 1")
         self.obs, self.ddplans, self.nbeams, self.world = obs, list(ddplans), nbeams, world
@@ -369,7 +377,7 @@ class Pointing:
         t0 = self.ts.slice(sl)[0]
         return t0 // self.ts.blk, self.ts.nown_blocks(sl)
 
-    def predicted_ms(self, fixed_ms=6.0, beam_ms=61.9):
+    def predicted_ms(self, fixed_ms=POINTING_FIXED_MS, beam_ms=POINTING_BEAM_MS):
         """Predicted node time per pointing from the slice cost model (a prediction, not a
         measurement): the slowest rank's units."""
         fr = [(self.ts.slice(k)[1]) / float(self.obs.N) for k in range(self.nslices())]
