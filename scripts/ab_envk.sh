@@ -15,5 +15,5 @@ for e in "$@"; do
   python3 scripts/kstats.py "$(find $d -name '*.db' | head -1)" $d.csv
   s=$(python3 scripts/benchline.py $d.log ms) || { echo "no bench line [$e]"; exit 1; }
   echo "== [$e] $s"
-  python3 scripts/kstats_grep.py $d.csv ${WORDS:-fix8}
+  python3 scripts/kstats_grep.py $d.csv ${WORDS:-fix8 transpose}
 done
