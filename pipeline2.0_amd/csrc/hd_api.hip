@@ -21,6 +21,7 @@
 #include <deque>
 #include <mutex>
 #include <map>
+#include <memory>
 #include <tuple>
 #include <chrono>
 #include <string>
@@ -207,6 +208,20 @@ static hipError_t sync_all(hd_ctx* c)
     return e;
 }
 
+// The start / end events of a stage-2 launch.  A multi-pass launch (hd_run_dedisp_multi)
+// records one pair for all the passes it carries, and every plan's dd_cur points at it: one
+// event per plan after the launch had cost the command processor ~5 us each, ~0.3 ms of idle
+// GPU after a 28-pass stage.  Shared ownership keeps a pair valid while any plan refers to it;
+// a later record into it by its owner only moves the end later (a conservative wait).
+struct DdEv {
+    hipEvent_t e[2] = {nullptr, nullptr};
+    ~DdEv()
+    {
+        for (hipEvent_t x : e)
+            if (x) (void)hipEventDestroy(x);
+    }
+};
+
 struct hd_plan {
     hd_ctx* ctx = nullptr;
     hd_pass pass{};
@@ -251,11 +266,12 @@ struct hd_plan {
     int32_t s1_variant = 0;         // stage 1: 0 auto, 1 direct, 2 float tiled, 3 8-bit integer
     int32_t probe = 0;              // profiling switches (hd_plan_set_variant bits 16-23)
     int32_t pair_persist = 0;       // hd_plan_set_variant bits 24-25 (pair kernel tile scheduling)
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t ev[2] = {nullptr, nullptr};   // stage 1: start, end (recorded by the call's first plan)
+    std::shared_ptr<DdEv> dd_own, dd_cur;    // stage 2: this plan's pair; the pair ending its last stage 2
     hipEvent_t ev_copy = nullptr;   // after the writer's copies of this plan's series
     bool copy_pending = false;
     bool ran_sub = false, ran_dd = false;
-    hipStream_t dd_stream = nullptr;  // stream of the last hd_run_dedisp (its ev[3] marks the end)
+    hipStream_t dd_stream = nullptr;  // stream of the last hd_run_dedisp (dd_end() marks the end)
     hd::FftState* fft = nullptr;    // realfft state (hd_fft.hip, from hd_ctx::fft_cache)
     bool ran_fft = false;
     // barycentric output (hd_plan_set_bary): stage 2 writes the topocentric series to d_topo,
@@ -271,6 +287,9 @@ struct hd_plan {
     float* d_padv = nullptr;
     struct SpPlan* sp = nullptr;    // single-pulse search state (hd_single_pulse_launch / _collect)
 };
+
+static hipEvent_t dd_start(const hd_plan* p) { return p->dd_cur ? p->dd_cur->e[0] : nullptr; }
+static hipEvent_t dd_end(const hd_plan* p) { return p->dd_cur ? p->dd_cur->e[1] : nullptr; }
 
 // Device buffers of one single-pulse search in flight (block coefficients, hit list, hit
 // count, bad flags) and the event after its device half: a context pool, taken by a launch
@@ -1403,6 +1422,8 @@ static void plan_free(hd_plan* p)
     p->fft = nullptr;
     for (auto& e : p->ev)
         if (e) (void)hipEventDestroy(e);
+    p->dd_cur.reset();
+    p->dd_own.reset();
     if (p->ev_copy) (void)hipEventDestroy(p->ev_copy);
     if (p->sp) {
         if (p->sp->b) {                               // a search never collected: its buffers back
@@ -1989,7 +2010,12 @@ extern "C" int hd_plan_create(hd_ctx* c, const hd_pass* ps, hd_plan** out)
     if (e == hipSuccess) e = hipMemcpy(p->d_omin, omin.data(), sizeof(int32_t) * omin.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&p->d_boff, sizeof(int32_t) * boff.size());
     if (e == hipSuccess) e = hipMemcpy(p->d_boff, boff.data(), sizeof(int32_t) * boff.size(), hipMemcpyHostToDevice);
-    for (int i = 0; i < 4 && e == hipSuccess; i++) e = hipEventCreate(&p->ev[i]);
+    for (int i = 0; i < 2 && e == hipSuccess; i++) e = hipEventCreate(&p->ev[i]);
+    if (e == hipSuccess) {
+        p->dd_own = std::make_shared<DdEv>();
+        p->dd_cur = p->dd_own;
+        for (int i = 0; i < 2 && e == hipSuccess; i++) e = hipEventCreate(&p->dd_own->e[i]);
+    }
     if (e != hipSuccess) {
         rc = fail(c, HD_E_HIP, "hd_plan_create: %s", hipGetErrorString(e));
         plan_free(p);
@@ -2950,7 +2976,7 @@ extern "C" int hd_run_subband_multi(hd_plan** plans, int32_t n)
         // overlaps the current stage's stage 2)
         for (int i = 0; i < n; i++)
             if (plans[i]->ran_dd && plans[i]->dd_stream == c->stream2)
-                HIPCHK(c, hipStreamWaitEvent(c->stream, plans[i]->ev[3], 0));
+                HIPCHK(c, hipStreamWaitEvent(c->stream, dd_end(plans[i]), 0));
     } else {
         HIPCHK(c, join_stream2(c));      // a stage-2 pass on stream2 may still read these subbands
     }
@@ -3523,7 +3549,7 @@ extern "C" int hd_series_sum_multi(hd_plan* const* plans, int32_t n, int32_t dm,
     for (int i = 0; i < n; i++) {
         hd_plan* p = plans[i];
         if (count[i] == 0) continue;
-        if (p->dd_stream && p->dd_stream != c->stream) HIPCHK(c, hipStreamWaitEvent(c->stream, p->ev[3], 0));
+        if (p->dd_stream && p->dd_stream != c->stream) HIPCHK(c, hipStreamWaitEvent(c->stream, dd_end(p), 0));
         HIPCHK(c, hd::launch_series_sum(p->d_out + (size_t)dm * p->out_stride + t0[i], count[i],
                                         c->d_sum_parts_multi + (size_t)i * kParts, kParts, c->stream));
     }
@@ -3545,7 +3571,8 @@ extern "C" int hd_series_fill(hd_plan* p, int64_t t0, float value)
     if (t0 < 0 || t0 > p->numout) return fail(c, HD_E_INVAL, "hd_series_fill: t0 outside [0, %lld]", (long long)p->numout);
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hd::launch_series_fill(p->d_out, p->out_stride, p->pass.numdms, t0, p->numout, value, p->dd_stream));
-    HIPCHK(c, hipEventRecord(p->ev[3], p->dd_stream));   // the series' end: hd_write_series copies after it
+    p->dd_cur = p->dd_own;           // (a pair this plan shared with a multi launch's other passes stays theirs)
+    HIPCHK(c, hipEventRecord(dd_end(p), p->dd_stream));   // the series' end: hd_write_series copies after it
     return HD_OK;
 }
 
@@ -3684,8 +3711,8 @@ extern "C" int hd_plan_set_bary(hd_plan* p, const int32_t* diffbins, int32_t ndi
     }
     HIPCHK(c, hipSetDevice(c->device));
     // the old segment table may still be read by this plan's queued stage 2 / k_bary, and its
-    // series by the writer: wait for exactly those (ev[3] ends the plan's last hd_run_dedisp)
-    if (p->ran_dd && p->ev[3]) HIPCHK(c, hipEventSynchronize(p->ev[3]));
+    // series by the writer: wait for exactly those (dd_end ends the plan's last hd_run_dedisp)
+    if (p->ran_dd && dd_end(p)) HIPCHK(c, hipEventSynchronize(dd_end(p)));
     if (p->copy_pending && c->writer) HIPCHK(c, hipEventSynchronize(p->ev_copy));
     dfree(p->d_bseg);
     p->d_bseg = nullptr;
@@ -3749,7 +3776,7 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
         HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
     }
-    if (p->ran_dd && p->dd_stream != st) HIPCHK(c, hipStreamWaitEvent(st, p->ev[3], 0));
+    if (p->ran_dd && p->dd_stream != st) HIPCHK(c, hipStreamWaitEvent(st, dd_end(p), 0));
     if (p->copy_pending) {            // the writer may still be copying the previous series
         HIPCHK(c, hipStreamWaitEvent(st, p->ev_copy, 0));
         p->copy_pending = false;
@@ -3813,7 +3840,8 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
     a.omin = p->d_omin;
     a.wstride = p->wstride;
     a.dms_per_blk = p->dpb;
-    HIPCHK(c, hipEventRecord(p->ev[2], st));
+    p->dd_cur = p->dd_own;
+    HIPCHK(c, hipEventRecord(dd_start(p), st));
     if (use_wide) {
         const hd_plan::Wide& w = p->wide[wk];
         a.off = w.d_boff;
@@ -3862,7 +3890,7 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
     else if (pad)
         HIPCHK(c, hd::launch_pad(p->d_out, p->out_stride, p->pass.numdms, p->nds, p->numout, partial, ntiles,
                                  c->opts.pad_mode, st));
-    HIPCHK(c, hipEventRecord(p->ev[3], st));
+    HIPCHK(c, hipEventRecord(dd_end(p), st));
     if (alt) {
         HIPCHK(c, hipEventRecord(c->ev_join, st));
         c->s2_pending = true;
@@ -3930,7 +3958,7 @@ static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
                 return fail(c, HD_E_NOMEM, "cannot allocate %zu bytes of DM series", bytes);
             }
         }
-        if (p->ran_dd && p->dd_stream != st) HIPCHK(c, hipStreamWaitEvent(st, p->ev[3], 0));
+        if (p->ran_dd && p->dd_stream != st) HIPCHK(c, hipStreamWaitEvent(st, dd_end(p), 0));
         if (p->copy_pending) {
             HIPCHK(c, hipStreamWaitEvent(st, p->ev_copy, 0));
             p->copy_pending = false;
@@ -4001,7 +4029,8 @@ static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
         q.nbp = w.nbp;
         q.umax = w.umax;
     }
-    HIPCHK(c, hipEventRecord(p0->ev[2], st));
+    p0->dd_cur = p0->dd_own;
+    HIPCHK(c, hipEventRecord(dd_start(p0), st));
     if (wk == 5) HIPCHK(c, hd::launch_stage2_rw_multi(a, m, w0.q, st));
     else if (wk == 6) HIPCHK(c, hd::launch_stage2_qp_multi(a, m, w0.q, w0.r, ppc6, st));
     else HIPCHK(c, hd::launch_stage2_pair_multi(a, m, w0.q, w0.r, 2, st));
@@ -4009,10 +4038,10 @@ static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
         for (int i = 0; i < n; i++)
             HIPCHK(c, hd::launch_pad(g[i]->d_out, g[i]->out_stride, g[i]->pass.numdms, g[i]->nds, g[i]->numout,
                                      m.p[i].partial, ntiles, c->opts.pad_mode, st));
+    HIPCHK(c, hipEventRecord(dd_end(p0), st));       // one pair for every pass of the launch
     for (int i = 0; i < n; i++) {
         hd_plan* p = g[i];
-        if (i > 0) HIPCHK(c, hipEventRecord(p->ev[2], st));
-        HIPCHK(c, hipEventRecord(p->ev[3], st));
+        p->dd_cur = p0->dd_own;
         p->ran_dd = true;
         p->dd_stream = st;
         p->s2passes = i == 0 ? n : 0;
@@ -4081,7 +4110,7 @@ extern "C" int hd_write_series(hd_plan* p, const char* const* paths, int32_t wai
     if (!c->writer) HIPCHK(c, hd::writer_open(&c->writer, c->device));
     if (!p->ev_copy) HIPCHK(c, hipEventCreateWithFlags(&p->ev_copy, hipEventDisableTiming));
     std::string err;
-    int rc = hd::writer_series(c->writer, p->ev[3], p->d_out, p->out_stride, p->pass.numdms, p->numout, paths, err);
+    int rc = hd::writer_series(c->writer, dd_end(p), p->d_out, p->out_stride, p->pass.numdms, p->numout, paths, err);
     // even after a failure part-way (a file that cannot be created, a copy that fails), the
     // chunks queued before it keep copying from p->d_out: a later hd_run_dedisp of this plan
     // must wait for them, so the copy event is recorded whatever rc is
@@ -4121,8 +4150,8 @@ extern "C" int hd_plan_last_ms(const hd_plan* p, float* ms_sub, float* ms_dd)
     if (ms_dd) {
         *ms_dd = 0.0f;
         if (p->ran_dd) {
-            HIPCHK(c, hipEventSynchronize(p->ev[3]));
-            if (p->s2passes > 0) HIPCHK(c, hipEventElapsedTime(ms_dd, p->ev[2], p->ev[3]));
+            HIPCHK(c, hipEventSynchronize(dd_end(p)));
+            if (p->s2passes > 0) HIPCHK(c, hipEventElapsedTime(ms_dd, dd_start(p), dd_end(p)));
         }
     }
     return HD_OK;
