@@ -174,40 +174,18 @@ __global__ __launch_bounds__(1024) void k_clip_block(ClipArgs a)
     if (threadIdx.x == 0) a.numgood[b] = cnt;
 }
 
-// ---- per block: avg_var over the good points, in time order (one wave per block) ------
-// The block's good points are first compacted into LDS in time order by the whole wave
-// (coalesced loads, none of them on the recurrence's path); lane 0 then runs the recurrence
-// from LDS.  One thread per block walking global memory had waited on a load per spectrum:
-// 0.52 ms per beam alone, 2.1 ms beside the channel-major copy's HBM traffic.
+// ---- per block: avg_var over the good points, in time order (one thread per block) --
 __global__ __launch_bounds__(64) void k_clip_as52(ClipArgs a)
 {
-    __shared__ float xs[kClipMaxBlock];
-    const int b = blockIdx.x;
+    const int b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= a.rd.nblk) return;
     const int64_t t0 = (int64_t)b * a.rd.blk;
     const int nb = (int)min((int64_t)a.rd.blk, a.rd.N - t0);
-    const int lane = threadIdx.x;
-    int n = 0;
-    for (int k0 = 0; k0 < nb; k0 += 256) {        // four spectra per lane in flight
-        bool g[4];
-        float z[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int k = k0 + 64 * j + lane;
-            g[j] = k < nb && a.good[t0 + k];
-            z[j] = k < nb ? a.zdm[t0 + k] : 0.0f;
-        }
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint64_t m = __ballot(g[j]);
-            if (g[j]) xs[n + __popcll(m & ((1ull << lane) - 1ull))] = z[j];
-            n += __popcll(m);
-        }
-    }
-    __syncthreads();
-    if (lane != 0) return;
     double mean = 0.0, var = 0.0, an1 = 0.0;
-    for (int i = 0; i < n; i++) {
-        const double x = (double)xs[i];
+    int i = 0;
+    for (int k = 0; k < nb; k++) {
+        if (!a.good[t0 + k]) continue;
+        const double x = (double)a.zdm[t0 + k];
         if (i == 0) {
             mean = x;
         } else {
@@ -217,8 +195,9 @@ __global__ __launch_bounds__(64) void k_clip_as52(ClipArgs a)
             var += an * an1 * dx * dx;
             mean += dx;
         }
+        i++;
     }
-    if (n > 1) var /= an1;
+    if (i > 1) var /= an1;
     a.bavg[b] = mean;
     a.bstd[b] = sqrt(var);
 }
@@ -589,7 +568,7 @@ hipError_t launch_clip_stats(const ClipArgs& a, hipStream_t st, hipEvent_t after
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(k_clip_block, dim3((unsigned)rd.nblk), dim3(1024), 0, st, a);
-    hipLaunchKernelGGL(k_clip_as52, dim3((unsigned)rd.nblk), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(k_clip_as52, dim3((unsigned)((rd.nblk + 63) / 64)), dim3(64), 0, st, a);
     if (rd.nbits == 8 && !calib && rd.rowbytes % 4 == 0)
         hipLaunchKernelGGL(k_clip_chan_u8, dim3((unsigned)rd.nblk), dim3(256), 0, st, a);
     else if (rd.nbits == 4 && !calib && rd.rowbytes % 4 == 0)
