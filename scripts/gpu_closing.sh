@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-5 closing measurements: the default bench line (the driver's command), kernel stats of
+# Closing measurements of a round: the default bench line (the driver's command), kernel stats of
 # the bench step, the 4-bit beam, and one rank's time slice alone at G = 2 / 8 (ranks 0 and 7).
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
