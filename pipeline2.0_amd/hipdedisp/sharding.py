@@ -290,10 +290,10 @@ class TimeSlices:
 # ---------------------------------------------------------------------------------------
 
 # slice cost model t(x) = a + b x (ms per slice of x of a beam), fitted to round 5's one-rank
-# measurements (profiles/r05_simslice.jsonl, profiles/r05_bench.jsonl): the whole beam 58.2 ms,
-# slice 0 of 8 12.7 ms, the last slice of 8 13.2 ms -> b = 52.0, a = 6.5 (between the first
+# measurements (profiles/r05_simslice.jsonl, profiles/r05_bench.jsonl): the whole beam 57.2 ms,
+# slice 0 of 8 12.2 ms, the last slice of 8 12.3 ms -> b = 51.4, a = 5.7 (between the first
 # and the last slice's fixed cost)
-POINTING_FIXED_MS, POINTING_BEAM_MS = 6.5, 52.0
+POINTING_FIXED_MS, POINTING_BEAM_MS = 5.7, 51.4
 
 
 def helper_fraction(nbeams, nhelpers, fixed_ms, beam_ms):
