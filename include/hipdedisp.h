@@ -370,7 +370,9 @@ HD_API int hd_write_series(hd_plan* plan, const char* const* paths, int32_t wait
  * writer threads' cumulative busy seconds and bytes written since hd_open.  Returns the
  * first I/O error of the writes (HD_E_IO) if any.                                       */
 HD_API int hd_wait_writes(hd_ctx* ctx, double* write_seconds, int64_t* bytes);
-/* Device-time of the last hd_run_subband / hd_run_dedisp of this plan, ms.           */
+/* Device-time of the last hd_run_subband / hd_run_dedisp of this plan, ms.  A multi-pass
+ * call (hd_run_subband_multi / hd_run_dedisp_multi) charges its whole launch to its first
+ * plan; the other plans it carried report 0 for that stage (one event pair per launch).  */
 HD_API int hd_plan_last_ms(const hd_plan* plan, float* ms_subband, float* ms_dedisp);
 /* Name of the stage-2 kernel the last hd_run_dedisp of this plan launched, as rocprofv3
  * prints it without namespace and arguments (e.g. "k_stage2_qp<5, 3, 4, true, false>": every
