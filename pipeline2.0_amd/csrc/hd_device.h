@@ -162,7 +162,11 @@ __device__ __forceinline__ void s1_zero_masked_rows(uint32_t* lds, int G, int W,
         const int r = threadIdx.x;
         const int c = c0 + (rd.flip ? G - 1 - r : r);
         zf = rd.zidx != nullptr;
-        for (int i = 0; i < nb && zf; i++) zf = zap_at(rd, b0 + i, c);
+        // blocks past the last one are the last one (as blk_of has it): a tile that runs past N
+        // must not index zidx beyond nblk -- an unclamped read there took a stray row index
+        // from whatever followed the table and faulted in the zrows lookup
+        const int64_t bl = min(b0 + (int64_t)nb - 1, (int64_t)rd.nblk - 1);
+        for (int64_t b = b0; b <= bl && zf; b++) zf = zap_at(rd, b, c);
         zrow[r] = zf;
     }
     if (!__syncthreads_or(zf)) return;
