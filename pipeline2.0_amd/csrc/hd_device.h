@@ -37,14 +37,19 @@ __device__ __host__ __forceinline__ int64_t blk_of(const RawDesc& rd, int64_t t)
     return b < rd.nblk ? b : rd.nblk - 1;
 }
 
+// Per-block lookups.  A block index past the last block is the last block (blk_of's rule:
+// rows past N belong to it): callers derive b0 + 1 / b0 + 2 for tiles that may run past N,
+// and an unclamped zidx read there had taken a stray row index into zrows and faulted.
+__device__ __forceinline__ int64_t blk_clamp(const RawDesc& rd, int64_t b) { return b < rd.nblk ? b : rd.nblk - 1; }
+
 __device__ __forceinline__ float pad_at(const RawDesc& rd, int64_t b, int c)
 {
-    return rd.pad ? rd.pad[b * rd.pad_stride + c] : 0.0f;
+    return rd.pad ? rd.pad[blk_clamp(rd, b) * rd.pad_stride + c] : 0.0f;
 }
 
 __device__ __forceinline__ bool zap_at(const RawDesc& rd, int64_t b, int c)
 {
-    return rd.zidx && rd.zrows[(int64_t)rd.zidx[b] * rd.nchan + c];
+    return rd.zidx && rd.zrows[(int64_t)rd.zidx[blk_clamp(rd, b)] * rd.nchan + c];
 }
 
 // The cleaned sample X'(t, c) of the per-block model (oracle/oracle.h), exactly.
