@@ -1984,6 +1984,13 @@ extern "C" int hd_plan_create(hd_ctx* c, const hd_pass* ps, hd_plan** out)
     std::vector<int32_t> qpb[3];
     qp_tables(p, c->opts.sub_dtype == HD_SUB_I16, p->wide[6], womin[6], wboff[6], qpb);
 
+    // The stage-2 kernels copy a chunk's offset block into LDS in whole 1 KiB pieces, so the
+    // last chunk's copy reads up to 1 KiB past the table's end: every offset table carries
+    // 256 zero ints of tail (without it the read crossed the allocation's end whenever the
+    // device address layout put the table last in its mapping, an order-dependent fault)
+    for (int k = 0; k < 7; k++) wboff[k].resize(wboff[k].size() + 256, 0);
+    for (int qi = 0; qi < 3; qi++)
+        if (!qpb[qi].empty()) qpb[qi].resize(qpb[qi].size() + 256, 0);
     int rc = HD_OK;
     hipError_t e = hipSetDevice(c->device);
     for (int k = 0; k < 7 && e == hipSuccess; k++) {
