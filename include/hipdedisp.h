@@ -144,8 +144,19 @@ HD_API const char* hd_version(void);
 HD_API void        hd_opts_default(hd_opts* opts);
 HD_API void        hd_synth_default(hd_synth* s);
 HD_API int         hd_device_count(int* n);
+/* device = HD_HOST_ONLY: a context bound to no device (its device entry points fail with
+ * HD_E_HIP); it exists for tests of the context life cycle on machines without a GPU.     */
+#define HD_HOST_ONLY (-1)
 HD_API int         hd_open(int device, hd_ctx** out);
+/* Releases everything the context holds.  After a device fault (a sticky HIP error such as
+ * an illegal memory access, seen by any earlier call on the context) the device is unusable
+ * for the rest of the process: hd_close then makes NO device call (HIP's teardown calls on a
+ * faulted device can abort the process), releases the host side only and returns HD_E_HIP,
+ * so the caller's failure path (PrestoError -> the job pool's retry,
+ * lib/python/job.py:140-165) still runs.  hd_plan_destroy behaves the same way.            */
 HD_API int         hd_close(hd_ctx* ctx);
+/* Test hook: mark the context faulted as a sticky HIP error would (no device call).        */
+HD_API int         hd_debug_fault(hd_ctx* ctx);
 HD_API const char* hd_last_error(const hd_ctx* ctx);
 HD_API int         hd_sync(hd_ctx* ctx);
 /* Streams for stage 2 (default 1).  With 2, consecutive hd_run_dedisp calls alternate
@@ -276,6 +287,29 @@ HD_API int hd_clip_set_stats(hd_ctx* ctx, const double* stats);
 HD_API int hd_plan_tables(const hd_obs* obs, const hd_opts* opts, const hd_pass* pass,
                    int32_t* chan_delays, int32_t* dm_offsets,
                    double* sub_lofreq, double* sub_chanwid, double* sub_dt);
+/* Host-only extent check of the stage-2 kernels that copy global memory into LDS in whole
+ * 1 KiB DMA pieces (k_stage2_ring, k_stage2_pair, k_stage2_rw, k_stage2_qp): for each such
+ * kernel the plan would build and each buffer it copies from, `reach` = bytes from the
+ * buffer's start to the end of the furthest piece any workgroup issues (derived from the
+ * same tile, window and piece counts the kernels use) and `size` = the bytes hd_plan_create
+ * allocates.  hd_plan_create fails with HD_E_INVAL when any reach exceeds its size, and
+ * sizes each offset table's zero tail from this reach (no fixed slack).  out[cap] receives
+ * the records, *n their count (HD_E_NOMEM when more than cap; out may be NULL with cap 0 to
+ * count).  kernel = the hd_plan_set_variant stage-2 number (5 ring, 6 / 7 pair with 1 / 2
+ * pairs per chunk, 8 register windows, 9 quarter-layout pairs); ppc = the pairs per chunk
+ * the offsets table serves (k_stage2_qp keeps one table per 4, 3, 2).                     */
+#define HD_EXT_SUBBANDS 0     /* the int16 subband block [nsub][sub_stride]            */
+#define HD_EXT_OFFSETS  1     /* the per-chunk LDS offset table                        */
+typedef struct {
+    int32_t kernel;
+    int32_t region;      /* HD_EXT_*                                                     */
+    int32_t ppc;
+    int32_t _pad0;
+    int64_t reach;       /* bytes, exclusive                                             */
+    int64_t size;        /* bytes allocated                                              */
+} hd_extent;
+HD_API int hd_plan_extents(const hd_obs* obs, const hd_opts* opts, const hd_pass* pass,
+                           hd_extent* out, int32_t cap, int32_t* n);
 HD_API int hd_plan_create(hd_ctx* ctx, const hd_pass* pass, hd_plan** out);
 HD_API int hd_plan_destroy(hd_plan* plan);
 /* Integer delay tables: chan_delays[nchan] (stage-1 idispdt, samples at dt) and

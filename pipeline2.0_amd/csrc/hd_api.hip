@@ -55,8 +55,12 @@ struct PinSet {
 };
 
 struct hd_ctx {
-    int device = -1;
+    int device = -1;                   // HD_HOST_ONLY (-1): no device (life-cycle tests)
     int ncu = 256;                     // compute units (persistent stage-2 workgroups)
+    // a sticky HIP error (device fault) was seen: the device is unusable for the rest of the
+    // process, so teardown makes no device call (hd_close, hd_plan_destroy)
+    bool faulted = false;
+    std::string fault_msg;
     hipStream_t stream = nullptr;
     std::string err;
     bool have_obs = false;
@@ -337,12 +341,38 @@ static int fail(hd_ctx* ctx, int code, const char* fmt, ...)
     return code;
 }
 
+// HIP errors after which the device context is unusable (a kernel faulted): later runtime
+// calls return them again, and some teardown calls on such a device abort the process.
+static bool hip_sticky(hipError_t e)
+{
+    switch (e) {
+    case hipErrorIllegalAddress:
+    case hipErrorLaunchFailure:
+    case hipErrorAssert:
+    case hipErrorLaunchTimeOut:
+    case hipErrorECCNotCorrectable:
+        return true;
+    default:
+        return false;
+    }
+}
+
+static void note_hip_error(hd_ctx* c, hipError_t e, const char* what)
+{
+    if (c && hip_sticky(e) && !c->faulted) {
+        c->faulted = true;
+        c->fault_msg = std::string(what) + ": " + hipGetErrorString(e);
+    }
+}
+
 #define HIPCHK(ctx, expr)                                                                          \
     do {                                                                                           \
         hipError_t e_ = (expr);                                                                    \
-        if (e_ != hipSuccess)                                                                      \
+        if (e_ != hipSuccess) {                                                                    \
+            note_hip_error((ctx), e_, #expr);                                                      \
             return fail((ctx), HD_E_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_),    \
                         __FILE__, __LINE__);                                                       \
+        }                                                                                          \
     } while (0)
 
 static void dfree(void* p)
@@ -410,6 +440,10 @@ extern "C" int hd_open(int device, hd_ctx** out)
 {
     if (!out) return fail(nullptr, HD_E_INVAL, "hd_open: out is NULL");
     *out = nullptr;
+    if (device == HD_HOST_ONLY) {      // no device: streams, events and buffers stay NULL
+        *out = new hd_ctx();
+        return HD_OK;
+    }
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
         return fail(nullptr, HD_E_NODEV, "hd_open: no HIP device available");
@@ -465,6 +499,7 @@ static void free_clip(hd_ctx* c)
 }
 
 static void pf_stop(hd_ctx* c);
+static void pf_abandon(hd_ctx* c);
 
 static void free_obs_buffers(hd_ctx* c)
 {
@@ -487,11 +522,40 @@ static void free_obs_buffers(hd_ctx* c)
     c->dtint = 0.0;
 }
 
+// Teardown of a context whose device faulted (or that never had one): host threads and
+// host memory only.  Device buffers, streams, events, pinned blocks and hipFFT plans are
+// left to the process exit -- the runtime's own teardown calls on a faulted device are what
+// aborted the process in round 5 (hd_close after an illegal memory access).
+static int close_without_device(hd_ctx* c)
+{
+    const bool had = c->faulted;
+    const std::string msg = c->fault_msg;
+    if (c->writer) {
+        hd::writer_abandon(c->writer);
+        c->writer = nullptr;
+    }
+    if (c->pf) pf_abandon(c);
+    for (SpBufs* b : c->sp_all) delete b;
+    c->sp_all.clear();
+    c->sp_free.clear();
+    c->special_cache.clear();
+    c->fft_cache.clear();
+    delete c;
+    if (!had) return HD_OK;
+    return fail(nullptr, HD_E_HIP, "hd_close: the device faulted earlier (%s); device memory is left to the process exit",
+                msg.c_str());
+}
+
 extern "C" int hd_close(hd_ctx* c)
 {
     if (!c) return HD_OK;
+    if (c->device == HD_HOST_ONLY || c->faulted) return close_without_device(c);
     (void)hipSetDevice(c->device);
-    (void)sync_all(c);
+    {
+        const hipError_t e = sync_all(c);
+        note_hip_error(c, e, "hd_close: stream synchronize");
+        if (c->faulted) return close_without_device(c);
+    }
     if (c->writer) {
         std::string e;
         (void)hd::writer_wait(c->writer, e, nullptr, nullptr);
@@ -521,6 +585,14 @@ extern "C" int hd_close(hd_ctx* c)
     c->fft_cache.clear();
     (void)hipStreamDestroy(c->stream);
     delete c;
+    return HD_OK;
+}
+
+extern "C" int hd_debug_fault(hd_ctx* c)
+{
+    if (!c) return fail(nullptr, HD_E_INVAL, "hd_debug_fault: NULL context");
+    c->faulted = true;
+    c->fault_msg = "hd_debug_fault";
     return HD_OK;
 }
 
@@ -646,9 +718,11 @@ extern "C" int hd_set_obs(hd_ctx* c, const hd_obs* o, const hd_opts* opts)
         return fail(c, HD_E_INVAL, "clip_sigma must be finite and >= 0 (0 = -noclip)");
     if (op.clip_sigma > 0.0f && o->nsblk > hd::clip_max_block())
         return fail(c, HD_E_INVAL, "clipping needs nsblk <= %d (got %d)", hd::clip_max_block(), o->nsblk);
-    HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, sync_all(c));
-    free_obs_buffers(c);
+    if (c->device != HD_HOST_ONLY) {
+        HIPCHK(c, hipSetDevice(c->device));
+        HIPCHK(c, sync_all(c));
+        free_obs_buffers(c);
+    }
     c->obs = *o;
     c->opts = op;
     c->rowbytes = (int32_t)((int64_t)o->nchan * o->nbits / 8);
@@ -1007,6 +1081,22 @@ static void pf_stop(hd_ctx* c)
     if (pf->ev_free) (void)hipEventDestroy(pf->ev_free);
     if (pf->ev_done) (void)hipEventDestroy(pf->ev_done);
     if (pf->st) (void)hipStreamDestroy(pf->st);
+    delete pf;
+    c->pf = nullptr;
+}
+
+// After a device fault: the reader thread stopped, nothing on the device released.
+static void pf_abandon(hd_ctx* c)
+{
+    hd_ctx::Prefetch* pf = c->pf;
+    if (!pf) return;
+    {
+        std::lock_guard<std::mutex> lk(pf->mu);
+        pf->stop = true;
+        pf->q.clear();
+    }
+    pf->cv.notify_all();
+    if (pf->th.joinable()) pf->th.join();
     delete pf;
     c->pf = nullptr;
 }
@@ -1575,7 +1665,7 @@ static void wide_tables(hd_plan* p, int nwmax, bool dbuf, bool i16, hd_plan::Wid
     w.sc = sc;
     w.npw = npw;
     w.nbp = nbp;
-    boff.resize((size_t)nyb * nsub * dpb + (ring ? 256 : 0));   // ring: the last DMA piece may over-read
+    boff.resize((size_t)nyb * nsub * dpb);   // (the ring's DMA tail: stage2_host_tables)
     for (int yb = 0; yb < nyb; yb++)
         for (int s = 0; s < nsub; s++)
             for (int k = 0; k < dpb; k++) {
@@ -1650,7 +1740,7 @@ static void pair_tables(hd_plan* p, bool i16, int ppc, hd_plan::Wide& w, std::ve
     if (2 * ppc * npw + nbp > nw || hd::stage2_pair_lds_bytes(ws, npw, nbp, nsub, umax, ppc) > 160 * 1024 ||
         !hd::stage2_pair_supports(Q, R))
         return;
-    boff.assign((size_t)nyb * npair * dpb + 256, 0);   // the last DMA piece may over-read
+    boff.assign((size_t)nyb * npair * dpb, 0);   // (the DMA tail: stage2_host_tables)
     for (int yb = 0; yb < nyb; yb++)
         for (int c = 0; c < npair; c++) {
             const std::vector<int32_t>& r = rs[(size_t)yb * npair + c];
@@ -1760,7 +1850,7 @@ static void qp_tables(hd_plan* p, bool i16, hd_plan::Wide& w, std::vector<int32_
         std::vector<int32_t>& bo = boffp[qi];
         bo.clear();
         if (q > ppc || (nsub / 2) % q) continue;
-        bo.assign((size_t)nyb * npair * dpb + 256, 0);   // the last DMA piece may over-read
+        bo.assign((size_t)nyb * npair * dpb, 0);   // (the DMA tail: stage2_host_tables)
         for (int yb = 0; yb < nyb; yb++)
             for (int c = 0; c < npair; c++) {
                 const std::vector<int32_t>& r = rs[(size_t)yb * npair + c];
@@ -1910,6 +2000,133 @@ static int32_t stage1_sub_bound(const hd_ctx* c, const hd_plan* p)
     return b > 32767.0 ? 32767 : (int32_t)b;
 }
 
+// Lengths, strides and the integer tables of a plan (host only; hd_plan_create, hd_plan_extents).
+static void plan_geometry(hd_plan* p, const hd_obs& o, const hd_pass* ps, Tables& T)
+{
+    p->pass = *ps;
+    p->nds = o.N / ps->ds;
+    p->numout = ps->numout > 0 ? ps->numout : p->nds;
+    p->nvalid = std::min(p->nds, p->numout);
+    int32_t maxoff = 0;
+    for (int32_t v : T.off) maxoff = std::max(maxoff, v);
+    // zero tail after N/ds: stage-2 windows (tile + offsets + DMA pieces) may read into it;
+    // stage2_extents proves every window's last piece ends inside the block
+    p->sub_stride = (int64_t)round_up((size_t)std::max<int64_t>(p->nds, 1) + (size_t)maxoff + 4096, 64);
+    p->out_stride = (int64_t)round_up((size_t)p->numout, 64);
+    p->idispdt = std::move(T.idispdt);
+    p->off = std::move(T.off);
+    p->maxdelay = T.maxdelay;
+    p->sub_lofreq = T.lof;
+    p->sub_chanwid = T.sbw;
+    p->sub_dt = T.sdt;
+}
+
+// The host half of a plan's stage-2 variant tables: [k] the pair / window tables (womin) and
+// offset tables (wboff) of p->wide[k], qpb the k_stage2_qp offsets for 4 / 3 / 2 pairs per
+// chunk, and the DMA extents of every kernel that copies whole pieces (stage2_extents).
+struct S2Host {
+    std::vector<int32_t> womin[7], wboff[7], qpb[3];
+    std::vector<hd_extent> ext;
+};
+
+// The furthest byte each whole-piece DMA of the stage-2 kernels can touch, per variant and
+// buffer, from the same tile / window / piece numbers the kernels use:
+//   windows: subband s's row + (t0 + b - (b & 1)) elements, then npw pieces of 1 KiB, with
+//            t0 <= (ntiles - 1) T (the last tile any workgroup takes, persistent or not) and b
+//            the window base of s in its y-block: the ring's omin (k_stage2_ring,
+//            hd_stage2.hip:657-663), the pair table's base0 / b1 (k_stage2_pair :1018-1025,
+//            k_stage2_rw :1449-1457, k_stage2_qp :2124-2131);
+//   offsets: the table + (y-block, first row of the chunk) ints, then nbp pieces (ring
+//            :664-667, pair :1026-1029, qp :2132-2135 -- sized for 4 pairs whatever the
+//            launch's pairs per chunk), the register-window kernel one 1 KiB block (:1459).
+// Each offset table gets exactly the zero tail its reach needs.
+static void stage2_extents(const hd_plan* p, S2Host& h)
+{
+    const int nsub = p->pass.nsub, npair = nsub / 2, numdms = p->pass.numdms;
+    const int64_t sub_bytes = (int64_t)2 * nsub * p->sub_stride;
+    h.ext.clear();
+    auto table = [&](int kernel, int ppc, std::vector<int32_t>& tab, int64_t reach) {
+        const size_t need = (size_t)((reach + 3) / 4);
+        if (tab.size() < need) tab.resize(need, 0);
+        h.ext.push_back(hd_extent{kernel, HD_EXT_OFFSETS, ppc, 0, reach, (int64_t)(4 * tab.size())});
+    };
+    for (int k = 2; k <= 6; k++) {
+        const hd_plan::Wide& w = p->wide[k];
+        if (!w.ok || p->nvalid <= 0) continue;
+        const int64_t T = 256 * (int64_t)w.r, ntiles = (p->nvalid + T - 1) / T, t0max = (ntiles - 1) * T;
+        const int nyb = (numdms + w.dpb - 1) / w.dpb, dpb = w.dpb;
+        int64_t sreach = 0;
+        auto window = [&](int s, int32_t b) {
+            sreach = std::max(sreach, ((int64_t)s * p->sub_stride + t0max + b - (b & 1)) * 2 + (int64_t)w.npw * 1024);
+        };
+        for (int yb = 0; yb < nyb; yb++) {
+            if (k == 2) {
+                for (int s = 0; s < nsub; s++) window(s, h.womin[2][(size_t)yb * nsub + s]);
+            } else {
+                for (int pr = 0; pr < npair; pr++)
+                    for (int side = 0; side < 2; side++)
+                        window(2 * pr + side, h.womin[k][((size_t)yb * npair + pr) * hd::kPairTab + side]);
+            }
+        }
+        h.ext.push_back(hd_extent{k + 3, HD_EXT_SUBBANDS, k == 2 ? 0 : k == 3 ? 1 : k == 6 ? w.sc : 2, 0, sreach, sub_bytes});
+        const int64_t nbp = (int64_t)w.nbp * 1024;
+        if (k == 2) {
+            const int nch = nsub / hd::kRingSC;
+            table(5, 0, h.wboff[2], ((int64_t)(nyb - 1) * nsub * dpb + (int64_t)(nch - 1) * hd::kRingSC * dpb) * 4 + nbp);
+        } else if (k == 3 || k == 4) {
+            const int ppc = k == 3 ? 1 : 2;
+            table(k + 3, ppc, h.wboff[k], ((int64_t)(nyb - 1) * npair * dpb + (int64_t)(npair / ppc - 1) * ppc * dpb) * 4 + nbp);
+        } else if (k == 5) {
+            const int nch = npair / 2;
+            table(8, 2, h.wboff[5], ((int64_t)(nyb - 1) * nch + nch - 1) * hd::kRwBlock * 4 + 1024);
+        } else {
+            for (int qi = 0; qi < 3; qi++) {
+                const int q = 4 - qi;
+                if (h.qpb[qi].empty()) continue;
+                table(9, q, h.qpb[qi], ((int64_t)(nyb - 1) * npair * dpb + (int64_t)(npair / q - 1) * q * dpb) * 4 + nbp);
+            }
+            h.wboff[6] = h.qpb[4 - w.sc];
+        }
+    }
+}
+
+static void stage2_host_tables(hd_plan* p, bool i16, S2Host& h)
+{
+    for (int k = 0; k < 3; k++)
+        wide_tables(p, k == 1 ? 8 : 16, k != 1, i16, p->wide[k], h.womin[k], h.wboff[k], k == 2);
+    pair_tables(p, i16, 1, p->wide[3], h.womin[3], h.wboff[3]);
+    pair_tables(p, i16, 2, p->wide[4], h.womin[4], h.wboff[4]);
+    rw_tables(p, i16, p->wide[5], h.womin[5], h.wboff[5]);
+    qp_tables(p, i16, p->wide[6], h.womin[6], h.wboff[6], h.qpb);
+    // the plain-load wide kernels ([0], [1]) read their tables exactly; a small tail anyway
+    for (int k = 0; k < 2; k++)
+        if (p->wide[k].ok) h.wboff[k].resize(h.wboff[k].size() + 256, 0);
+    stage2_extents(p, h);
+}
+
+extern "C" int hd_plan_extents(const hd_obs* o, const hd_opts* opts, const hd_pass* ps, hd_extent* out, int32_t cap,
+                               int32_t* n)
+{
+    int rc = check_obs(nullptr, o);
+    if (rc) return rc;
+    if (!ps || !n) return fail(nullptr, HD_E_INVAL, "hd_plan_extents: NULL argument");
+    if (cap < 0 || (cap > 0 && !out)) return fail(nullptr, HD_E_INVAL, "hd_plan_extents: bad output buffer");
+    hd_opts op;
+    if (opts) op = *opts; else hd_opts_default(&op);
+    Tables T;
+    if ((rc = compute_tables(nullptr, *o, op, ps, T))) return rc;
+    if (o->N / ps->ds < 1) return fail(nullptr, HD_E_INVAL, "hd_plan_extents: no sample at -downsamp %d", ps->ds);
+    hd_plan p;
+    plan_geometry(&p, *o, ps, T);
+    S2Host h;
+    stage2_host_tables(&p, op.sub_dtype == HD_SUB_I16, h);
+    *n = (int32_t)h.ext.size();
+    if ((int32_t)h.ext.size() > cap && cap > 0)
+        return fail(nullptr, HD_E_NOMEM, "hd_plan_extents: %d records, room for %d", *n, cap);
+    for (size_t i = 0; i < h.ext.size() && (int32_t)i < cap; i++) out[i] = h.ext[i];
+    return HD_OK;
+}
+
 extern "C" int hd_plan_create(hd_ctx* c, const hd_pass* ps, hd_plan** out)
 {
     if (!c) return fail(nullptr, HD_E_INVAL, "hd_plan_create: NULL context");
@@ -1925,24 +2142,8 @@ extern "C" int hd_plan_create(hd_ctx* c, const hd_pass* ps, hd_plan** out)
 
     hd_plan* p = new hd_plan();
     p->ctx = c;
-    p->pass = *ps;
-    p->nds = o.N / ps->ds;
-    p->numout = ps->numout > 0 ? ps->numout : p->nds;
-    p->nvalid = std::min(p->nds, p->numout);
-    {
-        int32_t maxoff = 0;
-        for (int32_t v : T.off) maxoff = std::max(maxoff, v);
-        // zero tail after N/ds: stage-2 windows (tile + offsets + DMA pieces) may read into it
-        p->sub_stride = (int64_t)round_up((size_t)std::max<int64_t>(p->nds, 1) + (size_t)maxoff + 4096, 64);
-    }
-    p->out_stride = (int64_t)round_up((size_t)p->numout, 64);
+    plan_geometry(p, o, ps, T);
     const int nchan = o.nchan, nsub = ps->nsub;
-    p->idispdt = std::move(T.idispdt);
-    p->off = std::move(T.off);
-    p->maxdelay = T.maxdelay;
-    p->sub_lofreq = T.lof;
-    p->sub_chanwid = T.sbw;
-    p->sub_dt = T.sdt;
 
     // LDS-variant tables
     const int need = (ps->numdms + 3) / 4;
@@ -1975,22 +2176,24 @@ extern "C" int hd_plan_create(hd_ctx* c, const hd_pass* ps, hd_plan** out)
                 boff[((size_t)yb * nsub + s) * p->dpb + k] = ((sl * 4 + (o2 & 3)) * p->wstride + (o2 & ~3)) * 2;
             }
 
-    std::vector<int32_t> womin[7], wboff[7];
-    for (int k = 0; k < 3; k++)
-        wide_tables(p, k == 1 ? 8 : 16, k != 1, c->opts.sub_dtype == HD_SUB_I16, p->wide[k], womin[k], wboff[k], k == 2);
-    pair_tables(p, c->opts.sub_dtype == HD_SUB_I16, 1, p->wide[3], womin[3], wboff[3]);
-    pair_tables(p, c->opts.sub_dtype == HD_SUB_I16, 2, p->wide[4], womin[4], wboff[4]);
-    rw_tables(p, c->opts.sub_dtype == HD_SUB_I16, p->wide[5], womin[5], wboff[5]);
-    std::vector<int32_t> qpb[3];
-    qp_tables(p, c->opts.sub_dtype == HD_SUB_I16, p->wide[6], womin[6], wboff[6], qpb);
-
-    // The stage-2 kernels copy a chunk's offset block into LDS in whole 1 KiB pieces, so the
-    // last chunk's copy reads up to 1 KiB past the table's end: every offset table carries
-    // 256 zero ints of tail (without it the read crossed the allocation's end whenever the
-    // device address layout put the table last in its mapping, an order-dependent fault)
-    for (int k = 0; k < 7; k++) wboff[k].resize(wboff[k].size() + 256, 0);
-    for (int qi = 0; qi < 3; qi++)
-        if (!qpb[qi].empty()) qpb[qi].resize(qpb[qi].size() + 256, 0);
+    S2Host h;
+    stage2_host_tables(p, c->opts.sub_dtype == HD_SUB_I16, h);
+    for (const hd_extent& x : h.ext)
+        if (x.reach > x.size) {
+            const int rc = fail(c, HD_E_INVAL, "hd_plan_create: stage-2 variant %d's DMA reaches byte %lld of a %lld-byte %s "
+                                "(internal geometry error)", x.kernel, (long long)x.reach, (long long)x.size,
+                                x.region == HD_EXT_SUBBANDS ? "subband block" : "offset table");
+            plan_free(p);
+            delete p;
+            return rc;
+        }
+    std::vector<int32_t>(&womin)[7] = h.womin;
+    std::vector<int32_t>(&wboff)[7] = h.wboff;
+    std::vector<int32_t>(&qpb)[3] = h.qpb;
+    if (c->device == HD_HOST_ONLY) {   // host tables only (life-cycle tests): nothing on a device
+        *out = p;
+        return HD_OK;
+    }
     int rc = HD_OK;
     hipError_t e = hipSetDevice(c->device);
     for (int k = 0; k < 7 && e == hipSuccess; k++) {
@@ -2037,6 +2240,17 @@ extern "C" int hd_plan_destroy(hd_plan* p)
 {
     if (!p) return HD_OK;
     hd_ctx* c = p->ctx;
+    if (c->device == HD_HOST_ONLY || c->faulted) {
+        // no device call (see hd_close): host state only; device buffers and events stay
+        if (p->dd_own) p->dd_own->e[0] = p->dd_own->e[1] = nullptr;
+        if (p->dd_cur) p->dd_cur->e[0] = p->dd_cur->e[1] = nullptr;
+        delete p->sp;                 // (its buffer set belongs to the context's sp_all)
+        if (p->fft && hd::fft_owner(p->fft) == p) hd::fft_set_owner(p->fft, nullptr);
+        delete p;
+        if (!c->faulted) return HD_OK;
+        return fail(c, HD_E_HIP, "hd_plan_destroy: the device faulted earlier (%s); device memory is left to the process exit",
+                    c->fault_msg.c_str());
+    }
     (void)hipSetDevice(c->device);
     (void)sync_all(c);
     if (p->copy_pending && c->writer) (void)hipEventSynchronize(p->ev_copy);   // copies read p->d_out

@@ -10,6 +10,7 @@ namespace hd {
 struct Writer;
 hipError_t writer_open(Writer** out, int device);
 void writer_close(Writer* w);
+void writer_abandon(Writer* w);   // device faulted: threads stopped, host memory only
 hipStream_t writer_stream(Writer* w);
 // Queue numdms series [numdms][out_stride] (numout samples each) to paths[d], after `after`.
 int writer_series(Writer* w, hipEvent_t after, const float* d_out, int64_t out_stride, int numdms, int64_t numout,

@@ -144,6 +144,26 @@ void writer_close(Writer* w)
     delete w;
 }
 
+// After a device fault: stop the threads (queued chunks are dropped; a thread inside a
+// hipEventSynchronize gets the fault's error back) and free the host side only.
+void writer_abandon(Writer* w)
+{
+    if (!w) return;
+    {
+        std::lock_guard<std::mutex> lk(w->mu);
+        w->stop = true;
+        for (const Task& t : w->queue)
+            if (t.file->left.fetch_sub(1) == 1) {
+                close(t.file->fd);
+                delete t.file;
+            }
+        w->queue.clear();
+    }
+    w->cv_task.notify_all();
+    for (auto& t : w->threads) t.join();
+    delete w;
+}
+
 int writer_series(Writer* w, hipEvent_t after, const float* d_out, int64_t out_stride, int numdms, int64_t numout,
                   const char* const* paths, std::string& err)
 {

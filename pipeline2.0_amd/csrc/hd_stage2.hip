@@ -2263,24 +2263,30 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
     expand(0, 0);
     ring_barrier();
 
+    // The offsets table places pair k of a tile's chunk chk in expanded buffer set (chk & 1),
+    // while expand() writes the workgroup's running chunk c into set (c & 1): with an odd chunk
+    // count per tile they differ on every other tile a persistent workgroup takes, so the sums
+    // shift the table's offsets by one buffer set there (uniform, one scalar per chunk).
+    const uint32_t set_bytes = (uint32_t)(PPC * umax * E * 8);
     int chk = 0, ktile = 0;
     for (int c = 0; c < ntot; c++) {
         if (!(PRB && (a.probe & 2))) dma(c + NS - 1);
         const int chn = chk + 1 == nchunk ? 0 : chk + 1;
         if (c + 1 < ntot && !(PRB && (a.probe & 8))) expand(c + 1, chn);
         const int voff = read_voff(c);
+        const uint32_t lane_c = lane_byte + (((c ^ chk) & 1) ? ((c & 1) ? set_bytes : 0u - set_bytes) : 0u);
         if (!(PRB && (a.probe & 1))) {
             constexpr int nsteps = PPC * Q, LA = qp_la<Q, RQ>() < nsteps - 1 ? qp_la<Q, RQ>() : nsteps - 1;
             uint64_t bb[LA + 1][RQ];
 #pragma unroll
             for (int e = 0; e < LA; e++)
-                lds_read_r<RQ>(bb[e], (uint32_t)__builtin_amdgcn_readlane(voff, e) + lane_byte);
+                lds_read_r<RQ>(bb[e], (uint32_t)__builtin_amdgcn_readlane(voff, e) + lane_c);
 #pragma unroll
             for (int e = 0; e < nsteps; e++) {
                 uint64_t (&cur)[RQ] = bb[e % (LA + 1)];
                 if (e + LA < nsteps) {
                     lds_read_r<RQ>(bb[(e + LA) % (LA + 1)],
-                                   (uint32_t)__builtin_amdgcn_readlane(voff, e + LA) + lane_byte);
+                                   (uint32_t)__builtin_amdgcn_readlane(voff, e + LA) + lane_c);
                     lds_wait_n<LA * RQ>(cur);
                 } else if (e + 4 == nsteps && LA >= 3) {
                     lds_wait_n<3 * RQ>(cur);

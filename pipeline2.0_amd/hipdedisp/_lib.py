@@ -24,6 +24,8 @@ HD_DS_SUM, HD_DS_MEAN = 0, 1
 HD_PAD_MEAN, HD_PAD_ZERO, HD_PAD_DM0 = 0, 1, 2
 HD_ROUND_PRESTO, HD_ROUND_NEAREST = 0, 1
 HD_PASS_SUB_INPUT = 1
+HD_HOST_ONLY = -1
+HD_EXT_SUBBANDS, HD_EXT_OFFSETS = 0, 1
 
 ERROR_NAMES = {HD_E_INVAL: "HD_E_INVAL", HD_E_NODEV: "HD_E_NODEV", HD_E_HIP: "HD_E_HIP",
                HD_E_NOMEM: "HD_E_NOMEM", HD_E_STATE: "HD_E_STATE", HD_E_IO: "HD_E_IO"}
@@ -45,6 +47,7 @@ EXPORTED = [
     "hd_realfft", "hd_fft_prepare", "hd_zap_ranges", "hd_zapbirds", "hd_rednoise_blocks", "hd_rednoise", "hd_get_fft",
     "hd_bary_diffbins", "hd_plan_set_bary", "hd_plan_data_end", "hd_run_dedisp_multi", "hd_plan_launch_passes", "hd_sp_prune",
     "hd_prefetch_raw_file", "hd_prefetch_raw_file_band", "hd_prefetch_fill", "hd_swap_raw",
+    "hd_plan_extents", "hd_debug_fault",
 ]
 
 
@@ -70,6 +73,11 @@ class hd_pass(ctypes.Structure):
     _fields_ = [("subdm", ctypes.c_double), ("lodm", ctypes.c_double), ("dmstep", ctypes.c_double),
                 ("numdms", ctypes.c_int32), ("nsub", ctypes.c_int32), ("ds", ctypes.c_int32),
                 ("flags", ctypes.c_int32), ("numout", ctypes.c_int64)]
+
+
+class hd_extent(ctypes.Structure):
+    _fields_ = [("kernel", ctypes.c_int32), ("region", ctypes.c_int32), ("ppc", ctypes.c_int32),
+                ("_pad0", ctypes.c_int32), ("reach", ctypes.c_int64), ("size", ctypes.c_int64)]
 
 
 _NPSR = 8
@@ -194,6 +202,8 @@ def load():
                                            P(ctypes.c_uint8), P(i64)]),
         "hd_single_pulse_launch": (ctypes.c_int, [vp, ctypes.c_double, ctypes.c_double, ctypes.c_double]),
         "hd_single_pulse_collect": (ctypes.c_int, [vp, vp, i64, P(i64), P(ctypes.c_uint8), P(i64)]),
+        "hd_plan_extents": (ctypes.c_int, [P(hd_obs), P(hd_opts), P(hd_pass), P(hd_extent), i32, P(i32)]),
+        "hd_debug_fault": (ctypes.c_int, [vp]),
         "hd_plan_tables": (ctypes.c_int, [P(hd_obs), P(hd_opts), P(hd_pass), P(ctypes.c_int32),
                                           P(ctypes.c_int32), P(ctypes.c_double), P(ctypes.c_double),
                                           P(ctypes.c_double)]),

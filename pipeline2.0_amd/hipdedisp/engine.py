@@ -6,6 +6,7 @@ raised at :123-128), so callers' retry/cleanup semantics are unchanged.
 """
 import ctypes
 import os
+import weakref
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -110,6 +111,22 @@ def plan_tables(obs: "ObsParams", opts: "Opts", pp: "PassParams"):
     return idd, off, (a.value, b.value, c.value)
 
 
+def plan_extents(obs: "ObsParams", opts: "Opts", pp: "PassParams"):
+    """Host-only DMA extent check of the stage-2 kernels a plan would build (hd_plan_extents):
+    a list of dicts {kernel, region ('subbands' | 'offsets'), ppc, reach, size} in bytes."""
+    L = _lib.load()
+    o, p, q = obs.to_c(), (opts or Opts()).to_c(), pp.to_c()
+    n = ctypes.c_int32(0)
+    _check(L.hd_plan_extents(ctypes.byref(o), ctypes.byref(p), ctypes.byref(q), None, 0, ctypes.byref(n)),
+           "hd_plan_extents")
+    buf = (_lib.hd_extent * max(n.value, 1))()
+    _check(L.hd_plan_extents(ctypes.byref(o), ctypes.byref(p), ctypes.byref(q), buf, len(buf), ctypes.byref(n)),
+           "hd_plan_extents")
+    names = {_lib.HD_EXT_SUBBANDS: "subbands", _lib.HD_EXT_OFFSETS: "offsets"}
+    return [dict(kernel=x.kernel, region=names[x.region], ppc=x.ppc, reach=x.reach, size=x.size)
+            for x in buf[:n.value]]
+
+
 def bary_diffbins(topo, bary, tdt, dsdt):
     """prepsubband's add/remove-bin list [PRESTO-ext] from a TEMPO table (hd_bary_diffbins;
     host only): topo/bary MJDs spaced tdt s, output sample time dsdt s.  int32 array, > 0 =
@@ -149,7 +166,8 @@ def _f32p(a):
 
 
 class Engine:
-    """One device context (hd_ctx)."""
+    """One device context (hd_ctx).  device = _lib.HD_HOST_ONLY opens a context bound to no
+    device (host tables only; for life-cycle tests without a GPU)."""
 
     def __init__(self, device=0):
         self._L = _lib.load()
@@ -159,18 +177,40 @@ class Engine:
         self.obs: Optional[ObsParams] = None
         self.opts: Optional[Opts] = None
         self._keep = []
+        self._plans = weakref.WeakSet()     # live plans: destroyed before the context
 
     # -- lifecycle --
-    def close(self):
-        if self._ctx:
-            self._L.hd_close(self._ctx)
-            self._ctx = ctypes.c_void_p()
+    def close(self, check=True):
+        """Destroy the live plans, then the context.  After a device fault (a sticky HIP error
+        an earlier call already reported) both make no device call and return HD_E_HIP, which
+        is raised here as PrestoError when check is true -- the process stays alive, so the
+        caller's failure path runs (the job pool retries the beam, job.py:140-165)."""
+        if not self._ctx:
+            return
+        first = None
+        for pl in list(self._plans):
+            rc = pl._destroy_rc()
+            if rc != _lib.HD_OK and first is None:
+                first = (rc, "hd_plan_destroy", _lib.last_error(self._ctx))
+        self._plans = weakref.WeakSet()
+        rc = self._L.hd_close(self._ctx)
+        self._ctx = ctypes.c_void_p()
+        if rc != _lib.HD_OK:
+            first = (rc, "hd_close", _lib.last_error(None))
+        if check and first is not None:
+            raise PrestoError("Execution of command (%s) failed with status (%s)! %s"
+                              % (first[1], _lib.ERROR_NAMES.get(first[0], first[0]), first[2]))
+
+    def debug_fault(self):
+        """Mark the context faulted as a sticky HIP error would (hd_debug_fault; tests only)."""
+        self._chk(self._L.hd_debug_fault(self._ctx), "hd_debug_fault")
 
     def __enter__(self):
         return self
 
     def __exit__(self, *exc):
-        self.close()
+        # an exception already in flight is the one to report
+        self.close(check=exc[0] is None)
 
     def _chk(self, rc, what):
         _check(rc, what, self._ctx)
@@ -416,11 +456,17 @@ class Plan:
                                            ctypes.byref(nds)), "hd_plan_sub_params")
         self.sub_lofreq, self.sub_chanwid, self.sub_dt, self.nds = lof.value, cw.value, dt.value, nds.value
         self.numout = pp.numout if pp.numout > 0 else self.nds
+        eng._plans.add(self)
+
+    def _destroy_rc(self):
+        rc = _lib.HD_OK
+        if self._p:
+            rc = self.eng._L.hd_plan_destroy(self._p)
+            self._p = ctypes.c_void_p()
+        return rc
 
     def destroy(self):
-        if self._p:
-            self.eng._L.hd_plan_destroy(self._p)
-            self._p = ctypes.c_void_p()
+        self._destroy_rc()
 
     def __del__(self):
         try:
