@@ -251,6 +251,7 @@ struct hd_plan {
         bool ok = false;
         int32_t q = 0, r = 0, nw = 0, dpb = 0, ws = 0, sc = 0, npw = 0, nbp = 0;
         int32_t umax = 0;               // [3] only: largest pattern count of a subband pair
+        int32_t setb[3] = {0, 0, 0};    // [6]: bytes of one expanded buffer set at 4, 3, 2 pairs per chunk
         int32_t* d_omin = nullptr;      // [3]: the pair table (kPairTab ints per y-block and pair)
         int32_t* d_boff = nullptr;
         int32_t* d_boffp[3] = {nullptr, nullptr, nullptr};   // [6]: the offsets for 4, 3, 2 pairs per chunk
@@ -1830,6 +1831,24 @@ static void qp_tables(hd_plan* p, bool i16, hd_plan::Wide& w, std::vector<int32_
             Emax = std::max(Emax, t[9]);
             umax = std::max(umax, (int)r.size());
         }
+    // the chunk's pairs packed in its buffer set, per pairs-per-chunk q dividing the pair count:
+    // pair c at byte pb_q(c) = the U x E bytes of the chunk's pairs before it; the set is the
+    // largest chunk's (every chunk of every y-block)
+    int32_t setb[3] = {0, 0, 0};
+    for (int qi = 0; qi < 3; qi++) {
+        const int q = 4 - qi;
+        if (npair % q) continue;
+        for (int yb = 0; yb < nyb; yb++)
+            for (int ch = 0; ch < npair / q; ch++) {
+                int32_t run = 0;
+                for (int k = 0; k < q; k++) {
+                    int32_t* t = &ptab[((size_t)yb * npair + q * ch + k) * hd::kPairTab];
+                    t[hd::kQpPb + qi] = run;
+                    run += t[2] * t[9] * 8;
+                }
+                setb[qi] = std::max(setb[qi], (int32_t)round_up((size_t)run, 32));
+            }
+    }
     // the expand reads staging elements up to 4 g + 3 S + k + 7 < E + 3 S + k1max + 8
     // the most pairs per chunk (4, 3, 2 dividing the pair count) whose LDS fits; a shared launch
     // takes the smallest of its passes' (the offset block per chunk is sized for 4 pairs)
@@ -1838,13 +1857,13 @@ static void qp_tables(hd_plan* p, bool i16, hd_plan::Wide& w, std::vector<int32_
     int ppc = 0;
     for (int cand : {4, 3, 2})
         if ((nsub / 2) % cand == 0 && 2 * cand * npw + nbp <= 32 &&
-            hd::stage2_qp_lds_bytes(Emax, npw, nbp, nsub, umax, cand) <= 160 * 1024) {
+            hd::stage2_qp_lds_bytes(setb[4 - cand], npw, nbp, nsub, cand) <= 160 * 1024) {
             ppc = cand;
             break;
         }
     if (!ppc || !hd::stage2_qp_supports(Q, RQ) || (size_t)npw * 512 > 4096) return;
     // one offsets table per pairs-per-chunk a shared launch may take (ppc and every smaller
-    // candidate dividing the pair count): buffer ((c / q) & 1) * q + c % q of pair c
+    // candidate dividing the pair count): set (c / q) & 1, pair c at pb_q(c)
     for (int qi = 0; qi < 3; qi++) {
         const int q = 4 - qi;
         std::vector<int32_t>& bo = boffp[qi];
@@ -1855,12 +1874,13 @@ static void qp_tables(hd_plan* p, bool i16, hd_plan::Wide& w, std::vector<int32_
             for (int c = 0; c < npair; c++) {
                 const std::vector<int32_t>& r = rs[(size_t)yb * npair + c];
                 const int32_t base0 = ptab[((size_t)yb * npair + c) * hd::kPairTab];
-                const int buf = ((c / q) & 1) * q + c % q;
+                const int32_t* t = &ptab[((size_t)yb * npair + c) * hd::kPairTab];
+                const int64_t set0 = (int64_t)((c / q) & 1) * setb[qi] + t[hd::kQpPb + qi];
                 for (int k = 0; k < dpb; k++) {
                     const int dm = dmof(yb, k);
                     const int32_t o0 = p->off[(size_t)dm * nsub + 2 * c], o1 = p->off[(size_t)dm * nsub + 2 * c + 1];
                     const int u = (int)(std::lower_bound(r.begin(), r.end(), o1 - o0) - r.begin());
-                    bo[((size_t)yb * npair + c) * dpb + k] = (int32_t)((((int64_t)buf * umax + u) * Emax + (o0 - base0)) * 8);
+                    bo[((size_t)yb * npair + c) * dpb + k] = (int32_t)(set0 + ((int64_t)u * t[9] + (o0 - base0)) * 8);
                 }
             }
     }
@@ -1876,6 +1896,7 @@ static void qp_tables(hd_plan* p, bool i16, hd_plan::Wide& w, std::vector<int32_
     w.npw = npw;
     w.nbp = nbp;
     w.umax = umax;
+    for (int qi = 0; qi < 3; qi++) w.setb[qi] = setb[qi];
 }
 
 // Tables of the register-window pair kernel (k_stage2_rw): y-blocks of 8 waves x Q DMs, two
@@ -4076,6 +4097,7 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         a.ptab = w.d_omin;
         a.umax = w.umax;
         a.nonneg = p->sub_nonneg ? 1 : 0;
+        a.qp_setb = wk == 6 ? w.setb[4 - w.sc] : 0;
         a.nwg = p->pair_persist != 2 ? c->ncu : 0;   // persistent by default (measured 1.29 vs 1.36 ms, stage-0 pass)
         if (wk == 0) HIPCHK(c, hd::launch_stage2_wide(a, w.q, w.r, w.nw, st));
         else if (wk == 1) HIPCHK(c, hd::launch_stage2_wide2(a, w.q, w.r, w.nw, st));
@@ -4249,6 +4271,7 @@ static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
         q.npw = w.npw;
         q.nbp = w.nbp;
         q.umax = w.umax;
+        q.setb = wk == 6 ? w.setb[4 - ppc6] : 0;
     }
     p0->dd_cur = p0->dd_own;
     HIPCHK(c, hipEventRecord(dd_start(p0), st));

@@ -108,6 +108,7 @@ struct Stage2Args {
     const int32_t* ptab;
     int32_t umax;
     int32_t nonneg;           // pair variant: every subband value is >= 0 (unsigned packed halves)
+    int32_t qp_setb;          // k_stage2_qp: bytes of one expanded buffer set at the launch's pairs per chunk
 };
 
 hipError_t launch_stage1_direct(const Stage1Args& a, hipStream_t st);
@@ -141,6 +142,9 @@ constexpr int kRingSC = 4, kRingNS = 5;   // ring variant: subbands per chunk, s
 size_t stage2_ring_lds_bytes(int wstride, int npw, int nbp, int nsub);
 hipError_t launch_stage2_ring(const Stage2Args& a, int q, int r, hipStream_t st);
 constexpr int kPairUMax = 6, kPairTab = 16;   // pair variant: patterns per pair, table ints per pair
+// k_stage2_qp pair table: [9] entries per pattern E_k, [kQpPb + 4 - q] the byte offset of the
+// pair's patterns inside its chunk's buffer set when a launch takes q pairs per chunk
+constexpr int kQpPb = 10;
 size_t stage2_pair_lds_bytes(int wstride, int npw, int nbp, int nsub, int umax, int ppc);
 bool stage2_pair_supports(int q, int r);
 // Per-pass buffers and table geometry of one pass in a pair launch.  One launch may carry up
@@ -155,6 +159,7 @@ struct S2Pass {
     double* partial;
     int64_t sub_stride;
     int32_t ws, npw, nbp, umax;
+    int32_t setb, _pad1;      // k_stage2_qp: bytes of one expanded buffer set (the launch's ppc)
 };
 constexpr int kS2MaxPass = 28;
 struct S2Multi {
@@ -170,7 +175,7 @@ size_t stage2_rw_lds_bytes(int ws, int npw, int nsub, int umax);
 hipError_t launch_stage2_rw_multi(const Stage2Args& a, const S2Multi& m, int q, hipStream_t st);
 hipError_t launch_stage2_pair_multi(const Stage2Args& a, const S2Multi& m, int q, int r, int ppc, hipStream_t st);
 // quarter-layout pair kernel (k_stage2_qp): ws = entries per pattern buffer, ppc 2..4 pairs per chunk
-size_t stage2_qp_lds_bytes(int E, int npw, int nbp, int nsub, int umax, int ppc);
+size_t stage2_qp_lds_bytes(int setb, int npw, int nbp, int nsub, int ppc);
 bool stage2_qp_supports(int q, int r);
 hipError_t launch_stage2_qp_multi(const Stage2Args& a, const S2Multi& m, int q, int r, int ppc, hipStream_t st);
 hipError_t launch_stage2_wide2(const Stage2Args& a, int q, int r, int nw, hipStream_t st);

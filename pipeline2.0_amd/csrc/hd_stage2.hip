@@ -1897,6 +1897,7 @@ S2Pass stage2_pass_of(const Stage2Args& a)
     p.npw = a.ring_npw;
     p.nbp = a.ring_nbp;
     p.umax = a.umax;
+    p.setb = a.qp_setb;
     return p;
 }
 
@@ -1993,9 +1994,12 @@ hipError_t launch_stage2_wide(const Stage2Args& a, int q, int r, int nw, hipStre
 // Output lane l, read m, quarter j is sample t0 + j S + 64 m + l: dword stores, 256 bytes
 // contiguous per wave-instruction.
 // Table per (y-block, pair): [0] base0, [1] b1, [2] U, [3..3+U) k1[u], [9] E_k (entries,
-// multiple of 4).  Offsets block per chunk: int32 LDS byte offsets from the expanded area,
-// [pair k][DM slot] = ((buf * umax + u) * E + o2) * 8, buf = (chunk & 1) * PPC + k (the host
-// keeps one such table per pairs-per-chunk a launch may take).
+// multiple of 4), [kQpPb + 4 - PPC] pb_k: the byte offset of the pair's U_k x E_k entries inside
+// its chunk's buffer set (the chunk's pairs packed one after another, so a set holds the
+// chunk's own patterns, not PPC x the plan's largest U x the largest E).  Offsets block per
+// chunk: int32 LDS byte offsets from the expanded area, [pair k][DM slot] = (chunk & 1) * setb
+// + pb_k + (u E_k + o2) * 8 (the host keeps one such table per pairs-per-chunk a launch may
+// take; setb = the largest set over the chunks, per pairs-per-chunk).
 
 // 4 int16 elements x .. x+3 of a staging window (any x) as 2 packed pairs: two aligned
 // ds_read_b64 cover dwords (x>>1 & ~1) .. +3, a select picks the 3 that hold them.
@@ -2047,10 +2051,9 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
     const int nthr = blockDim.x;
     const int dpb = a.dms_per_blk;
     const int dblk0 = yb * dpb;
-    const int E = P.ws;                          // entries per pattern buffer (max over pairs)
+    const int setb = P.setb;                     // bytes of one expanded buffer set (PPC pairs' patterns)
     const int npw = P.npw;                       // 1 KiB DMA pieces per window
     const int nbp = P.nbp;                       // pieces of a chunk's offset block
-    const int umax = P.umax;
     const int npiece = 2 * PPC * npw + nbp;      // DMA pieces per chunk (<= 32: two per wave)
     const int pw = (npiece - wave + NW - 1) / NW;  // this wave's pieces per chunk: 0 .. 3
     const int slot_bytes = npiece * 1024;
@@ -2188,7 +2191,7 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
             }
             // entry i = (q0, q1 | q2, q3) of element i: the low halves of a pair-dword are element 2h
             constexpr uint32_t LO = 0x05040100u, HI = 0x07060302u;
-            uint4* d = (uint4*)(lds_raw + exp0) + ((size_t)(((((cc & 1) * PPC + k) * umax) + u) * E + 4 * g) >> 1);
+            uint4* d = (uint4*)(lds_raw + exp0 + (cc & 1) * setb + pt[kQpPb + 4 - PPC]) + ((u * pt[9] + 4 * g) >> 1);
             d[0] = make_uint4(__builtin_amdgcn_perm(Pq[1][0], Pq[0][0], LO), __builtin_amdgcn_perm(Pq[3][0], Pq[2][0], LO),
                               __builtin_amdgcn_perm(Pq[1][0], Pq[0][0], HI), __builtin_amdgcn_perm(Pq[3][0], Pq[2][0], HI));
             d[1] = make_uint4(__builtin_amdgcn_perm(Pq[1][1], Pq[0][1], LO), __builtin_amdgcn_perm(Pq[3][1], Pq[2][1], LO),
@@ -2267,7 +2270,7 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
     // while expand() writes the workgroup's running chunk c into set (c & 1): with an odd chunk
     // count per tile they differ on every other tile a persistent workgroup takes, so the sums
     // shift the table's offsets by one buffer set there (uniform, one scalar per chunk).
-    const uint32_t set_bytes = (uint32_t)(PPC * umax * E * 8);
+    const uint32_t set_bytes = (uint32_t)setb;
     int chk = 0, ktile = 0;
     for (int c = 0; c < ntot; c++) {
         if (!(PRB && (a.probe & 2))) dma(c + NS - 1);
@@ -2317,11 +2320,10 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may land after the workgroup ends
 }
 
-size_t stage2_qp_lds_bytes(int E, int npw, int nbp, int nsub, int umax, int ppc)
+size_t stage2_qp_lds_bytes(int setb, int npw, int nbp, int nsub, int ppc)
 {
     const int ns = ppc >= 4 ? 3 : 4;
-    return (size_t)(nsub / 2) * kPairTab * 4 + (size_t)ns * (2 * ppc * npw + nbp) * 1024 +
-           (size_t)2 * ppc * umax * E * 8;
+    return (size_t)(nsub / 2) * kPairTab * 4 + (size_t)ns * (2 * ppc * npw + nbp) * 1024 + (size_t)2 * setb;
 }
 
 template <int Q, int RQ, int PPC, bool NN, bool PRB>
@@ -2338,7 +2340,8 @@ static hipError_t launch_qp_n(const Stage2Args& a, const S2Multi& m, int nyblk, 
     size_t lds = 0;
     for (int i = 0; i < m.npass; i++) {
         if (2 * PPC * m.p[i].npw + m.p[i].nbp > 32) return hipErrorInvalidValue;
-        lds = std::max(lds, stage2_qp_lds_bytes(m.p[i].ws, m.p[i].npw, m.p[i].nbp, a.nsub, m.p[i].umax, PPC));
+        if (m.p[i].setb <= 0 || m.p[i].setb % 32) return hipErrorInvalidValue;
+        lds = std::max(lds, stage2_qp_lds_bytes(m.p[i].setb, m.p[i].npw, m.p[i].nbp, a.nsub, PPC));
     }
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     S2Multi mm = m;
