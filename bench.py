@@ -604,8 +604,9 @@ def pointing_main(args, world, rank, local, dist, torch):
                    "cuts": ts.cuts, "halo": ts.halo},
         "this_rank": {"rank": rank, "units": pt.units(rank), "kernel_ms_per_step": {"stage1": ms1, "stage2": ms2}},
         "predicted_ms_per_pointing": pt.predicted_ms(),
-        "prediction_note": "sharding.Pointing.predicted_ms: slice cost t(x) = 6.0 + 61.9 x ms from the round-4 "
-                           "one-rank slice timings (a prediction, not a measurement)",
+        "prediction_note": "sharding.Pointing.predicted_ms: slice cost t(x) = %.1f + %.1f x ms fitted to one-rank "
+                           "slice timings (a prediction, not a measurement)"
+                           % (S.POINTING_FIXED_MS, S.POINTING_BEAM_MS),
     }
     if args.check_union:
         mine_ck = {(b, sl): slice_checksums(ts, sl, [pl]) for b, sl, _, pl in work}

@@ -298,15 +298,15 @@ POINTING_FIXED_MS, POINTING_BEAM_MS = 5.7, 51.4
 
 def helper_fraction(nbeams, nhelpers, fixed_ms, beam_ms):
     """Home share f of each beam that balances a home rank (one slice of f N spectra) against
-    a helper (its share of every beam's tail), for a slice cost t(x) = a + b x (a = fixed_ms,
-    b = beam_ms): a + b f = k (a + b (1 - f) / 1) with k = nbeams / nhelpers tails per helper,
-    solved for f and clamped to [0.5, 1].  With no helpers every rank keeps whole beams."""
+    a helper, for a slice cost t(x) = a + b x (a = fixed_ms, b = beam_ms).  Pointing.units gives
+    EACH of the H helpers one slice of EVERY beam, (1 - f) / H of it, so a helper pays the fixed
+    cost once per beam: home a + b f = helper n a + (n / H) b (1 - f) with n = nbeams, solved for
+    f and clamped to [0.5, 1].  With no helpers every rank keeps whole beams."""
     if nhelpers <= 0:
         return 1.0
-    k = nbeams / float(nhelpers)                 # beam tails per helper
+    n, H = float(nbeams), float(nhelpers)
     a, b = float(fixed_ms), float(beam_ms)
-    # home: a + b f ;  helper: k (a + b (1 - f))
-    f = (k * a + k * b - a) / (b * (1.0 + k))
+    f = ((n - 1.0) * a + (n / H) * b) / (b * (1.0 + n / H))
     return min(1.0, max(0.5, f))
 
 

@@ -301,6 +301,25 @@ def test_pointing_schedule_shapes():
     assert S.helper_fraction(7, 0, 6.0, 62.0) == 1.0
 
 
+@pytest.mark.parametrize("nbeams,world", [(7, 8), (3, 8), (2, 6), (5, 7)])
+def test_pointing_balances_home_and_helpers(nbeams, world):
+    """with H > 1 helpers each helper still pays the fixed cost once per beam; the
+    chosen cut makes the model's home and helper times equal (unless clamped), and
+    predicted_ms is the slower of them."""
+    obs = palfa_obs(N=1 << 22)
+    a, b = S.POINTING_FIXED_MS, S.POINTING_BEAM_MS
+    pt = S.Pointing(obs, P.ddplans_for("pdev"), nbeams, world)
+    H = world - nbeams
+    f = pt.frac
+    home, helper = a + b * f, nbeams * a + nbeams * b * (1 - f) / H
+    if 0.5 < f < 1.0:
+        assert abs(home - helper) < 1e-9 * home
+    # predicted_ms uses the slices actually cut (whole multiples of the slice unit)
+    fr = [pt.ts.slice(k)[1] / obs.N for k in range(pt.nslices())]
+    want = max(a + b * fr[0], max(sum(a + b * fr[sl] for _, sl in pt.units(r)) for r in range(nbeams, world)))
+    assert abs(pt.predicted_ms() - want) < 1e-9 * want
+
+
 class _FakePlan:
     def __init__(self, eng, idx, ds, numout):
         from hipdedisp import PassParams
