@@ -4102,20 +4102,25 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         if (wk == 0) HIPCHK(c, hd::launch_stage2_wide(a, w.q, w.r, w.nw, st));
         else if (wk == 1) HIPCHK(c, hd::launch_stage2_wide2(a, w.q, w.r, w.nw, st));
         else if (wk == 2) HIPCHK(c, hd::launch_stage2_ring(a, w.q, w.r, st));
-        else if (wk == 5 || wk == 6) {
+        int qp_ns = 0;
+        if (wk == 5 || wk == 6) {
             hd::S2Multi m{};
             m.npass = 1;
             m.p[0] = hd::stage2_pass_of(a);
             if (wk == 5) HIPCHK(c, hd::launch_stage2_rw_multi(a, m, w.q, st));
-            else HIPCHK(c, hd::launch_stage2_qp_multi(a, m, w.q, w.r, w.sc, st));
-        } else HIPCHK(c, hd::launch_stage2_pair(a, w.q, w.r, wk == 4 ? 2 : 1, st));
+            else {
+                qp_ns = hd::stage2_qp_ns(m, a.nsub, w.sc);
+                HIPCHK(c, hd::launch_stage2_qp_multi(a, m, w.q, w.r, w.sc, st));
+            }
+        } else if (wk > 2) HIPCHK(c, hd::launch_stage2_pair(a, w.q, w.r, wk == 4 ? 2 : 1, st));
         // the names rocprofv3 prints (template arguments as the compiler spells them)
         if (wk == 0) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_wide<%d, %d, %d>", w.q, w.r, w.sc);
         else if (wk == 1) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_wide2<%d, %d, %d>", w.q, w.r, w.sc);
         else if (wk == 2) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_ring<%d, %d>", w.q, w.r);
         else if (wk == 5) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_rw<%d>", w.q);
-        else if (wk == 6) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_qp<%d, %d, %d, %s, %s>", w.q, w.r, w.sc,
-                                   a.nonneg && !(p->probe & 64) ? "true" : "false", (p->probe & 15) ? "true" : "false");
+        else if (wk == 6) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_qp<%d, %d, %d, %s, %s, %d>", w.q, w.r, w.sc,
+                                   a.nonneg && !(p->probe & 64) ? "true" : "false", (p->probe & 15) ? "true" : "false",
+                                   qp_ns);
         else snprintf(p->s2name, sizeof(p->s2name), "k_stage2_pair<%d, %d, %d, %s, %s>", w.q, w.r, wk == 4 ? 2 : 1,
                       a.nonneg && !(p->probe & 64) ? "true" : "false", (p->probe & 15) ? "true" : "false");
     } else if (use_lds) {
@@ -4275,6 +4280,7 @@ static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
     }
     p0->dd_cur = p0->dd_own;
     HIPCHK(c, hipEventRecord(dd_start(p0), st));
+    const int qp_ns = wk == 6 ? hd::stage2_qp_ns(m, a.nsub, ppc6) : 0;
     if (wk == 5) HIPCHK(c, hd::launch_stage2_rw_multi(a, m, w0.q, st));
     else if (wk == 6) HIPCHK(c, hd::launch_stage2_qp_multi(a, m, w0.q, w0.r, ppc6, st));
     else HIPCHK(c, hd::launch_stage2_pair_multi(a, m, w0.q, w0.r, 2, st));
@@ -4290,8 +4296,9 @@ static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
         p->dd_stream = st;
         p->s2passes = i == 0 ? n : 0;
         if (wk == 5) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_rw<%d>", w0.q);
-        else if (wk == 6) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_qp<%d, %d, %d, %s, %s>", w0.q, w0.r, ppc6,
-                                   a.nonneg && !(a.probe & 64) ? "true" : "false", (a.probe & 15) ? "true" : "false");
+        else if (wk == 6) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_qp<%d, %d, %d, %s, %s, %d>", w0.q, w0.r, ppc6,
+                                   a.nonneg && !(a.probe & 64) ? "true" : "false", (a.probe & 15) ? "true" : "false",
+                                   qp_ns);
         else snprintf(p->s2name, sizeof(p->s2name), "k_stage2_pair<%d, %d, 2, %s, %s>", w0.q, w0.r,
                       a.nonneg && !(a.probe & 64) ? "true" : "false", (a.probe & 15) ? "true" : "false");
     }

@@ -2029,13 +2029,14 @@ constexpr int qp_nw() { return 16; }
 template <int Q, int RQ>
 constexpr int qp_la() { return 1; }
 
-template <int Q, int RQ, int PPC, bool NN, bool PRB>
+template <int Q, int RQ, int PPC, bool NN, bool PRB, int NS>
 __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2Multi m)
 {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
     const int pi = (int)blockIdx.y / m.nyblk;
     const S2Pass& P = m.p[pi];
-    constexpr int NS = qp_ns<PPC>(), S = 64 * RQ, T = 4 * S, NW = qp_nw<Q>();
+    constexpr int S = 64 * RQ, T = 4 * S, NW = qp_nw<Q>();
+    static_assert(NS >= 3 && NS <= 4, "NS");
     int tb, ntl;
     if (a.nwg == 0) {
         tb = xcd_remap(blockIdx.x, gridDim.x);
@@ -2320,17 +2321,33 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may land after the workgroup ends
 }
 
-size_t stage2_qp_lds_bytes(int setb, int npw, int nbp, int nsub, int ppc)
+size_t stage2_qp_lds_bytes(int setb, int npw, int nbp, int nsub, int ppc, int ns)
 {
-    const int ns = ppc >= 4 ? 3 : 4;
+    if (ns <= 0) ns = ppc >= 4 ? 3 : 4;
     return (size_t)(nsub / 2) * kPairTab * 4 + (size_t)ns * (2 * ppc * npw + nbp) * 1024 + (size_t)2 * setb;
 }
 
-template <int Q, int RQ, int PPC, bool NN, bool PRB>
+// Staging slots of a launch: 4 (a chunk's DMA may land while the next two chunks compute) where
+// the LDS allows it at 4 pairs per chunk and HD_QP_NS=4 asks for it (A/B); else 3 at 4 pairs
+// per chunk, 4 below.
+int stage2_qp_ns(const S2Multi& m, int nsub, int ppc)
+{
+    if (ppc < 4) return 4;
+    static const int want = [] {
+        const char* e = getenv("HD_QP_NS");
+        return e ? atoi(e) : 3;
+    }();
+    if (want != 4) return 3;
+    for (int i = 0; i < m.npass; i++)
+        if (stage2_qp_lds_bytes(m.p[i].setb, m.p[i].npw, m.p[i].nbp, nsub, ppc, 4) > 160 * 1024) return 3;
+    return 4;
+}
+
+template <int Q, int RQ, int PPC, bool NN, bool PRB, int NS>
 static hipError_t launch_qp_n(const Stage2Args& a, const S2Multi& m, int nyblk, hipStream_t st)
 {
     {
-        const hipError_t e = set_max_lds((const void*)k_stage2_qp<Q, RQ, PPC, NN, PRB>, 160 * 1024);
+        const hipError_t e = set_max_lds((const void*)k_stage2_qp<Q, RQ, PPC, NN, PRB, NS>, 160 * 1024);
         if (e != hipSuccess) return e;
     }
     const unsigned ntiles = (unsigned)((a.nvalid + 256 * RQ - 1) / (256 * RQ));
@@ -2341,23 +2358,36 @@ static hipError_t launch_qp_n(const Stage2Args& a, const S2Multi& m, int nyblk, 
     for (int i = 0; i < m.npass; i++) {
         if (2 * PPC * m.p[i].npw + m.p[i].nbp > 32) return hipErrorInvalidValue;
         if (m.p[i].setb <= 0 || m.p[i].setb % 32) return hipErrorInvalidValue;
-        lds = std::max(lds, stage2_qp_lds_bytes(m.p[i].setb, m.p[i].npw, m.p[i].nbp, a.nsub, PPC));
+        lds = std::max(lds, stage2_qp_lds_bytes(m.p[i].setb, m.p[i].npw, m.p[i].nbp, a.nsub, PPC, NS));
     }
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     S2Multi mm = m;
     mm.nyblk = nyblk;
-    hipLaunchKernelGGL((k_stage2_qp<Q, RQ, PPC, NN, PRB>), dim3(nx, (unsigned)(nyblk * m.npass)), dim3(qp_nw<Q>() * 64),
+    hipLaunchKernelGGL((k_stage2_qp<Q, RQ, PPC, NN, PRB, NS>), dim3(nx, (unsigned)(nyblk * m.npass)), dim3(qp_nw<Q>() * 64),
                        lds, st, b, mm);
     return hipGetLastError();
+}
+
+template <int Q, int RQ, int PPC, int NS>
+static hipError_t launch_qp_s(const Stage2Args& a, const S2Multi& m, int nyblk, hipStream_t st)
+{
+    const bool prb = (a.probe & 15) != 0;
+    if (a.nonneg && !(a.probe & 64))
+        return prb ? launch_qp_n<Q, RQ, PPC, true, true, NS>(a, m, nyblk, st)
+                   : launch_qp_n<Q, RQ, PPC, true, false, NS>(a, m, nyblk, st);
+    return prb ? launch_qp_n<Q, RQ, PPC, false, true, NS>(a, m, nyblk, st)
+               : launch_qp_n<Q, RQ, PPC, false, false, NS>(a, m, nyblk, st);
 }
 
 template <int Q, int RQ, int PPC>
 static hipError_t launch_qp_p(const Stage2Args& a, const S2Multi& m, int nyblk, hipStream_t st)
 {
-    const bool prb = (a.probe & 15) != 0;
-    if (a.nonneg && !(a.probe & 64))
-        return prb ? launch_qp_n<Q, RQ, PPC, true, true>(a, m, nyblk, st) : launch_qp_n<Q, RQ, PPC, true, false>(a, m, nyblk, st);
-    return prb ? launch_qp_n<Q, RQ, PPC, false, true>(a, m, nyblk, st) : launch_qp_n<Q, RQ, PPC, false, false>(a, m, nyblk, st);
+    if constexpr (PPC >= 4) {
+        if (stage2_qp_ns(m, a.nsub, PPC) == 4) return launch_qp_s<Q, RQ, PPC, 4>(a, m, nyblk, st);
+        return launch_qp_s<Q, RQ, PPC, 3>(a, m, nyblk, st);
+    } else {
+        return launch_qp_s<Q, RQ, PPC, 4>(a, m, nyblk, st);
+    }
 }
 
 #define HD_QP_QR(X) X(5, 3) X(4, 3)
