@@ -1790,7 +1790,10 @@ static void qp_tables(hd_plan* p, bool i16, hd_plan::Wide& w, std::vector<int32_
 {
     w = hd_plan::Wide{};
     constexpr int RQ = 3, S = 64 * RQ, T = 4 * S;
-    constexpr int NW = 16, qlo = 4, qhi = 5;            // 16 waves x Q = 4..5 DMs
+    // 16 waves x Q = 4..5 DMs (128 VGPRs: one step of LDS read lookahead), or (HD_QP_W12=1, A/B)
+    // 12 waves x Q = 6..7 DMs (168 VGPRs: two steps)
+    static const bool w12 = getenv("HD_QP_W12") && atoi(getenv("HD_QP_W12")) != 0;
+    const int NW = w12 ? 12 : 16, qlo = w12 ? 6 : 4, qhi = w12 ? 7 : 5;
     const int nsub = p->pass.nsub, numdms = p->pass.numdms;
     if (!i16 || nsub % 2 || numdms < 1) return;
     int nyb = (numdms + qhi * NW - 1) / (qhi * NW);

@@ -906,6 +906,8 @@ __global__ __launch_bounds__(512) void k_stage1_q8(Stage1Multi a)
                 if (mean && DS > 1) {
                     const float inv = 1.0f / (float)DS, half = 0.5f / (float)DS;
                     auto divpk = [&](uint32_t v) {
+                        // DS = 2: trunc(v * 0.5f + 0.25f) = floor(v / 2) exactly, both halves at once
+                        if constexpr (DS == 2) return (v >> 1) & 0x7FFF7FFFu;
                         const uint32_t lo = (uint32_t)((float)(v & 0xFFFFu) * inv + half);
                         const uint32_t hi = (uint32_t)((float)(v >> 16) * inv + half);
                         return lo | (hi << 16);

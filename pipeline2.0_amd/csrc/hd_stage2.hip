@@ -2022,12 +2022,12 @@ constexpr int qp_ns() { return PPC >= 4 ? 3 : 4; }
 // variant with 256 VGPRs was tried in round 5: the compiler spills its accumulators beyond one
 // step of LDS read lookahead, which removed its point, and it was dropped.)
 template <int Q>
-constexpr int qp_nw() { return 16; }
+constexpr int qp_nw() { return Q >= 6 ? 12 : 16; }
 
 // LDS read lookahead of the sums (steps of RQ reads) in the VGPRs left beside the accumulators:
 // one step fits beside the 90 accumulator registers
 template <int Q, int RQ>
-constexpr int qp_la() { return 1; }
+constexpr int qp_la() { return Q >= 6 ? 2 : 1; }
 
 template <int Q, int RQ, int PPC, bool NN, bool PRB, int NS>
 __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2Multi m)
@@ -2390,7 +2390,7 @@ static hipError_t launch_qp_p(const Stage2Args& a, const S2Multi& m, int nyblk, 
     }
 }
 
-#define HD_QP_QR(X) X(5, 3) X(4, 3)
+#define HD_QP_QR(X) X(5, 3) X(4, 3) X(7, 3) X(6, 3)
 
 bool stage2_qp_supports(int q, int r)
 {
