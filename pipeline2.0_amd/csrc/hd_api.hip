@@ -164,6 +164,10 @@ struct hd_ctx {
     // by a reader thread through its own pinned blocks on its own copy stream
     struct Prefetch;
     Prefetch* pf = nullptr;
+    // diagnostics (HD_S2_STAMPS=<file>): k_stage2_qp phase stamps of the last launch, written
+    // to the file by hd_sync
+    uint32_t* d_stamps = nullptr;
+    bool stamps_pending = false;
 };
 
 struct PfJob {
@@ -574,6 +578,7 @@ extern "C" int hd_close(hd_ctx* c)
     if (c->ssp) (void)hipStreamDestroy(c->ssp);
     dfree(c->d_sum_parts);
     dfree(c->d_sum_parts_multi);
+    dfree(c->d_stamps);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_aux0) (void)hipEventDestroy(c->ev_aux0);
     if (c->ev_aux1) (void)hipEventDestroy(c->ev_aux1);
@@ -681,11 +686,32 @@ static hipError_t join_aux(hd_ctx* c)
 
 extern "C" const char* hd_last_error(const hd_ctx* c) { return c ? c->err.c_str() : g_err.c_str(); }
 
+static size_t stamps_bytes() { return (size_t)hd::kStampWG * 16 * hd::kStampChunks * hd::kStampPh * 4; }
+
+// k_stage2_qp phase stamps (diagnostics): the device buffer when HD_S2_STAMPS names a file
+static uint32_t* stamps_buf(hd_ctx* c)
+{
+    const char* path = getenv("HD_S2_STAMPS");
+    if (!path || !*path) return nullptr;
+    if (!c->d_stamps && hipMalloc(&c->d_stamps, stamps_bytes()) != hipSuccess) c->d_stamps = nullptr;
+    if (c->d_stamps) c->stamps_pending = true;
+    return c->d_stamps;
+}
+
 extern "C" int hd_sync(hd_ctx* c)
 {
     if (!c) return fail(nullptr, HD_E_INVAL, "hd_sync: NULL context");
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, sync_all(c));
+    if (c->stamps_pending) {
+        c->stamps_pending = false;
+        std::vector<uint32_t> h(stamps_bytes() / 4);
+        HIPCHK(c, hipMemcpy(h.data(), c->d_stamps, stamps_bytes(), hipMemcpyDeviceToHost));
+        if (FILE* f = fopen(getenv("HD_S2_STAMPS"), "wb")) {
+            (void)fwrite(h.data(), 4, h.size(), f);
+            fclose(f);
+        }
+    }
     return HD_OK;
 }
 
@@ -4079,6 +4105,7 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
     a.out = bary ? p->d_topo : p->d_out;
     a.out_stride = p->out_stride;
     a.partial = partial;
+    a.partial_ndm = c->opts.pad_mode == HD_PAD_DM0 ? 1 : 0;   // the padding reads DM 0's sums only
     a.ntiles = ntiles;
     a.tile = tile;
     a.maxabs = p->d_maxabs;
@@ -4101,6 +4128,7 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         a.umax = w.umax;
         a.nonneg = p->sub_nonneg ? 1 : 0;
         a.qp_setb = wk == 6 ? w.setb[4 - w.sc] : 0;
+        a.stamps = wk == 6 ? stamps_buf(c) : nullptr;
         a.nwg = p->pair_persist != 2 ? c->ncu : 0;   // persistent by default (measured 1.29 vs 1.36 ms, stage-0 pass)
         if (wk == 0) HIPCHK(c, hd::launch_stage2_wide(a, w.q, w.r, w.nw, st));
         else if (wk == 1) HIPCHK(c, hd::launch_stage2_wide2(a, w.q, w.r, w.nw, st));
@@ -4245,6 +4273,7 @@ static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
     a.out = p0->d_out;
     a.out_stride = p0->out_stride;
     a.partial = partial;
+    a.partial_ndm = c->opts.pad_mode == HD_PAD_DM0 ? 1 : 0;   // the padding reads DM 0's sums only
     a.ntiles = ntiles;
     a.tile = tile;
     a.maxabs = p0->d_maxabs;
@@ -4260,6 +4289,7 @@ static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
     a.umax = w0.umax;
     a.nonneg = p0->sub_nonneg ? 1 : 0;
     a.nwg = c->ncu;
+    a.stamps = wk == 6 ? stamps_buf(c) : nullptr;
     hd::S2Multi m{};
     m.npass = n;
     int ppc6 = 4;                       // k_stage2_qp: the smallest pairs-per-chunk of the passes

@@ -109,7 +109,13 @@ struct Stage2Args {
     int32_t umax;
     int32_t nonneg;           // pair variant: every subband value is >= 0 (unsigned packed halves)
     int32_t qp_setb;          // k_stage2_qp: bytes of one expanded buffer set at the launch's pairs per chunk
+    int32_t partial_ndm;      // k_stage2_qp: DMs whose per-tile sums the padding reads (0: all; 1: HD_PAD_DM0)
+    uint32_t* stamps;         // k_stage2_qp diagnostics (HD_S2_STAMPS): per-phase shader-clock stamps, or null
 };
+// k_stage2_qp phase stamps: workgroups x < kStampWG of y 0, each wave's first kStampChunks chunks,
+// kStampPh stamps per chunk (iteration start, DMA issued, expand issued, sums done, ring wait
+// done; the flush's end in slot 5 of a tile's last chunk)
+constexpr int kStampWG = 8, kStampChunks = 32, kStampPh = 6;
 
 hipError_t launch_stage1_direct(const Stage1Args& a, hipStream_t st);
 size_t stage1_tiled_lds_bytes(const Stage1Multi& a);

@@ -1099,7 +1099,7 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, S2Multi m)
                     }
                 }
             }
-            if (dv && P.partial) {
+            if (dv && P.partial && (a.partial_ndm == 0 || d < a.partial_ndm)) {   // (uniform per wave)
     #pragma unroll
                 for (int m = 32; m >= 1; m >>= 1) part += __shfl_xor(part, m, 64);
                 if (lane == 0) P.partial[(int64_t)d * a.ntiles + tile] = (double)part;
@@ -1516,7 +1516,7 @@ __global__ __launch_bounds__(512, 4) void k_stage2_rw(Stage2Args a, S2Multi m)
                     }
                 }
             }
-            if (dv && P.partial) {
+            if (dv && P.partial && (a.partial_ndm == 0 || d < a.partial_ndm)) {   // (uniform per wave)
 #pragma unroll
                 for (int mm = 32; mm >= 1; mm >>= 1) part += __shfl_xor(part, mm, 64);
                 if (lane == 0) P.partial[(int64_t)d * a.ntiles + tile] = (double)part;
@@ -2230,7 +2230,7 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
                             }
                 }
             }
-            if (dv && P.partial) {
+            if (dv && P.partial && (a.partial_ndm == 0 || d < a.partial_ndm)) {   // (uniform per wave)
                 // (uniform) a lane's partial is at most RQ * 4 series values of |v| <= nsub *
                 // max|subband|: when 32 of them fit int32, the DPP sum; else the int64 butterfly
                 if (small_part) {
@@ -2272,11 +2272,24 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
     // count per tile they differ on every other tile a persistent workgroup takes, so the sums
     // shift the table's offsets by one buffer set there (uniform, one scalar per chunk).
     const uint32_t set_bytes = (uint32_t)setb;
+    // diagnostics: shader-clock stamps of each phase (PRB builds with a.stamps set), kept in the
+    // LDS past the expanded sets and copied out at the end
+    const bool stamping = PRB && a.stamps && blockIdx.x < kStampWG && blockIdx.y == 0;
+    uint32_t* lst = (uint32_t*)(lds_raw + exp0 + 2 * setb);
+    auto stamp = [&](int c, int ph) {
+        if (stamping && c < kStampChunks) {
+            const uint32_t t = (uint32_t)clock64();
+            if (lane == 0) lst[(wave * kStampChunks + c) * kStampPh + ph] = t;
+        }
+    };
     int chk = 0, ktile = 0;
     for (int c = 0; c < ntot; c++) {
+        stamp(c, 0);
         if (!(PRB && (a.probe & 2))) dma(c + NS - 1);
+        stamp(c, 1);
         const int chn = chk + 1 == nchunk ? 0 : chk + 1;
         if (c + 1 < ntot && !(PRB && (a.probe & 8))) expand(c + 1, chn);
+        stamp(c, 2);
         const int voff = read_voff(c);
         const uint32_t lane_c = lane_byte + (((c ^ chk) & 1) ? ((c & 1) ? set_bytes : 0u - set_bytes) : 0u);
         if (!(PRB && (a.probe & 1))) {
@@ -2313,12 +2326,22 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
                 }
             }
         }
+        stamp(c, 3);
         wait_ring();
+        stamp(c, 4);
         ring_barrier();
-        if (chk == nchunk - 1) flush(tb + ktile++);
+        if (chk == nchunk - 1) {
+            flush(tb + ktile++);
+            stamp(c, 5);
+        }
         chk = chn;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may land after the workgroup ends
+    if (stamping) {
+        __syncthreads();
+        const int n = NW * kStampChunks * kStampPh;
+        for (int i = threadIdx.x; i < n; i += nthr) a.stamps[(int64_t)blockIdx.x * n + i] = lst[i];
+    }
 }
 
 size_t stage2_qp_lds_bytes(int setb, int npw, int nbp, int nsub, int ppc, int ns)
@@ -2360,6 +2383,7 @@ static hipError_t launch_qp_n(const Stage2Args& a, const S2Multi& m, int nyblk, 
         if (m.p[i].setb <= 0 || m.p[i].setb % 32) return hipErrorInvalidValue;
         lds = std::max(lds, stage2_qp_lds_bytes(m.p[i].setb, m.p[i].npw, m.p[i].nbp, a.nsub, PPC, NS));
     }
+    if (PRB && a.stamps) lds += (size_t)qp_nw<Q>() * kStampChunks * kStampPh * 4;
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     S2Multi mm = m;
     mm.nyblk = nyblk;
@@ -2371,7 +2395,7 @@ static hipError_t launch_qp_n(const Stage2Args& a, const S2Multi& m, int nyblk, 
 template <int Q, int RQ, int PPC, int NS>
 static hipError_t launch_qp_s(const Stage2Args& a, const S2Multi& m, int nyblk, hipStream_t st)
 {
-    const bool prb = (a.probe & 15) != 0;
+    const bool prb = (a.probe & 15) != 0 || a.stamps;
     if (a.nonneg && !(a.probe & 64))
         return prb ? launch_qp_n<Q, RQ, PPC, true, true, NS>(a, m, nyblk, st)
                    : launch_qp_n<Q, RQ, PPC, true, false, NS>(a, m, nyblk, st);
