@@ -2115,6 +2115,12 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
 
     const int ntot = ntl * nchunk;
     int dchunk = 0, dtile = 0, dcount = 0;
+    // the pair table in global memory through the scalar cache: the DMA's window bases and the
+    // expand's per-chunk item counts are wave-uniform, and an LDS read of them (as before) queued
+    // behind the other waves' expand traffic -- the in-kernel stamps put ~1,000 cycles of each
+    // chunk's DMA issue there, later waves the longest (scripts/qp_stamps.py)
+    typedef const int32_t __attribute__((address_space(4))) cint32;
+    const cint32* ptg = (const cint32*)(P.ptab + (int64_t)yb * npair * kPairTab);
     // the DMA of one chunk: piece pc of the chunk from wave pc % 16 (pc / 16: its second piece)
     auto dma = [&](int cc) {
         const int c2 = dchunk;
@@ -2129,7 +2135,7 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
                 const int win = pc / npw, pcs = pc - win * npw;      // window win: pair win / 2, side win % 2
                 const int pr = PPC * c2 + (win >> 1);
                 const int s = 2 * pr + (win & 1);
-                const int b = __builtin_amdgcn_readfirstlane(ltab[pr * kPairTab + (win & 1)]);
+                const int b = ptg[pr * kPairTab + (win & 1)];
                 const int64_t e0 = t0 + b - (b & 1);
                 const char* src = (const char*)(sub + (int64_t)s * P.sub_stride + e0) + pcs * 1024;
                 dma16s(src, (uint32_t)lane * 16u, slot + (uint32_t)(pc * 1024));
@@ -2163,7 +2169,7 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
         nk[0] = 0;
 #pragma unroll
         for (int k = 0; k < PPC; k++) {
-            const int32_t* pt = ltab + (PPC * chk + k) * kPairTab;
+            const cint32* pt = ptg + (PPC * chk + k) * kPairTab;
             nk[k + 1] = nk[k] + pt[2] * (pt[9] >> 2);
         }
         // item (pair k, pattern u, entry group g): entries 4g .. 4g+3 of pattern u
