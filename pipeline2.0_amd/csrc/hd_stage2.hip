@@ -2165,28 +2165,39 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
     // Item (pair k, entry group g): entries 4g .. 4g+3 of each of the pair's U patterns.
     auto expand = [&](int cc, int chk) {
         const char* slot = lds_raw + ring0 + (cc % NS) * slot_bytes;
-        int nk[PPC + 1];
+        // the chunk's pairs' item counts, entry groups, buffer offsets and base parities in
+        // scalar registers (scalar-cache loads): an item's decode needs no LDS round trip, and
+        // its one table read (k1[u]) goes out with nothing before it
+        int nk[PPC + 1], ngk[PPC], pbk[PPC], p0k[PPC];
         nk[0] = 0;
 #pragma unroll
         for (int k = 0; k < PPC; k++) {
             const cint32* pt = ptg + (PPC * chk + k) * kPairTab;
-            nk[k + 1] = nk[k] + pt[2] * (pt[9] >> 2);
+            ngk[k] = pt[9] >> 2;
+            nk[k + 1] = nk[k] + pt[2] * ngk[k];
+            pbk[k] = pt[kQpPb + 4 - PPC];
+            p0k[k] = pt[0] & 1;
         }
         // item (pair k, pattern u, entry group g): entries 4g .. 4g+3 of pattern u
         for (int idx = threadIdx.x; idx < nk[PPC]; idx += nthr) {
-            int k = 0;
+            int k = 0, ng = ngk[0], pb = pbk[0], p0 = p0k[0], n0 = 0;
 #pragma unroll
             for (int kk = 1; kk < PPC; kk++)
-                if (idx >= nk[kk]) k = kk;
+                if (idx >= nk[kk]) {
+                    k = kk;
+                    ng = ngk[kk];
+                    pb = pbk[kk];
+                    p0 = p0k[kk];
+                    n0 = nk[kk];
+                }
             const int32_t* pt = ltab + (PPC * chk + k) * kPairTab;
-            const int ng = pt[9] >> 2;
-            int g = idx - nk[k], u = 0;
+            int g = idx - n0, u = 0;
 #pragma unroll
             for (int uu = 1; uu < kPairUMax; uu++)
                 if (g >= ng) { g -= ng; u++; }
             const uint32_t* S0 = (const uint32_t*)(slot + (2 * k) * npw * 1024);
             const uint32_t* S1 = (const uint32_t*)(slot + (2 * k + 1) * npw * 1024);
-            const int x0 = 4 * g + (pt[0] & 1), x1 = 4 * g + pt[3 + u];
+            const int x0 = 4 * g + p0, x1 = 4 * g + pt[3 + u];
             uint32_t Pq[4][2];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -2198,7 +2209,7 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
             }
             // entry i = (q0, q1 | q2, q3) of element i: the low halves of a pair-dword are element 2h
             constexpr uint32_t LO = 0x05040100u, HI = 0x07060302u;
-            uint4* d = (uint4*)(lds_raw + exp0 + (cc & 1) * setb + pt[kQpPb + 4 - PPC]) + ((u * pt[9] + 4 * g) >> 1);
+            uint4* d = (uint4*)(lds_raw + exp0 + (cc & 1) * setb + pb) + ((u * 4 * ng + 4 * g) >> 1);
             d[0] = make_uint4(__builtin_amdgcn_perm(Pq[1][0], Pq[0][0], LO), __builtin_amdgcn_perm(Pq[3][0], Pq[2][0], LO),
                               __builtin_amdgcn_perm(Pq[1][0], Pq[0][0], HI), __builtin_amdgcn_perm(Pq[3][0], Pq[2][0], HI));
             d[1] = make_uint4(__builtin_amdgcn_perm(Pq[1][1], Pq[0][1], LO), __builtin_amdgcn_perm(Pq[3][1], Pq[2][1], LO),
