@@ -686,6 +686,12 @@ static hipError_t join_aux(hd_ctx* c)
 
 extern "C" const char* hd_last_error(const hd_ctx* c) { return c ? c->err.c_str() : g_err.c_str(); }
 
+static int qp_loader()
+{
+    static const int v = getenv("HD_QP_LOADER") ? atoi(getenv("HD_QP_LOADER")) : 0;
+    return v;
+}
+
 static size_t stamps_bytes() { return (size_t)hd::kStampWG * 16 * hd::kStampChunks * hd::kStampPh * 4; }
 
 // k_stage2_qp phase stamps (diagnostics): the device buffer when HD_S2_STAMPS names a file
@@ -3156,7 +3162,24 @@ static int run_subband_fused(hd_ctx* c, hd_plan** plans, int n)
         mp.probe = p0->probe & (1 | 2 | 4 | 8);    // profiling (results invalid): skip sums / fill / float folds / stores
         HIPCHK(c, hd::launch_stage1_q8m(mp, c->stream));
     }
-    // per DDplan stage (ds): the special tiles on the float kernel
+    // the special tiles on the float kernel: every pass in ONE launch (per-pass ds, a.pass_ds;
+    // the tile is 4 S raw rows whatever the ds), or (HD_S1_SPMERGE=0) one launch per DDplan stage
+    static const bool sp_merge = !(getenv("HD_S1_SPMERGE") && atoi(getenv("HD_S1_SPMERGE")) == 0);
+    if (nsp && sp_merge) {
+        hd::Stage1Multi f = m;
+        int fvw = 4;
+        f.pass_ds = 1;
+        if (!stage1_tiling_fixed(c, nsub, 1, dmax, 4 * S, f, fvw))
+            return fail(c, HD_E_INVAL, "stage 1: no float tiling for the fused launch's special tiles");
+        f.ntiles = m.ntiles;
+        const size_t flds = hd::stage1_tiled_lds_bytes(f);
+        if (flds > c->lds_attr_set) {
+            HIPCHK(c, hd::stage1_tiled_set_lds_limit(flds));
+            c->lds_attr_set = flds;
+        }
+        HIPCHK(c, hd::launch_stage1_tiled(f, fvw, d_sp, nsp, true, c->stream));
+    }
+    // per DDplan stage (ds): the fixup groups (and the special tiles when not merged)
     std::vector<hd::Stage1Multi> groups;
     for (int i0 = 0; i0 < n;) {
         int i1 = i0;
@@ -3176,7 +3199,7 @@ static int run_subband_fused(hd_ctx* c, hd_plan** plans, int n)
             g.ostride[k] = plans[i]->sub_stride;
             g.dmax = std::max(g.dmax, plans[i]->maxdelay);
         }
-        if (nsp) {
+        if (nsp && !sp_merge) {
             hd::Stage1Multi f = g;
             int fvw = 4;
             f.dmax = dmax;                            // the fused tiles' rows: 4 S + dmax
@@ -4129,6 +4152,7 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         a.nonneg = p->sub_nonneg ? 1 : 0;
         a.qp_setb = wk == 6 ? w.setb[4 - w.sc] : 0;
         a.stamps = wk == 6 ? stamps_buf(c) : nullptr;
+        a.qp_loader = qp_loader();
         a.nwg = p->pair_persist != 2 ? c->ncu : 0;   // persistent by default (measured 1.29 vs 1.36 ms, stage-0 pass)
         if (wk == 0) HIPCHK(c, hd::launch_stage2_wide(a, w.q, w.r, w.nw, st));
         else if (wk == 1) HIPCHK(c, hd::launch_stage2_wide2(a, w.q, w.r, w.nw, st));
@@ -4290,6 +4314,7 @@ static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
     a.nonneg = p0->sub_nonneg ? 1 : 0;
     a.nwg = c->ncu;
     a.stamps = wk == 6 ? stamps_buf(c) : nullptr;
+    a.qp_loader = qp_loader();
     hd::S2Multi m{};
     m.npass = n;
     int ppc6 = 4;                       // k_stage2_qp: the smallest pairs-per-chunk of the passes

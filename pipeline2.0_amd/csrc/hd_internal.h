@@ -62,7 +62,7 @@ struct Stage1Multi {
     double tie_eps;           // 8-bit integer path: margin the rounding of a masked subband's pad
                               // constant needs (float-fold error, plus the /ds rounding in mean mode)
     int32_t ntiles, ngroups;
-    int32_t pass_ds;                // k_stage1_fix8: 1 = per-pass ds in pds[] (ds = their max)
+    int32_t pass_ds;                // k_stage1_fix8 / SPECIAL k_stage1_tiled: 1 = per-pass ds in pds[]
     int32_t wps2;                   // k_stage1_q8 with sg >= 4: 2 waves per subband (8-wave blocks)
     int32_t pds[kMaxPass];          // k_stage1_q8m / pass_ds: per-pass downsampling
     double ptie[kMaxPass];          // k_stage1_q8m: per-pass tie_eps (its ds)
@@ -111,6 +111,7 @@ struct Stage2Args {
     int32_t qp_setb;          // k_stage2_qp: bytes of one expanded buffer set at the launch's pairs per chunk
     int32_t partial_ndm;      // k_stage2_qp: DMs whose per-tile sums the padding reads (0: all; 1: HD_PAD_DM0)
     uint32_t* stamps;         // k_stage2_qp diagnostics (HD_S2_STAMPS): per-phase shader-clock stamps, or null
+    int32_t qp_loader;        // k_stage2_qp: 1 = one wave issues every DMA piece (HD_QP_LOADER=1, A/B)
 };
 // k_stage2_qp phase stamps: workgroups x < kStampWG of y 0, each wave's first kStampChunks chunks,
 // kStampPh stamps per chunk (iteration start, DMA issued, expand issued, sums done, ring wait

@@ -168,17 +168,18 @@ __device__ __forceinline__ float s1_sample(const Stage1Multi& a, const uint8_t* 
 template <int NBITS, int CPS, bool CALIB, int MODE, bool TAIL>
 __device__ __forceinline__ void form_outputs(const Stage1Multi& a, const uint8_t* lraw, const SubState<CPS>& st,
                                              const int* livr, int c_first, int brow, int rows_valid,
-                                             int64_t tO0, int lane, int s, int p, int& amax)
+                                             int64_t tO0, int lane, int s, int p, int& amax, int ds, int to, int64_t nds)
 {
     // Two outputs per lane per iteration (j, j+64): two independent add chains for ILP.
-    // Uniform trip count; only the last iteration can diverge.
-    const int jmax = (int)min((int64_t)a.to, a.nds - tO0);
+    // Uniform trip count; only the last iteration can diverge.  (ds, to, nds: the launch's, or
+    // the pass's own in a SPECIAL launch over several DDplan stages, a.pass_ds)
+    const int jmax = (int)min((int64_t)to, nds - tO0);
     for (int j0 = lane; j0 < jmax; j0 += 128) {
         const bool has1 = j0 + 64 < jmax;
         const int j1 = has1 ? j0 + 64 : j0;          // duplicate work, result discarded
-        const int jr0 = j0 * a.ds, jr1 = j1 * a.ds;
+        const int jr0 = j0 * ds, jr1 = j1 * ds;
         float acc0 = 0.0f, acc1 = 0.0f;
-        for (int k = 0; k < a.ds; k++) {
+        for (int k = 0; k < ds; k++) {
             const uint8_t* rp0 = lraw + (jr0 + k) * a.rs;
             const uint8_t* rp1 = lraw + (jr1 + k) * a.rs;
             float sk0 = 0.0f, sk1 = 0.0f;
@@ -191,8 +192,8 @@ __device__ __forceinline__ void form_outputs(const Stage1Multi& a, const uint8_t
             acc1 += sk1;
         }
         if (a.ds_mode == 1) {
-            acc0 = acc0 / (float)a.ds;
-            acc1 = acc1 / (float)a.ds;
+            acc0 = acc0 / (float)ds;
+            acc1 = acc1 / (float)ds;
         }
         const int64_t tp0 = tO0 + j0, tp1 = tO0 + j1;
         if (a.sub_dtype == 0) {
@@ -326,24 +327,32 @@ void k_stage1_tiled(Stage1Multi a, const int* __restrict__ special_tiles)
             st.dly[cc] = a.dly[p][c0 + cl0 + cc];
             st.off[cc] = st.dly[cc] * a.rs + lrc * NBITS / 8;
         }
+        // a SPECIAL launch over the passes of several DDplan stages (the fused k_stage1_q8m
+        // call's special tiles, a.pass_ds): the tile is 4 S raw rows for every pass (a.to *
+        // a.ds), each pass forms its own to = 4 S / ds outputs of it
+        const bool pds = SPECIAL && a.pass_ds;
+        const int dsp = pds ? a.pds[p] : a.ds;
+        const int top = pds ? a.to * a.ds / dsp : a.to;
+        const int64_t ndsp = pds ? a.rd.N / dsp : a.nds;
+        const int64_t tO0 = (int64_t)tile * top;
         int amax = 0;
         if (!SPECIAL) {
             // (a tile over two read blocks stays here when the launch allows it, a.two_ok)
             if (!any_zap)
-                form_outputs<NBITS, CPS, CALIB, kModeClean, false>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax);
+                form_outputs<NBITS, CPS, CALIB, kModeClean, false>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax, dsp, top, ndsp);
             else if (mode == kModeTwo)
-                form_outputs<NBITS, CPS, CALIB, kModeTwo, false>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax);
+                form_outputs<NBITS, CPS, CALIB, kModeTwo, false>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax, dsp, top, ndsp);
             else
-                form_outputs<NBITS, CPS, CALIB, kModeFast, false>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax);
+                form_outputs<NBITS, CPS, CALIB, kModeFast, false>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax, dsp, top, ndsp);
         } else if (!tail) {
             if (mode == kModeFast)
-                form_outputs<NBITS, CPS, CALIB, kModeFast, false>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax);
+                form_outputs<NBITS, CPS, CALIB, kModeFast, false>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax, dsp, top, ndsp);
             else if (mode == kModeTwo)
-                form_outputs<NBITS, CPS, CALIB, kModeTwo, false>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax);
+                form_outputs<NBITS, CPS, CALIB, kModeTwo, false>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax, dsp, top, ndsp);
             else
-                form_outputs<NBITS, CPS, CALIB, kModeGen, false>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax);
+                form_outputs<NBITS, CPS, CALIB, kModeGen, false>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax, dsp, top, ndsp);
         } else {
-            form_outputs<NBITS, CPS, CALIB, kModeGen, true>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax);
+            form_outputs<NBITS, CPS, CALIB, kModeGen, true>(a, lraw, st, livr, lrc0, brow, rows_valid, tO0, lane, s, p, amax, dsp, top, ndsp);
         }
         if (a.sub_dtype == 0) {
             amax = wave_max_i32(amax);

@@ -2056,7 +2056,11 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
     const int npw = P.npw;                       // 1 KiB DMA pieces per window
     const int nbp = P.nbp;                       // pieces of a chunk's offset block
     const int npiece = 2 * PPC * npw + nbp;      // DMA pieces per chunk (<= 32: two per wave)
-    const int pw = (npiece - wave + NW - 1) / NW;  // this wave's pieces per chunk: 0 .. 3
+    // DMA pieces of a chunk: piece pc from wave pc % NW, or (a.qp_loader, A/B) all of them from
+    // the last wave, which has the fewest expand items
+    const bool one_loader = a.qp_loader != 0;
+    const int pc0 = one_loader ? (wave == NW - 1 ? 0 : npiece) : wave, pcd = one_loader ? 1 : NW;
+    const int pw = one_loader ? (wave == NW - 1 ? npiece : 0) : (npiece - wave + NW - 1) / NW;   // this wave's pieces
     const int slot_bytes = npiece * 1024;
     const int npair = a.nsub >> 1;
     const int tab_bytes = npair * kPairTab * 4;
@@ -2130,7 +2134,7 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
             if (++dchunk == nchunk) { dchunk = 0; dtile++; }
         }
         const uint32_t slot = ring0 + (uint32_t)((cc % NS) * slot_bytes);
-        for (int pc = wave; pc < npiece; pc += NW) {
+        for (int pc = pc0; pc < npiece; pc += pcd) {
             if (pc < 2 * PPC * npw) {
                 const int win = pc / npw, pcs = pc - win * npw;      // window win: pair win / 2, side win % 2
                 const int pr = PPC * c2 + (win >> 1);
@@ -2152,7 +2156,7 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
     // reused, measured slower: 34.3 vs 33.3 ms of stage 2 per beam.)
     constexpr int DL = NS - 3;
     auto wait_ring = [&]() {
-        if constexpr (DL == 0) {
+        if (DL == 0 || one_loader) {          // (one loader: every piece waited for, as at DL 0)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else {
             if (pw >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * DL) : "memory");
