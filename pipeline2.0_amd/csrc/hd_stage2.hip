@@ -2058,7 +2058,7 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
     const int npiece = 2 * PPC * npw + nbp;      // DMA pieces per chunk (<= 32: two per wave)
     // DMA pieces of a chunk: piece pc from wave pc % NW, or (a.qp_loader, A/B) all of them from
     // the last wave, which has the fewest expand items
-    const bool one_loader = a.qp_loader != 0;
+    const bool one_loader = a.qp_loader == 1;
     const int pc0 = one_loader ? (wave == NW - 1 ? 0 : npiece) : wave, pcd = one_loader ? 1 : NW;
     const int pw = one_loader ? (wave == NW - 1 ? npiece : 0) : (npiece - wave + NW - 1) / NW;   // this wave's pieces
     const int slot_bytes = npiece * 1024;
@@ -2182,8 +2182,11 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
             pbk[k] = pt[kQpPb + 4 - PPC];
             p0k[k] = pt[0] & 1;
         }
-        // item (pair k, pattern u, entry group g): entries 4g .. 4g+3 of pattern u
-        for (int idx = threadIdx.x; idx < nk[PPC]; idx += nthr) {
+        // item (pair k, pattern u, entry group g): entries 4g .. 4g+3 of pattern u (a.qp_loader 2,
+        // A/B: items from the last thread down, so the first waves -- the ones with a second DMA
+        // piece -- take the idle tail)
+        const int tid_e = a.qp_loader == 2 ? nthr - 1 - (int)threadIdx.x : (int)threadIdx.x;
+        for (int idx = tid_e; idx < nk[PPC]; idx += nthr) {
             int k = 0, ng = ngk[0], pb = pbk[0], p0 = p0k[0], n0 = 0;
 #pragma unroll
             for (int kk = 1; kk < PPC; kk++)
