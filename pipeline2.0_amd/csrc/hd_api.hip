@@ -1812,6 +1812,14 @@ static bool qp_auto()
     return v != 0;
 }
 
+// k_stage2_qp: a y-block's unused DM slots one each to its last waves (HD_QP_SLACK=0: the
+// slots in DM order, the unused ones at the end); the tables and the launch read the same switch
+static int qp_slack()
+{
+    static const int v = getenv("HD_QP_SLACK") ? atoi(getenv("HD_QP_SLACK")) : 1;
+    return v != 0;
+}
+
 // Tables of the quarter-layout pair kernel (k_stage2_qp): y-blocks of 16 waves x Q DMs (Q 4
 // or 5), tiles of T = 4 S = 768 samples, ppc pairs per chunk.  Per (y-block, pair) the pair
 // kernel's {base0, b1, U, k1[U]} and [9] E_k = the pair's entries per pattern (S + its own
@@ -1839,6 +1847,14 @@ static void qp_tables(hd_plan* p, bool i16, hd_plan::Wide& w, std::vector<int32_
     int32_t Emax = 0, k1max = 0;
     int umax = 0;
     auto dmof = [&](int yb, int k) { return std::min(yb * dpb + k, numdms - 1); };
+    // the kernel's slot -> DM map (k_stage2_qp's slot0): with qp_slack() the block's unused
+    // slots go one each to its last waves, whose last slot is then unused (any DM will do)
+    auto slot_dm = [&](int yb, int k) {
+        const int nd = std::min(dpb, numdms - yb * dpb), nsl = dpb - nd, w = k / Q, qq = k - w * Q;
+        if (!qp_slack() || nsl <= 0 || nsl > NW || w < NW - nsl) return dmof(yb, k);
+        if (qq == Q - 1) return dmof(yb, k);
+        return yb * dpb + (NW - nsl) * Q + (w - (NW - nsl)) * (Q - 1) + qq;
+    };
     for (int yb = 0; yb < nyb; yb++)
         for (int c = 0; c < npair; c++) {
             int32_t lo = INT32_MAX, hi = INT32_MIN;
@@ -1912,7 +1928,7 @@ static void qp_tables(hd_plan* p, bool i16, hd_plan::Wide& w, std::vector<int32_
                 const int32_t* t = &ptab[((size_t)yb * npair + c) * hd::kPairTab];
                 const int64_t set0 = (int64_t)((c / q) & 1) * setb[qi] + t[hd::kQpPb + qi];
                 for (int k = 0; k < dpb; k++) {
-                    const int dm = dmof(yb, k);
+                    const int dm = slot_dm(yb, k);
                     const int32_t o0 = p->off[(size_t)dm * nsub + 2 * c], o1 = p->off[(size_t)dm * nsub + 2 * c + 1];
                     const int u = (int)(std::lower_bound(r.begin(), r.end(), o1 - o0) - r.begin());
                     bo[((size_t)yb * npair + c) * dpb + k] = (int32_t)(set0 + ((int64_t)u * t[9] + (o0 - base0)) * 8);
@@ -2887,6 +2903,39 @@ static int special_tiles(hd_ctx* c, const hd::Stage1Multi& m, int** d_sp, int* n
     return HD_OK;
 }
 
+// The same list cut into q sub-tiles per tile (tile t -> t q .. t q + q - 1: ALL of them, since
+// the integer kernel skipped the whole tile), for a float launch of to / q outputs per tile:
+// q times the workgroups on a q-th of the rows each (the few special tiles' float folds are
+// latency-bound).  Cached beside the plain lists (key: to < 0).
+static int special_subtiles(hd_ctx* c, const hd::Stage1Multi& m, int q, int** d_sp, int* nsp_out)
+{
+    *d_sp = nullptr;
+    *nsp_out = 0;
+    const int key = -(m.to / q);
+    for (const auto& e : c->special_cache)
+        if (e.to == key && e.ds == m.ds && e.dmax == m.dmax && e.ntiles == m.ntiles * q && e.two_ok == m.two_ok) {
+            *d_sp = e.d;
+            *nsp_out = e.n;
+            return HD_OK;
+        }
+    const int nsp = hd::stage1_special_tiles(m, nullptr);
+    std::vector<int> h(nsp), sub;
+    if (nsp) hd::stage1_special_tiles(m, h.data());
+    const int64_t rows_sub = (int64_t)(m.to / q) * m.ds;
+    for (int t : h)
+        for (int k = 0; k < q; k++)
+            if ((int64_t)(t * q + k) * rows_sub < c->obs.N) sub.push_back(t * q + k);   // (rows past N: no output)
+    hd_ctx::SpecialList e{key, m.ds, m.dmax, m.ntiles * q, m.two_ok, (int)sub.size(), nullptr};
+    if (!sub.empty()) {
+        HIPCHK(c, hipMalloc(&e.d, sizeof(int) * sub.size()));
+        HIPCHK(c, hipMemcpy(e.d, sub.data(), sizeof(int) * sub.size(), hipMemcpyHostToDevice));
+    }
+    c->special_cache.push_back(e);
+    *d_sp = e.d;
+    *nsp_out = e.n;
+    return HD_OK;
+}
+
 static void clear_special_cache(hd_ctx* c)
 {
     if (!c->special_cache.empty()) (void)hipStreamSynchronize(c->stream);
@@ -3166,18 +3215,23 @@ static int run_subband_fused(hd_ctx* c, hd_plan** plans, int n)
     // the tile is 4 S raw rows whatever the ds), or (HD_S1_SPMERGE=0) one launch per DDplan stage
     static const bool sp_merge = !(getenv("HD_S1_SPMERGE") && atoi(getenv("HD_S1_SPMERGE")) == 0);
     if (nsp && sp_merge) {
+        // in quarter sub-tiles (S raw rows, S / ds outputs of every pass; S = 960 is a multiple
+        // of every ds the fused launch takes)
         hd::Stage1Multi f = m;
-        int fvw = 4;
+        int fvw = 4, *d_sub = nullptr, nsub_t = 0;
         f.pass_ds = 1;
-        if (!stage1_tiling_fixed(c, nsub, 1, dmax, 4 * S, f, fvw))
+        if (!stage1_tiling_fixed(c, nsub, 1, dmax, S, f, fvw))
             return fail(c, HD_E_INVAL, "stage 1: no float tiling for the fused launch's special tiles");
-        f.ntiles = m.ntiles;
+        f.to = S;
+        f.ntiles = 4 * m.ntiles;
+        rc = special_subtiles(c, m, 4, &d_sub, &nsub_t);
+        if (rc) return rc;
         const size_t flds = hd::stage1_tiled_lds_bytes(f);
         if (flds > c->lds_attr_set) {
             HIPCHK(c, hd::stage1_tiled_set_lds_limit(flds));
             c->lds_attr_set = flds;
         }
-        HIPCHK(c, hd::launch_stage1_tiled(f, fvw, d_sp, nsp, true, c->stream));
+        if (nsub_t) HIPCHK(c, hd::launch_stage1_tiled(f, fvw, d_sub, nsub_t, true, c->stream));
     }
     // per DDplan stage (ds): the fixup groups (and the special tiles when not merged)
     std::vector<hd::Stage1Multi> groups;
@@ -4153,6 +4207,7 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         a.qp_setb = wk == 6 ? w.setb[4 - w.sc] : 0;
         a.stamps = wk == 6 ? stamps_buf(c) : nullptr;
         a.qp_loader = qp_loader();
+        a.qp_slack = wk == 6 ? qp_slack() : 0;
         a.nwg = p->pair_persist != 2 ? c->ncu : 0;   // persistent by default (measured 1.29 vs 1.36 ms, stage-0 pass)
         if (wk == 0) HIPCHK(c, hd::launch_stage2_wide(a, w.q, w.r, w.nw, st));
         else if (wk == 1) HIPCHK(c, hd::launch_stage2_wide2(a, w.q, w.r, w.nw, st));
@@ -4315,6 +4370,7 @@ static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
     a.nwg = c->ncu;
     a.stamps = wk == 6 ? stamps_buf(c) : nullptr;
     a.qp_loader = qp_loader();
+    a.qp_slack = wk == 6 ? qp_slack() : 0;
     hd::S2Multi m{};
     m.npass = n;
     int ppc6 = 4;                       // k_stage2_qp: the smallest pairs-per-chunk of the passes

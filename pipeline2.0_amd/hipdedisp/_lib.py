@@ -9,7 +9,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "libhipdedisp.so")
+# HD_LIB (A/B of two builds in one session): another build of the same library
+LIB_PATH = os.environ.get("HD_LIB") or os.path.join(os.path.dirname(_HERE), "libhipdedisp.so")
 
 HD_OK = 0
 HD_E_INVAL = -1
