@@ -1812,14 +1812,6 @@ static bool qp_auto()
     return v != 0;
 }
 
-// k_stage2_qp: a y-block's unused DM slots one each to its last waves (HD_QP_SLACK=0: the
-// slots in DM order, the unused ones at the end); the tables and the launch read the same switch
-static int qp_slack()
-{
-    static const int v = getenv("HD_QP_SLACK") ? atoi(getenv("HD_QP_SLACK")) : 1;
-    return v != 0;
-}
-
 // Tables of the quarter-layout pair kernel (k_stage2_qp): y-blocks of 16 waves x Q DMs (Q 4
 // or 5), tiles of T = 4 S = 768 samples, ppc pairs per chunk.  Per (y-block, pair) the pair
 // kernel's {base0, b1, U, k1[U]} and [9] E_k = the pair's entries per pattern (S + its own
@@ -1847,14 +1839,6 @@ static void qp_tables(hd_plan* p, bool i16, hd_plan::Wide& w, std::vector<int32_
     int32_t Emax = 0, k1max = 0;
     int umax = 0;
     auto dmof = [&](int yb, int k) { return std::min(yb * dpb + k, numdms - 1); };
-    // the kernel's slot -> DM map (k_stage2_qp's slot0): with qp_slack() the block's unused
-    // slots go one each to its last waves, whose last slot is then unused (any DM will do)
-    auto slot_dm = [&](int yb, int k) {
-        const int nd = std::min(dpb, numdms - yb * dpb), nsl = dpb - nd, w = k / Q, qq = k - w * Q;
-        if (!qp_slack() || nsl <= 0 || nsl > NW || w < NW - nsl) return dmof(yb, k);
-        if (qq == Q - 1) return dmof(yb, k);
-        return yb * dpb + (NW - nsl) * Q + (w - (NW - nsl)) * (Q - 1) + qq;
-    };
     for (int yb = 0; yb < nyb; yb++)
         for (int c = 0; c < npair; c++) {
             int32_t lo = INT32_MAX, hi = INT32_MIN;
@@ -1928,7 +1912,7 @@ static void qp_tables(hd_plan* p, bool i16, hd_plan::Wide& w, std::vector<int32_
                 const int32_t* t = &ptab[((size_t)yb * npair + c) * hd::kPairTab];
                 const int64_t set0 = (int64_t)((c / q) & 1) * setb[qi] + t[hd::kQpPb + qi];
                 for (int k = 0; k < dpb; k++) {
-                    const int dm = slot_dm(yb, k);
+                    const int dm = dmof(yb, k);
                     const int32_t o0 = p->off[(size_t)dm * nsub + 2 * c], o1 = p->off[(size_t)dm * nsub + 2 * c + 1];
                     const int u = (int)(std::lower_bound(r.begin(), r.end(), o1 - o0) - r.begin());
                     bo[((size_t)yb * npair + c) * dpb + k] = (int32_t)(set0 + ((int64_t)u * t[9] + (o0 - base0)) * 8);
@@ -4207,7 +4191,6 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         a.qp_setb = wk == 6 ? w.setb[4 - w.sc] : 0;
         a.stamps = wk == 6 ? stamps_buf(c) : nullptr;
         a.qp_loader = qp_loader();
-        a.qp_slack = wk == 6 ? qp_slack() : 0;
         a.nwg = p->pair_persist != 2 ? c->ncu : 0;   // persistent by default (measured 1.29 vs 1.36 ms, stage-0 pass)
         if (wk == 0) HIPCHK(c, hd::launch_stage2_wide(a, w.q, w.r, w.nw, st));
         else if (wk == 1) HIPCHK(c, hd::launch_stage2_wide2(a, w.q, w.r, w.nw, st));
@@ -4370,7 +4353,6 @@ static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
     a.nwg = c->ncu;
     a.stamps = wk == 6 ? stamps_buf(c) : nullptr;
     a.qp_loader = qp_loader();
-    a.qp_slack = wk == 6 ? qp_slack() : 0;
     hd::S2Multi m{};
     m.npass = n;
     int ppc6 = 4;                       // k_stage2_qp: the smallest pairs-per-chunk of the passes

@@ -5,8 +5,6 @@
 // helpers) so the two halves compile in parallel.
 #include "hd_device.h"
 
-#include <type_traits>
-
 namespace hd {
 
 // ------------------------------------------------------------------------------------
@@ -1078,9 +1076,9 @@ __global__ __launch_bounds__(1024) void k_stage2_pair(Stage2Args a, S2Multi m)
         widen();
     #pragma unroll
         for (int q = 0; q < Q; q++) {
-            const int dl = slot0 + q;
+            const int dl = wave * Q + q;
             const int d = dblk0 + dl;
-            const bool dv = dl < dpb && d < a.numdms && !(short_w && q == Q - 1);
+            const bool dv = dl < dpb && d < a.numdms;
             int64_t part = 0;
     #pragma unroll
             for (int r = 0; r < R; r++) {
@@ -2054,15 +2052,6 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
     const int nthr = blockDim.x;
     const int dpb = a.dms_per_blk;
     const int dblk0 = yb * dpb;
-    // DM slots: wave w, slot q -> DM w Q + q of the y-block; with a.qp_slack the block's unused
-    // slots (dpb - nd of them, at most one per wave) go one each to the LAST waves, which then
-    // sum Q - 1 DMs per pair (the last waves to resume from each chunk's barrier set the chunk's
-    // end, in-kernel stamps), the others Q
-    const int nd_blk = min(dpb, a.numdms - dblk0);
-    const int nslack = dpb - nd_blk;
-    const bool short_w = a.qp_slack && nslack > 0 && nslack <= NW && wave >= NW - nslack;
-    const int slot0 = a.qp_slack && nslack > 0 && nslack <= NW && wave > NW - nslack
-                          ? (NW - nslack) * Q + (wave - (NW - nslack)) * (Q - 1) : wave * Q;
     const int setb = P.setb;                     // bytes of one expanded buffer set (PPC pairs' patterns)
     const int npw = P.npw;                       // 1 KiB DMA pieces per window
     const int nbp = P.nbp;                       // pieces of a chunk's offset block
@@ -2327,23 +2316,18 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
         stamp(c, 2);
         const int voff = read_voff(c);
         const uint32_t lane_c = lane_byte + (((c ^ chk) & 1) ? ((c & 1) ? set_bytes : 0u - set_bytes) : 0u);
-        // the chunk's sums, QE DMs per pair (Q, or Q - 1 on a short wave): step e = pair e / QE,
-        // DM e % QE, its offsets in lane (e / QE) Q + e % QE of voff.  Two static copies, so no
-        // branch sits between an LDS read and its counted wait.
-        auto sums = [&](auto qe) {
-            constexpr int QE = decltype(qe)::value;
-            constexpr int nsteps = PPC * QE, LA = qp_la<Q, RQ>() < nsteps - 1 ? qp_la<Q, RQ>() : nsteps - 1;
-            auto vl = [](int e) { return (e / QE) * Q + e % QE; };
+        if (!(PRB && (a.probe & 1))) {
+            constexpr int nsteps = PPC * Q, LA = qp_la<Q, RQ>() < nsteps - 1 ? qp_la<Q, RQ>() : nsteps - 1;
             uint64_t bb[LA + 1][RQ];
 #pragma unroll
             for (int e = 0; e < LA; e++)
-                lds_read_r<RQ>(bb[e], (uint32_t)__builtin_amdgcn_readlane(voff, vl(e)) + lane_c);
+                lds_read_r<RQ>(bb[e], (uint32_t)__builtin_amdgcn_readlane(voff, e) + lane_c);
 #pragma unroll
             for (int e = 0; e < nsteps; e++) {
                 uint64_t (&cur)[RQ] = bb[e % (LA + 1)];
                 if (e + LA < nsteps) {
                     lds_read_r<RQ>(bb[(e + LA) % (LA + 1)],
-                                   (uint32_t)__builtin_amdgcn_readlane(voff, vl(e + LA)) + lane_c);
+                                   (uint32_t)__builtin_amdgcn_readlane(voff, e + LA) + lane_c);
                     lds_wait_n<LA * RQ>(cur);
                 } else if (e + 4 == nsteps && LA >= 3) {
                     lds_wait_n<3 * RQ>(cur);
@@ -2354,21 +2338,17 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
                 } else {
                     lds_wait_n<0>(cur);
                 }
-                const int q = e % QE;
+                const int q = e % Q;
 #pragma unroll
                 for (int r = 0; r < RQ; r++) {
                     acc16[q][r][0] += __builtin_bit_cast(short2v, (uint32_t)cur[r]);
                     acc16[q][r][1] += __builtin_bit_cast(short2v, (uint32_t)(cur[r] >> 32));
                 }
-                if (q == QE - 1 && ++gcount == G) {
+                if (q == Q - 1 && ++gcount == G) {
                     gcount = 0;
                     widen();
                 }
             }
-        };
-        if (!(PRB && (a.probe & 1))) {
-            if (short_w) sums(std::integral_constant<int, Q - 1>{});
-            else sums(std::integral_constant<int, Q>{});
         }
         stamp(c, 3);
         wait_ring();
