@@ -686,12 +686,6 @@ static hipError_t join_aux(hd_ctx* c)
 
 extern "C" const char* hd_last_error(const hd_ctx* c) { return c ? c->err.c_str() : g_err.c_str(); }
 
-static int qp_loader()
-{
-    static const int v = getenv("HD_QP_LOADER") ? atoi(getenv("HD_QP_LOADER")) : 0;
-    return v;
-}
-
 static size_t stamps_bytes() { return (size_t)hd::kStampWG * 16 * hd::kStampChunks * hd::kStampPh * 4; }
 
 // k_stage2_qp phase stamps (diagnostics): the device buffer when HD_S2_STAMPS names a file
@@ -4190,7 +4184,6 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         a.nonneg = p->sub_nonneg ? 1 : 0;
         a.qp_setb = wk == 6 ? w.setb[4 - w.sc] : 0;
         a.stamps = wk == 6 ? stamps_buf(c) : nullptr;
-        a.qp_loader = qp_loader();
         a.nwg = p->pair_persist != 2 ? c->ncu : 0;   // persistent by default (measured 1.29 vs 1.36 ms, stage-0 pass)
         if (wk == 0) HIPCHK(c, hd::launch_stage2_wide(a, w.q, w.r, w.nw, st));
         else if (wk == 1) HIPCHK(c, hd::launch_stage2_wide2(a, w.q, w.r, w.nw, st));
@@ -4352,7 +4345,6 @@ static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
     a.nonneg = p0->sub_nonneg ? 1 : 0;
     a.nwg = c->ncu;
     a.stamps = wk == 6 ? stamps_buf(c) : nullptr;
-    a.qp_loader = qp_loader();
     hd::S2Multi m{};
     m.npass = n;
     int ppc6 = 4;                       // k_stage2_qp: the smallest pairs-per-chunk of the passes

@@ -111,7 +111,6 @@ struct Stage2Args {
     int32_t qp_setb;          // k_stage2_qp: bytes of one expanded buffer set at the launch's pairs per chunk
     int32_t partial_ndm;      // k_stage2_qp: DMs whose per-tile sums the padding reads (0: all; 1: HD_PAD_DM0)
     uint32_t* stamps;         // k_stage2_qp diagnostics (HD_S2_STAMPS): per-phase shader-clock stamps, or null
-    int32_t qp_loader;        // k_stage2_qp: 1 = one wave issues every DMA piece (HD_QP_LOADER=1, A/B)
 };
 // k_stage2_qp phase stamps: workgroups x < kStampWG of y 0, each wave's first kStampChunks chunks,
 // kStampPh stamps per chunk (iteration start, DMA issued, expand issued, sums done, ring wait

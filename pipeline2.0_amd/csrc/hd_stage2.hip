@@ -2056,11 +2056,7 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
     const int npw = P.npw;                       // 1 KiB DMA pieces per window
     const int nbp = P.nbp;                       // pieces of a chunk's offset block
     const int npiece = 2 * PPC * npw + nbp;      // DMA pieces per chunk (<= 32: two per wave)
-    // DMA pieces of a chunk: piece pc from wave pc % NW, or (a.qp_loader, A/B) all of them from
-    // the last wave, which has the fewest expand items
-    const bool one_loader = a.qp_loader == 1;
-    const int pc0 = one_loader ? (wave == NW - 1 ? 0 : npiece) : wave, pcd = one_loader ? 1 : NW;
-    const int pw = one_loader ? (wave == NW - 1 ? npiece : 0) : (npiece - wave + NW - 1) / NW;   // this wave's pieces
+    const int pw = (npiece - wave + NW - 1) / NW;  // this wave's pieces per chunk: 0 .. 3
     const int slot_bytes = npiece * 1024;
     const int npair = a.nsub >> 1;
     const int tab_bytes = npair * kPairTab * 4;
@@ -2119,12 +2115,6 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
 
     const int ntot = ntl * nchunk;
     int dchunk = 0, dtile = 0, dcount = 0;
-    // the pair table in global memory through the scalar cache: the DMA's window bases and the
-    // expand's per-chunk item counts are wave-uniform, and an LDS read of them (as before) queued
-    // behind the other waves' expand traffic -- the in-kernel stamps put ~1,000 cycles of each
-    // chunk's DMA issue there, later waves the longest (scripts/qp_stamps.py)
-    typedef const int32_t __attribute__((address_space(4))) cint32;
-    const cint32* ptg = (const cint32*)(P.ptab + (int64_t)yb * npair * kPairTab);
     // the DMA of one chunk: piece pc of the chunk from wave pc % 16 (pc / 16: its second piece)
     auto dma = [&](int cc) {
         const int c2 = dchunk;
@@ -2134,12 +2124,12 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
             if (++dchunk == nchunk) { dchunk = 0; dtile++; }
         }
         const uint32_t slot = ring0 + (uint32_t)((cc % NS) * slot_bytes);
-        for (int pc = pc0; pc < npiece; pc += pcd) {
+        for (int pc = wave; pc < npiece; pc += NW) {
             if (pc < 2 * PPC * npw) {
                 const int win = pc / npw, pcs = pc - win * npw;      // window win: pair win / 2, side win % 2
                 const int pr = PPC * c2 + (win >> 1);
                 const int s = 2 * pr + (win & 1);
-                const int b = ptg[pr * kPairTab + (win & 1)];
+                const int b = __builtin_amdgcn_readfirstlane(ltab[pr * kPairTab + (win & 1)]);
                 const int64_t e0 = t0 + b - (b & 1);
                 const char* src = (const char*)(sub + (int64_t)s * P.sub_stride + e0) + pcs * 1024;
                 dma16s(src, (uint32_t)lane * 16u, slot + (uint32_t)(pc * 1024));
@@ -2156,7 +2146,7 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
     // reused, measured slower: 34.3 vs 33.3 ms of stage 2 per beam.)
     constexpr int DL = NS - 3;
     auto wait_ring = [&]() {
-        if (DL == 0 || one_loader) {          // (one loader: every piece waited for, as at DL 0)
+        if constexpr (DL == 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else {
             if (pw >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * DL) : "memory");
@@ -2169,42 +2159,28 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
     // Item (pair k, entry group g): entries 4g .. 4g+3 of each of the pair's U patterns.
     auto expand = [&](int cc, int chk) {
         const char* slot = lds_raw + ring0 + (cc % NS) * slot_bytes;
-        // the chunk's pairs' item counts, entry groups, buffer offsets and base parities in
-        // scalar registers (scalar-cache loads): an item's decode needs no LDS round trip, and
-        // its one table read (k1[u]) goes out with nothing before it
-        int nk[PPC + 1], ngk[PPC], pbk[PPC], p0k[PPC];
+        int nk[PPC + 1];
         nk[0] = 0;
 #pragma unroll
         for (int k = 0; k < PPC; k++) {
-            const cint32* pt = ptg + (PPC * chk + k) * kPairTab;
-            ngk[k] = pt[9] >> 2;
-            nk[k + 1] = nk[k] + pt[2] * ngk[k];
-            pbk[k] = pt[kQpPb + 4 - PPC];
-            p0k[k] = pt[0] & 1;
+            const int32_t* pt = ltab + (PPC * chk + k) * kPairTab;
+            nk[k + 1] = nk[k] + pt[2] * (pt[9] >> 2);
         }
-        // item (pair k, pattern u, entry group g): entries 4g .. 4g+3 of pattern u (a.qp_loader 2,
-        // A/B: items from the last thread down, so the first waves -- the ones with a second DMA
-        // piece -- take the idle tail)
-        const int tid_e = a.qp_loader == 2 ? nthr - 1 - (int)threadIdx.x : (int)threadIdx.x;
-        for (int idx = tid_e; idx < nk[PPC]; idx += nthr) {
-            int k = 0, ng = ngk[0], pb = pbk[0], p0 = p0k[0], n0 = 0;
+        // item (pair k, pattern u, entry group g): entries 4g .. 4g+3 of pattern u
+        for (int idx = threadIdx.x; idx < nk[PPC]; idx += nthr) {
+            int k = 0;
 #pragma unroll
             for (int kk = 1; kk < PPC; kk++)
-                if (idx >= nk[kk]) {
-                    k = kk;
-                    ng = ngk[kk];
-                    pb = pbk[kk];
-                    p0 = p0k[kk];
-                    n0 = nk[kk];
-                }
+                if (idx >= nk[kk]) k = kk;
             const int32_t* pt = ltab + (PPC * chk + k) * kPairTab;
-            int g = idx - n0, u = 0;
+            const int ng = pt[9] >> 2;
+            int g = idx - nk[k], u = 0;
 #pragma unroll
             for (int uu = 1; uu < kPairUMax; uu++)
                 if (g >= ng) { g -= ng; u++; }
             const uint32_t* S0 = (const uint32_t*)(slot + (2 * k) * npw * 1024);
             const uint32_t* S1 = (const uint32_t*)(slot + (2 * k + 1) * npw * 1024);
-            const int x0 = 4 * g + p0, x1 = 4 * g + pt[3 + u];
+            const int x0 = 4 * g + (pt[0] & 1), x1 = 4 * g + pt[3 + u];
             uint32_t Pq[4][2];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -2216,7 +2192,7 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
             }
             // entry i = (q0, q1 | q2, q3) of element i: the low halves of a pair-dword are element 2h
             constexpr uint32_t LO = 0x05040100u, HI = 0x07060302u;
-            uint4* d = (uint4*)(lds_raw + exp0 + (cc & 1) * setb + pb) + ((u * 4 * ng + 4 * g) >> 1);
+            uint4* d = (uint4*)(lds_raw + exp0 + (cc & 1) * setb + pt[kQpPb + 4 - PPC]) + ((u * pt[9] + 4 * g) >> 1);
             d[0] = make_uint4(__builtin_amdgcn_perm(Pq[1][0], Pq[0][0], LO), __builtin_amdgcn_perm(Pq[3][0], Pq[2][0], LO),
                               __builtin_amdgcn_perm(Pq[1][0], Pq[0][0], HI), __builtin_amdgcn_perm(Pq[3][0], Pq[2][0], HI));
             d[1] = make_uint4(__builtin_amdgcn_perm(Pq[1][1], Pq[0][1], LO), __builtin_amdgcn_perm(Pq[3][1], Pq[2][1], LO),

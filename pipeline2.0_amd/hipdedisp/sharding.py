@@ -289,11 +289,11 @@ class TimeSlices:
 # configs[4]: the 7 beams of an ALFA pointing on one node (beam x time partitioning)
 # ---------------------------------------------------------------------------------------
 
-# slice cost model t(x) = a + b x (ms per slice of x of a beam), fitted to round 5's one-rank
-# measurements (profiles/r05_simslice.jsonl, profiles/r05_bench.jsonl): the whole beam 57.2 ms,
-# slice 0 of 8 12.2 ms, the last slice of 8 12.3 ms -> b = 51.4, a = 5.7 (between the first
-# and the last slice's fixed cost)
-POINTING_FIXED_MS, POINTING_BEAM_MS = 5.7, 51.4
+# slice cost model t(x) = a + b x (ms per slice of x of a beam), fitted to round 6's one-rank
+# measurements (profiles/r06_simslice.jsonl, profiles/r06_ab_stage2_sload.txt): the whole beam
+# 56.8 ms, slice 0 of 8 (x = 1/8 + the 18,432-spectrum halo) 11.2 ms, the last slice of 8 12.1 ms
+# -> b = 51.7, a = 5.1 (the mean of the two slices' fixed costs); round 5: 5.7 / 51.4
+POINTING_FIXED_MS, POINTING_BEAM_MS = 5.1, 51.7
 
 
 def helper_fraction(nbeams, nhelpers, fixed_ms, beam_ms):
