@@ -1884,12 +1884,17 @@ static void qp_tables(hd_plan* p, bool i16, hd_plan::Wide& w, std::vector<int32_
     const int npw = (int)((((size_t)Emax + 3 * S + k1max + 8) * 2 + 1023) / 1024);
     const int nbp = (int)(((size_t)4 * dpb * 4 + 1023) / 1024);
     int ppc = 0;
+    static const int ppc_cap = getenv("HD_QP_PPC") ? atoi(getenv("HD_QP_PPC")) : 4;   // (A/B)
     for (int cand : {4, 3, 2})
-        if ((nsub / 2) % cand == 0 && 2 * cand * npw + nbp <= 32 &&
+        if (cand <= ppc_cap && (nsub / 2) % cand == 0 && 2 * cand * npw + nbp <= 32 &&
             hd::stage2_qp_lds_bytes(setb[4 - cand], npw, nbp, nsub, cand) <= 160 * 1024) {
             ppc = cand;
             break;
         }
+    if (getenv("HD_QP_INFO"))
+        fprintf(stderr, "qp_tables: nsub %d numdms %d Q %d ppc %d npw %d nbp %d setb %d/%d/%d lds %zu\n", nsub, numdms,
+                Q, ppc, npw, nbp, setb[0], setb[1], setb[2],
+                ppc ? hd::stage2_qp_lds_bytes(setb[4 - ppc], npw, nbp, nsub, ppc) : (size_t)0);
     if (!ppc || !hd::stage2_qp_supports(Q, RQ) || (size_t)npw * 512 > 4096) return;
     // one offsets table per pairs-per-chunk a shared launch may take (ppc and every smaller
     // candidate dividing the pair count): set (c / q) & 1, pair c at pb_q(c)
@@ -4189,6 +4194,7 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         else if (wk == 1) HIPCHK(c, hd::launch_stage2_wide2(a, w.q, w.r, w.nw, st));
         else if (wk == 2) HIPCHK(c, hd::launch_stage2_ring(a, w.q, w.r, st));
         int qp_ns = 0;
+        bool qp_sy = false;
         if (wk == 5 || wk == 6) {
             hd::S2Multi m{};
             m.npass = 1;
@@ -4196,6 +4202,7 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
             if (wk == 5) HIPCHK(c, hd::launch_stage2_rw_multi(a, m, w.q, st));
             else {
                 qp_ns = hd::stage2_qp_ns(m, a.nsub, w.sc);
+                qp_sy = hd::stage2_qp_sync(m, a.nsub, w.sc);
                 HIPCHK(c, hd::launch_stage2_qp_multi(a, m, w.q, w.r, w.sc, st));
             }
         } else if (wk > 2) HIPCHK(c, hd::launch_stage2_pair(a, w.q, w.r, wk == 4 ? 2 : 1, st));
@@ -4204,9 +4211,9 @@ extern "C" int hd_run_dedisp(hd_plan* p, float* host_out)
         else if (wk == 1) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_wide2<%d, %d, %d>", w.q, w.r, w.sc);
         else if (wk == 2) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_ring<%d, %d>", w.q, w.r);
         else if (wk == 5) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_rw<%d>", w.q);
-        else if (wk == 6) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_qp<%d, %d, %d, %s, %s, %d>", w.q, w.r, w.sc,
+        else if (wk == 6) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_qp<%d, %d, %d, %s, %s, %d, %s>", w.q, w.r, w.sc,
                                    a.nonneg && !(p->probe & 64) ? "true" : "false", (p->probe & 15) ? "true" : "false",
-                                   qp_ns);
+                                   qp_ns, qp_sy ? "true" : "false");
         else snprintf(p->s2name, sizeof(p->s2name), "k_stage2_pair<%d, %d, %d, %s, %s>", w.q, w.r, wk == 4 ? 2 : 1,
                       a.nonneg && !(p->probe & 64) ? "true" : "false", (p->probe & 15) ? "true" : "false");
     } else if (use_lds) {
@@ -4369,6 +4376,7 @@ static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
     p0->dd_cur = p0->dd_own;
     HIPCHK(c, hipEventRecord(dd_start(p0), st));
     const int qp_ns = wk == 6 ? hd::stage2_qp_ns(m, a.nsub, ppc6) : 0;
+    const bool qp_sy = wk == 6 && hd::stage2_qp_sync(m, a.nsub, ppc6);
     if (wk == 5) HIPCHK(c, hd::launch_stage2_rw_multi(a, m, w0.q, st));
     else if (wk == 6) HIPCHK(c, hd::launch_stage2_qp_multi(a, m, w0.q, w0.r, ppc6, st));
     else HIPCHK(c, hd::launch_stage2_pair_multi(a, m, w0.q, w0.r, 2, st));
@@ -4384,9 +4392,9 @@ static int run_dedisp_group(hd_ctx* c, hd_plan* const* g, int n)
         p->dd_stream = st;
         p->s2passes = i == 0 ? n : 0;
         if (wk == 5) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_rw<%d>", w0.q);
-        else if (wk == 6) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_qp<%d, %d, %d, %s, %s, %d>", w0.q, w0.r, ppc6,
+        else if (wk == 6) snprintf(p->s2name, sizeof(p->s2name), "k_stage2_qp<%d, %d, %d, %s, %s, %d, %s>", w0.q, w0.r, ppc6,
                                    a.nonneg && !(a.probe & 64) ? "true" : "false", (a.probe & 15) ? "true" : "false",
-                                   qp_ns);
+                                   qp_ns, qp_sy ? "true" : "false");
         else snprintf(p->s2name, sizeof(p->s2name), "k_stage2_pair<%d, %d, 2, %s, %s>", w0.q, w0.r,
                       a.nonneg && !(a.probe & 64) ? "true" : "false", (a.probe & 15) ? "true" : "false");
     }

@@ -181,8 +181,10 @@ size_t stage2_rw_lds_bytes(int ws, int npw, int nsub, int umax);
 hipError_t launch_stage2_rw_multi(const Stage2Args& a, const S2Multi& m, int q, hipStream_t st);
 hipError_t launch_stage2_pair_multi(const Stage2Args& a, const S2Multi& m, int q, int r, int ppc, hipStream_t st);
 // quarter-layout pair kernel (k_stage2_qp): ws = entries per pattern buffer, ppc 2..4 pairs per chunk
-size_t stage2_qp_lds_bytes(int setb, int npw, int nbp, int nsub, int ppc, int ns = 0);   // ns 0: the default
+size_t stage2_qp_lds_bytes(int setb, int npw, int nbp, int nsub, int ppc, int ns = 0,
+                           bool sync = false);   // ns 0: the default
 int stage2_qp_ns(const struct S2Multi& m, int nsub, int ppc);   // staging slots a launch takes
+bool stage2_qp_sync(const struct S2Multi& m, int nsub, int ppc);   // the barrier-free variant (A/B)
 bool stage2_qp_supports(int q, int r);
 hipError_t launch_stage2_qp_multi(const Stage2Args& a, const S2Multi& m, int q, int r, int ppc, hipStream_t st);
 hipError_t launch_stage2_wide2(const Stage2Args& a, int q, int r, int nw, hipStream_t st);

@@ -2029,14 +2029,14 @@ constexpr int qp_nw() { return Q >= 6 ? 12 : 16; }
 template <int Q, int RQ>
 constexpr int qp_la() { return Q >= 6 ? 2 : 1; }
 
-template <int Q, int RQ, int PPC, bool NN, bool PRB, int NS>
+template <int Q, int RQ, int PPC, bool NN, bool PRB, int NS, bool SY>
 __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2Multi m)
 {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
     const int pi = (int)blockIdx.y / m.nyblk;
     const S2Pass& P = m.p[pi];
     constexpr int S = 64 * RQ, T = 4 * S, NW = qp_nw<Q>();
-    static_assert(NS >= 3 && NS <= 4, "NS");
+    static_assert(NS >= 3 && NS <= 4 && (!SY || NS == 3), "NS");
     int tb, ntl;
     if (a.nwg == 0) {
         tb = xcd_remap(blockIdx.x, gridDim.x);
@@ -2069,6 +2069,9 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
     const int nchunk = npair / PPC;
 
     for (int i = threadIdx.x; i < npair * kPairTab; i += nthr) ltab[i] = P.ptab[(int64_t)yb * npair * kPairTab + i];
+    // SY: the two progress counters past the three expanded sets (see the SY loop below)
+    uint32_t* ctr = (uint32_t*)(lds_raw + exp0 + 3 * setb);
+    if (SY && threadIdx.x < 2) ctr[threadIdx.x] = 0;
     __syncthreads();
 
     int maxabs = *P.maxabs;
@@ -2192,7 +2195,7 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
             }
             // entry i = (q0, q1 | q2, q3) of element i: the low halves of a pair-dword are element 2h
             constexpr uint32_t LO = 0x05040100u, HI = 0x07060302u;
-            uint4* d = (uint4*)(lds_raw + exp0 + (cc & 1) * setb + pt[kQpPb + 4 - PPC]) + ((u * pt[9] + 4 * g) >> 1);
+            uint4* d = (uint4*)(lds_raw + exp0 + (SY ? cc % 3 : cc & 1) * setb + pt[kQpPb + 4 - PPC]) + ((u * pt[9] + 4 * g) >> 1);
             d[0] = make_uint4(__builtin_amdgcn_perm(Pq[1][0], Pq[0][0], LO), __builtin_amdgcn_perm(Pq[3][0], Pq[2][0], LO),
                               __builtin_amdgcn_perm(Pq[1][0], Pq[0][0], HI), __builtin_amdgcn_perm(Pq[3][0], Pq[2][0], HI));
             d[1] = make_uint4(__builtin_amdgcn_perm(Pq[1][1], Pq[0][1], LO), __builtin_amdgcn_perm(Pq[3][1], Pq[2][1], LO),
@@ -2259,14 +2262,6 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
         const int32_t* sboff = (const int32_t*)(lds_raw + ring0 + (cc % NS) * slot_bytes + 2 * PPC * npw * 1024);
         return lane < PPC * Q ? sboff[(lane / Q) * dpb + wave * Q + lane % Q] : 0;
     };
-    // prologue: chunks 0 and 1 in LDS (chunk 1 is expanded in iteration 0)
-#pragma unroll
-    for (int cc = 0; cc < NS - 1; cc++) dma(cc);
-    wait_ring();
-    ring_barrier();
-    expand(0, 0);
-    ring_barrier();
-
     // The offsets table places pair k of a tile's chunk chk in expanded buffer set (chk & 1),
     // while expand() writes the workgroup's running chunk c into set (c & 1): with an odd chunk
     // count per tile they differ on every other tile a persistent workgroup takes, so the sums
@@ -2275,23 +2270,15 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
     // diagnostics: shader-clock stamps of each phase (PRB builds with a.stamps set), kept in the
     // LDS past the expanded sets and copied out at the end
     const bool stamping = PRB && a.stamps && blockIdx.x < kStampWG && blockIdx.y == 0;
-    uint32_t* lst = (uint32_t*)(lds_raw + exp0 + 2 * setb);
+    uint32_t* lst = (uint32_t*)(lds_raw + exp0 + (SY ? 3 * setb + 16 : 2 * setb));
     auto stamp = [&](int c, int ph) {
         if (stamping && c < kStampChunks) {
             const uint32_t t = (uint32_t)clock64();
             if (lane == 0) lst[(wave * kStampChunks + c) * kStampPh + ph] = t;
         }
     };
-    int chk = 0, ktile = 0;
-    for (int c = 0; c < ntot; c++) {
-        stamp(c, 0);
-        if (!(PRB && (a.probe & 2))) dma(c + NS - 1);
-        stamp(c, 1);
-        const int chn = chk + 1 == nchunk ? 0 : chk + 1;
-        if (c + 1 < ntot && !(PRB && (a.probe & 8))) expand(c + 1, chn);
-        stamp(c, 2);
-        const int voff = read_voff(c);
-        const uint32_t lane_c = lane_byte + (((c ^ chk) & 1) ? ((c & 1) ? set_bytes : 0u - set_bytes) : 0u);
+    // the sums of chunk c: PPC x Q steps of RQ aligned ds_read_b64 from the chunk's buffer set
+    auto sums = [&](const int voff, const uint32_t lane_c) {
         if (!(PRB && (a.probe & 1))) {
             constexpr int nsteps = PPC * Q, LA = qp_la<Q, RQ>() < nsteps - 1 ? qp_la<Q, RQ>() : nsteps - 1;
             uint64_t bb[LA + 1][RQ];
@@ -2326,15 +2313,101 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
                 }
             }
         }
-        stamp(c, 3);
-        wait_ring();
-        stamp(c, 4);
-        ring_barrier();
-        if (chk == nchunk - 1) {
-            flush(tb + ktile++);
-            stamp(c, 5);
+    };
+
+    if constexpr (!SY) {
+    // prologue: chunks 0 and 1 in LDS (chunk 1 is expanded in iteration 0)
+#pragma unroll
+    for (int cc = 0; cc < NS - 1; cc++) dma(cc);
+    wait_ring();
+    ring_barrier();
+    expand(0, 0);
+    ring_barrier();
+
+        int chk = 0, ktile = 0;
+        for (int c = 0; c < ntot; c++) {
+            stamp(c, 0);
+            if (!(PRB && (a.probe & 2))) dma(c + NS - 1);
+            stamp(c, 1);
+            const int chn = chk + 1 == nchunk ? 0 : chk + 1;
+            if (c + 1 < ntot && !(PRB && (a.probe & 8))) expand(c + 1, chn);
+            stamp(c, 2);
+            const int voff = read_voff(c);
+            sums(voff, lane_byte + (((c ^ chk) & 1) ? ((c & 1) ? set_bytes : 0u - set_bytes) : 0u));
+            stamp(c, 3);
+            wait_ring();
+            stamp(c, 4);
+            ring_barrier();
+            if (chk == nchunk - 1) {
+                flush(tb + ktile++);
+                stamp(c, 5);
+            }
+            chk = chn;
         }
-        chk = chn;
+    } else {
+        // Barrier-free variant (HD_QP_SYNC=1): three expanded sets, so a wave may expand chunk
+        // c + 1 while slower waves still sum chunk c - 1, and two LDS progress counters in place
+        // of the per-chunk barrier.  ctr[0] gets +1 per wave and iteration once its share of
+        // chunk c + 1 is expanded (its offsets read) and its DMA pieces of chunk c + 2 have
+        // landed; ctr[1] gets +1 once its sums of chunk c are done.  Iteration c waits for
+        // ctr[0] >= NW (c + 1): chunk c fully expanded (the set its sums read), chunk c + 1 in
+        // LDS (the slot its expand reads) and slot c % 3 free for the DMA of chunk c + 3; and for
+        // ctr[1] >= NW (c - 1): set (c + 1) % 3 (chunk c - 2's) no longer read.  A wave thus
+        // runs up to one iteration ahead of the slowest instead of waiting at a barrier.
+        auto signal = [&](int i) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (lane == 0) __hip_atomic_fetch_add(ctr + i, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        };
+        bool stalled = false;
+        auto wait_ge = [&](int i, uint32_t target) {
+            // bounded (about 0.1 s): a broken count ends the kernel with wrong sums, not a hang
+            for (int n = 0; n < (1 << 22) && !stalled; n++) {
+                const uint32_t v = __builtin_amdgcn_readfirstlane(*(volatile uint32_t*)(ctr + i));
+                if (v >= target) {
+                    asm volatile("" ::: "memory");
+                    return;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            stalled = true;
+        };
+        dma(0);
+        dma(1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        ring_barrier();
+        if (!(PRB && (a.probe & 8))) expand(0, 0);
+        int voff_cur = read_voff(0);
+        dma(2);
+        signal(0);
+        int chk = 0, ktile = 0, c3 = 0;
+        for (int c = 0; c < ntot; c++) {
+            stamp(c, 0);
+            wait_ge(0, (uint32_t)(NW * (c + 1)));
+            if (c >= 1) wait_ge(1, (uint32_t)(NW * (c - 1)));
+            stamp(c, 1);
+            const int chn = chk + 1 == nchunk ? 0 : chk + 1;
+            int voff_next = 0;
+            if (c + 1 < ntot) {
+                if (!(PRB && (a.probe & 8))) expand(c + 1, chn);
+                voff_next = read_voff(c + 1);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA pieces of chunk c + 2
+            signal(0);
+            stamp(c, 2);
+            if (c + 3 < ntot && !(PRB && (a.probe & 2))) dma(c + 3);
+            // the table's set (chk & 1) -> the running set c % 3
+            sums(voff_cur, lane_byte + (uint32_t)c3 * set_bytes - (uint32_t)(chk & 1) * set_bytes);
+            stamp(c, 3);
+            signal(1);
+            stamp(c, 4);
+            if (chk == nchunk - 1) {
+                flush(tb + ktile++);
+                stamp(c, 5);
+            }
+            chk = chn;
+            voff_cur = voff_next;
+            c3 = c3 == 2 ? 0 : c3 + 1;
+        }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may land after the workgroup ends
     if (stamping) {
@@ -2344,10 +2417,12 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
     }
 }
 
-size_t stage2_qp_lds_bytes(int setb, int npw, int nbp, int nsub, int ppc, int ns)
+size_t stage2_qp_lds_bytes(int setb, int npw, int nbp, int nsub, int ppc, int ns, bool sy)
 {
     if (ns <= 0) ns = ppc >= 4 ? 3 : 4;
-    return (size_t)(nsub / 2) * kPairTab * 4 + (size_t)ns * (2 * ppc * npw + nbp) * 1024 + (size_t)2 * setb;
+    if (sy) ns = 3;
+    return (size_t)(nsub / 2) * kPairTab * 4 + (size_t)ns * (2 * ppc * npw + nbp) * 1024 + (size_t)(sy ? 3 : 2) * setb +
+           (sy ? 16 : 0);
 }
 
 // Staging slots of a launch: 4 (a chunk's DMA may land while the next two chunks compute) where
@@ -2355,6 +2430,7 @@ size_t stage2_qp_lds_bytes(int setb, int npw, int nbp, int nsub, int ppc, int ns
 // per chunk, 4 below.
 int stage2_qp_ns(const S2Multi& m, int nsub, int ppc)
 {
+    if (stage2_qp_sync(m, nsub, ppc)) return 3;
     if (ppc < 4) return 4;
     static const int want = [] {
         const char* e = getenv("HD_QP_NS");
@@ -2366,11 +2442,21 @@ int stage2_qp_ns(const S2Multi& m, int nsub, int ppc)
     return 4;
 }
 
-template <int Q, int RQ, int PPC, bool NN, bool PRB, int NS>
+// The barrier-free variant (HD_QP_SYNC=1, A/B) where its third buffer set fits the LDS
+bool stage2_qp_sync(const S2Multi& m, int nsub, int ppc)
+{
+    static const bool want = getenv("HD_QP_SYNC") && atoi(getenv("HD_QP_SYNC")) != 0;
+    if (!want) return false;
+    for (int i = 0; i < m.npass; i++)
+        if (stage2_qp_lds_bytes(m.p[i].setb, m.p[i].npw, m.p[i].nbp, nsub, ppc, 3, true) > 160 * 1024) return false;
+    return true;
+}
+
+template <int Q, int RQ, int PPC, bool NN, bool PRB, int NS, bool SY>
 static hipError_t launch_qp_n(const Stage2Args& a, const S2Multi& m, int nyblk, hipStream_t st)
 {
     {
-        const hipError_t e = set_max_lds((const void*)k_stage2_qp<Q, RQ, PPC, NN, PRB, NS>, 160 * 1024);
+        const hipError_t e = set_max_lds((const void*)k_stage2_qp<Q, RQ, PPC, NN, PRB, NS, SY>, 160 * 1024);
         if (e != hipSuccess) return e;
     }
     const unsigned ntiles = (unsigned)((a.nvalid + 256 * RQ - 1) / (256 * RQ));
@@ -2381,36 +2467,37 @@ static hipError_t launch_qp_n(const Stage2Args& a, const S2Multi& m, int nyblk, 
     for (int i = 0; i < m.npass; i++) {
         if (2 * PPC * m.p[i].npw + m.p[i].nbp > 32) return hipErrorInvalidValue;
         if (m.p[i].setb <= 0 || m.p[i].setb % 32) return hipErrorInvalidValue;
-        lds = std::max(lds, stage2_qp_lds_bytes(m.p[i].setb, m.p[i].npw, m.p[i].nbp, a.nsub, PPC, NS));
+        lds = std::max(lds, stage2_qp_lds_bytes(m.p[i].setb, m.p[i].npw, m.p[i].nbp, a.nsub, PPC, NS, SY));
     }
     if (PRB && a.stamps) lds += (size_t)qp_nw<Q>() * kStampChunks * kStampPh * 4;
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     S2Multi mm = m;
     mm.nyblk = nyblk;
-    hipLaunchKernelGGL((k_stage2_qp<Q, RQ, PPC, NN, PRB, NS>), dim3(nx, (unsigned)(nyblk * m.npass)), dim3(qp_nw<Q>() * 64),
-                       lds, st, b, mm);
+    hipLaunchKernelGGL((k_stage2_qp<Q, RQ, PPC, NN, PRB, NS, SY>), dim3(nx, (unsigned)(nyblk * m.npass)),
+                       dim3(qp_nw<Q>() * 64), lds, st, b, mm);
     return hipGetLastError();
 }
 
-template <int Q, int RQ, int PPC, int NS>
+template <int Q, int RQ, int PPC, int NS, bool SY>
 static hipError_t launch_qp_s(const Stage2Args& a, const S2Multi& m, int nyblk, hipStream_t st)
 {
     const bool prb = (a.probe & 15) != 0 || a.stamps;
     if (a.nonneg && !(a.probe & 64))
-        return prb ? launch_qp_n<Q, RQ, PPC, true, true, NS>(a, m, nyblk, st)
-                   : launch_qp_n<Q, RQ, PPC, true, false, NS>(a, m, nyblk, st);
-    return prb ? launch_qp_n<Q, RQ, PPC, false, true, NS>(a, m, nyblk, st)
-               : launch_qp_n<Q, RQ, PPC, false, false, NS>(a, m, nyblk, st);
+        return prb ? launch_qp_n<Q, RQ, PPC, true, true, NS, SY>(a, m, nyblk, st)
+                   : launch_qp_n<Q, RQ, PPC, true, false, NS, SY>(a, m, nyblk, st);
+    return prb ? launch_qp_n<Q, RQ, PPC, false, true, NS, SY>(a, m, nyblk, st)
+               : launch_qp_n<Q, RQ, PPC, false, false, NS, SY>(a, m, nyblk, st);
 }
 
 template <int Q, int RQ, int PPC>
 static hipError_t launch_qp_p(const Stage2Args& a, const S2Multi& m, int nyblk, hipStream_t st)
 {
+    if (stage2_qp_sync(m, a.nsub, PPC)) return launch_qp_s<Q, RQ, PPC, 3, true>(a, m, nyblk, st);
     if constexpr (PPC >= 4) {
-        if (stage2_qp_ns(m, a.nsub, PPC) == 4) return launch_qp_s<Q, RQ, PPC, 4>(a, m, nyblk, st);
-        return launch_qp_s<Q, RQ, PPC, 3>(a, m, nyblk, st);
+        if (stage2_qp_ns(m, a.nsub, PPC) == 4) return launch_qp_s<Q, RQ, PPC, 4, false>(a, m, nyblk, st);
+        return launch_qp_s<Q, RQ, PPC, 3, false>(a, m, nyblk, st);
     } else {
-        return launch_qp_s<Q, RQ, PPC, 4>(a, m, nyblk, st);
+        return launch_qp_s<Q, RQ, PPC, 4, false>(a, m, nyblk, st);
     }
 }
 
