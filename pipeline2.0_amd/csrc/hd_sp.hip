@@ -487,16 +487,39 @@ __global__ __launch_bounds__(NW * 64) void k_sp_hits(SpArgs a)
         // the above-threshold bins of widths r0 .. r0+nr-1 (bad blocks included: the script
         // prunes before it looks at blocks): lane = bin, one ballot per 64 bins (consecutive
         // lanes read consecutive P entries: no bank conflicts)
+        // Wave wv takes the contiguous items [t0, t1) of the nr x 125 (width, 64 bins): at most
+        // two widths, whose parameters it loads once, and four boxcars' LDS reads in flight
+        // before their ballots (was: every 16th item, the width and scale reloaded per item and
+        // each compare waiting on its own two reads).  The boxcar values are the same doubles.
         uint32_t nhit_wv = 0;                                 // (HD_SP_STATS)
-        for (int t = wv; t < nr * (kSpChunk / 64); t += NW) {
-            const int j = t / (kSpChunk / 64), q = t - j * (kSpChunk / 64);
-            const bool hit = !(a.probe & 4) && boxcar(r0 + j, 64 * q + ln) > a.threshold;
-            const uint64_t m = __ballot(hit);
-            if (ln == 0) {
-                bits[j][2 * q] = (uint32_t)m;
-                bits[j][2 * q + 1] = (uint32_t)(m >> 32);
+        constexpr int kQ = kSpChunk / 64;
+        const int t1 = (wv + 1) * nr * kQ / NW;
+        for (int t = wv * nr * kQ / NW; t < t1;) {
+            const int j = t / kQ;
+            const int te = min(t1, (j + 1) * kQ);
+            const int w = a.widths[r0 + j];
+            const double rs = a.rsw[r0 + j];
+            const int dlo = kSpHalo - w / 2, dhi = kSpHalo + ((w & 1) ? w / 2 : w / 2 - 1) + 1;
+            auto put = [&](int q, double v) {
+                const uint64_t m = __ballot(!(a.probe & 4) && v > a.threshold);
+                if (ln == 0) {
+                    bits[j][2 * q] = (uint32_t)m;
+                    bits[j][2 * q + 1] = (uint32_t)(m >> 32);
+                }
+                nhit_wv += (uint32_t)__popcll(m);
+            };
+            for (; t + 4 <= te; t += 4) {
+                const int o = 64 * (t - j * kQ) + ln;
+                double v[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) v[u] = (P[o + 64 * u + dhi] - P[o + 64 * u + dlo]) * rs;
+#pragma unroll
+                for (int u = 0; u < 4; u++) put(t - j * kQ + u, v[u]);
             }
-            nhit_wv += (uint32_t)__popcll(m);
+            for (; t < te; t++) {
+                const int o = 64 * (t - j * kQ) + ln;
+                put(t - j * kQ, (P[o + dhi] - P[o + dlo]) * rs);
+            }
         }
         if (sst && ln == 0 && nhit_wv) atomicAdd(sst + 11, nhit_wv);
         __syncthreads();
