@@ -188,10 +188,10 @@ __device__ __forceinline__ void q8m_pass(const Stage1Multi& a, int p, int s, int
                     ao = divpk(ao);
                 }
                 int16_t* o = (int16_t*)a.out[p] + (int64_t)s * a.ostride[p] + tO0 + lane + 64 * m;
-                o[0] = (int16_t)(ae & 0xFFFFu);
-                o[JQ] = (int16_t)(ao & 0xFFFFu);
-                o[2 * JQ] = (int16_t)(ae >> 16);
-                o[3 * JQ] = (int16_t)(ao >> 16);
+                __builtin_nontemporal_store((int16_t)(ae & 0xFFFFu), o);     // (non-temporal: as k_stage1_q8)
+                __builtin_nontemporal_store((int16_t)(ao & 0xFFFFu), o + JQ);
+                __builtin_nontemporal_store((int16_t)(ae >> 16), o + 2 * JQ);
+                __builtin_nontemporal_store((int16_t)(ao >> 16), o + 3 * JQ);
                 mx = max(mx, (int)max(max(ae & 0xFFFFu, ae >> 16), max(ao & 0xFFFFu, ao >> 16)));
             } else {
                 float* o = (float*)a.out[p] + (int64_t)s * a.ostride[p] + tO0 + lane + 64 * m;
