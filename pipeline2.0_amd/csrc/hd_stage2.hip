@@ -2330,7 +2330,12 @@ __global__ __launch_bounds__(qp_nw<Q>() * 64) void k_stage2_qp(Stage2Args a, S2M
             if (!(PRB && (a.probe & 2))) dma(c + NS - 1);
             stamp(c, 1);
             const int chn = chk + 1 == nchunk ? 0 : chk + 1;
+            // the expand at raised wave priority: every wave's sums of the next chunk wait on
+            // the slowest wave's expand at the barrier (stage 2 33.15-33.19 -> 32.68-32.89 ms
+            // per beam; the sums at raised priority instead: 33.9-34.0, profiles/r06_ab_qp_prio.txt)
+            __builtin_amdgcn_s_setprio(2);
             if (c + 1 < ntot && !(PRB && (a.probe & 8))) expand(c + 1, chn);
+            __builtin_amdgcn_s_setprio(0);
             stamp(c, 2);
             const int voff = read_voff(c);
             sums(voff, lane_byte + (((c ^ chk) & 1) ? ((c & 1) ? set_bytes : 0u - set_bytes) : 0u));
